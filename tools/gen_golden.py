@@ -1,0 +1,256 @@
+"""Generate golden vectors from the REAL reference code (this container only).
+
+    python tools/gen_golden.py            # writes tests/golden/*.safetensors + *.json
+
+Runs the reference's own ``DecoderWithAttention`` / ``TransformerDecoder`` modules and its own
+``train.trainWithTeacherForcing`` / ``trainMultiGPU.trainWithTeacherForcing`` functions (imported
+from /root/reference with placeholder modules for the absent torchvision/gensim/h5py/nltk
+names, see tools/ref_import.py) on deterministic inputs from tests/golden_util.py, and stores
+inputs + outputs as data fixtures.  Reference source never leaves /root/reference.
+
+Fixtures:
+  lstm_tf_small       decoder.py:104-148 + train.py:240-302 (LSTM, 1 step, clip 5, Adam 1e-4)
+  transformer_tf_small transformerDecoder.py:88-108 + train.py:270-302 (key-padding mask)
+  ddp2_lstm            trainMultiGPU.py:339-420, 2-rank gloo DDP, different shard per rank
+  lstm_full_spot / transformer_full_spot   full-size dims (E=768, V=9490, L=52), B=2:
+                       loss + sampled logits; weights regenerated from the recipe at test time
+"""
+import copy
+import json
+import os
+import sys
+import tempfile
+
+import torch
+import torch.multiprocessing as mp
+from safetensors.torch import save_file
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(HERE, "..", "tests"))
+import ref_import  # noqa: E402
+from golden_util import GOLDEN_DIR, make_captions, make_features, make_params, word_map  # noqa: E402
+
+torch.set_num_threads(8)
+torch.use_deterministic_algorithms(True)
+
+LSTM_SMALL = dict(B=3, L=14, caplens=[12, 9, 6], V=50, E=32, A=16, D=16, Em=16, S=2, seed=11)
+TRF_SMALL = dict(B=3, L=12, caplens=[12, 7, 9], V=50, E=48, d=32, ff=64, H=4, layers=2, S=2, seed=22)
+LSTM_FULL = dict(B=2, L=52, caplens=[52, 40], V=9490, E=768, A=512, D=512, Em=512, S=7, seed=33)
+TRF_FULL = dict(B=2, L=52, caplens=[52, 37], V=9490, E=768, d=512, ff=512, H=8, layers=6, S=7, seed=44)
+
+
+class PassThroughEncoder(torch.nn.Module):
+    """Stands in for Encoder: the 'images' handed to the train function are already features."""
+
+    def forward(self, x):
+        return x
+
+
+def _train_module(lstm):
+    tr = ref_import.load("train.py", "ref_train", argv=["train.py", "--teacherForcing"])
+    tr.lstmDecoder = lstm
+    return tr
+
+
+def _named_shapes(module):
+    return {n: tuple(p.shape) for n, p in module.named_parameters()}
+
+
+def _grads(module):
+    return {"grad." + n: p.grad.detach().clone() for n, p in module.named_parameters() if p.grad is not None}
+
+
+def _lstm_decoder(cfg):
+    _train_module(True)
+    dec_mod = sys.modules["models.decoder"]
+    dec = dec_mod.DecoderWithAttention(attention_dim=cfg["A"], embed_dim=cfg["Em"], decoder_dim=cfg["D"],
+                                       vocab_size=cfg["V"], device="cpu", encoder_dim=cfg["E"], dropout=0.0)
+    dec.load_state_dict(make_params(_named_shapes(dec), cfg["seed"]))
+    return dec
+
+
+def _transformer_decoder(cfg):
+    _train_module(False)
+    tmod = sys.modules["models.transformerDecoder"]
+    dec = tmod.TransformerDecoder(embed_dim=cfg["d"], decoder_dim=cfg["ff"], vocab_size=cfg["V"], maxLen=cfg["L"],
+                                  device="cpu", wordMap=None, pretrained_embeddings_path=None,
+                                  fine_tune_embeddings=True, dropout=0.0, encoder_dim=cfg["E"],
+                                  num_heads=cfg["H"], num_layers=cfg["layers"])
+    sd = dict(dec.state_dict())
+    sd.update(make_params(_named_shapes(dec), cfg["seed"]))
+    dec.load_state_dict(sd)
+    return dec
+
+
+def _inputs(cfg):
+    enc = make_features((cfg["B"], cfg["S"], cfg["S"], cfg["E"]), cfg["seed"] + 1)
+    caps, caplens = make_captions(cfg["B"], cfg["L"], cfg["caplens"], cfg["V"], cfg["seed"] + 2)
+    return enc, caps, caplens
+
+
+def lstm_loss(dec, enc, caps, caplens, alphaC=1.0):
+    """train.py:263-269 verbatim in behaviour (packing + CE + doubly-stochastic reg)."""
+    from torch.nn.utils.rnn import pack_padded_sequence
+    scores, caps_sorted, dls, alphas, sort_ind = dec(teacherForcing=True, encoder_out=enc,
+                                                     encoded_captions=caps, caption_lengths=caplens)
+    targets = caps_sorted[:, 1:]
+    packed = pack_padded_sequence(scores, dls, batch_first=True).data
+    tpacked = pack_padded_sequence(targets, dls, batch_first=True).data
+    ce = torch.nn.CrossEntropyLoss()(packed, tpacked)
+    reg = alphaC * ((1.0 - alphas.sum(dim=1)) ** 2).mean()
+    return dict(scores=scores, caps_sorted=caps_sorted, dls=dls, alphas=alphas, sort_ind=sort_ind,
+                packed=packed, tpacked=tpacked, ce=ce, loss=ce + reg)
+
+
+def transformer_loss(dec, enc, caps, caplens):
+    """train.py:271-276 in behaviour."""
+    from torch.nn.utils.rnn import pack_padded_sequence
+    mask = caps == 0
+    scores, caps_out, dls = dec(teacherForcing=True, encoder_out=enc, encoded_captions=caps,
+                                caption_lengths=caplens, tgt_key_padding_mask=mask)
+    targets = caps_out[:, 1:]
+    packed = pack_padded_sequence(scores, dls, batch_first=True, enforce_sorted=False).data
+    tpacked = pack_padded_sequence(targets, dls, batch_first=True, enforce_sorted=False).data
+    loss = torch.nn.CrossEntropyLoss()(packed, tpacked)
+    return dict(scores=scores, dls=dls, packed=packed, tpacked=tpacked, loss=loss)
+
+
+def _run_ref_train_step(tr, dec, enc, caps, caplens, lstm):
+    """One call of the reference's own train.trainWithTeacherForcing over a one-batch loader."""
+    opt = torch.optim.Adam(params=filter(lambda p: p.requires_grad, dec.parameters()), lr=tr.decoderLr)
+    crit = torch.nn.CrossEntropyLoss()
+    out = tr.trainWithTeacherForcing(trainDataLoader=[(enc, caps, caplens)], encoder=PassThroughEncoder(),
+                                     decoder=dec, criterion=crit, encoderOptimizer=None,
+                                     decoderOptimizer=opt, epoch=0, device="cpu")
+    return out, {"post." + n: p.detach().clone() for n, p in dec.named_parameters()}
+
+
+def gen_lstm_small():
+    cfg = LSTM_SMALL
+    dec = _lstm_decoder(cfg)
+    enc, caps, caplens = _inputs(cfg)
+    params = {"param." + n: p.detach().clone() for n, p in dec.named_parameters()}
+    r = lstm_loss(dec, enc, caps, caplens)
+    r["loss"].backward()
+    grads = _grads(dec)
+    tr = _train_module(True)
+    dec2 = _lstm_decoder(cfg)
+    (loss_avg, top5, _, _), post = _run_ref_train_step(tr, dec2, enc, caps, caplens, True)
+    t = dict(enc=enc, caps=caps, caplens=caplens, predictions=r["scores"].detach(), alphas=r["alphas"].detach(),
+             caps_sorted=r["caps_sorted"], sort_ind=r["sort_ind"], packed_scores=r["packed"].detach(),
+             packed_targets=r["tpacked"], loss=r["loss"].detach().view(1), ce=r["ce"].detach().view(1),
+             ref_step_loss=torch.tensor([loss_avg]), ref_step_top5=torch.tensor([top5]))
+    t.update(params)
+    t.update(grads)
+    t.update(post)
+    meta = dict(cfg=cfg, decode_lengths=r["dls"], source="decoder.py:104-148; train.py:240-302")
+    return "lstm_tf_small", t, meta
+
+
+def gen_transformer_small():
+    cfg = TRF_SMALL
+    dec = _transformer_decoder(cfg)
+    enc, caps, caplens = _inputs(cfg)
+    params = {"param." + n: p.detach().clone() for n, p in dec.named_parameters()}
+    r = transformer_loss(dec, enc, caps, caplens)
+    r["loss"].backward()
+    grads = _grads(dec)
+    tr = _train_module(False)
+    tr.wordMap = word_map(cfg["V"])
+    dec2 = _transformer_decoder(cfg)
+    (loss_avg, top5, _, _), post = _run_ref_train_step(tr, dec2, enc, caps, caplens, False)
+    t = dict(enc=enc, caps=caps, caplens=caplens, predictions=r["scores"].detach(),
+             packed_scores=r["packed"].detach(), packed_targets=r["tpacked"], loss=r["loss"].detach().view(1),
+             pe=dec.pos_encoding.pe.detach().clone(),
+             ref_step_loss=torch.tensor([loss_avg]), ref_step_top5=torch.tensor([top5]))
+    t.update(params)
+    t.update(grads)
+    t.update(post)
+    meta = dict(cfg=cfg, decode_lengths=r["dls"], source="transformerDecoder.py:88-108; train.py:240-302")
+    return "transformer_tf_small", t, meta
+
+
+def _ddp_worker(rank, world, initfile, outdir):
+    import torch.distributed as dist
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", init_method="file://" + initfile, rank=rank, world_size=world)
+    tm = ref_import.load("trainMultiGPU.py", "ref_trainMultiGPU", argv=["trainMultiGPU.py", "--teacherForcing"])
+    tm.lstmDecoder = True
+    cfg = LSTM_SMALL
+    dec = _lstm_decoder(cfg)  # identical init on both ranks (recipe), like a rank-0 broadcast
+    # different shard per rank
+    enc = make_features((cfg["B"], cfg["S"], cfg["S"], cfg["E"]), 100 + rank)
+    caps, caplens = make_captions(cfg["B"], cfg["L"], [[12, 9, 6], [10, 11, 5]][rank], cfg["V"], 200 + rank)
+    ddp = DDP(dec)
+    opt = torch.optim.Adam(params=filter(lambda p: p.requires_grad, ddp.parameters()), lr=tm.decoderLr)
+    out = tm.trainWithTeacherForcing([(enc, caps, caplens)], PassThroughEncoder(), ddp, torch.nn.CrossEntropyLoss(),
+                                     None, opt, 0, "cpu", world)
+    t = {f"rank{rank}.enc": enc, f"rank{rank}.caps": caps, f"rank{rank}.caplens": caplens}
+    if rank == 0:
+        t.update({"post." + n: p.detach().clone() for n, p in dec.named_parameters()})
+        t["ref_loss"] = torch.tensor([out[0]])
+        t["ref_top5"] = torch.tensor([out[1]])
+    save_file({k: v.contiguous() for k, v in t.items()}, os.path.join(outdir, f"r{rank}.safetensors"))
+    dist.destroy_process_group()
+
+
+def gen_ddp2():
+    from safetensors.torch import load_file
+    with tempfile.TemporaryDirectory() as td:
+        initfile = os.path.join(td, "init")
+        mp.spawn(_ddp_worker, args=(2, initfile, td), nprocs=2, join=True)
+        t = {}
+        for r in range(2):
+            t.update(load_file(os.path.join(td, f"r{r}.safetensors")))
+    meta = dict(cfg=LSTM_SMALL, world_size=2, caplens=[[12, 9, 6], [10, 11, 5]],
+                source="trainMultiGPU.py:96-108,339-420 under 2-rank gloo DDP")
+    return "ddp2_lstm", t, meta
+
+
+def _spot_indices(n_rows, V, k, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, n_rows, (k,), generator=g), torch.randint(0, V, (k,), generator=g)
+
+
+def gen_lstm_full():
+    cfg = LSTM_FULL
+    dec = _lstm_decoder(cfg)
+    enc, caps, caplens = _inputs(cfg)
+    with torch.no_grad():
+        r = lstm_loss(dec, enc, caps, caplens)
+    ri, vi = _spot_indices(r["packed"].shape[0], cfg["V"], 256, 5)
+    t = dict(loss=r["loss"].view(1), ce=r["ce"].view(1), rows=ri, cols=vi, values=r["packed"][ri, vi],
+             alphas=r["alphas"], sort_ind=r["sort_ind"])
+    meta = dict(cfg=cfg, decode_lengths=r["dls"], torch=torch.__version__,
+                note="weights: tests/golden_util.make_params(named_shapes, cfg.seed); not stored")
+    return "lstm_full_spot", t, meta
+
+
+def gen_transformer_full():
+    cfg = TRF_FULL
+    dec = _transformer_decoder(cfg)
+    enc, caps, caplens = _inputs(cfg)
+    with torch.no_grad():
+        r = transformer_loss(dec, enc, caps, caplens)
+    ri, vi = _spot_indices(r["packed"].shape[0], cfg["V"], 256, 6)
+    t = dict(loss=r["loss"].view(1), rows=ri, cols=vi, values=r["packed"][ri, vi])
+    meta = dict(cfg=cfg, decode_lengths=r["dls"], torch=torch.__version__,
+                note="weights: tests/golden_util.make_params(named_shapes, cfg.seed); not stored")
+    return "transformer_full_spot", t, meta
+
+
+def main():
+    os.makedirs(GOLDEN_DIR, exist_ok=True)
+    for fn in (gen_lstm_small, gen_transformer_small, gen_ddp2, gen_lstm_full, gen_transformer_full):
+        name, tensors, meta = fn()
+        save_file({k: v.detach().contiguous() for k, v in tensors.items()},
+                  os.path.join(GOLDEN_DIR, name + ".safetensors"))
+        with open(os.path.join(GOLDEN_DIR, name + ".json"), "w") as f:
+            json.dump(meta, f, indent=1)
+        print("wrote", name, sum(v.numel() for v in tensors.values()), "values")
+
+
+if __name__ == "__main__":
+    main()
