@@ -1,0 +1,100 @@
+"""ctypes binding of libimgcap_hip.so (include/imgcap_abi.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` / ``make -C
+imagecaptioningconvnext_amd/csrc``.  There is no fallback: if the shared object is missing
+or fails to load, importing the product path raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libimgcap_hip.so")
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2
+
+c_void_p, c_int, c_int64, c_float, c_uint64, c_uint32 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
+                                                         ctypes.c_float, ctypes.c_uint64, ctypes.c_uint32)
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [
+        ("bias", c_void_p), ("colscale", c_void_p), ("rowscale", c_void_p), ("res", c_void_p), ("aux", c_void_p),
+        ("ldr", c_int64), ("ldaux", c_int64), ("drop_ld", c_int64), ("seed", c_uint64),
+        ("alpha", c_float), ("beta", c_float), ("drop_p", c_float), ("aux_scale", c_float),
+        ("act", ctypes.c_int32), ("c_dtype", ctypes.c_int32), ("rows_per_scale", ctypes.c_int32),
+        ("drop_stream", c_uint32),
+    ]
+
+
+class LstmDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("dtype", "B", "P", "E", "A", "D", "M", "T")] + [
+        (n, c_void_p) for n in ("w_hcat", "b_hcat", "w_ih", "w_f", "enc", "att1", "xe", "c0", "dl", "g1", "alphas",
+                                "awe", "zs", "gates", "cs", "hs", "hprev", "g2", "dhs", "dreg", "dcat", "dz", "dh",
+                                "dc", "datt1", "dwf")]
+
+
+# name -> argtypes  (every entry point declared in include/imgcap_abi.h)
+_SIGS = {
+    "imgcap_version": [],
+    "imgcap_gemm": [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int64, c_void_p, c_int64,
+                    c_int64, c_void_p, c_int64, c_int64, c_int, ctypes.POINTER(Epilogue), c_void_p],
+    "imgcap_colsum": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_float, c_void_p],
+    "imgcap_add_layernorm_fwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_uint64, c_uint32, c_void_p,
+                                 c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_add_layernorm_bwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                                 c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_convnext_stem": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p],
+    "imgcap_dwconv7_ln": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p, c_void_p],
+    "imgcap_ln_patchify2": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_adaptive_pool_nhwc": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "imgcap_embedding_fwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_float, c_uint64, c_uint32,
+                             c_void_p, c_void_p],
+    "imgcap_embedding_bwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_uint64, c_uint32, c_void_p,
+                             c_void_p],
+    "imgcap_ce_fwd": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_ce_bwd": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                      c_void_p],
+    "imgcap_clamp_adam": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
+                          c_float, c_int, c_float, c_float, c_void_p],
+    "imgcap_lstm_tf_fwd": [ctypes.POINTER(LstmDesc), c_void_p],
+    "imgcap_lstm_tf_bwd": [ctypes.POINTER(LstmDesc), c_void_p],
+    "imgcap_attn_reg": [c_int, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
+    "imgcap_dropout": [c_int, c_int64, c_void_p, c_float, c_uint64, c_uint32, c_void_p, c_void_p],
+    "imgcap_loss_finalize": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_cast": [c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p],
+    "imgcap_fill": [c_int, c_int64, c_float, c_void_p, c_void_p],
+}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the shared library; raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run __graft_entry__.build() (hipcc gfx950). "
+                               "There is no CPU/eager fallback for the HIP path.")
+        L = ctypes.CDLL(LIB_PATH)
+        L.imgcap_last_error_string.restype = ctypes.c_char_p
+        L.imgcap_last_error_string.argtypes = []
+        for name, argt in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = c_int
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return ["imgcap_last_error_string"] + list(_SIGS)
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().imgcap_last_error_string().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (rc={rc}): {msg}")

@@ -1,0 +1,98 @@
+// Cross-entropy over vocab rows with fused top-5 hit test.
+//   fwd  (train.py:268 / :276 CrossEntropyLoss on packed scores; utils.py:248-250 topk(5)):
+//        one pass over the row: online max / sum-exp, plus the count of logits strictly
+//        greater than the target's (hit5 = count < 5).
+//   bwd: dlogits = (exp(logit - lse) - onehot) * scale, scale read from device memory so the
+//        token count never needs a host sync.
+#include "common.h"
+
+namespace imgcap {
+
+template <typename T>
+__global__ __launch_bounds__(256) void ce_fwd_kernel(int V, const T* __restrict__ logits, long ld,
+                                                     const int64_t* __restrict__ tgt, float* __restrict__ lse_o,
+                                                     float* __restrict__ loss_o, float* __restrict__ hit_o) {
+  __shared__ float red[3][4];
+  const int row = blockIdx.x;
+  const T* x = logits + (long)row * ld;
+  const long t = tgt[row];
+  const float xt = (t >= 0 && t < V) ? to_f(x[t]) : 0.f;
+  float m = -INFINITY, s = 0.f, cnt = 0.f;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    const float v = to_f(x[c]);
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
+    else s += __expf(v - m);
+    cnt += (v > xt) ? 1.f : 0.f;
+  }
+  // combine (m, s) pairs across the wave then the block
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    const float mn = fmaxf(m, m2);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mn));
+    m = mn;
+  }
+  cnt = wave_sum(cnt);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = m; red[1][w] = s; red[2][w] = cnt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = red[0][0];
+    for (int i = 1; i < 4; ++i) M = fmaxf(M, red[0][i]);
+    float S = 0.f, C = 0.f;
+    for (int i = 0; i < 4; ++i) { S += red[1][i] * __expf(red[0][i] - M); C += red[2][i]; }
+    const float lse = M + logf(S);
+    lse_o[row] = lse;
+    const bool valid = t >= 0 && t < V;
+    if (loss_o) loss_o[row] = valid ? lse - xt : 0.f;
+    if (hit_o) hit_o[row] = (valid && C < 5.f) ? 1.f : 0.f;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(int V, const T* __restrict__ logits, long ld,
+                                                     const int64_t* __restrict__ tgt, const float* __restrict__ lse_i,
+                                                     const float* __restrict__ scale_p, T* __restrict__ d, long ldd) {
+  const int row = blockIdx.x;
+  const long t = tgt[row];
+  const T* x = logits + (long)row * ld;
+  T* o = d + (long)row * ldd;
+  const bool valid = t >= 0 && t < V;
+  const float lse = lse_i[row], sc = valid ? *scale_p : 0.f;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    const float p = __expf(to_f(x[c]) - lse);
+    o[c] = from_f<T>(sc * (p - (c == t ? 1.f : 0.f)));
+  }
+}
+
+}  // namespace imgcap
+
+using namespace imgcap;
+
+extern "C" int imgcap_ce_fwd(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
+                             float* lse, float* loss, float* hit5, void* stream) {
+  if (n == 0) return 0;
+  IMGCAP_REQUIRE(V > 0 && ld >= V, "imgcap_ce_fwd: bad V/ld");
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(ce_fwd_kernel<bf16>, dim3(n), dim3(256), 0, (hipStream_t)stream, V, (const bf16*)logits, ld,
+                       targets, lse, loss, hit5);
+  else
+    hipLaunchKernelGGL(ce_fwd_kernel<float>, dim3(n), dim3(256), 0, (hipStream_t)stream, V, (const float*)logits, ld,
+                       targets, lse, loss, hit5);
+  IMGCAP_CHECK_LAUNCH("imgcap_ce_fwd");
+  return 0;
+}
+
+extern "C" int imgcap_ce_bwd(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
+                             const float* lse, const float* scale, void* dlogits, int64_t ldd, void* stream) {
+  if (n == 0) return 0;
+  IMGCAP_REQUIRE(V > 0 && ld >= V && ldd >= V, "imgcap_ce_bwd: bad V/ld");
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(ce_bwd_kernel<bf16>, dim3(n), dim3(256), 0, (hipStream_t)stream, V, (const bf16*)logits, ld,
+                       targets, lse, scale, (bf16*)dlogits, ldd);
+  else
+    hipLaunchKernelGGL(ce_bwd_kernel<float>, dim3(n), dim3(256), 0, (hipStream_t)stream, V, (const float*)logits, ld,
+                       targets, lse, scale, (float*)dlogits, ldd);
+  IMGCAP_CHECK_LAUNCH("imgcap_ce_bwd");
+  return 0;
+}

@@ -1,0 +1,97 @@
+// Shared device/host helpers for the imgcap HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <cmath>
+#include <string>
+
+#include "../../include/imgcap_abi.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+#define DEV __device__ __forceinline__
+
+namespace imgcap {
+
+// ---- error plumbing (host) -------------------------------------------------------------
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define IMGCAP_CHECK_LAUNCH(what)                                                   \
+  do {                                                                             \
+    hipError_t _e = hipGetLastError();                                             \
+    if (_e != hipSuccess) return ::imgcap::fail((int)_e, std::string(what) + ": " + \
+                                                hipGetErrorString(_e));            \
+  } while (0)
+
+#define IMGCAP_REQUIRE(cond, msg)                                      \
+  do {                                                                 \
+    if (!(cond)) return ::imgcap::fail(IMGCAP_EINVAL, std::string(msg)); \
+  } while (0)
+
+inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+// ---- scalar conversions -------------------------------------------------------------------
+DEV float to_f(float x) { return x; }
+DEV float to_f(bf16 x) { return (float)x; }
+template <typename T> DEV T from_f(float x);
+template <> DEV float from_f<float>(float x) { return x; }
+template <> DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+DEV float load_as_f(const void* p, long i, int dtype) {
+  return dtype == IMGCAP_F32 ? ((const float*)p)[i] : (float)((const bf16*)p)[i];
+}
+DEV void store_from_f(void* p, long i, int dtype, float v) {
+  if (dtype == IMGCAP_F32) ((float*)p)[i] = v; else ((bf16*)p)[i] = (bf16)v;
+}
+
+// ---- wave / block reductions (wave64) --------------------------------------------------
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Sum over the whole block; `red` must hold blockDim.x/64 floats.  All threads get the result.
+DEV float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+// ---- counter-based RNG for dropout / stochastic depth -------------------------------------
+// A mask element is a pure function of (seed, stream, index), so the backward kernels
+// recompute it instead of storing it.
+DEV uint32_t hash3(uint64_t seed, uint32_t stream, uint64_t idx) {
+  uint64_t x = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(stream + 1)) ^ (idx * 0xD1B54A32D192ED03ull);
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+// keep iff u >= p ; returns scale 1/(1-p) or 0
+DEV float dropout_scale(uint64_t seed, uint32_t stream, uint64_t idx, float p) {
+  if (p <= 0.f) return 1.f;
+  const float u = (hash3(seed, stream, idx) >> 8) * (1.0f / 16777216.0f);
+  return u >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+}  // namespace imgcap

@@ -1,0 +1,212 @@
+// HBM-bound elementwise kernels of the step: fused clip+Adam over the flat parameter
+// buffer, token embedding (+dropout +positional encoding) and its scatter-add backward,
+// casts and fills.
+#include "common.h"
+
+namespace imgcap {
+
+// utils.py:183-192 clamp_(-clip, clip) then torch.optim.Adam (train.py:110, .step at :291),
+// same formula as torch's single-tensor Adam:
+//   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
+//   p -= (lr / (1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)
+__global__ __launch_bounds__(256) void clamp_adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         bf16* __restrict__ shadow, float lr, float b1, float b2,
+                                                         float eps, float step_size, float bc2_sqrt, float clip,
+                                                         float inv_div) {
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4 gg = ((const f32x4*)g)[i], mm = ((f32x4*)m)[i], vv = ((f32x4*)v)[i], pp = ((f32x4*)p)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = fminf(fmaxf(gg[j] * inv_div, -clip), clip);
+      mm[j] = b1 * mm[j] + (1.f - b1) * gj;
+      vv[j] = b2 * vv[j] + (1.f - b2) * gj * gj;
+      const float denom = sqrtf(vv[j]) / bc2_sqrt + eps;
+      pp[j] = pp[j] - step_size * (mm[j] / denom);
+    }
+    ((f32x4*)m)[i] = mm;
+    ((f32x4*)v)[i] = vv;
+    ((f32x4*)p)[i] = pp;
+    if (shadow) {
+      bf16x4 s = {(bf16)pp[0], (bf16)pp[1], (bf16)pp[2], (bf16)pp[3]};
+      ((bf16x4*)shadow)[i] = s;
+    }
+  }
+  // tail
+  for (long i = n4 * 4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float gj = fminf(fmaxf(g[i] * inv_div, -clip), clip);
+    m[i] = b1 * m[i] + (1.f - b1) * gj;
+    v[i] = b2 * v[i] + (1.f - b2) * gj * gj;
+    p[i] = p[i] - step_size * (m[i] / (sqrtf(v[i]) / bc2_sqrt + eps));
+    if (shadow) shadow[i] = (bf16)p[i];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(int n, int dim, const int64_t* __restrict__ ids,
+                                                            const float* __restrict__ table,
+                                                            const float* __restrict__ pe, int L, float p,
+                                                            uint64_t seed, uint32_t sid, T* __restrict__ out) {
+  const long total = (long)n * dim;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long r = e / dim;
+    const int c = (int)(e % dim);
+    float v = table[ids[r] * (long)dim + c] * dropout_scale(seed, sid, e, p);
+    if (pe) v += pe[(r % L) * dim + c];
+    out[e] = from_f<T>(v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(int n, int dim, const int64_t* __restrict__ ids,
+                                                            const T* __restrict__ dout, float p, uint64_t seed,
+                                                            uint32_t sid, float* __restrict__ dtable) {
+  const long total = (long)n * dim;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long r = e / dim;
+    const int c = (int)(e % dim);
+    const float d = to_f(dout[e]) * dropout_scale(seed, sid, e, p);
+    if (d != 0.f) atomicAdd(&dtable[ids[r] * (long)dim + c], d);
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(long n, const TI* __restrict__ x, TO* __restrict__ y) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = from_f<TO>(to_f(x[i]));
+}
+
+template <typename T>
+__global__ void fill_kernel(long n, float v, T* __restrict__ x) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) x[i] = from_f<T>(v);
+}
+
+template <typename T>
+__global__ void dropout_kernel(long n, const T* __restrict__ x, float p, uint64_t seed, uint32_t sid,
+                               T* __restrict__ y) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    y[i] = from_f<T>(to_f(x[i]) * dropout_scale(seed, sid, i, p));
+}
+
+__global__ void loss_finalize_kernel(int n, const float* __restrict__ loss_rows, const float* __restrict__ hit5,
+                                     const int64_t* __restrict__ tgt, const float* __restrict__ extra,
+                                     float* __restrict__ out) {
+  __shared__ float red[16];
+  float l = 0.f, c = 0.f, h = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    if (tgt[i] >= 0) { l += loss_rows[i]; c += 1.f; h += hit5[i]; }
+  }
+  l = block_sum(l, red);
+  c = block_sum(c, red);
+  h = block_sum(h, red);
+  if (threadIdx.x == 0) {
+    const float cnt = c > 0.f ? c : 1.f;
+    out[0] = l / cnt + (extra ? *extra : 0.f);
+    out[1] = c;
+    out[2] = h;
+    out[3] = 1.f / cnt;
+  }
+}
+
+static dim3 grid_for(long n) {
+  long b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return dim3((unsigned)b);
+}
+
+}  // namespace imgcap
+
+using namespace imgcap;
+
+extern "C" int imgcap_clamp_adam(int64_t n, float* param, const float* grad, float* m, float* v, void* shadow_bf16,
+                                 float lr, float beta1, float beta2, float eps, int step, float clip, float grad_div,
+                                 void* stream) {
+  if (n == 0) return 0;
+  IMGCAP_REQUIRE(step >= 1, "imgcap_clamp_adam: step must be >= 1");
+  IMGCAP_REQUIRE(aligned16(param) && aligned16(grad) && aligned16(m) && aligned16(v),
+                 "imgcap_clamp_adam: buffers must be 16-byte aligned");
+  IMGCAP_REQUIRE(shadow_bf16 == nullptr || (((uintptr_t)shadow_bf16) & 7) == 0, "imgcap_clamp_adam: shadow align");
+  const double bc1 = 1.0 - std::pow((double)beta1, step);
+  const double bc2 = 1.0 - std::pow((double)beta2, step);
+  hipLaunchKernelGGL(clamp_adam_kernel, grid_for(n / 4 + 1), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad,
+                     m, v, (bf16*)shadow_bf16, lr, beta1, beta2, eps, (float)(lr / bc1), (float)std::sqrt(bc2), clip,
+                     1.0f / grad_div);
+  IMGCAP_CHECK_LAUNCH("imgcap_clamp_adam");
+  return 0;
+}
+
+extern "C" int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* ids, const float* table, const float* pe,
+                                    int L, float drop_p, uint64_t seed, uint32_t drop_stream, void* out, void* stream) {
+  if (n == 0) return 0;
+  IMGCAP_REQUIRE(pe == nullptr || L > 0, "imgcap_embedding_fwd: L");
+  const long total = (long)n * dim;
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(embedding_fwd_kernel<bf16>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
+                       table, pe, L, drop_p, seed, drop_stream, (bf16*)out);
+  else
+    hipLaunchKernelGGL(embedding_fwd_kernel<float>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
+                       table, pe, L, drop_p, seed, drop_stream, (float*)out);
+  IMGCAP_CHECK_LAUNCH("imgcap_embedding_fwd");
+  return 0;
+}
+
+extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* ids, const void* dout, float drop_p,
+                                    uint64_t seed, uint32_t drop_stream, float* dtable, void* stream) {
+  if (n == 0) return 0;
+  const long total = (long)n * dim;
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(embedding_bwd_kernel<bf16>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
+                       (const bf16*)dout, drop_p, seed, drop_stream, dtable);
+  else
+    hipLaunchKernelGGL(embedding_bwd_kernel<float>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
+                       (const float*)dout, drop_p, seed, drop_stream, dtable);
+  IMGCAP_CHECK_LAUNCH("imgcap_embedding_bwd");
+  return 0;
+}
+
+extern "C" int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint64_t seed, uint32_t drop_stream,
+                              void* y, void* stream) {
+  if (n == 0) return 0;
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(dropout_kernel<bf16>, grid_for(n), dim3(256), 0, (hipStream_t)stream, (long)n, (const bf16*)x,
+                       p, seed, drop_stream, (bf16*)y);
+  else
+    hipLaunchKernelGGL(dropout_kernel<float>, grid_for(n), dim3(256), 0, (hipStream_t)stream, (long)n,
+                       (const float*)x, p, seed, drop_stream, (float*)y);
+  IMGCAP_CHECK_LAUNCH("imgcap_dropout");
+  return 0;
+}
+
+extern "C" int imgcap_loss_finalize(int n, const float* loss_rows, const float* hit5, const int64_t* targets,
+                                    const float* extra, float* out, void* stream) {
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n, loss_rows, hit5, targets,
+                     extra, out);
+  IMGCAP_CHECK_LAUNCH("imgcap_loss_finalize");
+  return 0;
+}
+
+extern "C" int imgcap_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream) {
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (in_dtype == IMGCAP_F32 && out_dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), grid_for(n), dim3(256), 0, st, (long)n, (const float*)x, (bf16*)y);
+  else if (in_dtype == IMGCAP_BF16 && out_dtype == IMGCAP_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), grid_for(n), dim3(256), 0, st, (long)n, (const bf16*)x, (float*)y);
+  else if (in_dtype == IMGCAP_F32 && out_dtype == IMGCAP_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), grid_for(n), dim3(256), 0, st, (long)n, (const float*)x, (float*)y);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), grid_for(n), dim3(256), 0, st, (long)n, (const bf16*)x, (bf16*)y);
+  IMGCAP_CHECK_LAUNCH("imgcap_cast");
+  return 0;
+}
+
+extern "C" int imgcap_fill(int dtype, int64_t n, float value, void* x, void* stream) {
+  if (n == 0) return 0;
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(fill_kernel<bf16>, grid_for(n), dim3(256), 0, (hipStream_t)stream, (long)n, value, (bf16*)x);
+  else
+    hipLaunchKernelGGL(fill_kernel<float>, grid_for(n), dim3(256), 0, (hipStream_t)stream, (long)n, value, (float*)x);
+  IMGCAP_CHECK_LAUNCH("imgcap_fill");
+  return 0;
+}

@@ -1,0 +1,208 @@
+"""Tensor-level wrappers over the C ABI (device pointers + current HIP stream).
+
+All functions enqueue on ``torch.cuda.current_stream()``; none allocates unless it is asked to
+return a fresh output.  Inputs must already live on the GPU; there is no CPU path.
+"""
+import ctypes
+
+import torch
+
+from . import _abi
+from ._abi import ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, Epilogue  # noqa: F401
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dt(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}") from None
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check_dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("imgcap kernels need GPU tensors (no CPU fallback)")
+
+
+def _ld(t, trans):
+    """Leading dimension of a 2-D operand view whose innermost stride is 1."""
+    if t.stride(-1) != 1:
+        raise ValueError("operand must have unit inner stride")
+    return t.stride(-2) if t.dim() >= 2 else t.shape[-1]
+
+
+def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None, bias=None, act=ACT_NONE, alpha=1.0,
+         beta=0.0, res=None, aux=None, aux_scale=1.0, colscale=None, rowscale=None, rows_per_scale=1, drop_p=0.0,
+         seed=0, drop_stream=0, drop_ld=None, M=None, N=None, K=None):
+    """out[M,N] = epilogue(op(a) @ op(b)); op(x) = x.T if trans else x (torch semantics).
+
+    ``a``/``b`` are 2-D views (unit inner stride).  With trans_b=True, b is an nn.Linear
+    weight [N, K] and the call is ``a @ b.T``.
+    """
+    _check_dev(a, b, out, bias, res, aux)
+    if a.dtype != b.dtype:
+        raise TypeError("a and b must share dtype")
+    if M is None:
+        M = a.shape[1] if trans_a else a.shape[0]
+    if K is None:
+        K = a.shape[0] if trans_a else a.shape[1]
+    if N is None:
+        N = b.shape[0] if trans_b else b.shape[1]
+    kb = b.shape[1] if trans_b else b.shape[0]
+    if kb != K:
+        raise ValueError(f"gemm: K mismatch {K} vs {kb}")
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=out_dtype or a.dtype)
+    ep = Epilogue()
+    ep.bias = ptr(bias)
+    ep.colscale = ptr(colscale)
+    ep.rowscale = ptr(rowscale)
+    ep.rows_per_scale = rows_per_scale
+    ep.res = ptr(res)
+    ep.ldr = 0 if res is None else res.stride(0)
+    ep.aux = ptr(aux)
+    ep.ldaux = 0 if aux is None else aux.stride(0)
+    ep.aux_scale = aux_scale
+    ep.alpha = alpha
+    ep.beta = beta
+    ep.act = act
+    ep.c_dtype = dt(out)
+    ep.drop_p = drop_p
+    ep.seed = seed
+    ep.drop_stream = drop_stream
+    ep.drop_ld = N if drop_ld is None else drop_ld
+    _abi.call("imgcap_gemm", dt(a), 0 if trans_a else 1, 1 if trans_b else 0, M, N, K,
+              a.data_ptr(), _ld(a, trans_a), 0, b.data_ptr(), _ld(b, trans_b), 0,
+              out.data_ptr(), out.stride(0), 0, 1, ctypes.byref(ep), stream())
+    return out
+
+
+def gemm_raw(dtype, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, C, ldc, c_dtype, *, batch=1, sA=0, sB=0, sC=0,
+             bias=None, act=ACT_NONE, alpha=1.0, beta=0.0, rowscale=None, rows_per_scale=1, drop_p=0.0, seed=0,
+             drop_stream=0, drop_ld=0):
+    """Pointer-level GEMM for strided / batched operand views."""
+    ep = Epilogue()
+    ep.bias = bias
+    ep.rowscale = rowscale
+    ep.rows_per_scale = rows_per_scale
+    ep.alpha = alpha
+    ep.beta = beta
+    ep.act = act
+    ep.c_dtype = c_dtype
+    ep.drop_p = drop_p
+    ep.seed = seed
+    ep.drop_stream = drop_stream
+    ep.drop_ld = drop_ld
+    _abi.call("imgcap_gemm", dtype, a_kmajor, b_kmajor, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch,
+              ctypes.byref(ep), stream())
+
+
+def colsum(x, out, beta=0.0, rows=None, cols=None, ld=None):
+    rows = x.shape[0] if rows is None else rows
+    cols = x.shape[1] if cols is None else cols
+    _abi.call("imgcap_colsum", dt(x), rows, cols, x.data_ptr(), x.stride(0) if ld is None else ld, out.data_ptr(),
+              beta, stream())
+    return out
+
+
+def add_layernorm(x, r, gamma, beta, eps, *, drop_p=0.0, seed=0, drop_stream=0, s_out=None, y=None):
+    rows, cols = x.shape
+    y = torch.empty_like(x) if y is None else y
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    _abi.call("imgcap_add_layernorm_fwd", dt(x), rows, cols, x.data_ptr(), ptr(r), drop_p, seed, drop_stream,
+              gamma.data_ptr(), beta.data_ptr(), eps, ptr(s_out), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+              stream())
+    return y, mean, rstd
+
+
+def add_layernorm_bwd(dy, s, mean, rstd, gamma, dgamma, dbeta, *, drop_p=0.0, seed=0, drop_stream=0, dx=None,
+                      dr=None):
+    rows, cols = dy.shape
+    dx = torch.empty_like(dy) if dx is None else dx
+    _abi.call("imgcap_add_layernorm_bwd", dt(dy), rows, cols, dy.data_ptr(), s.data_ptr(), mean.data_ptr(),
+              rstd.data_ptr(), gamma.data_ptr(), drop_p, seed, drop_stream, dx.data_ptr(), ptr(dr), ptr(dgamma),
+              ptr(dbeta), stream())
+    return dx
+
+
+def ce_fwd(logits, targets, V, lse, loss, hit5):
+    n = targets.numel()
+    _abi.call("imgcap_ce_fwd", dt(logits), n, V, logits.data_ptr(), logits.stride(0), targets.data_ptr(),
+              lse.data_ptr(), ptr(loss), ptr(hit5), stream())
+
+
+def ce_bwd(logits, targets, V, lse, scale, dlogits):
+    n = targets.numel()
+    _abi.call("imgcap_ce_bwd", dt(logits), n, V, logits.data_ptr(), logits.stride(0), targets.data_ptr(),
+              lse.data_ptr(), scale.data_ptr(), dlogits.data_ptr(), dlogits.stride(0), stream())
+
+
+def loss_finalize(loss_rows, hit5, targets, extra, out):
+    _abi.call("imgcap_loss_finalize", targets.numel(), loss_rows.data_ptr(), hit5.data_ptr(), targets.data_ptr(),
+              ptr(extra), out.data_ptr(), stream())
+
+
+def clamp_adam(param, grad, m, v, shadow, lr, step, clip, grad_div=1.0, betas=(0.9, 0.999), eps=1e-8):
+    _abi.call("imgcap_clamp_adam", param.numel(), param.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(),
+              ptr(shadow), lr, betas[0], betas[1], eps, step, clip if clip is not None else 3.4e38, grad_div,
+              stream())
+
+
+def embedding_fwd(ids, table, out, *, pe=None, L=1, drop_p=0.0, seed=0, drop_stream=0):
+    _abi.call("imgcap_embedding_fwd", dt(out), ids.numel(), table.shape[1], ids.data_ptr(), table.data_ptr(),
+              ptr(pe), L, drop_p, seed, drop_stream, out.data_ptr(), stream())
+    return out
+
+
+def embedding_bwd(ids, dout, dtable, *, drop_p=0.0, seed=0, drop_stream=0):
+    _abi.call("imgcap_embedding_bwd", dt(dout), ids.numel(), dtable.shape[1], ids.data_ptr(), dout.data_ptr(),
+              drop_p, seed, drop_stream, dtable.data_ptr(), stream())
+
+
+def dropout(x, p, seed, drop_stream, out=None):
+    out = torch.empty_like(x) if out is None else out
+    _abi.call("imgcap_dropout", dt(x), x.numel(), x.data_ptr(), p, seed, drop_stream, out.data_ptr(), stream())
+    return out
+
+
+def cast(x, out):
+    _abi.call("imgcap_cast", dt(x), dt(out), x.numel(), x.data_ptr(), out.data_ptr(), stream())
+    return out
+
+
+def convnext_stem(images, w, bias, ln_w, ln_b, out):
+    B, _, H, W = images.shape
+    _abi.call("imgcap_convnext_stem", dt(out), B, H, W, w.shape[0], images.data_ptr(), w.data_ptr(),
+              bias.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(), out.data_ptr(), stream())
+    return out
+
+
+def dwconv7_ln(x, w49, bias, ln_w, ln_b, out):
+    B, H, W, C = x.shape
+    _abi.call("imgcap_dwconv7_ln", dt(x), B, H, W, C, x.data_ptr(), w49.data_ptr(), bias.data_ptr(),
+              ln_w.data_ptr(), ln_b.data_ptr(), out.data_ptr(), stream())
+    return out
+
+
+def ln_patchify2(x, ln_w, ln_b, out):
+    B, H, W, C = x.shape
+    _abi.call("imgcap_ln_patchify2", dt(x), B, H, W, C, x.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
+              out.data_ptr(), stream())
+    return out
+
+
+def adaptive_pool(x, OH, OW, out):
+    B, H, W, C = x.shape
+    _abi.call("imgcap_adaptive_pool_nhwc", dt(x), B, H, W, C, OH, OW, x.data_ptr(), out.data_ptr(), stream())
+    return out

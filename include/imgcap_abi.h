@@ -1,0 +1,206 @@
+/*
+ * imgcap_abi.h — C ABI of libimgcap_hip.so, the MI355X (gfx950) kernels behind the
+ * teacher-forced image-captioning train step of sa06840/ImageCaptioningConvNeXt.
+ *
+ * The reference has no native code and no FFI: its boundary is the PyTorch
+ * nn.Module surface of models/encoder.py, models/decoder.py, models/transformerDecoder.py and
+ * the train-step functions of train.py / trainMultiGPU.py.  Each entry point below replaces
+ * the torch/cuDNN/cuBLAS/NCCL work reached from one reference line (cited per function).
+ *
+ * Conventions
+ *   - Plain pointers to device memory + sizes; no torch types.  `stream` is a hipStream_t
+ *     (passed as void*); every call only enqueues work on it (no allocation, no sync), so a
+ *     caller may capture calls into a hipGraph.
+ *   - `dtype`: IMGCAP_F32 or IMGCAP_BF16 = element type of the activation/weight operands.
+ *     Accumulation is always fp32.  Optimizer state and master weights are fp32.
+ *   - Return 0 on success, a hipError_t (>0) or IMGCAP_E* (<0) otherwise;
+ *     imgcap_last_error_string() describes the last failure (thread-local).
+ *   - The caller owns every buffer (including workspaces); the library never allocates.
+ */
+#ifndef IMGCAP_ABI_H
+#define IMGCAP_ABI_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { IMGCAP_F32 = 0, IMGCAP_BF16 = 1 };
+enum { IMGCAP_OK = 0, IMGCAP_EINVAL = -1, IMGCAP_EUNSUPPORTED = -2 };
+enum { IMGCAP_ACT_NONE = 0, IMGCAP_ACT_GELU = 1, IMGCAP_ACT_RELU = 2 };
+
+const char* imgcap_last_error_string(void);
+int imgcap_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * GEMM with fused epilogue (MFMA: bf16 16x16x32 / f32 16x16x4).
+ *   acc[m,n] = sum_k A(m,k) * B(k,n)
+ *   A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]
+ *   B(k,n) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]      (b_kmajor = nn.Linear weight [N][K])
+ *   v = alpha*acc (+bias[n]) -> act -> dropout(p; seed,stream, index m*drop_ld+n)
+ *       -> (*= aux[m,n] > 0 ? aux_scale : 0) -> (*= colscale[n]) -> (*= rowscale[m/rows_per_scale])
+ *       -> (+= res[m,n]) -> (+= beta*C[m,n]) -> C[m,n] (c_dtype)
+ * Replaces every nn.Linear / 1x1-conv / patchify-conv / projection matmul on the path:
+ * decoder.py:61-63,100-101,139-144; transformerDecoder.py:95,104,106; torchvision CNBlock
+ * Linear pair + layer_scale + residual (reached via encoder.py:24); and their backward.
+ * -------------------------------------------------------------------------------------- */
+typedef struct imgcap_epilogue {
+  const float* bias;       /* [N] or NULL */
+  const float* colscale;   /* [N] or NULL (ConvNeXt layer_scale) */
+  const float* rowscale;   /* [M/rows_per_scale] or NULL (stochastic depth, per sample) */
+  const void* res;         /* residual [M, ldr] of c_dtype, or NULL */
+  const void* aux;         /* relu/dropout mask source [M, ldaux] of c_dtype, or NULL */
+  int64_t ldr;
+  int64_t ldaux;
+  int64_t drop_ld;
+  uint64_t seed;
+  float alpha;
+  float beta;
+  float drop_p;
+  float aux_scale;
+  int32_t act;
+  int32_t c_dtype;
+  int32_t rows_per_scale;
+  uint32_t drop_stream;
+} imgcap_epilogue;
+
+int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
+                const void* A, int64_t lda, int64_t strideA,
+                const void* B, int64_t ldb, int64_t strideB,
+                void* C, int64_t ldc, int64_t strideC, int batch,
+                const imgcap_epilogue* epi, void* stream);
+
+/* column sums of a [rows, cols] matrix into fp32 out[cols] (bias gradients); beta=1 accumulates */
+int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64_t ldx, float* out, float beta,
+                  void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * LayerNorm over the last dim, optionally of a sum:  s = x + dropout(r);  y = LN(s)*g + b.
+ * Replaces nn.TransformerDecoderLayer's post-norm residual blocks (norm_first=False,
+ * transformerDecoder.py:82,104) incl. the sublayer dropout.  Saves s, mean, rstd for bwd.
+ * -------------------------------------------------------------------------------------- */
+int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const void* x, const void* r,
+                             float drop_p, uint64_t seed, uint32_t drop_stream,
+                             const float* gamma, const float* beta, float eps,
+                             void* s_out, void* y, float* mean, float* rstd, void* stream);
+/* dS = LN backward of dy;  dx = dS;  dr = dS * dropmask  (dr may be NULL);
+ * dgamma/dbeta accumulated (+=) in fp32. */
+int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const void* dy, const void* s,
+                             const float* mean, const float* rstd, const float* gamma,
+                             float drop_p, uint64_t seed, uint32_t drop_stream,
+                             void* dx, void* dr, float* dgamma, float* dbeta, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * ConvNeXt trunk (torchvision features reached via encoder.py:24), NHWC activations.
+ * -------------------------------------------------------------------------------------- */
+/* features[0]: Conv2d(3,C0,4,s4)+LayerNorm2d(eps 1e-6).  images: f32 NCHW [B,3,H,W];
+ * w: f32 [C0][48] (ci,kh,kw order as torch); out: dtype NHWC [B,H/4,W/4,C0]. */
+int imgcap_convnext_stem(int dtype, int B, int H, int W, int C0, const float* images,
+                         const float* w, const float* bias, const float* ln_w, const float* ln_b,
+                         void* out, void* stream);
+/* CNBlock head: depthwise 7x7 (pad 3, bias) + LayerNorm(C, eps 1e-6).  w: f32 [49][C]. */
+int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const void* x, const float* w,
+                      const float* bias, const float* ln_w, const float* ln_b, void* out,
+                      void* stream);
+/* features[2,4,6] head: LayerNorm2d(C) then gather 2x2/s2 patches into rows
+ * out[B*(H/2)*(W/2)][4C] ordered (kh, kw, c) (weights repacked to match). */
+int imgcap_ln_patchify2(int dtype, int B, int H, int W, int C, const void* x, const float* ln_w,
+                        const float* ln_b, void* out, void* stream);
+/* AdaptiveAvgPool2d((OH,OW)) on NHWC (encoder.py:20,25) */
+int imgcap_adaptive_pool_nhwc(int dtype, int B, int H, int W, int C, int OH, int OW,
+                              const void* x, void* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Token embedding (+ dropout, + positional encoding) — decoder.py:119,
+ * transformerDecoder.py:97-98.  out[n, :] = drop(table[ids[n], :]) + (pe ? pe[n % L, :] : 0)
+ * -------------------------------------------------------------------------------------- */
+int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* ids, const float* table,
+                         const float* pe, int L, float drop_p, uint64_t seed, uint32_t drop_stream,
+                         void* out, void* stream);
+/* dtable[ids[n], :] += dout[n, :] * dropmask   (fp32 atomics) */
+int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* ids, const void* dout,
+                         float drop_p, uint64_t seed, uint32_t drop_stream, float* dtable,
+                         void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Cross-entropy over rows of logits (train.py:266-268,274-276 CrossEntropyLoss on packed
+ * scores) with fused top-5 hit (utils.py:248-250).  target < 0 = ignored row.
+ * fwd: lse[n], loss[n] = lse - logit[target] (0 if ignored), hit5[n] in {0,1}.
+ * bwd: dlogits = (softmax - onehot) * scale  (0 rows for ignored / padded columns)
+ * -------------------------------------------------------------------------------------- */
+int imgcap_ce_fwd(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
+                  float* lse, float* loss, float* hit5, void* stream);
+int imgcap_ce_bwd(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
+                  const float* lse, const float* scale, void* dlogits, int64_t ldd, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * clip_gradient (utils.py:183-192, clamp to +-clip) + torch.optim.Adam step
+ * (train.py:110,289-291) over a flat fp32 parameter buffer; optionally refreshes a bf16
+ * shadow copy of the weights used by the bf16 kernels.  grad is divided by grad_div first
+ * (DDP mean over ranks, trainMultiGPU.py:233,384).
+ * -------------------------------------------------------------------------------------- */
+int imgcap_clamp_adam(int64_t n, float* param, const float* grad, float* m, float* v,
+                      void* shadow_bf16, float lr, float beta1, float beta2, float eps,
+                      int step, float clip, float grad_div, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * LSTM + soft-attention decoder, teacher forced (decoder.py:104-148, Attention 60-66,
+ * LSTMCell at :141).  One call enqueues all T steps (4 kernels per step).  Batch-major
+ * buffers [B, T, .]; rows sorted by decode length (decoder.py:114); W3 = A + E + 4D.
+ * fwd requires: hprev[:,0,:] = h0, c0, xe = emb_t W_ih[:, :M]^T + b_ih + b_hh, att1.
+ * bwd requires: the saved forward buffers, dhs (dL/dh_t from fc), dreg; produces dcat
+ * (= per-step [d att2 | d gate_pre | d gates_preact]) for the weight-gradient GEMMs, dh/dc
+ * (= dL/dh0, dL/dc0), datt1 (sum over t of dL/datt1) and dwf partials [B, A].
+ * -------------------------------------------------------------------------------------- */
+typedef struct imgcap_lstm_desc {
+  int32_t dtype, B, P, E, A, D, M, T;
+  const void* w_hcat;   /* [W3, D] = [W_da; W_fb; W_hh]             */
+  const float* b_hcat;  /* [W3]   = [b_da; b_fb; 0]                 */
+  const void* w_ih;     /* [4D, M+E] LSTMCell weight_ih             */
+  const float* w_f;     /* [A] full_att weight                      */
+  const void* enc;      /* [B, P, E] encoder_out (sorted)           */
+  const void* att1;     /* [B, P, A]                                */
+  const float* xe;      /* [B, T, 4D]                               */
+  const float* c0;      /* [B, D]                                   */
+  const int32_t* dl;    /* [B] decode lengths (sorted, device)      */
+  float* g1;            /* [B, T, W3] saved                         */
+  float* alphas;        /* [B, T, P]  output (0 where t >= dl[b])   */
+  float* awe;           /* [B, T, E]  saved attention context       */
+  void* zs;             /* [B, T, E]  gate * context (LSTM input)   */
+  float* gates;         /* [B, T, 4D] activated i, f, g, o          */
+  float* cs;            /* [B, T, D]                                */
+  void* hs;             /* [B, T, D]  h_t                           */
+  void* hprev;          /* [B, T, D]  h_{t-1}; slot 0 = h0          */
+  float* g2;            /* [B, 4D] workspace                        */
+  const void* dhs;      /* [B, T, D]  bwd input                     */
+  const float* dreg;    /* [B, P]     bwd input                     */
+  void* dcat;           /* [B, T, W3] bwd output                    */
+  float* dz;            /* [B, E] workspace                         */
+  float* dh;            /* [B, D] out: dL/dh0                       */
+  float* dc;            /* [B, D] out: dL/dc0                       */
+  float* datt1;         /* [B, P, A] out                            */
+  float* dwf;           /* [B, A] out                               */
+} imgcap_lstm_desc;
+
+int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream);
+int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream);
+/* train.py:269: reg = alphaC*mean_{b,p}(1-sum_t alpha)^2 -> *reg_out; dreg[b,p] = d reg/d alpha */
+int imgcap_attn_reg(int B, int T, int P, const float* alphas, float alphaC, float* dreg, float* reg_out,
+                    void* stream);
+
+/* y = x * dropmask(seed, stream, i) (nn.Dropout, decoder.py:144 / transformer dropouts) */
+int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint64_t seed, uint32_t drop_stream, void* y,
+                   void* stream);
+/* Token-mean loss finalisation without host sync (train.py:268 + reduceLossAndTokens inputs):
+ * out[0] = sum(loss_rows)/count + (extra ? *extra : 0), out[1] = count (valid targets),
+ * out[2] = sum(hit5), out[3] = 1/count (the CE backward scale) */
+int imgcap_loss_finalize(int n, const float* loss_rows, const float* hit5, const int64_t* targets,
+                         const float* extra, float* out, void* stream);
+
+/* elementwise helpers */
+int imgcap_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);
+int imgcap_fill(int dtype, int64_t n, float value, void* x, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

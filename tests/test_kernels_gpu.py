@@ -1,0 +1,228 @@
+"""HIP kernels vs plain PyTorch fp32 references of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
+
+
+def _padded(x, dev, dtype):
+    """Copy x [r, c] into storage whose leading dim is a multiple of 8 (16-byte rows)."""
+    r, c = x.shape
+    buf = torch.zeros(r, (c + 7) // 8 * 8, dtype=dtype, device=dev)
+    buf[:, :c] = x.to(dtype)
+    return buf[:, :c]
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,Kd", [(37, 50, 72), (32, 3328, 512), (64, 200, 136), (300, 260, 1000), (1030, 520, 96)])
+def test_gemm_layouts(hip_device, dtype, tol, ta, tb, M, N, Kd):
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    a = torch.randn(M, Kd, generator=g)
+    b = torch.randn(Kd, N, generator=g)
+    ref = a @ b
+    ad = _padded(a.t() if ta else a, hip_device, dtype)
+    bd = _padded(b.t() if tb else b, hip_device, dtype)
+    out = K.gemm(ad, bd, trans_a=ta, trans_b=tb, out_dtype=torch.float32)
+    if dtype == torch.bfloat16:
+        ref = a.bfloat16().float() @ b.bfloat16().float()
+    assert _rel(out.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
+def test_gemm_epilogues(hip_device, dtype, tol):
+    torch.manual_seed(0)
+    M, N, Kd = 196, 96, 384
+    x = torch.randn(M, Kd)
+    w = torch.randn(N, Kd) / math.sqrt(Kd)
+    bias = torch.randn(N)
+    res = torch.randn(M, N)
+    gamma = torch.randn(N)
+    rs = torch.rand(4) + 0.5
+    dev = lambda t, d=dtype: t.to(hip_device, d)  # noqa: E731
+    # bias + GELU
+    out = K.gemm(dev(x), dev(w), trans_b=True, bias=dev(bias, torch.float32), act=K.ACT_GELU)
+    assert _rel(out.cpu(), F.gelu(x @ w.t() + bias)) < tol
+    # layer-scale * rowscale + residual (ConvNeXt block tail), output written in place of res
+    r = dev(res)
+    K.gemm(dev(x), dev(w), trans_b=True, bias=dev(bias, torch.float32), colscale=dev(gamma, torch.float32),
+           rowscale=dev(rs, torch.float32), rows_per_scale=49, res=r, out=r)
+    ref = res + (x @ w.t() + bias) * gamma * rs.repeat_interleave(49).view(M, 1)
+    assert _rel(r.cpu(), ref) < tol
+    # beta accumulate (fp32 out)
+    acc = torch.randn(M, N).to(hip_device)
+    acc0 = acc.cpu().clone()
+    K.gemm(dev(x), dev(w), trans_b=True, out=acc, beta=1.0, alpha=0.5)
+    assert _rel(acc.cpu(), acc0 + 0.5 * x @ w.t()) < tol
+    # relu + dropout: deterministic, p-fraction dropped, kept scaled by 1/(1-p)
+    o1 = K.gemm(dev(x), dev(w), trans_b=True, act=K.ACT_RELU, drop_p=0.5, seed=7, drop_stream=3, out_dtype=torch.float32)
+    o2 = K.gemm(dev(x), dev(w), trans_b=True, act=K.ACT_RELU, drop_p=0.5, seed=7, drop_stream=3, out_dtype=torch.float32)
+    assert torch.equal(o1, o2)
+    base = torch.relu(x @ w.t())
+    kept = (o1.cpu() != 0) & (base > 0)
+    frac = kept.sum().item() / (base > 0).sum().item()
+    assert 0.4 < frac < 0.6
+    assert _rel(o1.cpu()[kept], 2 * base[kept]) < tol
+
+
+def test_colsum(hip_device):
+    x = torch.randn(1000, 77)
+    out = torch.zeros(77, device=hip_device)
+    K.colsum(x.to(hip_device), out)
+    assert _rel(out.cpu(), x.sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+def test_add_layernorm_fwd_bwd(hip_device, dtype, tol):
+    torch.manual_seed(1)
+    rows, cols = 300, 512
+    x, r = torch.randn(rows, cols), torch.randn(rows, cols)
+    g, b = torch.randn(cols), torch.randn(cols)
+    dy = torch.randn(rows, cols)
+    xd, rd = x.to(hip_device, dtype), r.to(hip_device, dtype)
+    s = torch.empty_like(xd)
+    y, mean, rstd = K.add_layernorm(xd, rd, g.to(hip_device), b.to(hip_device), 1e-5, s_out=s)
+    xs = (x.to(dtype).float() + r.to(dtype).float()).requires_grad_(True)
+    gg, bb = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yref = F.layer_norm(xs, (cols,), gg, bb, 1e-5)
+    assert _rel(y.cpu(), yref) < tol
+    yref.backward(dy)
+    dg = torch.zeros(cols, device=hip_device)
+    db = torch.zeros(cols, device=hip_device)
+    dr = torch.empty_like(xd)
+    dx = K.add_layernorm_bwd(dy.to(hip_device, dtype), s, mean, rstd, g.to(hip_device), dg, db, dr=dr)
+    assert _rel(dx.cpu(), xs.grad) < tol and _rel(dr.cpu(), xs.grad) < tol
+    assert _rel(dg.cpu(), gg.grad) < tol and _rel(db.cpu(), bb.grad) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+def test_cross_entropy_top5(hip_device, dtype, tol):
+    torch.manual_seed(2)
+    n, V = 200, 9490
+    logits = torch.randn(n, V) * 3
+    tgt = torch.randint(0, V, (n,))
+    tgt[::7] = -1
+    ld = 9496
+    lg = torch.zeros(n, ld, dtype=dtype)
+    lg[:, :V] = logits.to(dtype)
+    lgd = lg.to(hip_device)
+    lse = torch.empty(n, device=hip_device)
+    loss = torch.empty(n, device=hip_device)
+    hit = torch.empty(n, device=hip_device)
+    td = tgt.to(hip_device)
+    K.ce_fwd(lgd, td, V, lse, loss, hit)
+    lf = lg[:, :V].float()
+    valid = tgt >= 0
+    ref_rows = F.cross_entropy(lf[valid], tgt[valid], reduction="none")
+    assert _rel(loss.cpu()[valid], ref_rows) < 1e-5
+    top5 = lf.topk(5, 1).indices
+    ref_hit = (top5 == tgt.clamp(min=0).view(-1, 1)).any(1) & valid
+    assert torch.equal(hit.cpu().bool(), ref_hit)
+    out = torch.empty(4, device=hip_device)
+    K.loss_finalize(loss, hit, td, None, out)
+    assert abs(out[0].item() - ref_rows.mean().item()) < 1e-4 and out[1].item() == valid.sum().item()
+    dl = torch.zeros(n, ld, dtype=dtype, device=hip_device)
+    K.ce_bwd(lgd, td, V, lse, out[3:4], dl)
+    x = lf.clone().requires_grad_(True)
+    F.cross_entropy(x[valid], tgt[valid]).backward()
+    assert _rel(dl[:, :V].cpu(), x.grad) < tol
+
+
+def test_clamp_adam_matches_oracle(hip_device):
+    from oracle import train_step
+    torch.manual_seed(3)
+    n = 10007
+    p, g = torch.randn(n), torch.randn(n) * 4
+    m, v = torch.zeros(n), torch.zeros(n)
+    pd, gd, md, vd = (t.to(hip_device) for t in (p, g, m, v))
+    shadow = torch.empty(n, dtype=torch.bfloat16, device=hip_device)
+    st = {}
+    ref = {"x": p}
+    for step in (1, 2, 3):
+        K.clamp_adam(pd, gd, md, vd, shadow, 1e-4, step, 5.0)
+        ref = train_step.adam_step(ref, train_step.clip_gradient({"x": g}, 5.0), st, 1e-4, step)
+    torch.testing.assert_close(pd.cpu(), ref["x"], rtol=1e-6, atol=1e-7)
+    assert torch.equal(shadow.cpu(), pd.cpu().bfloat16())
+
+
+def test_embedding_fwd_bwd(hip_device):
+    V, dim, n = 50, 64, 300
+    table = torch.randn(V, dim)
+    ids = torch.randint(0, V, (n,))
+    pe = torch.randn(12, dim)
+    out = torch.empty(n, dim, device=hip_device)
+    K.embedding_fwd(ids.to(hip_device), table.to(hip_device), out, pe=pe.to(hip_device), L=12)
+    ref = table[ids] + pe[torch.arange(n) % 12]
+    assert _rel(out.cpu(), ref) < 1e-6
+    dout = torch.randn(n, dim)
+    dt_ = torch.zeros(V, dim, device=hip_device)
+    K.embedding_bwd(ids.to(hip_device), dout.to(hip_device), dt_)
+    refd = torch.zeros(V, dim).index_add_(0, ids, dout)
+    assert _rel(dt_.cpu(), refd) < 1e-5
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
+@pytest.mark.parametrize("H,C", [(56, 96), (28, 192), (14, 384), (7, 768), (8, 256), (16, 128)])
+def test_dwconv7_ln(hip_device, dtype, tol, H, C):
+    torch.manual_seed(H + C)
+    B = 2
+    x = torch.randn(B, H, H, C)
+    w = torch.randn(C, 1, 7, 7) * 0.2
+    bias, lw, lb = torch.randn(C), torch.randn(C), torch.randn(C)
+    xin = x.to(dtype).float()
+    ref = F.conv2d(xin.permute(0, 3, 1, 2), w, bias, padding=3, groups=C).permute(0, 2, 3, 1)
+    ref = F.layer_norm(ref, (C,), lw, lb, 1e-6)
+    w49 = w.view(C, 49).t().contiguous().to(hip_device)
+    out = torch.empty(B, H, H, C, dtype=dtype, device=hip_device)
+    K.dwconv7_ln(x.to(hip_device, dtype), w49, bias.to(hip_device), lw.to(hip_device), lb.to(hip_device), out)
+    assert _rel(out.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("C0,HW", [(96, 224), (128, 224), (192, 256)])
+def test_stem(hip_device, dtype, tol, C0, HW):
+    torch.manual_seed(C0)
+    img = torch.randn(2, 3, HW, HW)
+    w = torch.randn(C0, 3, 4, 4) * 0.1
+    b, lw, lb = torch.randn(C0), torch.randn(C0), torch.randn(C0)
+    ref = F.conv2d(img, w, b, stride=4).permute(0, 2, 3, 1)
+    ref = F.layer_norm(ref, (C0,), lw, lb, 1e-6)
+    out = torch.empty(2, HW // 4, HW // 4, C0, dtype=dtype, device=hip_device)
+    K.convnext_stem(img.to(hip_device), w.view(C0, 48).contiguous().to(hip_device), b.to(hip_device),
+                    lw.to(hip_device), lb.to(hip_device), out)
+    assert _rel(out.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+def test_ln_patchify_and_downsample(hip_device, dtype, tol):
+    torch.manual_seed(5)
+    B, H, C = 2, 14, 384
+    x = torch.randn(B, H, H, C)
+    lw, lb = torch.randn(C), torch.randn(C)
+    wc = torch.randn(2 * C, C, 2, 2) * 0.05
+    bc = torch.randn(2 * C)
+    xin = x.to(dtype).float()
+    ref = F.layer_norm(xin, (C,), lw, lb, 1e-6).permute(0, 3, 1, 2)
+    ref = F.conv2d(ref, wc, bc, stride=2).permute(0, 2, 3, 1)
+    patches = torch.empty(B * (H // 2) ** 2, 4 * C, dtype=dtype, device=hip_device)
+    K.ln_patchify2(x.to(hip_device, dtype), lw.to(hip_device), lb.to(hip_device), patches)
+    wpk = wc.permute(0, 2, 3, 1).reshape(2 * C, 4 * C).to(hip_device, dtype)
+    out = K.gemm(patches, wpk, trans_b=True, bias=bc.to(hip_device), out_dtype=torch.float32)
+    assert _rel(out.cpu().view(B, H // 2, H // 2, 2 * C), ref) < tol
+
+
+def test_adaptive_pool(hip_device):
+    x = torch.randn(2, 8, 8, 64)
+    ref = F.adaptive_avg_pool2d(x.permute(0, 3, 1, 2), 7).permute(0, 2, 3, 1)
+    out = torch.empty(2, 7, 7, 64, device=hip_device)
+    K.adaptive_pool(x.to(hip_device), 7, 7, out)
+    assert _rel(out.cpu(), ref) < 1e-6
