@@ -1,0 +1,211 @@
+"""Teacher-forced train-step throughput (images/sec) on MI355X — BASELINE.json's metric.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Default workload = BASELINE.json configs[1] (C2): ConvNeXt-Tiny encoder (frozen, train mode)
++ LSTM-attention decoder, teacher forced, 32 images per GPU, 224x224x3, captions of length
+52 (decode length 51), vocab 9490, bf16 compute / fp32 master weights + Adam.  One step =
+the full train.py:251-299 body (encoder fwd, decoder fwd, CE + alpha reg, backward, RCCL grad
+all-reduce when N > 1, clip + Adam, metrics).  Synthetic data, pre-generated in HBM; weights
+randomly initialised (no network).  Per-GPU work is fixed as N grows ("scaling": "weak").
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+V = 9490
+CAPLEN = 52
+CONFIGS = {
+    "C2": dict(encoder="tiny", decoder="lstm", batch=32),
+    "C3": dict(encoder="tiny", decoder="transformer", batch=64),
+    "C4": dict(encoder="base", decoder="transformer", batch=32),
+}
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0       # HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def synthetic_batch(B, rank, step, device):
+    """U[0,1) images ImageNet-normalised; caps <start> w.. <end>, caplen 52."""
+    g = torch.Generator(device="cpu").manual_seed(1234 + 7919 * rank + step)
+    img = torch.rand(B, 3, 224, 224, generator=g)
+    mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    img = (img - mean) / std
+    caps = torch.randint(1, V - 3, (B, CAPLEN), generator=g)
+    caps[:, 0] = V - 2
+    caps[:, CAPLEN - 1] = V - 1
+    caplens = torch.full((B, 1), CAPLEN, dtype=torch.int64)
+    return img.to(device), caps.to(device), caplens.to(device)
+
+
+def build(cfg, device):
+    from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    enc = Encoder(variant=cfg["encoder"], compute_dtype=torch.bfloat16).to(device)
+    enc.fine_tune(False)
+    E = enc.encoder_dim
+    if cfg["decoder"] == "lstm":
+        dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=device,
+                                   encoder_dim=E, dropout=0.5, compute_dtype=torch.bfloat16).to(device)
+    else:
+        from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
+        dec = TransformerDecoder(embed_dim=512, decoder_dim=512, vocab_size=V, maxLen=CAPLEN, device=device,
+                                 wordMap=None, pretrained_embeddings_path=None, fine_tune_embeddings=True,
+                                 dropout=0.5, encoder_dim=E, compute_dtype=torch.bfloat16).to(device)
+    return enc, dec
+
+
+def flops_per_image(cfg, enc):
+    """Algorithmic FLOPs per image: frozen encoder fwd + 3x decoder fwd."""
+    enc_macs = enc.macs_per_image(224)
+    T, E, A, D, M = CAPLEN - 1, enc.encoder_dim, 512, 512, 512
+    if cfg["decoder"] == "lstm":
+        P = 49
+        dec_macs = (P * E * A                      # att1 (hoisted)
+                    + T * (D * (A + E + 4 * D)     # h -> [att2 | gate | hh]
+                           + P * A + P * E         # scores + context
+                           + E * 4 * D + M * 4 * D  # LSTMCell input GEMMs
+                           + D * V)                # fc
+                    + E * 2 * D)                   # init_h / init_c
+    else:
+        L, d, ff, layers, P = CAPLEN, 512, 512, 6, 49
+        per_layer = L * (3 * d * d + d * d) + L * L * d * 2 + L * d * d + P * d * 2 * d + L * P * d * 2 \
+            + L * d * d + 2 * L * d * ff
+        dec_macs = P * E * d + layers * per_layer + L * d * V
+    return 2 * enc_macs + 3 * 2 * dec_macs
+
+
+def cpu_baseline(seconds):
+    """Oracle (plain PyTorch CPU restatement) of the C1 train step: Tiny + LSTM, B=4, fp32."""
+    from oracle import convnext, decoders, shapes, train_step
+    nthreads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(nthreads)
+    B, E = 4, 768
+    sd = convnext.init_params("tiny")
+    g = torch.Generator().manual_seed(0)
+    p = {k: (torch.rand(s, generator=g) * 0.2 - 0.1) for k, s in shapes.lstm_decoder_shapes(E, 512, 512, 512, V).items()}
+    state = {}
+    img, caps, caplens = synthetic_batch(B, 0, 0, "cpu")
+    t_steps, n = 0.0, 0
+    step = 0
+    while True:
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            feats = convnext.encoder_forward(sd, "tiny", img)
+        pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+        preds, cs, dls, al, _ = decoders.lstm_tf_forward(pr, feats, caps, caplens)
+        loss, _, _ = train_step.lstm_loss(preds, cs, dls, al)
+        loss.backward()
+        step += 1
+        p = train_step.adam_step(p, train_step.clip_gradient({k: v.grad for k, v in pr.items()}, 5.0), state,
+                                 1e-4, step)
+        dt = time.perf_counter() - t0
+        if step > 1:  # first step is warm-up
+            t_steps += dt
+            n += 1
+        if (t_steps >= seconds and n >= 2) or step >= 50:
+            break
+    return dict(value=round(B * n / t_steps, 3), unit="images/s", cores=nthreads, kind="port",
+                sample=f"oracle C1 train step (ConvNeXt-Tiny + LSTM-attention, B=4, fp32, 224x224, L=52, "
+                       f"V={V}), {n} timed steps after 1 warm-up, {t_steps:.1f} s")
+
+
+def main():
+    args = parse()
+    cfg = CONFIGS[args.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
+                                device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.manual_seed(42 + rank)
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    enc, dec = build(cfg, device)
+    trainer = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm")
+    B = cfg["batch"]
+    batches = [synthetic_batch(B, rank, i, device) for i in range(4)]
+    for i in range(args.warmup):
+        trainer.step(*batches[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        trainer.step(*batches[i % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    metrics = trainer.drain_metrics()
+    ms = elapsed / args.steps * 1e3
+    imgs_per_s = B * world * args.steps / elapsed
+    fpi = flops_per_image(cfg, enc)
+    if rank == 0:
+        from imagecaptioningconvnext_amd import roofline
+        roof = roofline.measure(cfg, trainer, batches[0])
+        out = {
+            "metric": "images/sec (train step, teacher-forced)",
+            "value": round(imgs_per_s, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (224x224x3 U[0,1) ImageNet-normalised, random captions len 52), random-init weights",
+            "config": {"workload": f"{args.config}: ConvNeXt-{cfg['encoder'].capitalize()} (frozen) + "
+                                   f"{'LSTM-attention' if cfg['decoder'] == 'lstm' else 'Transformer'} decoder, "
+                                   f"teacher-forced train step",
+                       "per_gpu_batch": B, "global_batch": B * world, "image": 224, "caption_len": CAPLEN,
+                       "vocab": V, "parallelism": f"dp{world}"},
+            "step_flops_per_image": fpi,
+            "step_mfma_frac": round(imgs_per_s * fpi / (world * PEAK_BF16_TFLOPS * 1e12), 5),
+            "last_loss": round(metrics[-1][0], 5) if metrics else None,
+            "last_top5": round(metrics[-1][2], 4) if metrics else None,
+            "roofline": roof,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

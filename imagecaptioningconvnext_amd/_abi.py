@@ -30,8 +30,8 @@ class Epilogue(ctypes.Structure):
 class LstmDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("dtype", "B", "P", "E", "A", "D", "M", "T")] + [
         (n, c_void_p) for n in ("w_hcat", "b_hcat", "w_ih", "w_f", "enc", "att1", "xe", "c0", "dl", "g1", "alphas",
-                                "awe", "zs", "gates", "cs", "hs", "hprev", "g2", "dhs", "dreg", "dcat", "dz", "dh",
-                                "dc", "datt1", "dwf")]
+                                "awe", "zs", "gates", "cs", "hs", "hprev", "g2", "w_ihz_t", "w_hcat_t", "dhs", "dalpha",
+                                "dcat", "dz", "dh", "dc", "de", "datt1", "dwf", "dbea")]
 
 
 # name -> argtypes  (every entry point declared in include/imgcap_abi.h)
@@ -39,6 +39,7 @@ _SIGS = {
     "imgcap_version": [],
     "imgcap_gemm": [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                     c_int64, c_void_p, c_int64, c_int64, c_int, ctypes.POINTER(Epilogue), c_void_p],
+    "imgcap_transpose": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p],
     "imgcap_colsum": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_float, c_void_p],
     "imgcap_add_layernorm_fwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_uint64, c_uint32, c_void_p,
                                  c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
@@ -61,9 +62,10 @@ _SIGS = {
                           c_float, c_int, c_float, c_float, c_void_p],
     "imgcap_lstm_tf_fwd": [ctypes.POINTER(LstmDesc), c_void_p],
     "imgcap_lstm_tf_bwd": [ctypes.POINTER(LstmDesc), c_void_p],
-    "imgcap_attn_reg": [c_int, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
+    "imgcap_attn_reg": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     "imgcap_dropout": [c_int, c_int64, c_void_p, c_float, c_uint64, c_uint32, c_void_p, c_void_p],
     "imgcap_loss_finalize": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_mean_mid": [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "imgcap_cast": [c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p],
     "imgcap_fill": [c_int, c_int64, c_float, c_void_p, c_void_p],
 }

@@ -103,14 +103,13 @@ __global__ __launch_bounds__(256) void dwconv7_ln_kernel(int B, int H, int W, in
                                                          const float* __restrict__ w, const float* __restrict__ bias,
                                                          const float* __restrict__ lw, const float* __restrict__ lb,
                                                          T* __restrict__ out, int rows_per_block) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [rows_per_block * W][2]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [rows_per_block * W][2], then part
   const int CV = C / 8, G = W / PW, tpr = CV * G;
+  float* part = red + rows_per_block * W * 2;                    // [blockDim][PW]
   const int t = threadIdx.x;
   const int rl = t / tpr, within = t % tpr, g = within / CV, cv = within % CV;
   const long row = (long)blockIdx.x * rows_per_block + rl;  // (b*H + h)
   const bool active = rl < rows_per_block && row < (long)B * H;
-  for (int e = t; e < rows_per_block * W * 2; e += blockDim.x) red[e] = 0.f;
-  __syncthreads();
   float acc[PW][8];
   const int c0 = cv * 8, w0 = g * PW;
   int b = 0, h = 0;
@@ -145,26 +144,39 @@ __global__ __launch_bounds__(256) void dwconv7_ln_kernel(int B, int H, int W, in
           for (int j = 0; j < 8; ++j) acc[p][j] += win[p + kw][j] * wt[j];
       }
     }
-    // partial sums for the mean
+    // per-thread partial sums (fixed-order reduction below keeps results deterministic)
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
-      float s = 0.f;
+      float sum = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += acc[p][j];
-      atomicAdd(&red[(rl * W + w0 + p) * 2], s);
+      for (int j = 0; j < 8; ++j) sum += acc[p][j];
+      part[t * PW + p] = sum;
     }
+  }
+  __syncthreads();
+  const int gbase = t - cv;  // first thread of this (row, pixel group)
+  if (active && cv < PW) {
+    float sum = 0.f;
+    for (int c = 0; c < CV; ++c) sum += part[(gbase + c) * PW + cv];
+    red[(rl * W + w0 + cv) * 2] = sum / C;
   }
   __syncthreads();
   float mean[PW];
   if (active) {
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
-      mean[p] = red[(rl * W + w0 + p) * 2] / C;
-      float s = 0.f;
+      mean[p] = red[(rl * W + w0 + p) * 2];
+      float sq = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { const float d = acc[p][j] - mean[p]; s += d * d; }
-      atomicAdd(&red[(rl * W + w0 + p) * 2 + 1], s);
+      for (int j = 0; j < 8; ++j) { const float dd = acc[p][j] - mean[p]; sq += dd * dd; }
+      part[t * PW + p] = sq;
     }
+  }
+  __syncthreads();
+  if (active && cv < PW) {
+    float sq = 0.f;
+    for (int c = 0; c < CV; ++c) sq += part[(gbase + c) * PW + cv];
+    red[(rl * W + w0 + cv) * 2 + 1] = sq;
   }
   __syncthreads();
   if (active) {
@@ -244,11 +256,12 @@ static int launch_dw(int B, int H, int W, int C, const void* x, const float* w, 
                      const float* lb, void* out, hipStream_t st) {
   const int tpr = (C / 8) * (W / PW);
   IMGCAP_REQUIRE(tpr <= 256, "imgcap_dwconv7_ln: C*W too large for one block");
+  IMGCAP_REQUIRE(C / 8 >= PW, "imgcap_dwconv7_ln: C must be >= 8*pixels_per_thread");
   const int rpb = 256 / tpr;
   const int threads = ((rpb * tpr + 63) / 64) * 64;
   const long rows = (long)B * H;
   dim3 grid((unsigned)((rows + rpb - 1) / rpb));
-  const size_t shm = (size_t)rpb * W * 2 * sizeof(float);
+  const size_t shm = ((size_t)rpb * W * 2 + (size_t)threads * PW) * sizeof(float);
   hipLaunchKernelGGL((dwconv7_ln_kernel<T, PW>), grid, dim3(threads), shm, st, B, H, W, C, (const T*)x, w, bias, lw,
                      lb, (T*)out, rpb);
   IMGCAP_CHECK_LAUNCH("imgcap_dwconv7_ln");

@@ -108,6 +108,18 @@ __global__ void loss_finalize_kernel(int n, const float* __restrict__ loss_rows,
   }
 }
 
+// out[b, e] = mean_p x[b, p, e]  (decoder.py:99 encoder_out.mean(dim=1))
+template <typename TI, typename TO>
+__global__ void mean_mid_kernel(int B, int P, int E, const TI* __restrict__ x, TO* __restrict__ out) {
+  const long n = (long)B * E;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int b = (int)(i / E), e = (int)(i % E);
+    float s = 0.f;
+    for (int p = 0; p < P; ++p) s += to_f(x[((long)b * P + p) * E + e]);
+    out[i] = from_f<TO>(s / P);
+  }
+}
+
 static dim3 grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 4096) b = 4096;
@@ -183,6 +195,19 @@ extern "C" int imgcap_loss_finalize(int n, const float* loss_rows, const float* 
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n, loss_rows, hit5, targets,
                      extra, out);
   IMGCAP_CHECK_LAUNCH("imgcap_loss_finalize");
+  return 0;
+}
+
+extern "C" int imgcap_mean_mid(int dtype, int B, int P, int E, const void* x, void* out, void* stream) {
+  const long n = (long)B * E;
+  if (n == 0) return 0;
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL((mean_mid_kernel<bf16, bf16>), grid_for(n), dim3(256), 0, (hipStream_t)stream, B, P, E,
+                       (const bf16*)x, (bf16*)out);
+  else
+    hipLaunchKernelGGL((mean_mid_kernel<float, float>), grid_for(n), dim3(256), 0, (hipStream_t)stream, B, P, E,
+                       (const float*)x, (float*)out);
+  IMGCAP_CHECK_LAUNCH("imgcap_mean_mid");
   return 0;
 }
 

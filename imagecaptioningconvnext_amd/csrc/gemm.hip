@@ -1,17 +1,22 @@
 // MFMA GEMM with fused epilogue for gfx950 (bf16 16x16x32, exact-f32 16x16x4).
 //
-// One template covers every contraction on the hot path (SURVEY.md §2.2 rows "pointwise
-// MLP", "downsample", "projections", "vocab projection" and all their dgrad/wgrad forms):
+// One code base covers every contraction on the hot path (SURVEY.md §2.2 rows "pointwise
+// MLP", "downsample", "projections", "vocab projection" and their dgrad/wgrad forms):
+//
+// tiled kernel (M > 64): 256 threads = 4 wave64s (2x2), BM x BN x 32 tiles
 //   * operand layouts: A k-major ([M][K]) or m-major ([K][M]); B k-major ([N][K], nn.Linear
-//     weight) or n-major ([K][N]); m/n-major tiles are transposed while being written to LDS
-//   * LDS images are [row][k] with a 16-byte pad, read as one 16-byte fragment per lane
-//   * 256 threads = 4 wave64s laid out WM x WN x KS; KS>1 splits each LDS k-tile across wave
-//     groups (intra-block split-K for skinny M, e.g. the LSTM recurrence at M = batch) and
-//     reduces through LDS, which also makes the epilogue store coalesced
-//   * register-staged double buffering: the next k-tile's global loads are in flight while
-//     the current tile's MFMAs run
-//   * f32 mode feeds the same [row][8 k] fragment to 8 chained 16x16x4 f32 MFMAs (the k
-//     order inside a 32-slice is permuted identically for A and B, so the sum is unchanged)
+//     weight) or n-major ([K][N]); m/n-major tiles are transposed while written to LDS
+//   * branch-free staging: 16-byte vector loads from clamped addresses, zero-selected when the
+//     row/k is out of range (no per-element fallback, so nothing spills); the K tail of the
+//     last tile is masked word-wise
+//   * register-staged double buffering (next tile's global loads in flight under the MFMAs)
+//   * f32 mode feeds the same [row][8 k] fragment to 8 chained 16x16x4 f32 MFMAs (the k order
+//     inside a 32-slice is permuted identically for A and B, so the sum is unchanged)
+//   * epilogue staged through LDS: each thread finishes 8 consecutive columns of a row
+//     (vector bias/scale/residual loads, 16-byte stores)
+// skinny kernel (M <= 64, A and B k-major): the LSTM recurrence GEMMs at M = batch.  Each
+//   block owns 16 output columns; its 8 waves split K and stream A/B fragments straight from
+//   global into registers (no LDS round trip, no barriers in the loop), then reduce in LDS.
 #include "common.h"
 
 namespace imgcap {
@@ -30,13 +35,119 @@ DEV void mma(f32x4& acc, const Frag<float>& a, const Frag<float>& b) {
   for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[kk], b.hi[kk], acc, 0, 0, 0);
 }
 
+template <typename T> DEV Frag<T> frag_from(const uint4& lo, const uint4& hi);
+template <> DEV Frag<bf16> frag_from<bf16>(const uint4& lo, const uint4&) {
+  Frag<bf16> f;
+  f.v = __builtin_bit_cast(bf16x8, lo);
+  return f;
+}
+template <> DEV Frag<float> frag_from<float>(const uint4& lo, const uint4& hi) {
+  Frag<float> f;
+  f.lo = __builtin_bit_cast(f32x4, lo);
+  f.hi = __builtin_bit_cast(f32x4, hi);
+  return f;
+}
+
 template <typename T> DEV Frag<T> lds_frag(const T* p);
 template <> DEV Frag<bf16> lds_frag<bf16>(const bf16* p) { Frag<bf16> f; f.v = *(const bf16x8*)p; return f; }
 template <> DEV Frag<float> lds_frag<float>(const float* p) {
   Frag<float> f; f.lo = *(const f32x4*)p; f.hi = *(const f32x4*)(p + 4); return f;
 }
 
-DEV void epi_apply(const imgcap_epilogue& ep, void* C, long cidx, int m, int n, float v) {
+// zero the elements of a 16-byte vector whose index >= nvalid (0..VEC); word-wise, in registers
+template <typename T>
+DEV uint4 mask_tail(uint4 v, int nvalid) {
+  constexpr int EPW = 4 / sizeof(T);  // elements per 32-bit word
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e0 = i * EPW;
+    if (EPW == 1) {
+      if (e0 >= nvalid) w[i] = 0u;
+    } else {
+      if (e0 >= nvalid) w[i] = 0u;
+      else if (e0 + 1 >= nvalid) w[i] &= 0xFFFFu;
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ---------------------------------------------------------------------------------------
+// epilogue on 8 consecutive columns of one row (n0 .. n0+7), all in range and 16-B aligned
+struct EpiFlags {
+  bool bias, colscale, rowscale, res, aux, beta, drop;
+};
+
+DEV void epi_vec8(const imgcap_epilogue& ep, const EpiFlags& f, void* C, long cidx, int m, int n0, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= ep.alpha;
+  if (f.bias) {
+    const f32x4 b0 = *(const f32x4*)(ep.bias + n0), b1 = *(const f32x4*)(ep.bias + n0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[j + 4] += b1[j]; }
+  }
+  if (ep.act == IMGCAP_ACT_GELU) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+  } else if (ep.act == IMGCAP_ACT_RELU) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+  }
+  if (f.drop) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= dropout_scale(ep.seed, ep.drop_stream, (uint64_t)m * ep.drop_ld + n0 + j, ep.drop_p);
+  }
+  if (f.aux) {
+    const long ai = (long)m * ep.ldaux + n0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = load_as_f(ep.aux, ai + j, ep.c_dtype) > 0.f ? v[j] * ep.aux_scale : 0.f;
+  }
+  if (f.colscale) {
+    const f32x4 s0 = *(const f32x4*)(ep.colscale + n0), s1 = *(const f32x4*)(ep.colscale + n0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] *= s0[j]; v[j + 4] *= s1[j]; }
+  }
+  if (f.rowscale) {
+    const float s = ep.rowscale[m / ep.rows_per_scale];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= s;
+  }
+  if (ep.c_dtype == IMGCAP_BF16) {
+    if (f.res) {
+      const bf16x8 r = *(const bf16x8*)((const bf16*)ep.res + (long)m * ep.ldr + n0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += (float)r[j];
+    }
+    bf16* cp = (bf16*)C + cidx;
+    if (f.beta) {
+      const bf16x8 o = *(const bf16x8*)cp;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += ep.beta * (float)o[j];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+    *(bf16x8*)cp = o;
+  } else {
+    if (f.res) {
+      const float* rp = (const float*)ep.res + (long)m * ep.ldr + n0;
+      const f32x4 r0 = *(const f32x4*)rp, r1 = *(const f32x4*)(rp + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += r0[j]; v[j + 4] += r1[j]; }
+    }
+    float* cp = (float*)C + cidx;
+    if (f.beta) {
+      const f32x4 o0 = *(const f32x4*)cp, o1 = *(const f32x4*)(cp + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += ep.beta * o0[j]; v[j + 4] += ep.beta * o1[j]; }
+    }
+    *(f32x4*)cp = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)(cp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+// scalar epilogue for ragged / unaligned column tails
+DEV void epi_scalar(const imgcap_epilogue& ep, void* C, long cidx, int m, int n, float v) {
   v *= ep.alpha;
   if (ep.bias) v += ep.bias[n];
   if (ep.act == IMGCAP_ACT_GELU) v = gelu_erf(v);
@@ -50,21 +161,51 @@ DEV void epi_apply(const imgcap_epilogue& ep, void* C, long cidx, int m, int n, 
   store_from_f(C, cidx, ep.c_dtype, v);
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int KS, bool AK, bool BK_>
+// Finish a staged f32 tile rows [0, rows) x [0, BN) held in LDS (row stride LDT floats):
+// every thread handles 8-column vectors.  vec_ok: ldc, ldr, ldaux multiples of 8 and C/res
+// 16-byte aligned (host-checked).
+template <int BN>
+DEV void epilogue_from_lds(const imgcap_epilogue& ep, const float* tile, int LDT, int rows, int m_base, int n_base,
+                           int M, int N, void* C, long ldc, long cbase, bool vec_ok) {
+  const EpiFlags f{ep.bias != nullptr, ep.colscale != nullptr, ep.rowscale != nullptr, ep.res != nullptr,
+                   ep.aux != nullptr, ep.beta != 0.f, ep.drop_p > 0.f};
+  constexpr int NV = BN / 8;
+  for (int e = threadIdx.x; e < rows * NV; e += blockDim.x) {
+    const int r = e / NV, c8 = (e % NV) * 8;
+    const int m = m_base + r, n = n_base + c8;
+    if (m >= M || n >= N) continue;
+    float v[8];
+    const f32x4 a = *(const f32x4*)(tile + r * LDT + c8), b = *(const f32x4*)(tile + r * LDT + c8 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+    const long cidx = cbase + (long)m * ldc + n;
+    if (vec_ok && n + 8 <= N) {
+      epi_vec8(ep, f, C, cidx, m, n, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (n + j < N) epi_scalar(ep, C, cidx + j, m, n + j, v[j]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// tiled kernel
+template <typename T, int BM, int BN>
 struct GemmCfg {
   static constexpr int VEC = 16 / sizeof(T);
-  static constexpr int BK = 32 * KS;
-  static constexpr int LDK = BK + VEC;  // +16 bytes per row
-  static constexpr int TM = BM / WM / 16;
-  static constexpr int TN = BN / WN / 16;
+  static constexpr int BK = 32;
+  static constexpr int LDK = BK + VEC;  // +16 bytes per LDS row
+  static constexpr int TM = BM / 2 / 16;
+  static constexpr int TN = BN / 2 / 16;
   static constexpr int A_VECS = BM * BK / VEC / 256;
   static constexpr int B_VECS = BN * BK / VEC / 256;
   static constexpr int STAGE_BYTES = (BM + BN) * LDK * (int)sizeof(T);
-  static constexpr int RED_BYTES = KS > 1 ? KS * BM * BN * 4 : 0;
-  static constexpr int SMEM = STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES;
-  static_assert(WM * WN * KS == 4, "4 waves");
+  static constexpr int EPI_ROWS = BM / 2;   // one wave-row's worth of output per epilogue pass
+  static constexpr int LDT = BN + 4;
+  static constexpr int EPI_BYTES = EPI_ROWS * LDT * 4;
+  static constexpr int SMEM = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
   static_assert(A_VECS >= 1 && B_VECS >= 1, "tile too small for 256 threads");
-  static_assert(BM * BK % (VEC * 256) == 0 && BN * BK % (VEC * 256) == 0, "tile/thread mismatch");
 };
 
 // Load one operand tile (ROWS x BK) into registers.  KMAJ: element (r,k) at P[r*ld + k].
@@ -79,18 +220,13 @@ DEV void tile_load(uint4 (&reg)[NV], const T* __restrict__ P, long ld, int r0, i
     if (KMAJ) { r = v / (BK / VEC); k = (v % (BK / VEC)) * VEC; }
     else      { k = v / (ROWS / VEC); r = (v % (ROWS / VEC)) * VEC; }
     const int gr = r0 + r, gk = k0 + k;
-    const bool full = KMAJ ? (gr < R && gk + VEC <= K) : (gk < K && gr + VEC <= R);
-    if (full) {
-      reg[i] = KMAJ ? *(const uint4*)(P + (long)gr * ld + gk) : *(const uint4*)(P + (long)gk * ld + gr);
-    } else {
-      T tmp[VEC];
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        const int rr = KMAJ ? gr : gr + j, kk = KMAJ ? gk + j : gk;
-        tmp[j] = (rr < R && kk < K) ? (KMAJ ? P[(long)rr * ld + kk] : P[(long)kk * ld + rr]) : from_f<T>(0.f);
-      }
-      reg[i] = *(uint4*)tmp;
-    }
+    const int cr = gr < R ? gr : R - 1;  // clamped (always-valid) address
+    const int ck = gk < K ? gk : K - 1;
+    const uint4 x = KMAJ ? *(const uint4*)(P + (long)cr * ld + (ck / VEC) * VEC)
+                         : *(const uint4*)(P + (long)ck * ld + (cr / VEC) * VEC);
+    const bool ok = KMAJ ? (gr < R && gk < K) : (gk < K && gr < R);
+    reg[i] = ok ? x : make_uint4(0u, 0u, 0u, 0u);
+    if (KMAJ && gk + VEC > K) reg[i] = mask_tail<T>(reg[i], K - gk);
   }
 }
 
@@ -106,19 +242,27 @@ DEV void tile_store(T* S, const uint4 (&reg)[NV]) {
       *(uint4*)(S + r * LDK + k) = reg[i];
     } else {
       const int k = v / (ROWS / VEC), r = (v % (ROWS / VEC)) * VEC;
-      const T* t = (const T*)&reg[i];
+      const uint32_t w[4] = {reg[i].x, reg[i].y, reg[i].z, reg[i].w};
+      if (sizeof(T) == 2) {
+        unsigned short* s16 = (unsigned short*)S;
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) S[(r + j) * LDK + k] = t[j];
+        for (int j = 0; j < 8; ++j)
+          s16[(r + j) * LDK + k] = (unsigned short)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+      } else {
+        uint32_t* s32 = (uint32_t*)S;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s32[(r + j) * LDK + k] = w[j];
+      }
     }
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int KS, bool AK, bool BKM>
+template <typename T, int BM, int BN, bool AK, bool BKM>
 __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long lda, long sA,
                                                    const T* __restrict__ B, long ldb, long sB,
                                                    void* __restrict__ C, long ldc, long sC,
-                                                   int M, int N, int K, imgcap_epilogue ep) {
-  using G = GemmCfg<T, BM, BN, WM, WN, KS, AK, BKM>;
+                                                   int M, int N, int K, imgcap_epilogue ep, int vec_ok) {
+  using G = GemmCfg<T, BM, BN>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   T* As = (T*)smem;
   T* Bs = As + BM * G::LDK;
@@ -129,8 +273,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long
   const long cbase = (long)bz * sC;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ks = wave / (WM * WN), wmn = wave % (WM * WN);
-  const int rb = (wmn / WN) * (BM / WM), cb = (wmn % WN) * (BN / WN);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int rb = wm * (BM / 2), cb = wn * (BN / 2);
 
   f32x4 acc[G::TM][G::TN];
 #pragma unroll
@@ -145,12 +289,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long
   tile_store<T, BN, G::BK, G::LDK, G::B_VECS, BKM>(Bs, rbv);
   __syncthreads();
 
-  const int fr = lane & 15, fk = ks * 32 + 8 * (lane >> 4);
-  for (int k0 = 0; k0 < K; k0 += G::BK) {
-    const bool more = k0 + G::BK < K;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int nk = (K + G::BK - 1) / G::BK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
     if (more) {
-      tile_load<T, BM, G::BK, G::A_VECS, AK>(ra, A, lda, m0, k0 + G::BK, M, K);
-      tile_load<T, BN, G::BK, G::B_VECS, BKM>(rbv, B, ldb, n0, k0 + G::BK, N, K);
+      tile_load<T, BM, G::BK, G::A_VECS, AK>(ra, A, lda, m0, (kt + 1) * G::BK, M, K);
+      tile_load<T, BN, G::BK, G::B_VECS, BKM>(rbv, B, ldb, n0, (kt + 1) * G::BK, N, K);
     }
     Frag<T> af[G::TM], bfr[G::TN];
 #pragma unroll
@@ -169,47 +314,150 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long
     }
   }
 
-  if (KS == 1) {
+  // epilogue: two passes of BM/2 rows (one wave-row each) through LDS
+  float* tile = (float*)smem;
 #pragma unroll
-    for (int i = 0; i < G::TM; ++i)
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wm == pass) {
 #pragma unroll
-      for (int j = 0; j < G::TN; ++j)
+      for (int i = 0; i < G::TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + rb + i * 16 + 4 * (lane >> 4) + r;
-          const int n = n0 + cb + j * 16 + fr;
-          if (m < M && n < N) epi_apply(ep, C, cbase + (long)m * ldc + n, m, n, acc[i][j][r]);
-        }
-  } else {
-    float* part = (float*)smem;  // [KS][BM][BN]
+        for (int j = 0; j < G::TN; ++j)
 #pragma unroll
-    for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < G::TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          part[(ks * BM + rb + i * 16 + 4 * (lane >> 4) + r) * BN + cb + j * 16 + fr] = acc[i][j][r];
-    __syncthreads();
-    for (int e = threadIdx.x; e < BM * BN; e += 256) {
-      const int r = e / BN, c = e % BN;
-      float v = 0.f;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) v += part[s * BM * BN + e];
-      const int m = m0 + r, n = n0 + c;
-      if (m < M && n < N) epi_apply(ep, C, cbase + (long)m * ldc + n, m, n, v);
+          for (int r = 0; r < 4; ++r)
+            tile[(i * 16 + 4 * (lane >> 4) + r) * G::LDT + cb + j * 16 + fr] = acc[i][j][r];
     }
+    __syncthreads();
+    epilogue_from_lds<BN>(ep, tile, G::LDT, G::EPI_ROWS, m0 + pass * G::EPI_ROWS, n0, M, N, C, ldc, cbase,
+                          vec_ok != 0);
+    __syncthreads();
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int KS>
-static int launch_cfg(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
-                      long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
-                      hipStream_t st) {
+// ---------------------------------------------------------------------------------------
+// skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
+// SW waves split K; fragments come straight from global memory.
+template <typename T, int MT, int SW>
+__global__ __launch_bounds__(64 * SW) void gemm_skinny_kernel(const T* __restrict__ A, long lda,
+                                                              const T* __restrict__ B, long ldb,
+                                                              void* __restrict__ C, long ldc, int M, int N, int K,
+                                                              imgcap_epilogue ep, int vec_ok) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int LDT = 16 + 4;
+  __shared__ __attribute__((aligned(16))) float part[SW][MT * 16][LDT];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int nks = (K + 31) / 32;                     // k-steps of 32
+  const int per = (nks + SW - 1) / SW;
+  const int ks0 = w * per, ks1 = min(nks, ks0 + per);
+  // clamped row addresses (out-of-range rows/cols read row 0 / N-1 and are zeroed)
+  const T* arow[MT];
+  bool aok[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = t * 16 + fr;
+    aok[t] = m < M;
+    arow[t] = A + (long)(aok[t] ? m : 0) * lda;
+  }
+  const int n = n0 + fr;
+  const bool bok = n < N;
+  const T* brow = B + (long)(bok ? n : N - 1) * ldb;
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+  const int kfull = (K / 32) * 32;  // k-steps below this need no tail mask
+  int ks = ks0;
+  // main loop, unrolled x2 so two steps of loads are in flight
+  for (; ks + 2 <= ks1 && (ks + 2) * 32 <= kfull; ks += 2) {
+    uint4 a0[MT], a1[MT], b0lo, b0hi, b1lo, b1hi;
+    const int k0 = ks * 32 + fk, k1 = k0 + 32;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      a0[t] = *(const uint4*)(arow[t] + k0);
+      a1[t] = *(const uint4*)(arow[t] + k1);
+    }
+    b0lo = *(const uint4*)(brow + k0);
+    b1lo = *(const uint4*)(brow + k1);
+    if (sizeof(T) == 4) {
+      b0hi = *(const uint4*)(brow + k0 + 4);
+      b1hi = *(const uint4*)(brow + k1 + 4);
+    } else {
+      b0hi = b1hi = zero;
+    }
+    uint4 a0hi[MT], a1hi[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      if (sizeof(T) == 4) {
+        a0hi[t] = *(const uint4*)(arow[t] + k0 + 4);
+        a1hi[t] = *(const uint4*)(arow[t] + k1 + 4);
+      } else {
+        a0hi[t] = a1hi[t] = zero;
+      }
+    }
+    if (!bok) { b0lo = b0hi = b1lo = b1hi = zero; }
+    const Frag<T> fb0 = frag_from<T>(b0lo, b0hi), fb1 = frag_from<T>(b1lo, b1hi);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const uint4 x0 = aok[t] ? a0[t] : zero, x0h = aok[t] ? a0hi[t] : zero;
+      const uint4 x1 = aok[t] ? a1[t] : zero, x1h = aok[t] ? a1hi[t] : zero;
+      mma(acc[t], frag_from<T>(x0, x0h), fb0);
+      mma(acc[t], frag_from<T>(x1, x1h), fb1);
+    }
+  }
+  for (; ks < ks1; ++ks) {  // remainder (and masked K tail)
+    const int k0 = ks * 32 + fk;
+    const bool kin = k0 < K;
+    const int ck = kin ? k0 : 0;
+    uint4 blo = *(const uint4*)(brow + ck), bhi = zero;
+    if (sizeof(T) == 4 && ck + 4 < K) bhi = *(const uint4*)(brow + ck + 4);
+    if (!bok || !kin) { blo = bhi = zero; }
+    if (kin && k0 + 8 > K) {
+      if (sizeof(T) == 2) blo = mask_tail<T>(blo, K - k0);
+      else { blo = mask_tail<T>(blo, K - k0); bhi = mask_tail<T>(bhi, K - k0 - 4); }
+    }
+    const Frag<T> fb = frag_from<T>(blo, bhi);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      uint4 alo = *(const uint4*)(arow[t] + ck), ahi = zero;
+      if (sizeof(T) == 4 && ck + 4 < K) ahi = *(const uint4*)(arow[t] + ck + 4);
+      if (!aok[t] || !kin) { alo = ahi = zero; }
+      if (kin && k0 + 8 > K) {
+        if (sizeof(T) == 2) alo = mask_tail<T>(alo, K - k0);
+        else { alo = mask_tail<T>(alo, K - k0); ahi = mask_tail<T>(ahi, K - k0 - 4); }
+      }
+      mma(acc[t], frag_from<T>(alo, ahi), fb);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[w][t * 16 + 4 * (lane >> 4) + r][fr] = acc[t][r];
+  __syncthreads();
+  // reduce the SW partial tiles into part[0]
+  for (int e = threadIdx.x; e < MT * 16 * 16; e += 64 * SW) {
+    const int r = e / 16, c = e % 16;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < SW; ++q) s += part[q][r][c];
+    part[0][r][c] = s;
+  }
+  __syncthreads();
+  epilogue_from_lds<16>(ep, &part[0][0][0], LDT, MT * 16, 0, n0, M, N, C, ldc, 0, vec_ok != 0);
+}
+
+// ---------------------------------------------------------------------------------------
+template <typename T, int BM, int BN>
+static int launch_tiled(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
+                        long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
+                        int vec_ok, hipStream_t st) {
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
   const T* a = (const T*)A;
   const T* b = (const T*)B;
-#define L_(AKV, BKV) \
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, KS, AKV, BKV>), grid, dim3(256), 0, st, a, lda, sA, b, ldb, sB, C, ldc, sC, M, N, K, ep)
+#define L_(AKV, BKV)                                                                                       \
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, AKV, BKV>), grid, dim3(256), 0, st, a, lda, sA, b, ldb, sB, C, ldc, \
+                     sC, M, N, K, ep, vec_ok)
   if (ak && bk) L_(true, true);
   else if (ak && !bk) L_(true, false);
   else if (!ak && bk) L_(false, true);
@@ -222,15 +470,22 @@ static int launch_cfg(int ak, int bk, int M, int N, int K, const void* A, long l
 template <typename T>
 static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
                          long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
-                         hipStream_t st) {
-  if (M <= 32)
-    return launch_cfg<T, 32, 32, 1, 1, 4>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, st);
-  if (M <= 64)
-    return launch_cfg<T, 64, 32, 1, 1, 4>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, st);
+                         int vec_ok, hipStream_t st) {
+  if (M <= 64 && ak && bk && batch == 1) {
+    dim3 grid((N + 15) / 16);
+    if (M <= 32)
+      hipLaunchKernelGGL((gemm_skinny_kernel<T, 2, 8>), grid, dim3(512), 0, st, (const T*)A, lda, (const T*)B, ldb,
+                         C, ldc, M, N, K, ep, vec_ok);
+    else
+      hipLaunchKernelGGL((gemm_skinny_kernel<T, 4, 8>), grid, dim3(512), 0, st, (const T*)A, lda, (const T*)B, ldb,
+                         C, ldc, M, N, K, ep, vec_ok);
+    IMGCAP_CHECK_LAUNCH("imgcap_gemm(skinny)");
+    return 0;
+  }
   const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   if (tiles128 < 512)
-    return launch_cfg<T, 64, 64, 2, 2, 1>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, st);
-  return launch_cfg<T, 128, 128, 2, 2, 1>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, st);
+    return launch_tiled<T, 64, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
+  return launch_tiled<T, 128, 128>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
 }
 
 // bias-gradient style column sums: out[c] = beta*out[c] + sum_r x[r, c]
@@ -251,6 +506,23 @@ __global__ void colsum_kernel(int rows, int cols, const T* __restrict__ x, long 
   }
 }
 
+// out[c][r] = in[r][c] (2-D transpose through an LDS tile; weights -> k-major copies)
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in, long ldi,
+                                                        T* __restrict__ out, long ldo) {
+  __shared__ T tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int r = e / 64, c = e % 64;
+    if (r0 + r < rows && c0 + c < cols) tile[r][c] = in[(long)(r0 + r) * ldi + c0 + c];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int c = e / 64, r = e % 64;
+    if (r0 + r < rows && c0 + c < cols) out[(long)(c0 + c) * ldo + r0 + r] = tile[r][c];
+  }
+}
+
 }  // namespace imgcap
 
 using namespace imgcap;
@@ -261,21 +533,28 @@ extern "C" int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, 
   IMGCAP_REQUIRE(epi != nullptr, "imgcap_gemm: epilogue is NULL");
   IMGCAP_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "imgcap_gemm: bad sizes");
   if (M == 0 || N == 0) return 0;
+  IMGCAP_REQUIRE(K > 0, "imgcap_gemm: K == 0");
   IMGCAP_REQUIRE(dtype == IMGCAP_F32 || dtype == IMGCAP_BF16, "imgcap_gemm: bad dtype");
   const int vec = dtype == IMGCAP_F32 ? 4 : 8;
   IMGCAP_REQUIRE(aligned16(A) && aligned16(B), "imgcap_gemm: A/B must be 16-byte aligned");
   IMGCAP_REQUIRE(lda % vec == 0 && ldb % vec == 0 && strideA % vec == 0 && strideB % vec == 0,
                  "imgcap_gemm: leading dims/strides must be multiples of 16 bytes");
   IMGCAP_REQUIRE(epi->rows_per_scale > 0 || epi->rowscale == nullptr, "imgcap_gemm: rows_per_scale");
+  IMGCAP_REQUIRE(epi->bias == nullptr || aligned16(epi->bias), "imgcap_gemm: bias alignment");
+  IMGCAP_REQUIRE(epi->colscale == nullptr || aligned16(epi->colscale), "imgcap_gemm: colscale alignment");
+  // leading dims of the stored operands must cover the logical extent (loads may read a full
+  // 16-byte vector from the last valid row/column)
+  IMGCAP_REQUIRE(a_kmajor ? lda >= K : lda >= M, "imgcap_gemm: lda too small");
+  IMGCAP_REQUIRE(b_kmajor ? ldb >= K : ldb >= N, "imgcap_gemm: ldb too small");
+  const bool vec_ok = aligned16(C) && ldc % 8 == 0 && strideC % 8 == 0 &&
+                      (epi->res == nullptr || (aligned16(epi->res) && epi->ldr % 8 == 0)) &&
+                      (epi->aux == nullptr || epi->ldaux % 8 == 0);
   hipStream_t st = (hipStream_t)stream;
-  if (K == 0) {  // pure epilogue on zero accumulator is not needed on the path
-    return fail(IMGCAP_EINVAL, "imgcap_gemm: K == 0");
-  }
   if (dtype == IMGCAP_BF16)
     return gemm_dispatch<bf16>(a_kmajor, b_kmajor, M, N, K, A, lda, strideA, B, ldb, strideB, C, ldc, strideC,
-                               batch, *epi, st);
+                               batch, *epi, vec_ok, st);
   return gemm_dispatch<float>(a_kmajor, b_kmajor, M, N, K, A, lda, strideA, B, ldb, strideB, C, ldc, strideC,
-                              batch, *epi, st);
+                              batch, *epi, vec_ok, st);
 }
 
 extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64_t ldx, float* out, float beta,
@@ -289,5 +568,19 @@ extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const float*)x,
                        ldx, out, beta);
   IMGCAP_CHECK_LAUNCH("imgcap_colsum");
+  return 0;
+}
+
+extern "C" int imgcap_transpose(int dtype, int rows, int cols, const void* in, int64_t ldi, void* out, int64_t ldo,
+                                void* stream) {
+  if (rows == 0 || cols == 0) return 0;
+  dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(transpose_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const bf16*)in,
+                       ldi, (bf16*)out, ldo);
+  else
+    hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
+                       (const float*)in, ldi, (float*)out, ldo);
+  IMGCAP_CHECK_LAUNCH("imgcap_transpose");
   return 0;
 }

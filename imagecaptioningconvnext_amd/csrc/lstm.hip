@@ -7,38 +7,64 @@
 //     reference recomputes it every step)
 //   * the three GEMMs that read h_{t-1} (decoder_att, f_beta, LSTMCell weight_hh) are one
 //     GEMM against W_hcat = [W_da; W_fb; W_hh]
-//   * the embedding half of weight_ih (and both LSTM biases) is precomputed for all t (xe);
-//     only the attention half (z_t W_ih[:,M:]^T) stays in the loop
+//   * the embedding half of weight_ih (and bias_ih) is precomputed for all t (xe); only the
+//     attention half (z_t W_ih[:,M:]^T) stays in the loop
 //   * fc(dropout(h)) (decoder.py:144) runs once after the loop over all [B*T] rows
 //   * rows are never shrunk: rows with t >= decode_length[b] are computed and masked out
 //     (alphas = 0 there; the loss never reads their logits; their gradients are zero)
-// Per step (forward): GEMM(h->g1) -> attn_fwd (score, softmax_49, context, sigmoid gate) ->
-// GEMM(z->g2) -> cell_fwd.  Backward: cell_bwd -> GEMM(dgates->dz) -> attn_bwd ->
-// GEMM(dcat->dh).  Weight gradients are batched GEMMs over all B*T rows afterwards (host).
+//   * backward keeps only the recurrent chain in the loop: the encoder_att / full_att weight
+//     gradients are summed over t in ONE pass afterwards (attn_param_grad_kernel), from the
+//     saved softmax-input gradients de[b,t,p]
+// Per step (forward): skinny GEMM(h->g1) -> attn_fwd -> skinny GEMM(z->g2) -> cell_fwd.
+// Backward: cell_bwd -> skinny GEMM(dgates->dz) -> attn_bwd -> skinny GEMM(dcat->dh), with
+// the weights pre-transposed (w_ihz_t, w_hcat_t) so every step GEMM is k-major x k-major.
 #include "common.h"
 
 namespace imgcap {
 
-constexpr int ATT_THREADS = 256;
+constexpr int ATT_THREADS = 1024;
+constexpr int ATT_WAVES = ATT_THREADS / 64;
 constexpr int MAXP = 64;
 
-// ---- forward attention step ------------------------------------------------------------
+template <typename T> DEV void load8(const T* p, float (&v)[8]);
+template <> DEV void load8<bf16>(const bf16* p, float (&v)[8]) {
+  const bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
+template <> DEV void load8<float>(const float* p, float (&v)[8]) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+}
+
+// ---- forward attention step: one block (16 waves) per batch row ------------------------
 template <typename T>
 __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc d, int t) {
   const int b = blockIdx.x;
   const int P = d.P, E = d.E, A = d.A, Tn = d.T;
   const int W3 = A + E + 4 * d.D;
+  const long bt = (long)b * Tn + t;
   const bool active = t < d.dl[b];
-  const float* g1 = d.g1 + ((long)b * Tn + t) * W3;  // [att2 | gate_pre | hh]
+  const float* g1 = d.g1 + bt * W3;  // [att2 | gate_pre | hh]
   const T* att1 = (const T*)d.att1 + (long)b * P * A;
   const T* enc = (const T*)d.enc + (long)b * P * E;
   __shared__ float e_s[MAXP];
-  __shared__ float red[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // scores e_p = w_f . relu(att1_p + att2)   (full_att bias cancels in the softmax)
-  for (int p = w; p < P; p += 4) {
+  for (int p = w; p < P; p += ATT_WAVES) {
     float s = 0.f;
-    for (int a = lane; a < A; a += 64) s += d.w_f[a] * fmaxf(to_f(att1[(long)p * A + a]) + g1[a], 0.f);
+    for (int a = lane * 8; a < A; a += 512) {
+      float x[8];
+      load8<T>(att1 + (long)p * A + a, x);
+      const f32x4 g0 = *(const f32x4*)(g1 + a), g4 = *(const f32x4*)(g1 + a + 4);
+      const f32x4 w0 = *(const f32x4*)(d.w_f + a), w4 = *(const f32x4*)(d.w_f + a + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s += w0[j] * fmaxf(x[j] + g0[j], 0.f);
+        s += w4[j] * fmaxf(x[j + 4] + g4[j], 0.f);
+      }
+    }
     s = wave_sum(s);
     if (lane == 0) e_s[p] = s;
   }
@@ -51,14 +77,15 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
     const float al = ex / sum;
     if (lane < P) {
       e_s[lane] = al;
-      d.alphas[((long)b * Tn + t) * P + lane] = active ? al : 0.f;
+      d.alphas[bt * P + lane] = active ? al : 0.f;
     }
   }
   __syncthreads();
-  T* zs = (T*)d.zs + ((long)b * Tn + t) * E;
-  float* awe = d.awe + ((long)b * Tn + t) * E;
+  T* zs = (T*)d.zs + bt * E;
+  float* awe = d.awe + bt * E;
   for (int e = threadIdx.x; e < E; e += ATT_THREADS) {
     float s = 0.f;
+#pragma unroll 7
     for (int p = 0; p < P; ++p) s += e_s[p] * to_f(enc[(long)p * E + e]);
     const float gate = sigmoidf_(g1[A + e]);
     awe[e] = s;
@@ -108,13 +135,14 @@ __global__ __launch_bounds__(256) void cell_bwd_kernel(imgcap_lstm_desc d, int t
       d.dc[e] = 0.f;
       continue;
     }
-    const float dh = to_f(((const T*)d.dhs)[bt * D + j]) + d.dh[e];
+    const bool last = t + 1 >= Tn;  // no carry into the last step
+    const float dh = to_f(((const T*)d.dhs)[bt * D + j]) + (last ? 0.f : d.dh[e]);
     const float* ga = d.gates + bt * 4 * D;
     const float gi = ga[j], gf = ga[D + j], gg = ga[2 * D + j], go = ga[3 * D + j];
     const float c = d.cs[bt * D + j];
     const float cp = t == 0 ? d.c0[e] : d.cs[(bt - 1) * D + j];
     const float tc = tanhf(c);
-    const float dct = d.dc[e] + dh * go * (1.f - tc * tc);
+    const float dct = (last ? 0.f : d.dc[e]) + dh * go * (1.f - tc * tc);
     dg[j] = from_f<T>(dct * gg * gi * (1.f - gi));
     dg[D + j] = from_f<T>(dct * cp * gf * (1.f - gf));
     dg[2 * D + j] = from_f<T>(dct * gi * (1.f - gg * gg));
@@ -123,7 +151,7 @@ __global__ __launch_bounds__(256) void cell_bwd_kernel(imgcap_lstm_desc d, int t
   }
 }
 
-// ---- backward attention step -----------------------------------------------------------
+// ---- backward attention step: recurrent part only ---------------------------------------
 template <typename T>
 __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc d, int t) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -134,61 +162,119 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
   T* dcat = (T*)d.dcat + bt * W3;
   if (t >= d.dl[b]) {
     for (int i = threadIdx.x; i < A + E; i += ATT_THREADS) dcat[i] = from_f<T>(0.f);
+    if (threadIdx.x < P) d.de[bt * P + threadIdx.x] = 0.f;
     return;
   }
-  float* dawe = sm;            // [E]
-  float* al = sm + E;          // [MAXP]
-  float* dal = al + MAXP;      // [MAXP]
+  float* dawe = sm;              // [E]
+  float* al = sm + E;            // [MAXP]
+  float* dal = al + MAXP;        // [MAXP]
+  float* part = dal + MAXP;      // [2][A]
   const float* g1 = d.g1 + bt * W3;
   const float* dz = d.dz + (long)b * E;
   const float* awe = d.awe + bt * E;
   for (int e = threadIdx.x; e < E; e += ATT_THREADS) {
     const float s = sigmoidf_(g1[A + e]);
     dawe[e] = dz[e] * s;
-    dcat[A + e] = from_f<T>(dz[e] * awe[e] * s * (1.f - s));
+    dcat[A + e] = from_f<T>(dz[e] * awe[e] * s * (1.f - s));  // d gate_pre
   }
-  for (int p = threadIdx.x; p < P; p += ATT_THREADS) al[p] = d.alphas[bt * P + p];
+  if (threadIdx.x < P) al[threadIdx.x] = d.alphas[bt * P + threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const T* enc = (const T*)d.enc + (long)b * P * E;
-  for (int p = w; p < P; p += 4) {
+  for (int p = w; p < P; p += ATT_WAVES) {  // d alpha_p = enc_p . d awe  (+ reg/upstream term)
     float s = 0.f;
-    for (int e = lane; e < E; e += 64) s += to_f(enc[(long)p * E + e]) * dawe[e];
+    for (int e = lane * 8; e < E; e += 512) {
+      float x[8];
+      load8<T>(enc + (long)p * E + e, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += x[j] * dawe[e + j];
+    }
     s = wave_sum(s);
-    if (lane == 0) dal[p] = s + d.dreg[(long)b * P + p];
+    if (lane == 0) dal[p] = s + (d.dalpha ? d.dalpha[bt * P + p] : 0.f);
   }
   __syncthreads();
-  if (w == 0) {
+  if (w == 0) {  // softmax backward -> d score
     const float a = lane < P ? al[lane] : 0.f, da = lane < P ? dal[lane] : 0.f;
     const float dot = wave_sum(a * da);
-    if (lane < P) dal[lane] = a * (da - dot);  // d score
+    if (lane < P) {
+      const float de = a * (da - dot);
+      dal[lane] = de;
+      d.de[bt * P + lane] = de;
+    }
   }
   __syncthreads();
+  // d att2[a] = w_f[a] * sum_p de_p [att1[p,a] + att2[a] > 0]; two halves of p in parallel
   const T* att1 = (const T*)d.att1 + (long)b * P * A;
-  float* datt1 = d.datt1 + (long)b * P * A;
-  float* dwf = d.dwf + (long)b * A;
-  for (int a = threadIdx.x; a < A; a += ATT_THREADS) {
-    const float wf = d.w_f[a], a2 = g1[a];
-    float s_att2 = 0.f, s_wf = 0.f;
-    for (int p = 0; p < P; ++p) {
-      const float u = to_f(att1[(long)p * A + a]) + a2;
-      const float de = dal[p];
-      if (u > 0.f) {
-        const float du = de * wf;
-        s_att2 += du;
-        datt1[(long)p * A + a] += du;
-        s_wf += de * u;
+  const int half = threadIdx.x / 512, tid = threadIdx.x % 512;
+  const int p0 = half * ((P + 1) / 2), p1 = min(P, p0 + (P + 1) / 2);
+  for (int a = tid; a < A; a += 512) {
+    const float a2 = g1[a];
+    float s = 0.f;
+#pragma unroll 7
+    for (int p = p0; p < p1; ++p) s += (to_f(att1[(long)p * A + a]) + a2 > 0.f) ? dal[p] : 0.f;
+    part[half * A + a] = s;
+  }
+  __syncthreads();
+  for (int a = threadIdx.x; a < A; a += ATT_THREADS) dcat[a] = from_f<T>((part[a] + part[A + a]) * d.w_f[a]);
+}
+
+// ---- attention parameter gradients, summed over all steps at once -----------------------
+//   datt1[b,p,a]  = w_f[a] * sum_t de[b,t,p] [att1[b,p,a] + att2[b,t,a] > 0]
+//   dwf_part[b,a] = sum_{t,p} de[b,t,p] relu(att1[b,p,a] + att2[b,t,a])
+//   dbea_part[b,a] = sum_p datt1[b,p,a]
+// One thread per (b, a); its P att1 values and accumulators stay in registers.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_param_grad_kernel(imgcap_lstm_desc d) {
+  extern __shared__ __attribute__((aligned(16))) float de_s[];  // [T][P]
+  const int b = blockIdx.y;
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  const int P = d.P, A = d.A, E = d.E, Tn = d.T;
+  const int W3 = A + E + 4 * d.D;
+  for (int i = threadIdx.x; i < Tn * P; i += 256) de_s[i] = d.de[(long)b * Tn * P + i];
+  __syncthreads();
+  if (a >= A) return;
+  const T* att1 = (const T*)d.att1 + (long)b * P * A;
+  float x1[MAXP], acc[MAXP];
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    x1[p] = p < P ? to_f(att1[(long)p * A + a]) : 0.f;
+    acc[p] = 0.f;
+  }
+  float swf = 0.f;
+  const int tmax = min(Tn, d.dl[b]);
+  for (int t = 0; t < tmax; ++t) {
+    const float a2 = d.g1[((long)b * Tn + t) * W3 + a];
+    const float* de = de_s + t * P;
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+      if (p < P) {
+        const float u = x1[p] + a2;
+        const float g = de[p];
+        acc[p] += u > 0.f ? g : 0.f;
+        swf += g * fmaxf(u, 0.f);
       }
     }
-    dcat[a] = from_f<T>(s_att2);
-    dwf[a] += s_wf;
   }
+  const float wf = d.w_f[a];
+  float sb = 0.f;
+  T* out = (T*)d.datt1 + (long)b * P * A + a;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    if (p < P) {
+      const float v = acc[p] * wf;
+      out[(long)p * A] = from_f<T>(v);
+      sb += v;
+    }
+  }
+  d.dwf[(long)b * A + a] = swf;
+  d.dbea[(long)b * A + a] = sb;
 }
 
 // ---- doubly stochastic attention regularisation (train.py:269) --------------------------
-//   reg = alphaC * mean_{b,p} (1 - sum_t alpha[b,t,p])^2 ; dreg[b,p] = d reg / d alpha[b,t,p]
-__global__ void attn_reg_kernel(int B, int Tn, int P, const float* __restrict__ alphas, float alphaC,
-                                float* __restrict__ dreg, float* __restrict__ reg_out) {
+//   reg = alphaC * mean_{b,p} (1 - sum_t alpha[b,t,p])^2
+//   dalpha[b,t,p] = d reg / d alpha[b,t,p] for t < dl[b] (the written alphas), else 0
+__global__ void attn_reg_kernel(int B, int Tn, int P, const float* __restrict__ alphas, const int32_t* __restrict__ dl,
+                                float alphaC, float* __restrict__ dalpha, float* __restrict__ reg_out) {
   __shared__ float red[16];
   float acc = 0.f;
   for (int e = threadIdx.x; e < B * P; e += blockDim.x) {
@@ -196,7 +282,8 @@ __global__ void attn_reg_kernel(int B, int Tn, int P, const float* __restrict__ 
     float s = 0.f;
     for (int t = 0; t < Tn; ++t) s += alphas[((long)b * Tn + t) * P + p];
     acc += (1.f - s) * (1.f - s);
-    dreg[e] = alphaC * 2.f * (s - 1.f) / (float)(B * P);
+    const float g = alphaC * 2.f * (s - 1.f) / (float)(B * P);
+    for (int t = 0; t < Tn; ++t) dalpha[((long)b * Tn + t) * P + p] = t < dl[b] ? g : 0.f;
   }
   const float tot = block_sum(acc, red);
   if (threadIdx.x == 0) *reg_out = alphaC * tot / (float)(B * P);
@@ -207,24 +294,28 @@ static dim3 pw_grid(long n) {
   return dim3((unsigned)(b > 2048 ? 2048 : (b < 1 ? 1 : b)));
 }
 
-template <typename T>
-static int lstm_fwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
-  const int W3 = d.A + d.E + 4 * d.D;
-  const int ct = d.dtype;
+static imgcap_epilogue f32_epi(const float* bias) {
   imgcap_epilogue ep{};
   ep.alpha = 1.f;
   ep.c_dtype = IMGCAP_F32;
   ep.rows_per_scale = 1;
+  ep.bias = bias;
+  return ep;
+}
+
+template <typename T>
+static int lstm_fwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
+  const int W3 = d.A + d.E + 4 * d.D;
+  const int ct = d.dtype;
+  const imgcap_epilogue e1 = f32_epi(d.b_hcat), e2 = f32_epi(nullptr);
   for (int t = 0; t < d.T; ++t) {
-    imgcap_epilogue e1 = ep;
-    e1.bias = d.b_hcat;
     int rc = imgcap_gemm(ct, 1, 1, d.B, W3, d.D, (const T*)d.hprev + (long)t * d.D, (long)d.T * d.D, 0, d.w_hcat,
                          d.D, 0, d.g1 + (long)t * W3, (long)d.T * W3, 0, 1, &e1, st);
     if (rc) return rc;
     hipLaunchKernelGGL(attn_fwd_kernel<T>, dim3(d.B), dim3(ATT_THREADS), 0, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm attn_fwd");
     rc = imgcap_gemm(ct, 1, 1, d.B, 4 * d.D, d.E, (const T*)d.zs + (long)t * d.E, (long)d.T * d.E, 0,
-                     (const T*)d.w_ih + d.M, d.M + d.E, 0, d.g2, 4 * d.D, 0, 1, &ep, st);
+                     (const T*)d.w_ih + d.M, d.M + d.E, 0, d.g2, 4 * d.D, 0, 1, &e2, st);
     if (rc) return rc;
     hipLaunchKernelGGL(cell_fwd_kernel<T>, pw_grid((long)d.B * d.D), dim3(256), 0, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm cell_fwd");
@@ -236,30 +327,26 @@ template <typename T>
 static int lstm_bwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
   const int W3 = d.A + d.E + 4 * d.D;
   const int ct = d.dtype;
-  if (hipMemsetAsync(d.dh, 0, sizeof(float) * d.B * d.D, st) != hipSuccess ||
-      hipMemsetAsync(d.dc, 0, sizeof(float) * d.B * d.D, st) != hipSuccess ||
-      hipMemsetAsync(d.datt1, 0, sizeof(float) * (size_t)d.B * d.P * d.A, st) != hipSuccess ||
-      hipMemsetAsync(d.dwf, 0, sizeof(float) * (size_t)d.B * d.A, st) != hipSuccess)
-    return fail(IMGCAP_EINVAL, "lstm bwd: hipMemsetAsync failed");
-  imgcap_epilogue ep{};
-  ep.alpha = 1.f;
-  ep.c_dtype = IMGCAP_F32;
-  ep.rows_per_scale = 1;
-  const size_t shm = (d.E + 2 * MAXP) * sizeof(float);
+  const imgcap_epilogue ep = f32_epi(nullptr);
+  const size_t shm = (d.E + 2 * MAXP + 2 * d.A) * sizeof(float);
   for (int t = d.T - 1; t >= 0; --t) {
     hipLaunchKernelGGL(cell_bwd_kernel<T>, pw_grid((long)d.B * d.D), dim3(256), 0, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm cell_bwd");
-    // dz = dgates_t . W_ih[:, M:]      (W_ih [4D][M+E] read as [K=4D][N=E])
-    int rc = imgcap_gemm(ct, 1, 0, d.B, d.E, 4 * d.D, (const T*)d.dcat + (long)t * W3 + d.A + d.E, (long)d.T * W3, 0,
-                         (const T*)d.w_ih + d.M, d.M + d.E, 0, d.dz, d.E, 0, 1, &ep, st);
+    // dz = dgates_t . W_ih[:, M:]      (w_ihz_t = W_ih[:, M:]^T, [E][4D])
+    int rc = imgcap_gemm(ct, 1, 1, d.B, d.E, 4 * d.D, (const T*)d.dcat + (long)t * W3 + d.A + d.E, (long)d.T * W3,
+                         0, d.w_ihz_t, 4 * d.D, 0, d.dz, d.E, 0, 1, &ep, st);
     if (rc) return rc;
     hipLaunchKernelGGL(attn_bwd_kernel<T>, dim3(d.B), dim3(ATT_THREADS), shm, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm attn_bwd");
-    // dh_{t-1} = [d_att2 | d_gate_pre | dgates] . W_hcat   (W_hcat [W3][D] read as [K=W3][N=D])
-    rc = imgcap_gemm(ct, 1, 0, d.B, d.D, W3, (const T*)d.dcat + (long)t * W3, (long)d.T * W3, 0, d.w_hcat, d.D, 0,
+    // dh_{t-1} = [d att2 | d gate_pre | d gates] . W_hcat    (w_hcat_t = W_hcat^T, [D][W3]);
+    // at t = 0 this is dL/dh0
+    rc = imgcap_gemm(ct, 1, 1, d.B, d.D, W3, (const T*)d.dcat + (long)t * W3, (long)d.T * W3, 0, d.w_hcat_t, W3, 0,
                      d.dh, d.D, 0, 1, &ep, st);
     if (rc) return rc;
   }
+  const size_t shm2 = (size_t)d.T * d.P * sizeof(float);
+  hipLaunchKernelGGL(attn_param_grad_kernel<T>, dim3((d.A + 255) / 256, d.B), dim3(256), shm2, st, d);
+  IMGCAP_CHECK_LAUNCH("lstm attn_param_grad");
   return 0;
 }
 
@@ -283,14 +370,16 @@ extern "C" int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream) {
 
 extern "C" int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream) {
   if (int rc = check_desc(d)) return rc;
-  IMGCAP_REQUIRE(d->E + 2 * MAXP <= 16384, "lstm bwd: E too large");
+  IMGCAP_REQUIRE((d->E + 2 * MAXP + 2 * d->A) * 4 <= 65536, "lstm bwd: E/A too large for LDS");
+  IMGCAP_REQUIRE((size_t)d->T * d->P * 4 <= 65536, "lstm bwd: T*P too large for LDS");
+  IMGCAP_REQUIRE(d->w_ihz_t && d->w_hcat_t && d->de && d->dbea, "lstm bwd: transposed weights / de / dbea needed");
   if (d->dtype == IMGCAP_BF16) return lstm_bwd_impl<bf16>(*d, (hipStream_t)stream);
   return lstm_bwd_impl<float>(*d, (hipStream_t)stream);
 }
 
-extern "C" int imgcap_attn_reg(int B, int T, int P, const float* alphas, float alphaC, float* dreg, float* reg_out,
-                               void* stream) {
-  hipLaunchKernelGGL(attn_reg_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, T, P, alphas, alphaC, dreg,
+extern "C" int imgcap_attn_reg(int B, int T, int P, const float* alphas, const int32_t* dl, float alphaC,
+                               float* dalpha, float* reg_out, void* stream) {
+  hipLaunchKernelGGL(attn_reg_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, T, P, alphas, dl, alphaC, dalpha,
                      reg_out);
   IMGCAP_CHECK_LAUNCH("imgcap_attn_reg");
   return 0;

@@ -206,3 +206,17 @@ def adaptive_pool(x, OH, OW, out):
     B, H, W, C = x.shape
     _abi.call("imgcap_adaptive_pool_nhwc", dt(x), B, H, W, C, OH, OW, x.data_ptr(), out.data_ptr(), stream())
     return out
+
+
+def mean_mid(x, out):
+    B, P, E = x.shape
+    _abi.call("imgcap_mean_mid", dt(x), B, P, E, x.data_ptr(), out.data_ptr(), stream())
+    return out
+
+
+def transpose(x, out=None):
+    rows, cols = x.shape
+    out = torch.empty(cols, rows, device=x.device, dtype=x.dtype) if out is None else out
+    _abi.call("imgcap_transpose", dt(x), rows, cols, x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0),
+              stream())
+    return out

@@ -1,0 +1,221 @@
+"""Explicit forward/backward engine of the teacher-forced LSTM-attention decoder on HIP.
+
+Mirrors DecoderWithAttention.forwardWithTeacherForcing (models/decoder.py:104-148) plus the
+loss of train.py:263-269; the recurrence itself is one native call per direction
+(imgcap_lstm_tf_fwd / _bwd, csrc/lstm.hip).  Every GEMM is imgcap_gemm; the loss is the
+fused CE + top-5 kernel; parameters, grads, Adam state and the bf16 weight copy live in one
+FlatParams buffer whose groups make the concatenated operands zero-copy views:
+
+  hcat  = [attention.decoder_att.weight; f_beta.weight; decode_step.weight_hh]   [A+E+4D, D]
+  bhcat = [attention.decoder_att.bias;   f_beta.bias;   decode_step.bias_hh]     [A+E+4D]
+  init  = [init_h.weight; init_c.weight] [2D, E],  binit = [init_h.bias; init_c.bias]
+"""
+import ctypes
+
+import torch
+
+from . import _abi
+from . import kernels as K
+from .flat import FlatParams
+
+_STREAM_DROPOUT_H = 11  # dropout stream id for fc(dropout(h)) (decoder.py:144)
+
+
+def lstm_param_groups(dec):
+    n = dict(dec.named_parameters())
+    order = [
+        ["attention.decoder_att.weight", "f_beta.weight", "decode_step.weight_hh"],
+        ["attention.decoder_att.bias", "f_beta.bias", "decode_step.bias_hh"],
+        ["init_h.weight", "init_c.weight"],
+        ["init_h.bias", "init_c.bias"],
+        ["decode_step.weight_ih"], ["decode_step.bias_ih"],
+        ["attention.encoder_att.weight"], ["attention.encoder_att.bias"],
+        ["attention.full_att.weight"], ["attention.full_att.bias"],
+        ["embedding.weight"], ["fc.weight"], ["fc.bias"],
+    ]
+    seen = {x for g in order for x in g}
+    assert seen == set(n), f"unexpected decoder parameters: {set(n) ^ seen}"
+    return [[(k, n[k]) for k in g] for g in order]
+
+
+class LstmEngine:
+    def __init__(self, dec, device, compute_dtype=torch.bfloat16):
+        self.dec = dec
+        self.ct = compute_dtype
+        self.fp = FlatParams(lstm_param_groups(dec), device, compute_dtype)
+        self.E, self.A, self.D = dec.encoder_dim, dec.attention_dim, dec.decoder_dim
+        self.M, self.V = dec.embed_dim, dec.vocab_size
+        self.W3 = self.A + self.E + 4 * self.D
+        self.Vpad = (self.V + 7) // 8 * 8
+        self.seed = 1234
+        self.step_id = 0
+
+    # ---------------------------------------------------------------------------------------
+    def weights(self):
+        fp, A, E, D, M, V = self.fp, self.A, self.E, self.D, self.M, self.V
+        return dict(
+            hcat=fp.w("attention.decoder_att.weight", (self.W3, D), self.W3 * D),
+            bhcat=fp.f32("attention.decoder_att.bias", (self.W3,), self.W3),
+            init=fp.w("init_h.weight", (2 * D, E), 2 * D * E),
+            binit=fp.f32("init_h.bias", (2 * D,), 2 * D),
+            wih=fp.w("decode_step.weight_ih"), bih=fp.f32("decode_step.bias_ih"),
+            wea=fp.w("attention.encoder_att.weight"), bea=fp.f32("attention.encoder_att.bias"),
+            wf=fp.f32("attention.full_att.weight", (A,)),
+            emb=fp.f32("embedding.weight"),
+            wfc=fp.w("fc.weight"), bfc=fp.f32("fc.bias"),
+        )
+
+    def forward(self, encoder_out, encoded_captions, caption_lengths, *, fixed_T=False, dropout=None, loss=True,
+                alphaC=1.0):
+        """Runs decoder.py:104-148 (+ the train.py:265-269 loss when ``loss``).
+
+        fixed_T: run T = L-1 steps without reading decode lengths on the host (no sync; rows are
+        masked on device).  Otherwise T = max(decode_lengths) exactly as the reference.
+        Returns a dict of saved buffers (``s``) used by backward()."""
+        ct, dev = self.ct, encoder_out.device
+        A, E, D, M, V, W3 = self.A, self.E, self.D, self.M, self.V, self.W3
+        p_drop = self.dec.dropout_p if (dropout is None and self.dec.training) else (dropout or 0.0)
+        w = self.weights()
+        B = encoder_out.size(0)
+        enc = encoder_out.reshape(B, -1, E)
+        P = enc.size(1)
+        L = encoded_captions.size(1)
+        lens, sort_ind = caption_lengths.reshape(-1).sort(dim=0, descending=True, stable=True)
+        enc_s = enc.index_select(0, sort_ind).to(ct).contiguous()
+        caps_s = encoded_captions.index_select(0, sort_ind)
+        dl = (lens - 1).to(torch.int32)
+        if fixed_T:
+            T = L - 1
+            dls = None
+        else:
+            dls = (lens - 1).tolist()  # decoder.py:126 (host list, part of the reference API)
+            T = max(dls)
+        s = dict(B=B, P=P, T=T, L=L, sort_ind=sort_ind, caps_s=caps_s, dl=dl, dls=dls, p_drop=p_drop,
+                 seed=self.seed + self.step_id)
+        self.step_id += 1
+        f32 = dict(device=dev, dtype=torch.float32)
+        ctd = dict(device=dev, dtype=ct)
+        # ---- loop-invariant precompute ------------------------------------------------------
+        ids = caps_s[:, :T].contiguous()
+        emb = torch.empty(B * T, M, **ctd)
+        K.embedding_fwd(ids, w["emb"], emb)                                   # decoder.py:119
+        mean = torch.empty(B, E, **ctd)
+        K.mean_mid(enc_s, mean)                                               # decoder.py:99
+        h0c0 = K.gemm(mean, w["init"], trans_b=True, bias=w["binit"], out_dtype=torch.float32)  # :100-101
+        att1 = K.gemm(enc_s.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])             # :61 hoisted
+        xe = K.gemm(emb, w["wih"][:, :M], trans_b=True, bias=w["bih"], out_dtype=torch.float32)  # W_ih emb half
+        hprev = torch.empty(B, T, D, **ctd)
+        hprev[:, 0].copy_(h0c0[:, :D])
+        c0 = h0c0[:, D:].contiguous()
+        g1 = torch.empty(B, T, W3, **f32)
+        alphas = torch.empty(B, T, P, **f32)
+        awe = torch.empty(B, T, E, **f32)
+        zs = torch.empty(B, T, E, **ctd)
+        gates = torch.empty(B, T, 4 * D, **f32)
+        cs = torch.empty(B, T, D, **f32)
+        hs = torch.empty(B, T, D, **ctd)
+        g2 = torch.empty(B, 4 * D, **f32)
+        d = _abi.LstmDesc()
+        d.dtype, d.B, d.P, d.E, d.A, d.D, d.M, d.T = K.dt(emb), B, P, E, A, D, M, T
+        for k, v in dict(w_hcat=w["hcat"], b_hcat=w["bhcat"], w_ih=w["wih"], w_f=w["wf"], enc=enc_s, att1=att1,
+                         xe=xe, c0=c0, dl=dl, g1=g1, alphas=alphas, awe=awe, zs=zs, gates=gates, cs=cs, hs=hs,
+                         hprev=hprev, g2=g2).items():
+            setattr(d, k, v.data_ptr())
+        _abi.call("imgcap_lstm_tf_fwd", ctypes.byref(d), K.stream())
+        # ---- fc(dropout(h)) over all B*T rows (decoder.py:144) ----------------------------------
+        hd = hs.view(B * T, D)
+        if p_drop > 0:
+            hd = K.dropout(hd, p_drop, s["seed"], _STREAM_DROPOUT_H)
+        tmask = torch.arange(T, device=dev).view(1, T) < dl.view(B, 1)
+        s.update(enc_s=enc_s, ids=ids, emb=emb, mean=mean, att1=att1, xe=xe, c0=c0, g1=g1, alphas=alphas, awe=awe,
+                 zs=zs, gates=gates, cs=cs, hs=hs, hprev=hprev, g2=g2, hd=hd, tmask=tmask, desc=d)
+        if loss:
+            logits = torch.empty(B * T, self.Vpad, **ctd)
+            K.gemm(hd, w["wfc"], trans_b=True, bias=w["bfc"], out=logits, N=V)
+            targets = torch.where(tmask, caps_s[:, 1:T + 1], torch.full_like(caps_s[:, 1:T + 1], -1)).reshape(-1)
+            lse = torch.empty(B * T, **f32)
+            lrow = torch.empty(B * T, **f32)
+            hit = torch.empty(B * T, **f32)
+            K.ce_fwd(logits, targets, V, lse, lrow, hit)
+            dalpha = torch.empty(B, T, P, **f32)
+            reg = torch.empty(1, **f32)
+            _abi.call("imgcap_attn_reg", B, T, P, alphas.data_ptr(), dl.data_ptr(), alphaC, dalpha.data_ptr(),
+                      reg.data_ptr(), K.stream())
+            metrics = torch.empty(4, **f32)  # loss, tokens, top5 hits, 1/tokens
+            K.loss_finalize(lrow, hit, targets, reg, metrics)
+            s.update(logits=logits, targets=targets, lse=lse, dalpha=dalpha, metrics=metrics)
+        return s
+
+    def predictions(self, s):
+        """decoder.py:129,145: zero-filled predictions [B, T, V] (fp32) from the saved state."""
+        B, T, V = s["B"], s["T"], self.V
+        w = self.weights()
+        out = torch.empty(B * T, V, device=s["hs"].device, dtype=torch.float32)
+        K.gemm(s["hd"], w["wfc"], trans_b=True, bias=w["bfc"], out=out,
+               rowscale=s["tmask"].reshape(-1).float().contiguous(), rows_per_scale=1)
+        return out.view(B, T, V)
+
+    # ---------------------------------------------------------------------------------------
+    def backward(self, s, dlogits=None, dalpha=None, gbuf=None):
+        """Writes dL/dparams into ``gbuf`` (default: the flat grad buffer).  Default upstream:
+        the fused loss of forward(loss=True); otherwise ``dlogits`` [B*T, V(pad)] (compute
+        dtype) and ``dalpha`` [B, T, P] (f32)."""
+        fp, ct = self.fp, self.ct
+        gbuf = fp.grad if gbuf is None else gbuf
+
+        class _G:  # views into gbuf
+            @staticmethod
+            def g(name, shape=None, count=None):
+                return fp.g(name, shape, count, buf=gbuf)
+        B, P, T = s["B"], s["P"], s["T"]
+        A, E, D, M, V, W3 = self.A, self.E, self.D, self.M, self.V, self.W3
+        dev = s["hs"].device
+        w = self.weights()
+        gbuf.zero_()
+        if dlogits is None:
+            dlogits = torch.empty(B * T, self.Vpad, device=dev, dtype=ct)
+            K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
+            dalpha = s["dalpha"]
+        BT = B * T
+        # fc: dW_fc = dlogits^T hd ; db_fc = colsum ; dh = (dlogits W_fc) * dropmask
+        K.gemm(dlogits, s["hd"], trans_a=True, out=_G.g("fc.weight"), M=V)
+        K.colsum(dlogits, _G.g("fc.bias"), cols=V)
+        dhs = K.gemm(dlogits, w["wfc"], K=V, drop_p=s["p_drop"], seed=s["seed"], drop_stream=_STREAM_DROPOUT_H,
+                     drop_ld=D)
+        f32 = dict(device=dev, dtype=torch.float32)
+        dcat = torch.empty(B, T, W3, device=dev, dtype=ct)
+        dz, dh, dc = torch.empty(B, E, **f32), torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+        de = torch.empty(B, T, P, **f32)
+        datt1 = torch.empty(B * P, A, device=dev, dtype=ct)
+        dwf, dbea = torch.empty(B, A, **f32), torch.empty(B, A, **f32)
+        # k-major copies of the two weights the backward recurrence multiplies by
+        wihz_t = K.transpose(w["wih"][:, M:])            # [E, 4D]
+        whcat_t = K.transpose(w["hcat"])                 # [D, W3]
+        d = s["desc"]
+        for k, v in dict(w_ihz_t=wihz_t, w_hcat_t=whcat_t, dhs=dhs, dalpha=dalpha, dcat=dcat, dz=dz, dh=dh, dc=dc,
+                         de=de, datt1=datt1, dwf=dwf, dbea=dbea).items():
+            setattr(d, k, K.ptr(v))
+        _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream())
+        dc2 = dcat.view(BT, W3)
+        dgates = dc2[:, A + E:]
+        # W_hcat / b_hcat grads (batched over all B*T rows)
+        K.gemm(dc2, s["hprev"].view(BT, D), trans_a=True, out=_G.g("attention.decoder_att.weight", (W3, D), W3 * D))
+        K.colsum(dc2, _G.g("attention.decoder_att.bias", (W3,), W3))
+        # LSTMCell weight_ih (emb half | attention half), bias_ih
+        gwih = _G.g("decode_step.weight_ih")
+        K.gemm(dgates, s["emb"], trans_a=True, out=gwih[:, :M], M=4 * D)
+        K.gemm(dgates, s["zs"].view(BT, E), trans_a=True, out=gwih[:, M:], M=4 * D)
+        K.colsum(dgates, _G.g("decode_step.bias_ih"))
+        # embedding: d_emb = dgates W_ih[:, :M]  -> scatter-add rows
+        demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
+        K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
+        # init_h / init_c from dh0, dc0
+        dinit = torch.cat([dh, dc], dim=1).to(ct)
+        K.gemm(dinit, s["mean"], trans_a=True, out=_G.g("init_h.weight", (2 * D, E), 2 * D * E))
+        K.colsum(dinit, _G.g("init_h.bias", (2 * D,), 2 * D))
+        # encoder_att from the time-summed d att1
+        K.gemm(datt1, s["enc_s"].view(B * P, E), trans_a=True, out=_G.g("attention.encoder_att.weight"))
+        K.colsum(dbea, _G.g("attention.encoder_att.bias"))
+        K.colsum(dwf, _G.g("attention.full_att.weight", (A,)))
+        # full_att.bias: exactly zero gradient (softmax is shift-invariant) -> left at 0
+        return gbuf

@@ -1,0 +1,207 @@
+"""ConvNeXt encoder with the reference's class surface (models/encoder.py:14-34).
+
+``Encoder(encoded_image_size=7)`` exposes ``.convnext`` (the 8-child ``features`` Sequential,
+torchvision parameter names, so reference checkpoints' ``convnext.{i}...`` keys load
+unchanged), ``.adaptive_pool``, ``.forward(images) -> [B, 7, 7, E]`` and
+``.fine_tune(fine_tune, startingLayer)``.  The reference hard-codes ConvNeXt-Base with
+ImageNet weights (encoder.py:18); there is no network here, so weights are randomly
+initialised the torchvision way and ``variant`` selects tiny/base/large (BASELINE configs).
+
+forward runs the NHWC trunk on the HIP kernels: stem (conv4x4+LN) -> per CNBlock
+dwconv7x7+LN -> MFMA GEMM (Linear C->4C, +bias, GELU) -> MFMA GEMM (Linear 4C->C, +bias,
+*layer_scale, *stochastic-depth, +residual, in place) -> downsample LN + 2x2 patch GEMM ->
+adaptive pool.  Only the frozen-encoder (no-grad) path is on the hot path of the configs run
+here; a trainable encoder output raises (fine-tuning backward is SURVEY.md §8 C5, next round).
+"""
+import math
+
+import torch
+from torch import nn
+
+from .. import kernels as K
+
+VARIANTS = {
+    "tiny": ((96, 192, 384, 768), (3, 3, 9, 3), 0.1),
+    "small": ((96, 192, 384, 768), (3, 3, 27, 3), 0.4),
+    "base": ((128, 256, 512, 1024), (3, 3, 27, 3), 0.5),
+    "large": ((192, 384, 768, 1536), (3, 3, 27, 3), 0.5),
+}
+
+
+class _LayerNorm2d(nn.LayerNorm):
+    """Parameter holder with torchvision's LayerNorm2d names (weight, bias), eps 1e-6."""
+
+
+class _Permute(nn.Module):
+    def __init__(self, dims):
+        super().__init__()
+        self.dims = dims
+
+
+class CNBlock(nn.Module):
+    """torchvision CNBlock parameter layout: block.{0: dwconv, 2: LayerNorm, 3: Linear C->4C,
+    5: Linear 4C->C}, layer_scale [C,1,1]; stochastic-depth probability ``sd_prob``."""
+
+    def __init__(self, dim, layer_scale, sd_prob):
+        super().__init__()
+        self.block = nn.Sequential(
+            nn.Conv2d(dim, dim, kernel_size=7, padding=3, groups=dim, bias=True),
+            _Permute([0, 2, 3, 1]),
+            nn.LayerNorm(dim, eps=1e-6),
+            nn.Linear(dim, 4 * dim, bias=True),
+            nn.GELU(),
+            nn.Linear(4 * dim, dim, bias=True),
+            _Permute([0, 3, 1, 2]),
+        )
+        self.layer_scale = nn.Parameter(torch.ones(dim, 1, 1) * layer_scale)
+        self.sd_prob = sd_prob
+
+
+def build_features(variant):
+    chans, depths, sd_max = VARIANTS[variant]
+    layers = [nn.Sequential(nn.Conv2d(3, chans[0], kernel_size=4, stride=4, bias=True),
+                            _LayerNorm2d(chans[0], eps=1e-6))]
+    total = sum(depths)
+    bid = 0
+    for st in range(4):
+        blocks = []
+        for _ in range(depths[st]):
+            blocks.append(CNBlock(chans[st], 1e-6, sd_max * bid / (total - 1.0)))
+            bid += 1
+        layers.append(nn.Sequential(*blocks))
+        if st < 3:
+            layers.append(nn.Sequential(_LayerNorm2d(chans[st], eps=1e-6),
+                                        nn.Conv2d(chans[st], chans[st + 1], kernel_size=2, stride=2)))
+    feats = nn.Sequential(*layers)
+    for m in feats.modules():  # torchvision ConvNeXt init
+        if isinstance(m, (nn.Conv2d, nn.Linear)):
+            nn.init.trunc_normal_(m.weight, std=0.02)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+    return feats
+
+
+class Encoder(nn.Module):
+    def __init__(self, encoded_image_size=7, variant="base", compute_dtype=torch.bfloat16):
+        super().__init__()
+        self.enc_image_size = encoded_image_size
+        self.variant = variant
+        self.encoder_dim = VARIANTS[variant][0][3]
+        self.compute_dtype = compute_dtype
+        self.convnext = build_features(variant)
+        self.adaptive_pool = nn.AdaptiveAvgPool2d((encoded_image_size, encoded_image_size))
+        self.sd_seed = 0
+        self._packed = None
+        self._packed_key = None
+        self.fine_tune()
+
+    def fine_tune(self, fine_tune=True, startingLayer=7):
+        """encoder.py:29-34: freeze everything, then set requires_grad on children[startingLayer:]."""
+        for p in self.convnext.parameters():
+            p.requires_grad = False
+        for c in list(self.convnext.children())[startingLayer:]:
+            for p in c.parameters():
+                p.requires_grad = fine_tune
+
+    # -- weight packing into kernel layouts ----------------------------------------------------
+    def _pack_key(self):
+        ps = list(self.convnext.parameters())
+        return (self.compute_dtype, ps[0].device, tuple(p._version for p in ps), tuple(p.data_ptr() for p in ps))
+
+    def _pack(self):
+        key = self._pack_key()
+        if self._packed is not None and self._packed_key == key:
+            return self._packed
+        ct = self.compute_dtype
+        f = self.convnext
+        with torch.no_grad():
+            stem_conv, stem_ln = f[0][0], f[0][1]
+            pk = {"stem": (stem_conv.weight.reshape(stem_conv.out_channels, 48).float().contiguous(),
+                           stem_conv.bias.float().contiguous(), stem_ln.weight.float().contiguous(),
+                           stem_ln.bias.float().contiguous())}
+            stages = []
+            for st in range(4):
+                blocks = []
+                for blk in f[1 + 2 * st]:
+                    dw, ln, l1, l2 = blk.block[0], blk.block[2], blk.block[3], blk.block[5]
+                    C = dw.out_channels
+                    blocks.append(dict(
+                        w49=dw.weight.reshape(C, 49).t().float().contiguous(), dwb=dw.bias.float().contiguous(),
+                        lnw=ln.weight.float().contiguous(), lnb=ln.bias.float().contiguous(),
+                        w1=l1.weight.to(ct).contiguous(), b1=l1.bias.float().contiguous(),
+                        w2=l2.weight.to(ct).contiguous(), b2=l2.bias.float().contiguous(),
+                        gamma=blk.layer_scale.reshape(C).float().contiguous(), sd=blk.sd_prob))
+                down = None
+                if st < 3:
+                    ln, cv = f[2 + 2 * st][0], f[2 + 2 * st][1]
+                    down = dict(lnw=ln.weight.float().contiguous(), lnb=ln.bias.float().contiguous(),
+                                w=cv.weight.permute(0, 2, 3, 1).reshape(cv.out_channels, -1).to(ct).contiguous(),
+                                b=cv.bias.float().contiguous())
+                stages.append((blocks, down))
+            pk["stages"] = stages
+        self._packed, self._packed_key = pk, key
+        return pk
+
+    def _sd_scales(self, B, device):
+        """StochasticDepth(p, "row") per-sample scales keep/(1-p) for every block (train mode)."""
+        probs = [blk.sd_prob for s in range(4) for blk in self.convnext[1 + 2 * s]]
+        g = torch.Generator(device=device)
+        g.manual_seed(self.sd_seed)
+        self.sd_seed += 1
+        u = torch.rand(len(probs), B, device=device, generator=g)
+        p = torch.tensor(probs, device=device).view(-1, 1)
+        return torch.where(u >= p, 1.0 / (1.0 - p), torch.zeros_like(u)).contiguous()
+
+    def forward(self, images):
+        """encoder.py:23-27.  images [B,3,H,W] (f32, on GPU) -> [B, s, s, E] NHWC, compute dtype."""
+        if any(p.requires_grad for p in self.convnext.parameters()) and torch.is_grad_enabled():
+            raise NotImplementedError("encoder fine-tuning backward (startingLayer < 8 with fine_tune=True) is not "
+                                      "built yet (SURVEY.md §8 C5); call fine_tune(False) or run under no_grad")
+        if not images.is_cuda:
+            raise RuntimeError("Encoder.forward runs on the HIP kernels only; move images to the GPU")
+        pk = self._pack()
+        ct = self.compute_dtype
+        images = images.float().contiguous()
+        B, _, H, W = images.shape
+        dev = images.device
+        C0 = pk["stem"][0].shape[0]
+        x = torch.empty(B, H // 4, W // 4, C0, device=dev, dtype=ct)
+        K.convnext_stem(images, *pk["stem"], x)
+        sd = self._sd_scales(B, dev) if self.training else None
+        bid = 0
+        for blocks, down in pk["stages"]:
+            _, h, w, C = x.shape
+            M = B * h * w
+            z = torch.empty_like(x)
+            hid = torch.empty(M, 4 * C, device=dev, dtype=ct)
+            x2 = x.view(M, C)
+            for blk in blocks:
+                K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], z)
+                K.gemm(z.view(M, C), blk["w1"], trans_b=True, bias=blk["b1"], act=K.ACT_GELU, out=hid)
+                rs = sd[bid] if (sd is not None and blk["sd"] > 0) else None
+                K.gemm(hid, blk["w2"], trans_b=True, bias=blk["b2"], colscale=blk["gamma"], rowscale=rs,
+                       rows_per_scale=h * w, res=x2, out=x2)
+                bid += 1
+            if down is not None:
+                patches = torch.empty(B * (h // 2) * (w // 2), 4 * C, device=dev, dtype=ct)
+                K.ln_patchify2(x, down["lnw"], down["lnb"], patches)
+                C2 = down["w"].shape[0]
+                x = torch.empty(B, h // 2, w // 2, C2, device=dev, dtype=ct)
+                K.gemm(patches, down["w"], trans_b=True, bias=down["b"], out=x.view(-1, C2))
+        s = self.enc_image_size
+        if x.shape[1] == s and x.shape[2] == s:
+            return x
+        out = torch.empty(B, s, s, x.shape[3], device=dev, dtype=ct)
+        return K.adaptive_pool(x, s, s, out)
+
+    def macs_per_image(self, hw=224):
+        chans, depths, _ = VARIANTS[self.variant]
+        h = hw // 4
+        m = h * h * chans[0] * 48
+        for st in range(4):
+            C = chans[st]
+            m += depths[st] * (h * h * C * 49 + 2 * h * h * C * 4 * C)
+            if st < 3:
+                h //= 2
+                m += h * h * chans[st + 1] * 4 * C
+        return m

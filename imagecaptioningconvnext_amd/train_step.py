@@ -1,0 +1,65 @@
+"""Fused teacher-forced train step (train.py:240-302, trainMultiGPU.py:339-420) on HIP + RCCL.
+
+Per step, exactly the reference's work:
+  encoder(imgs) in train mode (frozen weights, stochastic depth active)      train.py:242,261
+  decoder teacher-forced forward + packed CE (+ alpha reg for LSTM)          :262-276
+  zero_grad + backward                                                        :278-281
+  DDP gradient averaging (one RCCL all-reduce over the flat grad buffer)      trainMultiGPU.py:233,384
+  clip_gradient (clamp +-5) + Adam step (one fused kernel)                    :284-291 / :387-394
+  loss/token/top-5 metrics (reduceLossAndTokens + accuracy all-reduces,
+  fused into one 3-float all-reduce; read back lazily, no per-step host sync) :396-403
+"""
+import torch
+import torch.distributed as dist
+
+
+class TeacherForcedTrainer:
+    def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, grad_clip=5.0, alphaC=1.0, pad_id=0,
+                 process_group=None):
+        self.encoder = encoder
+        self.decoder = decoder
+        self.lstm = lstm
+        self.decoder_lr = decoder_lr
+        self.grad_clip = grad_clip
+        self.alphaC = alphaC
+        self.pad_id = pad_id
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.eng = decoder.engine()
+        self._metric_log = []
+        if self.world > 1:
+            # DDP construction broadcasts rank 0's parameters (trainMultiGPU.py:233); the encoder is
+            # broadcast too because its weights are randomly initialised here (SURVEY.md §7 v)
+            dist.broadcast(self.eng.fp.flat, 0, group=process_group)
+            self.eng.fp.refresh_shadow()
+            for p in encoder.parameters():
+                dist.broadcast(p.data, 0, group=process_group)
+
+    def step(self, imgs, caps, caplens):
+        self.encoder.train()
+        self.decoder.train()
+        with torch.no_grad():
+            feats = self.encoder(imgs)
+        if self.lstm:
+            s = self.eng.forward(feats, caps, caplens, fixed_T=True, alphaC=self.alphaC)
+        else:
+            s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
+        self.eng.backward(s)
+        fp = self.eng.fp
+        if self.world > 1:
+            dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
+        fp.adam_step(self.decoder_lr, self.grad_clip, grad_div=float(self.world))
+        m = s["metrics"]
+        red = torch.stack([m[0] * m[1], m[1], m[2]])
+        if self.world > 1:
+            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)
+        self._metric_log.append(red)
+        return red
+
+    def drain_metrics(self):
+        """(globalLoss, tokens, top5 %) per logged step, like reduceLossAndTokens + accuracy."""
+        if not self._metric_log:
+            return []
+        r = torch.stack(self._metric_log).double().cpu()
+        self._metric_log = []
+        return [(float(a / b), float(b), float(c / b * 100.0)) for a, b, c in r]

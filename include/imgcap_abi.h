@@ -69,6 +69,10 @@ int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                 void* C, int64_t ldc, int64_t strideC, int batch,
                 const imgcap_epilogue* epi, void* stream);
 
+/* out[c, r] = in[r, c]  (weight transposes for the k-major skinny GEMMs) */
+int imgcap_transpose(int dtype, int rows, int cols, const void* in, int64_t ldi, void* out, int64_t ldo,
+                     void* stream);
+
 /* column sums of a [rows, cols] matrix into fp32 out[cols] (bias gradients); beta=1 accumulates */
 int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64_t ldx, float* out, float beta,
                   void* stream);
@@ -147,19 +151,19 @@ int imgcap_clamp_adam(int64_t n, float* param, const float* grad, float* m, floa
  * LSTMCell at :141).  One call enqueues all T steps (4 kernels per step).  Batch-major
  * buffers [B, T, .]; rows sorted by decode length (decoder.py:114); W3 = A + E + 4D.
  * fwd requires: hprev[:,0,:] = h0, c0, xe = emb_t W_ih[:, :M]^T + b_ih + b_hh, att1.
- * bwd requires: the saved forward buffers, dhs (dL/dh_t from fc), dreg; produces dcat
- * (= per-step [d att2 | d gate_pre | d gates_preact]) for the weight-gradient GEMMs, dh/dc
- * (= dL/dh0, dL/dc0), datt1 (sum over t of dL/datt1) and dwf partials [B, A].
+ * bwd requires: the saved forward buffers, dhs (dL/dh_t from fc), dalpha, transposed weights;
+ * produces dcat (= per-step [d att2 | d gate_pre | d gates_preact]) for the weight-gradient
+ * GEMMs, dh/dc (= dL/dh0, dL/dc0), datt1 (sum over t of dL/datt1) and dwf / dbea partials.
  * -------------------------------------------------------------------------------------- */
 typedef struct imgcap_lstm_desc {
   int32_t dtype, B, P, E, A, D, M, T;
   const void* w_hcat;   /* [W3, D] = [W_da; W_fb; W_hh]             */
-  const float* b_hcat;  /* [W3]   = [b_da; b_fb; 0]                 */
+  const float* b_hcat;  /* [W3]   = [b_da; b_fb; b_hh]              */
   const void* w_ih;     /* [4D, M+E] LSTMCell weight_ih             */
   const float* w_f;     /* [A] full_att weight                      */
   const void* enc;      /* [B, P, E] encoder_out (sorted)           */
   const void* att1;     /* [B, P, A]                                */
-  const float* xe;      /* [B, T, 4D]                               */
+  const float* xe;      /* [B, T, 4D] emb W_ih[:, :M]^T + b_ih      */
   const float* c0;      /* [B, D]                                   */
   const int32_t* dl;    /* [B] decode lengths (sorted, device)      */
   float* g1;            /* [B, T, W3] saved                         */
@@ -171,21 +175,26 @@ typedef struct imgcap_lstm_desc {
   void* hs;             /* [B, T, D]  h_t                           */
   void* hprev;          /* [B, T, D]  h_{t-1}; slot 0 = h0          */
   float* g2;            /* [B, 4D] workspace                        */
+  const void* w_ihz_t;  /* [E, 4D]  = W_ih[:, M:]^T   (bwd)         */
+  const void* w_hcat_t; /* [D, W3]  = W_hcat^T        (bwd)         */
   const void* dhs;      /* [B, T, D]  bwd input                     */
-  const float* dreg;    /* [B, P]     bwd input                     */
+  const float* dalpha;  /* [B, T, P]  bwd input dL/dalpha or NULL   */
   void* dcat;           /* [B, T, W3] bwd output                    */
   float* dz;            /* [B, E] workspace                         */
   float* dh;            /* [B, D] out: dL/dh0                       */
   float* dc;            /* [B, D] out: dL/dc0                       */
-  float* datt1;         /* [B, P, A] out                            */
-  float* dwf;           /* [B, A] out                               */
+  float* de;            /* [B, T, P] workspace: dL/d(attention score) */
+  void* datt1;          /* [B, P, A] out: sum_t dL/datt1 (dtype)    */
+  float* dwf;           /* [B, A] out: per-row partial of dL/dw_f   */
+  float* dbea;          /* [B, A] out: per-row partial of dL/db_ea  */
 } imgcap_lstm_desc;
 
 int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream);
 int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream);
-/* train.py:269: reg = alphaC*mean_{b,p}(1-sum_t alpha)^2 -> *reg_out; dreg[b,p] = d reg/d alpha */
-int imgcap_attn_reg(int B, int T, int P, const float* alphas, float alphaC, float* dreg, float* reg_out,
-                    void* stream);
+/* train.py:269: reg = alphaC*mean_{b,p}(1-sum_t alpha)^2 -> *reg_out;
+ * dalpha[b,t,p] = d reg / d alpha[b,t,p] (0 where t >= dl[b]) */
+int imgcap_attn_reg(int B, int T, int P, const float* alphas, const int32_t* dl, float alphaC, float* dalpha,
+                    float* reg_out, void* stream);
 
 /* y = x * dropmask(seed, stream, i) (nn.Dropout, decoder.py:144 / transformer dropouts) */
 int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint64_t seed, uint32_t drop_stream, void* y,
@@ -195,6 +204,9 @@ int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint64_t seed, 
  * out[2] = sum(hit5), out[3] = 1/count (the CE backward scale) */
 int imgcap_loss_finalize(int n, const float* loss_rows, const float* hit5, const int64_t* targets,
                          const float* extra, float* out, void* stream);
+
+/* out[b, e] = mean_p x[b, p, e] (decoder.py:99, input of init_h/init_c) */
+int imgcap_mean_mid(int dtype, int B, int P, int E, const void* x, void* out, void* stream);
 
 /* elementwise helpers */
 int imgcap_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);

@@ -24,7 +24,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
-@pytest.mark.parametrize("M,N,Kd", [(37, 50, 72), (32, 3328, 512), (64, 200, 136), (300, 260, 1000), (1030, 520, 96)])
+@pytest.mark.parametrize("M,N,Kd", [(37, 50, 72), (32, 3328, 512), (64, 200, 136), (300, 260, 1000), (1030, 520, 96),
+                                     (5, 50, 20), (17, 33, 40), (64, 100, 1000), (1, 16, 8), (130, 9490, 40)])
 def test_gemm_layouts(hip_device, dtype, tol, ta, tb, M, N, Kd):
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
     a = torch.randn(M, Kd, generator=g)
@@ -226,3 +227,11 @@ def test_adaptive_pool(hip_device):
     out = torch.empty(2, 7, 7, 64, device=hip_device)
     K.adaptive_pool(x.to(hip_device), 7, 7, out)
     assert _rel(out.cpu(), ref) < 1e-6
+
+
+def test_transpose(hip_device):
+    for dtype in (torch.float32, torch.bfloat16):
+        x = torch.randn(130, 200).to(hip_device, dtype)
+        view = x[:, 8:72]
+        out = K.transpose(view)
+        assert torch.equal(out.cpu(), view.cpu().t())
