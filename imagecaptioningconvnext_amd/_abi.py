@@ -34,6 +34,15 @@ class LstmDesc(ctypes.Structure):
                                 "dcat", "dz", "dh", "dc", "de", "datt1", "dwf", "dbea")]
 
 
+class MhaDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("dtype", "B", "H", "Lq", "Lk", "dh", "causal")] + [
+        ("pad_id", c_int64), ("ldq", c_int64), ("ldk", c_int64), ("ldv", c_int64), ("ldo", c_int64),
+        ("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("lse", c_void_p),
+        ("key_ids", c_void_p), ("scale", c_float), ("drop_p", c_float), ("seed", c_uint64),
+        ("drop_stream", c_uint32), ("dout", c_void_p), ("lddo", c_int64), ("dq", c_void_p), ("dk", c_void_p),
+        ("dv", c_void_p), ("lddq", c_int64), ("lddk", c_int64), ("lddv", c_int64)]
+
+
 # name -> argtypes  (every entry point declared in include/imgcap_abi.h)
 _SIGS = {
     "imgcap_version": [],
@@ -62,6 +71,8 @@ _SIGS = {
                           c_float, c_int, c_float, c_float, c_void_p],
     "imgcap_lstm_tf_fwd": [ctypes.POINTER(LstmDesc), c_void_p],
     "imgcap_lstm_tf_bwd": [ctypes.POINTER(LstmDesc), c_void_p],
+    "imgcap_mha_fwd": [ctypes.POINTER(MhaDesc), c_void_p],
+    "imgcap_mha_bwd": [ctypes.POINTER(MhaDesc), c_void_p],
     "imgcap_attn_reg": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     "imgcap_dropout": [c_int, c_int64, c_void_p, c_float, c_uint64, c_uint32, c_void_p, c_void_p],
     "imgcap_loss_finalize": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

@@ -9,61 +9,101 @@
 namespace imgcap {
 
 // ---------------------------------------------------------------------------------------
-// stem: one wave per output pixel (looped), lanes own channels c = lane + 64*i (C0 <= 256)
-// weights [48][C0] staged in LDS.  48 MACs per output, LN by wave shuffles.
+// stem: block = NPX output pixels; their 4x4x3 patches and the [48][C0] weights are staged in
+// LDS; thread = (pixel, 8 output channels): 48x8 MACs, then the per-pixel LayerNorm over C0
+// is a fixed-order LDS reduction across the pixel's C0/8 threads.
 template <typename T>
-__global__ __launch_bounds__(256) void stem_kernel(int B, int H, int W, int C0, const float* __restrict__ img,
-                                                   const float* __restrict__ w, const float* __restrict__ bias,
-                                                   const float* __restrict__ lw, const float* __restrict__ lb,
-                                                   T* __restrict__ out, int px_per_block) {
+__global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0, const float* __restrict__ img,
+                                                    const float* __restrict__ w, const float* __restrict__ bias,
+                                                    const float* __restrict__ lw, const float* __restrict__ lb,
+                                                    T* __restrict__ out, int npx) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* ws = sm;  // [48][C0]
+  const int CV = C0 / 8;
+  float* ws = sm;                     // [48][C0]
+  float* patch = ws + 48 * C0;        // [npx][48]
+  float* red = patch + npx * 48;      // [npx][CV]
+  float* stat = red + npx * CV;       // [npx][2]
+  const int HO = H / 4, WO = W / 4;
+  const long total = (long)B * HO * WO;
+  const long px0 = (long)blockIdx.x * npx;
   for (int e = threadIdx.x; e < 48 * C0; e += blockDim.x) {
     const int c = e / 48, k = e % 48;  // torch weight [C0][3][4][4] -> k = ci*16+kh*4+kw
     ws[k * C0 + c] = w[e];
   }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int HO = H / 4, WO = W / 4;
-  const long npx = (long)B * HO * WO;
-  for (int q = wv; q < px_per_block; q += 4) {
-    const long px = (long)blockIdx.x * px_per_block + q;
-    if (px >= npx) break;
-    const int b = (int)(px / (HO * WO)), rem = (int)(px % (HO * WO)), oh = rem / WO, ow = rem % WO;
-    float xv = 0.f;
-    if (lane < 48) {
-      const int ci = lane >> 4, kh = (lane >> 2) & 3, kw = lane & 3;
-      xv = img[(((long)b * 3 + ci) * H + oh * 4 + kh) * W + ow * 4 + kw];
+  for (int e = threadIdx.x; e < npx * 12; e += blockDim.x) {  // 12 float4 rows per patch
+    const int q = e / 12, r = e % 12, ci = r / 4, kh = r % 4;
+    const long px = px0 + q;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (px < total) {
+      const int b = (int)(px / (HO * WO)), rem = (int)(px % (HO * WO)), oh = rem / WO, ow = rem % WO;
+      v = *(const f32x4*)(img + (((long)b * 3 + ci) * H + oh * 4 + kh) * W + ow * 4);
     }
-    float xs[48];  // broadcast the 48 patch values to scalar registers
+    *(f32x4*)(patch + q * 48 + ci * 16 + kh * 4) = v;
+  }
+  __syncthreads();
+  const int q = threadIdx.x / CV, cv = threadIdx.x % CV, c0 = cv * 8;
+  const bool active = q < npx && px0 + q < total;
+  float acc[8];
 #pragma unroll
-    for (int k = 0; k < 48; ++k) xs[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), k));
-    float acc[4];
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (active) {
+    const f32x4 b0 = *(const f32x4*)(bias + c0), b1 = *(const f32x4*)(bias + c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { acc[j] = b0[j]; acc[j + 4] = b1[j]; }
+    const float* pp = patch + q * 48;
+#pragma unroll 8
+    for (int k = 0; k < 48; ++k) {
+      const float x = pp[k];
+      const f32x4 w0 = *(const f32x4*)(ws + k * C0 + c0), w1 = *(const f32x4*)(ws + k * C0 + c0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { acc[j] += x * w0[j]; acc[j + 4] += x * w1[j]; }
+    }
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = lane + 64 * i;
-      acc[i] = 0.f;
-      if (c < C0) {
-        float a = bias[c];
+    for (int j = 0; j < 8; ++j) s += acc[j];
+    red[q * CV + cv] = s;
+  }
+  __syncthreads();
+  if (active && cv == 0) {
+    float s = 0.f;
+    for (int i = 0; i < CV; ++i) s += red[q * CV + i];
+    stat[q * 2] = s / C0;
+  }
+  __syncthreads();
+  float mean = 0.f;
+  if (active) {
+    mean = stat[q * 2];
+    float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < 48; ++k) a += xs[k] * ws[k * C0 + c];
-        acc[i] = a;
-        s += a;
-      }
+    for (int j = 0; j < 8; ++j) { const float d = acc[j] - mean; s += d * d; }
+    red[q * CV + cv] = s;
+  }
+  __syncthreads();
+  if (active && cv == 0) {
+    float s = 0.f;
+    for (int i = 0; i < CV; ++i) s += red[q * CV + i];
+    stat[q * 2 + 1] = rsqrtf(s / C0 + 1e-6f);
+  }
+  __syncthreads();
+  if (active) {
+    const float rstd = stat[q * 2 + 1];
+    const f32x4 g0 = *(const f32x4*)(lw + c0), g1 = *(const f32x4*)(lw + c0 + 4);
+    const f32x4 h0 = *(const f32x4*)(lb + c0), h1 = *(const f32x4*)(lb + c0 + 4);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (acc[j] - mean) * rstd * g0[j] + h0[j];
+      o[j + 4] = (acc[j + 4] - mean) * rstd * g1[j] + h1[j];
     }
-    const float mean = wave_sum(s) / C0;
-    float sq = 0.f;
+    T* op = out + (px0 + q) * C0 + c0;
+    if (sizeof(T) == 2) {
+      bf16x8 v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = lane + 64 * i;
-      if (c < C0) { const float d = acc[i] - mean; sq += d * d; }
-    }
-    const float rstd = rsqrtf(wave_sum(sq) / C0 + 1e-6f);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = lane + 64 * i;
-      if (c < C0) out[px * C0 + c] = from_f<T>((acc[i] - mean) * rstd * lw[c] + lb[c]);
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)o[j];
+      *(bf16x8*)op = v;
+    } else {
+      *(f32x4*)op = f32x4{o[0], o[1], o[2], o[3]};
+      *(f32x4*)(op + 4) = f32x4{o[4], o[5], o[6], o[7]};
     }
   }
 }
@@ -274,18 +314,24 @@ using namespace imgcap;
 
 extern "C" int imgcap_convnext_stem(int dtype, int B, int H, int W, int C0, const float* images, const float* w,
                                     const float* bias, const float* ln_w, const float* ln_b, void* out, void* stream) {
-  IMGCAP_REQUIRE(H % 4 == 0 && W % 4 == 0 && C0 > 0 && C0 <= 256, "imgcap_convnext_stem: bad shape");
-  const long npx = (long)B * (H / 4) * (W / 4);
-  if (npx == 0) return 0;
-  const int ppb = 32;
-  dim3 grid((unsigned)((npx + ppb - 1) / ppb));
-  const size_t shm = 48 * C0 * sizeof(float);
+  IMGCAP_REQUIRE(H % 4 == 0 && W % 4 == 0 && C0 % 8 == 0 && C0 <= 1024, "imgcap_convnext_stem: bad shape");
+  IMGCAP_REQUIRE(aligned16(images) && aligned16(bias) && aligned16(ln_w) && aligned16(ln_b) && aligned16(out),
+                 "imgcap_convnext_stem: alignment");
+  const long total = (long)B * (H / 4) * (W / 4);
+  if (total == 0) return 0;
+  const int CV = C0 / 8;
+  int npx = 1024 / CV;
+  if (npx > 64) npx = 64;
+  const int threads = ((npx * CV + 63) / 64) * 64;
+  dim3 grid((unsigned)((total + npx - 1) / npx));
+  const size_t shm = (48 * C0 + npx * 48 + npx * CV + npx * 2) * sizeof(float);
+  IMGCAP_REQUIRE(shm <= 160 * 1024, "imgcap_convnext_stem: LDS");
   if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(stem_kernel<bf16>, grid, dim3(256), shm, (hipStream_t)stream, B, H, W, C0, images, w, bias,
-                       ln_w, ln_b, (bf16*)out, ppb);
+    hipLaunchKernelGGL(stem_kernel<bf16>, grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, images, w, bias,
+                       ln_w, ln_b, (bf16*)out, npx);
   else
-    hipLaunchKernelGGL(stem_kernel<float>, grid, dim3(256), shm, (hipStream_t)stream, B, H, W, C0, images, w, bias,
-                       ln_w, ln_b, (float*)out, ppb);
+    hipLaunchKernelGGL(stem_kernel<float>, grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, images, w, bias,
+                       ln_w, ln_b, (float*)out, npx);
   IMGCAP_CHECK_LAUNCH("imgcap_convnext_stem");
   return 0;
 }

@@ -336,22 +336,43 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
-// SW waves split K; fragments come straight from global memory.
-template <typename T, int MT, int SW>
+// SW waves split K; each wave issues the loads of up to DEPTH k-steps at once (one memory
+// round trip per chunk), fragments go straight from global memory to the MFMAs.
+template <typename T> struct SkinnyLd {
+  static constexpr int H = sizeof(T) == 4 ? 2 : 1;  // 16-byte vectors per 8-element fragment
+};
+
+template <typename T>
+DEV void skinny_load(uint4 (&dst)[SkinnyLd<T>::H], const T* row, int k0, int K, bool row_ok) {
+  constexpr int H = SkinnyLd<T>::H;
+  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+  const bool kin = row_ok && k0 < K;
+  const int ck = kin ? k0 : 0;
+  dst[0] = *(const uint4*)(row + ck);
+  if (H == 2) dst[H - 1] = (ck + 4 < K) ? *(const uint4*)(row + ck + 4) : zero;
+  if (!kin) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) dst[h] = zero;
+  } else if (k0 + 8 > K) {
+    dst[0] = mask_tail<T>(dst[0], K - k0);
+    if (H == 2) dst[H - 1] = mask_tail<T>(dst[H - 1], K - k0 - 4);
+  }
+}
+
+template <typename T, int MT, int SW, int DEPTH>
 __global__ __launch_bounds__(64 * SW) void gemm_skinny_kernel(const T* __restrict__ A, long lda,
                                                               const T* __restrict__ B, long ldb,
                                                               void* __restrict__ C, long ldc, int M, int N, int K,
                                                               imgcap_epilogue ep, int vec_ok) {
-  constexpr int VEC = 16 / sizeof(T);
+  constexpr int H = SkinnyLd<T>::H;
   constexpr int LDT = 16 + 4;
   __shared__ __attribute__((aligned(16))) float part[SW][MT * 16][LDT];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16;
   const int fr = lane & 15, fk = 8 * (lane >> 4);
-  const int nks = (K + 31) / 32;                     // k-steps of 32
+  const int nks = (K + 31) / 32;
   const int per = (nks + SW - 1) / SW;
   const int ks0 = w * per, ks1 = min(nks, ks0 + per);
-  // clamped row addresses (out-of-range rows/cols read row 0 / N-1 and are zeroed)
   const T* arow[MT];
   bool aok[MT];
 #pragma unroll
@@ -366,68 +387,25 @@ __global__ __launch_bounds__(64 * SW) void gemm_skinny_kernel(const T* __restric
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-  const int kfull = (K / 32) * 32;  // k-steps below this need no tail mask
-  int ks = ks0;
-  // main loop, unrolled x2 so two steps of loads are in flight
-  for (; ks + 2 <= ks1 && (ks + 2) * 32 <= kfull; ks += 2) {
-    uint4 a0[MT], a1[MT], b0lo, b0hi, b1lo, b1hi;
-    const int k0 = ks * 32 + fk, k1 = k0 + 32;
+  for (int base = ks0; base < ks1; base += DEPTH) {
+    const int cnt = min(DEPTH, ks1 - base);
+    uint4 ar[DEPTH][MT][H], br[DEPTH][H];
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      a0[t] = *(const uint4*)(arow[t] + k0);
-      a1[t] = *(const uint4*)(arow[t] + k1);
-    }
-    b0lo = *(const uint4*)(brow + k0);
-    b1lo = *(const uint4*)(brow + k1);
-    if (sizeof(T) == 4) {
-      b0hi = *(const uint4*)(brow + k0 + 4);
-      b1hi = *(const uint4*)(brow + k1 + 4);
-    } else {
-      b0hi = b1hi = zero;
-    }
-    uint4 a0hi[MT], a1hi[MT];
+    for (int i = 0; i < DEPTH; ++i) {
+      if (i < cnt) {
+        const int k0 = (base + i) * 32 + fk;
+        skinny_load<T>(br[i], brow, k0, K, bok);
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      if (sizeof(T) == 4) {
-        a0hi[t] = *(const uint4*)(arow[t] + k0 + 4);
-        a1hi[t] = *(const uint4*)(arow[t] + k1 + 4);
-      } else {
-        a0hi[t] = a1hi[t] = zero;
+        for (int t = 0; t < MT; ++t) skinny_load<T>(ar[i][t], arow[t], k0, K, aok[t]);
       }
     }
-    if (!bok) { b0lo = b0hi = b1lo = b1hi = zero; }
-    const Frag<T> fb0 = frag_from<T>(b0lo, b0hi), fb1 = frag_from<T>(b1lo, b1hi);
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const uint4 x0 = aok[t] ? a0[t] : zero, x0h = aok[t] ? a0hi[t] : zero;
-      const uint4 x1 = aok[t] ? a1[t] : zero, x1h = aok[t] ? a1hi[t] : zero;
-      mma(acc[t], frag_from<T>(x0, x0h), fb0);
-      mma(acc[t], frag_from<T>(x1, x1h), fb1);
-    }
-  }
-  for (; ks < ks1; ++ks) {  // remainder (and masked K tail)
-    const int k0 = ks * 32 + fk;
-    const bool kin = k0 < K;
-    const int ck = kin ? k0 : 0;
-    uint4 blo = *(const uint4*)(brow + ck), bhi = zero;
-    if (sizeof(T) == 4 && ck + 4 < K) bhi = *(const uint4*)(brow + ck + 4);
-    if (!bok || !kin) { blo = bhi = zero; }
-    if (kin && k0 + 8 > K) {
-      if (sizeof(T) == 2) blo = mask_tail<T>(blo, K - k0);
-      else { blo = mask_tail<T>(blo, K - k0); bhi = mask_tail<T>(bhi, K - k0 - 4); }
-    }
-    const Frag<T> fb = frag_from<T>(blo, bhi);
+    for (int i = 0; i < DEPTH; ++i) {
+      if (i < cnt) {
+        const Frag<T> fb = frag_from<T>(br[i][0], br[i][H - 1]);
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      uint4 alo = *(const uint4*)(arow[t] + ck), ahi = zero;
-      if (sizeof(T) == 4 && ck + 4 < K) ahi = *(const uint4*)(arow[t] + ck + 4);
-      if (!aok[t] || !kin) { alo = ahi = zero; }
-      if (kin && k0 + 8 > K) {
-        if (sizeof(T) == 2) alo = mask_tail<T>(alo, K - k0);
-        else { alo = mask_tail<T>(alo, K - k0); ahi = mask_tail<T>(ahi, K - k0 - 4); }
+        for (int t = 0; t < MT; ++t) mma(acc[t], frag_from<T>(ar[i][t][0], ar[i][t][H - 1]), fb);
       }
-      mma(acc[t], frag_from<T>(alo, ahi), fb);
     }
   }
 #pragma unroll
@@ -435,7 +413,6 @@ __global__ __launch_bounds__(64 * SW) void gemm_skinny_kernel(const T* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) part[w][t * 16 + 4 * (lane >> 4) + r][fr] = acc[t][r];
   __syncthreads();
-  // reduce the SW partial tiles into part[0]
   for (int e = threadIdx.x; e < MT * 16 * 16; e += 64 * SW) {
     const int r = e / 16, c = e % 16;
     float s = 0.f;
@@ -472,13 +449,20 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
                          long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
                          int vec_ok, hipStream_t st) {
   if (M <= 64 && ak && bk && batch == 1) {
-    dim3 grid((N + 15) / 16);
-    if (M <= 32)
-      hipLaunchKernelGGL((gemm_skinny_kernel<T, 2, 8>), grid, dim3(512), 0, st, (const T*)A, lda, (const T*)B, ldb,
-                         C, ldc, M, N, K, ep, vec_ok);
-    else
-      hipLaunchKernelGGL((gemm_skinny_kernel<T, 4, 8>), grid, dim3(512), 0, st, (const T*)A, lda, (const T*)B, ldb,
-                         C, ldc, M, N, K, ep, vec_ok);
+    const int blocks = (N + 15) / 16;
+    const bool wide = blocks < 96;  // few column blocks: split K over 16 waves instead of 8
+    const T* a = (const T*)A;
+    const T* b = (const T*)B;
+#define SK_(MT, SW, DEPTH)                                                                                   \
+  hipLaunchKernelGGL((gemm_skinny_kernel<T, MT, SW, DEPTH>), dim3(blocks), dim3(64 * SW), 0, st, a, lda, b, ldb, C, \
+                     ldc, M, N, K, ep, vec_ok)
+    constexpr bool F32 = sizeof(T) == 4;
+    if (M <= 32) {
+      if (wide) SK_(2, 16, F32 ? 2 : 4); else SK_(2, 8, F32 ? 2 : 8);
+    } else {
+      if (wide) SK_(4, 16, 2); else SK_(4, 8, F32 ? 2 : 4);
+    }
+#undef SK_
     IMGCAP_CHECK_LAUNCH("imgcap_gemm(skinny)");
     return 0;
   }
@@ -488,21 +472,47 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
   return launch_tiled<T, 128, 128>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
 }
 
-// bias-gradient style column sums: out[c] = beta*out[c] + sum_r x[r, c]
+// bias-gradient style column sums: out[c] = beta*out[c] + sum_r x[r, c].
+// Block = 64 columns (8 vectors of 8) x 32 row lanes; fixed-order LDS reduction (deterministic).
 template <typename T>
-__global__ void colsum_kernel(int rows, int cols, const T* __restrict__ x, long ld, float* __restrict__ out,
-                              float beta) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < cols)
-    for (int r = w; r < rows; r += 4) s += to_f(x[(long)r * ld + c]);
-  red[w][threadIdx.x & 63] = s;
+__global__ __launch_bounds__(256) void colsum_kernel(int rows, int cols, const T* __restrict__ x, long ld,
+                                                     float* __restrict__ out, float beta, int vec_ok) {
+  __shared__ float red[32][65];
+  const int cv = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * 64 + cv * 8;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (vec_ok && c0 + 8 <= cols) {
+    for (int r = rl; r < rows; r += 32) {
+      float v[8];
+      const T* p = x + (long)r * ld + c0;
+      if (sizeof(T) == 2) {
+        const bf16x8 q = *(const bf16x8*)p;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
+      } else {
+        const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
+    }
+  } else {
+    for (int r = rl; r < rows; r += 32)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c0 + j < cols) s[j] += to_f(x[(long)r * ld + c0 + j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cv * 8 + j] = s[j];
   __syncthreads();
-  if (w == 0 && c < cols) {
-    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    out[c] = (beta != 0.f ? beta * out[c] : 0.f) + t;
+  if (threadIdx.x < 64) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    float t = 0.f;
+    for (int i = 0; i < 32; ++i) t += red[i][threadIdx.x];
+    if (c < cols) out[c] = (beta != 0.f ? beta * out[c] : 0.f) + t;
   }
 }
 
@@ -561,12 +571,13 @@ extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64
                              void* stream) {
   if (cols == 0) return 0;
   dim3 grid((cols + 63) / 64);
+  const int vec_ok = aligned16(x) && ldx % 8 == 0;
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const bf16*)x, ldx,
-                       out, beta);
+                       out, beta, vec_ok);
   else
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const float*)x,
-                       ldx, out, beta);
+                       ldx, out, beta, vec_ok);
   IMGCAP_CHECK_LAUNCH("imgcap_colsum");
   return 0;
 }

@@ -220,54 +220,58 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
 
 // ---- attention parameter gradients, summed over all steps at once -----------------------
 //   datt1[b,p,a]  = w_f[a] * sum_t de[b,t,p] [att1[b,p,a] + att2[b,t,a] > 0]
-//   dwf_part[b,a] = sum_{t,p} de[b,t,p] relu(att1[b,p,a] + att2[b,t,a])
-//   dbea_part[b,a] = sum_p datt1[b,p,a]
-// One thread per (b, a); its P att1 values and accumulators stay in registers.
+//   dwf_part[b,c,a]  = sum_{t, p in chunk c} de[b,t,p] relu(att1[b,p,a] + att2[b,t,a])
+//   dbea_part[b,c,a] = sum_{p in chunk c} datt1[b,p,a]
+// Block = (chunk of PCH pixels, batch row); thread = attention unit a; the chunk's att1
+// values and accumulators stay in registers while t sweeps the saved att2 rows.
+constexpr int PCH = 7;
 template <typename T>
-__global__ __launch_bounds__(256) void attn_param_grad_kernel(imgcap_lstm_desc d) {
-  extern __shared__ __attribute__((aligned(16))) float de_s[];  // [T][P]
-  const int b = blockIdx.y;
-  const int a = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(512) void attn_param_grad_kernel(imgcap_lstm_desc d) {
+  extern __shared__ __attribute__((aligned(16))) float de_s[];  // [T][PCH]
+  const int b = blockIdx.y, c = blockIdx.x, nc = gridDim.x;
   const int P = d.P, A = d.A, E = d.E, Tn = d.T;
   const int W3 = A + E + 4 * d.D;
-  for (int i = threadIdx.x; i < Tn * P; i += 256) de_s[i] = d.de[(long)b * Tn * P + i];
-  __syncthreads();
-  if (a >= A) return;
-  const T* att1 = (const T*)d.att1 + (long)b * P * A;
-  float x1[MAXP], acc[MAXP];
-#pragma unroll
-  for (int p = 0; p < MAXP; ++p) {
-    x1[p] = p < P ? to_f(att1[(long)p * A + a]) : 0.f;
-    acc[p] = 0.f;
+  const int p0 = c * PCH;
+  for (int i = threadIdx.x; i < Tn * PCH; i += blockDim.x) {
+    const int t = i / PCH, q = i % PCH;
+    de_s[i] = p0 + q < P ? d.de[((long)b * Tn + t) * P + p0 + q] : 0.f;
   }
-  float swf = 0.f;
+  __syncthreads();
+  const T* att1 = (const T*)d.att1 + (long)b * P * A;
   const int tmax = min(Tn, d.dl[b]);
-  for (int t = 0; t < tmax; ++t) {
-    const float a2 = d.g1[((long)b * Tn + t) * W3 + a];
-    const float* de = de_s + t * P;
+  for (int a = threadIdx.x; a < A; a += blockDim.x) {
+    float x1[PCH], acc[PCH];
 #pragma unroll
-    for (int p = 0; p < MAXP; ++p) {
-      if (p < P) {
-        const float u = x1[p] + a2;
-        const float g = de[p];
-        acc[p] += u > 0.f ? g : 0.f;
+    for (int q = 0; q < PCH; ++q) {
+      x1[q] = p0 + q < P ? to_f(att1[(long)(p0 + q) * A + a]) : 0.f;
+      acc[q] = 0.f;
+    }
+    float swf = 0.f;
+    const float* a2p = d.g1 + (long)b * Tn * W3 + a;
+    for (int t = 0; t < tmax; ++t) {
+      const float a2 = a2p[(long)t * W3];
+#pragma unroll
+      for (int q = 0; q < PCH; ++q) {
+        const float u = x1[q] + a2;
+        const float g = de_s[t * PCH + q];
+        acc[q] += u > 0.f ? g : 0.f;
         swf += g * fmaxf(u, 0.f);
       }
     }
-  }
-  const float wf = d.w_f[a];
-  float sb = 0.f;
-  T* out = (T*)d.datt1 + (long)b * P * A + a;
+    const float wf = d.w_f[a];
+    float sb = 0.f;
+    T* out = (T*)d.datt1 + (long)b * P * A + a;
 #pragma unroll
-  for (int p = 0; p < MAXP; ++p) {
-    if (p < P) {
-      const float v = acc[p] * wf;
-      out[(long)p * A] = from_f<T>(v);
-      sb += v;
+    for (int q = 0; q < PCH; ++q) {
+      if (p0 + q < P) {
+        const float v = acc[q] * wf;
+        out[(long)(p0 + q) * A] = from_f<T>(v);
+        sb += v;
+      }
     }
+    d.dwf[((long)b * nc + c) * A + a] = swf;
+    d.dbea[((long)b * nc + c) * A + a] = sb;
   }
-  d.dwf[(long)b * A + a] = swf;
-  d.dbea[(long)b * A + a] = sb;
 }
 
 // ---- doubly stochastic attention regularisation (train.py:269) --------------------------
@@ -344,8 +348,9 @@ static int lstm_bwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
                      d.dh, d.D, 0, 1, &ep, st);
     if (rc) return rc;
   }
-  const size_t shm2 = (size_t)d.T * d.P * sizeof(float);
-  hipLaunchKernelGGL(attn_param_grad_kernel<T>, dim3((d.A + 255) / 256, d.B), dim3(256), shm2, st, d);
+  const size_t shm2 = (size_t)d.T * PCH * sizeof(float);
+  const int thr = d.A >= 512 ? 512 : ((d.A + 63) / 64) * 64;
+  hipLaunchKernelGGL(attn_param_grad_kernel<T>, dim3((d.P + PCH - 1) / PCH, d.B), dim3(thr), shm2, st, d);
   IMGCAP_CHECK_LAUNCH("lstm attn_param_grad");
   return 0;
 }
@@ -371,7 +376,7 @@ extern "C" int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream) {
 extern "C" int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream) {
   if (int rc = check_desc(d)) return rc;
   IMGCAP_REQUIRE((d->E + 2 * MAXP + 2 * d->A) * 4 <= 65536, "lstm bwd: E/A too large for LDS");
-  IMGCAP_REQUIRE((size_t)d->T * d->P * 4 <= 65536, "lstm bwd: T*P too large for LDS");
+  IMGCAP_REQUIRE((size_t)d->T * PCH * 4 <= 65536, "lstm bwd: T too large for LDS");
   IMGCAP_REQUIRE(d->w_ihz_t && d->w_hcat_t && d->de && d->dbea, "lstm bwd: transposed weights / de / dbea needed");
   if (d->dtype == IMGCAP_BF16) return lstm_bwd_impl<bf16>(*d, (hipStream_t)stream);
   return lstm_bwd_impl<float>(*d, (hipStream_t)stream);

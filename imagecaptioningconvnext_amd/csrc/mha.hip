@@ -1,0 +1,348 @@
+// Masked multi-head attention of nn.TransformerDecoderLayer (transformerDecoder.py:82,104):
+// self-attention (causal + key padding) and cross-attention over the 49 encoder pixels,
+// with attention-probability dropout, forward and backward.
+//
+// Captions are <= 52 tokens and the memory is 49 pixels, so one workgroup owns one
+// (batch, head) pair and keeps the whole problem on-chip: Q/K/V (and dO) tiles padded to 64
+// rows in LDS, S = Q K^T, the masked softmax and P V on MFMA (bf16 16x16x32 or exact-f32
+// 16x16x4); each of the 4 waves owns 16 query rows.  The forward saves the row
+// log-sum-exp; the backward recomputes P from it (no N^2 storage):
+//   dP~ = dO V^T,  dP = dP~ * mask/(1-p),  dS = P (dP - rowsum(P dP)),
+//   dV = P~^T dO,  dQ = scale dS K,  dK = scale dS^T Q.
+// Every MFMA operand is read k-contiguous from LDS; transposed images are written once.
+#include "common.h"
+
+namespace imgcap {
+
+constexpr int HD = 64;   // head dim
+constexpr int LP = 64;   // padded sequence length
+
+template <typename T> struct MFrag;
+template <> struct MFrag<bf16> { bf16x8 v; };
+template <> struct MFrag<float> { f32x4 lo, hi; };
+DEV void mfma16(f32x4& acc, const MFrag<bf16>& a, const MFrag<bf16>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc, 0, 0, 0);
+}
+DEV void mfma16(f32x4& acc, const MFrag<float>& a, const MFrag<float>& b) {
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[kk], b.lo[kk], acc, 0, 0, 0);
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[kk], b.hi[kk], acc, 0, 0, 0);
+}
+template <typename T> DEV MFrag<T> mfrag(const T* p);
+template <> DEV MFrag<bf16> mfrag<bf16>(const bf16* p) { MFrag<bf16> f; f.v = *(const bf16x8*)p; return f; }
+template <> DEV MFrag<float> mfrag<float>(const float* p) {
+  MFrag<float> f; f.lo = *(const f32x4*)p; f.hi = *(const f32x4*)(p + 4); return f;
+}
+
+template <typename T> struct Img {
+  static constexpr int LD = HD + 16 / (int)sizeof(T);  // +16 bytes per row
+  static constexpr int ELEMS = LP * LD;
+};
+
+// C[16 rows of this wave][64 cols] = sum_k A[row][k] * B[col][k]   (both k-contiguous, K = 64)
+template <typename T>
+DEV void wave_mm(f32x4 (&acc)[4], const T* A, const T* Bm, int row0, int lane) {
+  constexpr int LD = Img<T>::LD;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < HD; ks += 32) {
+    const MFrag<T> a = mfrag<T>(A + (row0 + fr) * LD + ks + fk);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mfma16(acc[j], a, mfrag<T>(Bm + (j * 16 + fr) * LD + ks + fk));
+  }
+}
+
+// stage rows [0, L) of a [L][HD] head slice (row stride ld) into an LDS image; rows >= L zero
+template <typename T>
+DEV void stage_rows(T* img, const T* src, long ld, int L) {
+  constexpr int LD = Img<T>::LD, VEC = 16 / sizeof(T);
+  for (int e = threadIdx.x; e < LP * (HD / VEC); e += blockDim.x) {
+    const int r = e / (HD / VEC), c = (e % (HD / VEC)) * VEC;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r < L) v = *(const uint4*)(src + (long)r * ld + c);
+    *(uint4*)(img + r * LD + c) = v;
+  }
+}
+// transposed image: img[c][r] = src row r, column c
+template <typename T>
+DEV void stage_rows_t(T* img, const T* src, long ld, int L) {
+  constexpr int LD = Img<T>::LD;
+  for (int e = threadIdx.x; e < LP * HD; e += blockDim.x) {
+    const int r = e / HD, c = e % HD;
+    img[c * LD + r] = r < L ? src[(long)r * ld + c] : from_f<T>(0.f);
+  }
+}
+// transpose an LDS image
+template <typename T>
+DEV void lds_transpose(T* dst, const T* src) {
+  constexpr int LD = Img<T>::LD;
+  for (int e = threadIdx.x; e < LP * HD; e += blockDim.x) {
+    const int r = e / HD, c = e % HD;
+    dst[c * LD + r] = src[r * LD + c];
+  }
+}
+
+DEV float row_max16(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+DEV float row_sum16(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+DEV bool key_masked(const imgcap_mha_desc& d, int b, int i, int j) {
+  if (j >= d.Lk) return true;
+  if (d.causal && j > i) return true;
+  if (d.key_ids && d.key_ids[(long)b * d.Lk + j] == d.pad_id) return true;
+  return false;
+}
+
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void mha_fwd_kernel(imgcap_mha_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int LD = Img<T>::LD;
+  T* Qs = (T*)smem;
+  T* Ks = Qs + Img<T>::ELEMS;   // reused for P~ after S is done
+  T* Vt = Ks + Img<T>::ELEMS;
+  const int bh = blockIdx.x, b = bh / d.H, h = bh % d.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const T* q = (const T*)d.q + (long)b * d.Lq * d.ldq + h * HD;
+  const T* k = (const T*)d.k + (long)b * d.Lk * d.ldk + h * HD;
+  const T* v = (const T*)d.v + (long)b * d.Lk * d.ldv + h * HD;
+  stage_rows<T>(Qs, q, d.ldq, d.Lq);
+  stage_rows<T>(Ks, k, d.ldk, d.Lk);
+  stage_rows_t<T>(Vt, v, d.ldv, d.Lk);
+  __syncthreads();
+  f32x4 s[4];
+  const int row0 = w * 16;
+  wave_mm<T>(s, Qs, Ks, row0, lane);
+  // masked, scaled, row softmax in registers: lane holds rows row0+4*(lane>>4)+r, cols j*16+(lane&15)
+  float lse_r[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = row0 + 4 * (lane >> 4) + r;
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = j * 16 + (lane & 15);
+      const float x = key_masked(d, b, i, col) ? -INFINITY : s[j][r] * d.scale;
+      s[j][r] = x;
+      m = fmaxf(m, x);
+    }
+    m = row_max16(m);
+    if (m == -INFINITY) m = 0.f;
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float e = __expf(s[j][r] - m);
+      s[j][r] = e;
+      sum += e;
+    }
+    sum = row_sum16(sum);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    lse_r[r] = m + logf(sum > 0.f ? sum : 1.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = j * 16 + (lane & 15);
+      float p = s[j][r] * inv;
+      if (d.drop_p > 0.f && i < d.Lq && col < d.Lk)
+        p *= dropout_scale(d.seed, d.drop_stream, (((uint64_t)bh * d.Lq + i) * d.Lk + col), d.drop_p);
+      s[j][r] = p;
+    }
+  }
+  __syncthreads();  // everyone is done reading Ks: reuse it for P~
+  T* Ps = Ks;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Ps[(row0 + 4 * (lane >> 4) + r) * LD + j * 16 + (lane & 15)] = from_f<T>(s[j][r]);
+  __syncthreads();
+  f32x4 o[4];
+  wave_mm<T>(o, Ps, Vt, row0, lane);
+  T* out = (T*)d.o + (long)b * d.Lq * d.ldo + h * HD;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = row0 + 4 * (lane >> 4) + r;
+    if (i < d.Lq) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[(long)i * d.ldo + j * 16 + (lane & 15)] = from_f<T>(o[j][r]);
+      if ((lane & 15) == 0) d.lse[(long)bh * d.Lq + i] = lse_r[r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void mha_bwd_kernel(imgcap_mha_desc d) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int LD = Img<T>::LD;
+  constexpr int NE = Img<T>::ELEMS;
+  T* Qs = (T*)smem;
+  T* Ks = Qs + NE;
+  T* Vs = Ks + NE;
+  T* dOs = Vs + NE;
+  T* X1 = dOs + NE;
+  T* X2 = X1 + NE;
+  const int bh = blockIdx.x, b = bh / d.H, h = bh % d.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const T* q = (const T*)d.q + (long)b * d.Lq * d.ldq + h * HD;
+  const T* k = (const T*)d.k + (long)b * d.Lk * d.ldk + h * HD;
+  const T* v = (const T*)d.v + (long)b * d.Lk * d.ldv + h * HD;
+  const T* dO = (const T*)d.dout + (long)b * d.Lq * d.lddo + h * HD;
+  stage_rows<T>(Qs, q, d.ldq, d.Lq);
+  stage_rows<T>(Ks, k, d.ldk, d.Lk);
+  stage_rows<T>(Vs, v, d.ldv, d.Lk);
+  stage_rows<T>(dOs, dO, d.lddo, d.Lq);
+  __syncthreads();
+  const int row0 = w * 16;
+  f32x4 p[4], dp[4];
+  wave_mm<T>(p, Qs, Ks, row0, lane);    // S
+  wave_mm<T>(dp, dOs, Vs, row0, lane);  // dP~ = dO V^T
+  // P from the saved lse; P~ = P * mask; dP = dP~ * mask; dS = P (dP - rowsum(P dP))
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = row0 + 4 * (lane >> 4) + r;
+    const float lse = i < d.Lq ? d.lse[(long)bh * d.Lq + i] : 0.f;
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = j * 16 + (lane & 15);
+      const bool masked = i >= d.Lq || key_masked(d, b, i, col);
+      const float pr = masked ? 0.f : __expf(p[j][r] * d.scale - lse);
+      const float ms = (d.drop_p > 0.f && !masked)
+                           ? dropout_scale(d.seed, d.drop_stream, (((uint64_t)bh * d.Lq + i) * d.Lk + col), d.drop_p)
+                           : 1.f;
+      const float dpv = dp[j][r] * ms;
+      dot += pr * dpv;
+      p[j][r] = pr;         // P (pre-dropout) for now
+      dp[j][r] = dpv;       // dP
+    }
+    dot = row_sum16(dot);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = j * 16 + (lane & 15);
+      const float pr = p[j][r];
+      dp[j][r] = pr * (dp[j][r] - dot);  // dS
+      const bool masked = i >= d.Lq || key_masked(d, b, i, col);
+      const float ms = (d.drop_p > 0.f && !masked)
+                           ? dropout_scale(d.seed, d.drop_stream, (((uint64_t)bh * d.Lq + i) * d.Lk + col), d.drop_p)
+                           : 1.f;
+      p[j][r] = pr * ms;                 // P~
+    }
+  }
+  // ---- dV = P~^T dO ----
+  // X1[j][i] = P~[i][j]; X2[c][i] = dO[i][c]
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) X1[(j * 16 + (lane & 15)) * LD + row0 + 4 * (lane >> 4) + r] = from_f<T>(p[j][r]);
+  lds_transpose<T>(X2, dOs);
+  __syncthreads();
+  f32x4 acc[4];
+  wave_mm<T>(acc, X1, X2, row0, lane);
+  {
+    T* dv = (T*)d.dv + (long)b * d.Lk * d.lddv + h * HD;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = row0 + 4 * (lane >> 4) + r;
+      if (j < d.Lk)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dv[(long)j * d.lddv + c * 16 + (lane & 15)] = from_f<T>(acc[c][r]);
+    }
+  }
+  __syncthreads();
+  // ---- dK = scale dS^T Q ----
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) X1[(j * 16 + (lane & 15)) * LD + row0 + 4 * (lane >> 4) + r] = from_f<T>(dp[j][r]);
+  lds_transpose<T>(X2, Qs);
+  __syncthreads();
+  wave_mm<T>(acc, X1, X2, row0, lane);
+  {
+    T* dk = (T*)d.dk + (long)b * d.Lk * d.lddk + h * HD;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = row0 + 4 * (lane >> 4) + r;
+      if (j < d.Lk)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dk[(long)j * d.lddk + c * 16 + (lane & 15)] = from_f<T>(acc[c][r] * d.scale);
+    }
+  }
+  __syncthreads();
+  // ---- dQ = scale dS K ----
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) X1[(row0 + 4 * (lane >> 4) + r) * LD + j * 16 + (lane & 15)] = from_f<T>(dp[j][r]);
+  lds_transpose<T>(X2, Ks);
+  __syncthreads();
+  wave_mm<T>(acc, X1, X2, row0, lane);
+  {
+    T* dq = (T*)d.dq + (long)b * d.Lq * d.lddq + h * HD;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = row0 + 4 * (lane >> 4) + r;
+      if (i < d.Lq)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dq[(long)i * d.lddq + c * 16 + (lane & 15)] = from_f<T>(acc[c][r] * d.scale);
+    }
+  }
+}
+
+static int check(const imgcap_mha_desc* d) {
+  IMGCAP_REQUIRE(d != nullptr, "mha desc NULL");
+  IMGCAP_REQUIRE(d->dh == HD, "mha: head dim must be 64");
+  IMGCAP_REQUIRE(d->Lq > 0 && d->Lq <= LP && d->Lk > 0 && d->Lk <= LP, "mha: sequence lengths must be in [1, 64]");
+  const int vec = d->dtype == IMGCAP_F32 ? 4 : 8;
+  IMGCAP_REQUIRE(d->ldq % vec == 0 && d->ldk % vec == 0 && d->ldv % vec == 0 && aligned16(d->q) && aligned16(d->k) &&
+                     aligned16(d->v),
+                 "mha: q/k/v must be 16-byte aligned with 16-byte row strides");
+  return 0;
+}
+
+}  // namespace imgcap
+
+using namespace imgcap;
+
+extern "C" int imgcap_mha_fwd(const imgcap_mha_desc* d, void* stream) {
+  if (int rc = check(d)) return rc;
+  const dim3 grid(d->B * d->H);
+  if (d->dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(mha_fwd_kernel<bf16>, grid, dim3(256), 3 * Img<bf16>::ELEMS * sizeof(bf16),
+                       (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(mha_fwd_kernel<float>, grid, dim3(256), 3 * Img<float>::ELEMS * sizeof(float),
+                       (hipStream_t)stream, *d);
+  IMGCAP_CHECK_LAUNCH("imgcap_mha_fwd");
+  return 0;
+}
+
+extern "C" int imgcap_mha_bwd(const imgcap_mha_desc* d, void* stream) {
+  if (int rc = check(d)) return rc;
+  const int vec = d->dtype == IMGCAP_F32 ? 4 : 8;
+  IMGCAP_REQUIRE(d->lddo % vec == 0 && aligned16(d->dout), "mha bwd: dout alignment");
+  const dim3 grid(d->B * d->H);
+  static bool attr_set = false;
+  if (!attr_set) {  // the f32 backward needs > 64 KiB of dynamic LDS
+    if (hipFuncSetAttribute((const void*)mha_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            6 * Img<float>::ELEMS * sizeof(float)) != hipSuccess)
+      return fail(IMGCAP_EINVAL, "mha bwd: cannot raise the LDS limit");
+    attr_set = true;
+  }
+  if (d->dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(mha_bwd_kernel<bf16>, grid, dim3(256), 6 * Img<bf16>::ELEMS * sizeof(bf16),
+                       (hipStream_t)stream, *d);
+  else
+    hipLaunchKernelGGL(mha_bwd_kernel<float>, grid, dim3(256), 6 * Img<float>::ELEMS * sizeof(float),
+                       (hipStream_t)stream, *d);
+  IMGCAP_CHECK_LAUNCH("imgcap_mha_bwd");
+  return 0;
+}

@@ -187,7 +187,8 @@ class LstmEngine:
         dz, dh, dc = torch.empty(B, E, **f32), torch.empty(B, D, **f32), torch.empty(B, D, **f32)
         de = torch.empty(B, T, P, **f32)
         datt1 = torch.empty(B * P, A, device=dev, dtype=ct)
-        dwf, dbea = torch.empty(B, A, **f32), torch.empty(B, A, **f32)
+        npc = (P + 6) // 7  # pixel chunks of attn_param_grad_kernel
+        dwf, dbea = torch.empty(B * npc, A, **f32), torch.empty(B * npc, A, **f32)
         # k-major copies of the two weights the backward recurrence multiplies by
         wihz_t = K.transpose(w["wih"][:, M:])            # [E, 4D]
         whcat_t = K.transpose(w["hcat"])                 # [D, W3]

@@ -1,0 +1,253 @@
+"""Explicit forward/backward engine of the teacher-forced Transformer decoder on HIP.
+
+Mirrors TransformerDecoder.forwardWithTeacherForcing (models/transformerDecoder.py:88-108)
+with torch.nn.TransformerDecoderLayer's post-norm math (norm_first=False, ReLU FFN,
+dropout after the embedding, on the attention probabilities, on each sublayer output and
+inside the FFN), plus the packed CE of train.py:271-276.
+
+Kernels per layer (forward): in-proj GEMM -> MHA (causal + key padding) -> out-proj GEMM ->
+add+dropout+LN -> q GEMM / kv GEMM on the memory -> MHA -> out-proj -> add+LN -> FFN GEMM
+(+bias, ReLU, dropout in the epilogue) -> GEMM -> add+LN.  Rows are batch-major [B*L, d]
+(the reference is seq-first; the permutes at transformerDecoder.py:95,99,105 are free here).
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _abi
+from . import kernels as K
+from .flat import FlatParams
+
+# dropout stream ids (each site gets its own counter-based mask stream)
+_S_EMB = 1
+
+
+def _s(layer, site):
+    return 100 + 16 * layer + site
+
+
+def transformer_param_groups(dec):
+    n = dict(dec.named_parameters())
+    groups = []
+    for k in n:
+        groups.append([k])
+    return [[(k, n[k]) for k in g] for g in groups]
+
+
+class TransformerEngine:
+    def __init__(self, dec, device, compute_dtype=torch.bfloat16):
+        self.dec = dec
+        self.ct = compute_dtype
+        self.fp = FlatParams(transformer_param_groups(dec), device, compute_dtype)
+        self.d = dec.embed_dim
+        self.H = dec.num_heads
+        self.ff = dec.decoder_dim
+        self.V = dec.vocab_size
+        self.E = dec.encoder_dim
+        self.layers = dec.num_layers
+        self.Vpad = (self.V + 7) // 8 * 8
+        self.has_proj = "encoder_proj.weight" in self.fp.params
+        if self.d // self.H != 64:
+            raise NotImplementedError("the HIP attention kernel needs head dim 64 (embed_dim = 64 * num_heads)")
+        self.seed = 4321
+        self.step_id = 0
+
+    def _lw(self, i, name):
+        return f"transformer_decoder.layers.{i}.{name}"
+
+    def _mha(self, *, B, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, causal, key_ids, pad_id, p, seed, sid,
+             dout=None, lddo=0, dq=None, lddq=0, dk=None, lddk=0, dv=None, lddv=0, bwd=False):
+        m = _abi.MhaDesc()
+        m.dtype, m.B, m.H, m.Lq, m.Lk, m.dh, m.causal = K.dt(q), B, self.H, Lq, Lk, 64, int(causal)
+        m.pad_id = pad_id
+        m.ldq, m.ldk, m.ldv, m.ldo = ldq, ldk, ldv, ldo
+        m.q, m.k, m.v, m.o, m.lse = q.data_ptr(), k.data_ptr(), v.data_ptr(), K.ptr(o), lse.data_ptr()
+        m.key_ids = K.ptr(key_ids)
+        m.scale = 1.0 / math.sqrt(64.0)
+        m.drop_p, m.seed, m.drop_stream = p, seed, sid
+        if bwd:
+            m.dout, m.lddo = dout.data_ptr(), lddo
+            m.dq, m.dk, m.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+            m.lddq, m.lddk, m.lddv = lddq, lddk, lddv
+            _abi.call("imgcap_mha_bwd", ctypes.byref(m), K.stream())
+        else:
+            _abi.call("imgcap_mha_fwd", ctypes.byref(m), K.stream())
+
+    # ---------------------------------------------------------------------------------------
+    def forward(self, encoder_out, encoded_captions, caption_lengths, *, key_ids=None, pad_id=0, dropout=None,
+                loss=True):
+        fp, ct, dev = self.fp, self.ct, encoder_out.device
+        d, ff, V = self.d, self.ff, self.V
+        p = self.dec.dropout_p if (dropout is None and self.dec.training) else (dropout or 0.0)
+        B = encoder_out.size(0)
+        enc = encoder_out.reshape(B, -1, self.E).to(ct).contiguous()
+        P = enc.size(1)
+        L = encoded_captions.size(1)
+        caps = encoded_captions.contiguous()
+        if key_ids is None:
+            key_ids = caps
+        seed = self.seed + 7919 * self.step_id
+        self.step_id += 1
+        s = dict(B=B, P=P, L=L, p=p, seed=seed, enc=enc, caps=caps, key_ids=key_ids, pad_id=pad_id, layers=[])
+        ctd = dict(device=dev, dtype=ct)
+        f32 = dict(device=dev, dtype=torch.float32)
+        BL, BP = B * L, B * P
+        # memory = encoder_proj(encoder_out)                                  transformerDecoder.py:95
+        if self.has_proj:
+            mem = K.gemm(enc.view(BP, self.E), fp.w("encoder_proj.weight"), trans_b=True,
+                         bias=fp.f32("encoder_proj.bias"))
+        else:
+            mem = enc.view(BP, d)
+        # tgt = pos_encoding(dropout(embedding(caps)))                       :97-98
+        x = torch.empty(BL, d, **ctd)
+        K.embedding_fwd(caps.view(-1), fp.f32("embedding.weight"), x, pe=self.dec.pos_encoding.pe.view(-1, d)[:L]
+                        .contiguous().float(), L=L, drop_p=p, seed=seed, drop_stream=_S_EMB)
+        s["x0"] = x
+        for i in range(self.layers):
+            lw = lambda n: self._lw(i, n)  # noqa: E731
+            st = {"x": x}
+            qkv = K.gemm(x, fp.w(lw("self_attn.in_proj_weight")), trans_b=True, bias=fp.f32(lw("self_attn.in_proj_bias")))
+            o = torch.empty(BL, d, **ctd)
+            lse1 = torch.empty(B, self.H, L, **f32)
+            self._mha(B=B, Lq=L, Lk=L, q=qkv, ldq=3 * d, k=qkv[:, d:], ldk=3 * d, v=qkv[:, 2 * d:], ldv=3 * d, o=o,
+                      ldo=d, lse=lse1, causal=True, key_ids=key_ids, pad_id=pad_id, p=p, seed=seed, sid=_s(i, 0))
+            y = K.gemm(o, fp.w(lw("self_attn.out_proj.weight")), trans_b=True, bias=fp.f32(lw("self_attn.out_proj.bias")))
+            s1 = torch.empty(BL, d, **ctd)
+            x1, mu1, rs1 = K.add_layernorm(x, y, fp.f32(lw("norm1.weight")), fp.f32(lw("norm1.bias")), 1e-5,
+                                           drop_p=p, seed=seed, drop_stream=_s(i, 1), s_out=s1)
+            wq = fp.w(lw("multihead_attn.in_proj_weight"))
+            bq = fp.f32(lw("multihead_attn.in_proj_bias"))
+            q2 = K.gemm(x1, wq[:d], trans_b=True, bias=bq[:d])
+            kv2 = K.gemm(mem, wq[d:], trans_b=True, bias=bq[d:])
+            o2 = torch.empty(BL, d, **ctd)
+            lse2 = torch.empty(B, self.H, L, **f32)
+            self._mha(B=B, Lq=L, Lk=P, q=q2, ldq=d, k=kv2, ldk=2 * d, v=kv2[:, d:], ldv=2 * d, o=o2, ldo=d, lse=lse2,
+                      causal=False, key_ids=None, pad_id=0, p=p, seed=seed, sid=_s(i, 2))
+            y2 = K.gemm(o2, fp.w(lw("multihead_attn.out_proj.weight")), trans_b=True,
+                        bias=fp.f32(lw("multihead_attn.out_proj.bias")))
+            s2 = torch.empty(BL, d, **ctd)
+            x2, mu2, rs2 = K.add_layernorm(x1, y2, fp.f32(lw("norm2.weight")), fp.f32(lw("norm2.bias")), 1e-5,
+                                           drop_p=p, seed=seed, drop_stream=_s(i, 3), s_out=s2)
+            hdn = K.gemm(x2, fp.w(lw("linear1.weight")), trans_b=True, bias=fp.f32(lw("linear1.bias")),
+                         act=K.ACT_RELU, drop_p=p, seed=seed, drop_stream=_s(i, 4))
+            y3 = K.gemm(hdn, fp.w(lw("linear2.weight")), trans_b=True, bias=fp.f32(lw("linear2.bias")))
+            s3 = torch.empty(BL, d, **ctd)
+            x3, mu3, rs3 = K.add_layernorm(x2, y3, fp.f32(lw("norm3.weight")), fp.f32(lw("norm3.bias")), 1e-5,
+                                           drop_p=p, seed=seed, drop_stream=_s(i, 5), s_out=s3)
+            st.update(qkv=qkv, o=o, lse1=lse1, s1=s1, mu1=mu1, rs1=rs1, x1=x1, q2=q2, kv2=kv2, o2=o2, lse2=lse2,
+                      s2=s2, mu2=mu2, rs2=rs2, x2=x2, hdn=hdn, s3=s3, mu3=mu3, rs3=rs3)
+            s["layers"].append(st)
+            x = x3
+        s["mem"] = mem
+        s["xL"] = x
+        dl = (caption_lengths.reshape(-1) - 1).to(torch.int64)
+        tmask = torch.arange(L, device=dev).view(1, L) < dl.view(B, 1)
+        s["tmask"] = tmask
+        if loss:
+            logits = torch.empty(BL, self.Vpad, **ctd)
+            K.gemm(x, fp.w("fc_out.weight"), trans_b=True, bias=fp.f32("fc_out.bias"), out=logits, N=V)
+            nxt = torch.cat([caps[:, 1:], caps[:, :1]], dim=1)  # target of position l is caps[:, l+1]
+            targets = torch.where(tmask, nxt, torch.full_like(nxt, -1)).reshape(-1)
+            lse = torch.empty(BL, **f32)
+            lrow = torch.empty(BL, **f32)
+            hit = torch.empty(BL, **f32)
+            K.ce_fwd(logits, targets, V, lse, lrow, hit)
+            metrics = torch.empty(4, **f32)
+            K.loss_finalize(lrow, hit, targets, None, metrics)
+            s.update(logits=logits, targets=targets, lse=lse, metrics=metrics)
+        return s
+
+    def predictions(self, s):
+        """transformerDecoder.py:106: fc_out over all L positions -> [B, L, V] fp32."""
+        B, L = s["B"], s["L"]
+        out = K.gemm(s["xL"], self.fp.w("fc_out.weight"), trans_b=True, bias=self.fp.f32("fc_out.bias"),
+                     out_dtype=torch.float32)
+        return out.view(B, L, self.V)
+
+    # ---------------------------------------------------------------------------------------
+    def backward(self, s, dlogits=None, gbuf=None, want_denc=False):
+        fp, ct = self.fp, self.ct
+        gbuf = fp.grad if gbuf is None else gbuf
+        G = lambda name, shape=None, count=None: fp.g(name, shape, count, buf=gbuf)  # noqa: E731
+        B, L, P, p, seed = s["B"], s["L"], s["P"], s["p"], s["seed"]
+        d, V = self.d, self.V
+        BL, BP = B * L, B * P
+        dev = s["xL"].device
+        gbuf.zero_()
+        if dlogits is None:
+            dlogits = torch.empty(BL, self.Vpad, device=dev, dtype=ct)
+            K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
+        K.gemm(dlogits, s["xL"], trans_a=True, out=G("fc_out.weight"), M=V)
+        K.colsum(dlogits, G("fc_out.bias"), cols=V)
+        dx = K.gemm(dlogits, fp.w("fc_out.weight"), K=V)                    # [BL, d]
+        dmem = torch.zeros(BP, d, device=dev, dtype=torch.float32)
+        for i in reversed(range(self.layers)):
+            lw = lambda n: self._lw(i, n)  # noqa: E731
+            st = s["layers"][i]
+            # x3 = LN3(x2 + drop(y3))
+            dy3 = torch.empty_like(dx)
+            ds3 = K.add_layernorm_bwd(dx, st["s3"], st["mu3"], st["rs3"], fp.f32(lw("norm3.weight")),
+                                      G(lw("norm3.weight")), G(lw("norm3.bias")), drop_p=p, seed=seed,
+                                      drop_stream=_s(i, 5), dr=dy3)
+            # y3 = hdn W2^T + b2 ; hdn = drop(relu(x2 W1^T + b1))
+            K.gemm(dy3, st["hdn"], trans_a=True, out=G(lw("linear2.weight")))
+            K.colsum(dy3, G(lw("linear2.bias")))
+            dpre = K.gemm(dy3, fp.w(lw("linear2.weight")), aux=st["hdn"], aux_scale=1.0 / (1.0 - p))
+            K.gemm(dpre, st["x2"], trans_a=True, out=G(lw("linear1.weight")))
+            K.colsum(dpre, G(lw("linear1.bias")))
+            K.gemm(dpre, fp.w(lw("linear1.weight")), out=ds3, beta=1.0)      # dx2 = ds3 + dpre W1
+            # x2 = LN2(x1 + drop(y2))
+            dy2 = torch.empty_like(dx)
+            ds2 = K.add_layernorm_bwd(ds3, st["s2"], st["mu2"], st["rs2"], fp.f32(lw("norm2.weight")),
+                                      G(lw("norm2.weight")), G(lw("norm2.bias")), drop_p=p, seed=seed,
+                                      drop_stream=_s(i, 3), dr=dy2)
+            K.gemm(dy2, st["o2"], trans_a=True, out=G(lw("multihead_attn.out_proj.weight")))
+            K.colsum(dy2, G(lw("multihead_attn.out_proj.bias")))
+            do2 = K.gemm(dy2, fp.w(lw("multihead_attn.out_proj.weight")))
+            dq2 = torch.empty(BL, d, device=dev, dtype=ct)
+            dkv2 = torch.empty(BP, 2 * d, device=dev, dtype=ct)
+            self._mha(B=B, Lq=L, Lk=P, q=st["q2"], ldq=d, k=st["kv2"], ldk=2 * d, v=st["kv2"][:, d:], ldv=2 * d,
+                      o=None, ldo=d, lse=st["lse2"], causal=False, key_ids=None, pad_id=0, p=p, seed=seed,
+                      sid=_s(i, 2), dout=do2, lddo=d, dq=dq2, lddq=d, dk=dkv2, lddk=2 * d, dv=dkv2[:, d:],
+                      lddv=2 * d, bwd=True)
+            gw = G(lw("multihead_attn.in_proj_weight"))
+            gb = G(lw("multihead_attn.in_proj_bias"))
+            wq = fp.w(lw("multihead_attn.in_proj_weight"))
+            K.gemm(dq2, st["x1"], trans_a=True, out=gw[:d])
+            K.colsum(dq2, gb[:d])
+            K.gemm(dkv2, s["mem"], trans_a=True, out=gw[d:])
+            K.colsum(dkv2, gb[d:])
+            K.gemm(dkv2, wq[d:], out=dmem, beta=1.0)                          # dmem += dkv2 W_kv
+            K.gemm(dq2, wq[:d], out=ds2, beta=1.0)                            # dx1 = ds2 + dq2 W_q
+            # x1 = LN1(x + drop(y))
+            dy = torch.empty_like(dx)
+            ds1 = K.add_layernorm_bwd(ds2, st["s1"], st["mu1"], st["rs1"], fp.f32(lw("norm1.weight")),
+                                      G(lw("norm1.weight")), G(lw("norm1.bias")), drop_p=p, seed=seed,
+                                      drop_stream=_s(i, 1), dr=dy)
+            K.gemm(dy, st["o"], trans_a=True, out=G(lw("self_attn.out_proj.weight")))
+            K.colsum(dy, G(lw("self_attn.out_proj.bias")))
+            do = K.gemm(dy, fp.w(lw("self_attn.out_proj.weight")))
+            dqkv = torch.empty(BL, 3 * d, device=dev, dtype=ct)
+            qkv = st["qkv"]
+            self._mha(B=B, Lq=L, Lk=L, q=qkv, ldq=3 * d, k=qkv[:, d:], ldk=3 * d, v=qkv[:, 2 * d:], ldv=3 * d,
+                      o=None, ldo=d, lse=st["lse1"], causal=True, key_ids=s["key_ids"], pad_id=s["pad_id"], p=p,
+                      seed=seed, sid=_s(i, 0), dout=do, lddo=d, dq=dqkv, lddq=3 * d, dk=dqkv[:, d:], lddk=3 * d,
+                      dv=dqkv[:, 2 * d:], lddv=3 * d, bwd=True)
+            K.gemm(dqkv, st["x"], trans_a=True, out=G(lw("self_attn.in_proj_weight")))
+            K.colsum(dqkv, G(lw("self_attn.in_proj_bias")))
+            K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
+            dx = ds1
+        # embedding (dropout mask recomputed; PE has no parameters)
+        K.embedding_bwd(s["caps"].view(-1), dx, G("embedding.weight"), drop_p=p, seed=seed, drop_stream=_S_EMB)
+        denc = None
+        if self.has_proj:
+            dmem_c = dmem.to(ct)
+            K.gemm(dmem_c, s["enc"].view(BP, self.E), trans_a=True, out=G("encoder_proj.weight"))
+            K.colsum(dmem, G("encoder_proj.bias"))
+            if want_denc:
+                denc = K.gemm(dmem_c, fp.w("encoder_proj.weight")).view(B, P, self.E)
+        elif want_denc:
+            denc = dmem.to(ct).view(B, P, d)
+        s["denc"] = denc
+        return gbuf

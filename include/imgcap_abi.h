@@ -185,8 +185,8 @@ typedef struct imgcap_lstm_desc {
   float* dc;            /* [B, D] out: dL/dc0                       */
   float* de;            /* [B, T, P] workspace: dL/d(attention score) */
   void* datt1;          /* [B, P, A] out: sum_t dL/datt1 (dtype)    */
-  float* dwf;           /* [B, A] out: per-row partial of dL/dw_f   */
-  float* dbea;          /* [B, A] out: per-row partial of dL/db_ea  */
+  float* dwf;           /* [B*ceil(P/7), A] out: partials of dL/dw_f  */
+  float* dbea;          /* [B*ceil(P/7), A] out: partials of dL/db_ea */
 } imgcap_lstm_desc;
 
 int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream);
@@ -195,6 +195,39 @@ int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream);
  * dalpha[b,t,p] = d reg / d alpha[b,t,p] (0 where t >= dl[b]) */
 int imgcap_attn_reg(int B, int T, int P, const float* alphas, const int32_t* dl, float alphaC, float* dalpha,
                     float* reg_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Multi-head attention of nn.TransformerDecoderLayer (transformerDecoder.py:82,104): one
+ * workgroup per (batch, head), head dim 64, Lq, Lk <= 64.  q/k/v/o are row-major [B*L, ld]
+ * activations with head h at column offset h*64 (the packed in_proj output can be passed
+ * directly).  Masks: causal (key j > query i), key padding (key_ids[b, j] == pad_id).
+ * Dropout p on the attention probabilities (nn.MultiheadAttention dropout).
+ * fwd saves lse[B, H, Lq]; bwd recomputes P from it and writes dq, dk, dv.
+ * -------------------------------------------------------------------------------------- */
+typedef struct imgcap_mha_desc {
+  int32_t dtype, B, H, Lq, Lk, dh, causal;
+  int64_t pad_id;
+  int64_t ldq, ldk, ldv, ldo;
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;
+  const int64_t* key_ids;
+  float scale;
+  float drop_p;
+  uint64_t seed;
+  uint32_t drop_stream;
+  const void* dout;
+  int64_t lddo;
+  void* dq;
+  void* dk;
+  void* dv;
+  int64_t lddq, lddk, lddv;
+} imgcap_mha_desc;
+
+int imgcap_mha_fwd(const imgcap_mha_desc* d, void* stream);
+int imgcap_mha_bwd(const imgcap_mha_desc* d, void* stream);
 
 /* y = x * dropmask(seed, stream, i) (nn.Dropout, decoder.py:144 / transformer dropouts) */
 int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint64_t seed, uint32_t drop_stream, void* y,

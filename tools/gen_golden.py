@@ -243,13 +243,40 @@ def gen_transformer_full():
 
 def main():
     os.makedirs(GOLDEN_DIR, exist_ok=True)
-    for fn in (gen_lstm_small, gen_transformer_small, gen_ddp2, gen_lstm_full, gen_transformer_full):
+    for fn in (gen_lstm_small, gen_transformer_small, gen_ddp2, gen_lstm_full, gen_transformer_full,
+               gen_transformer_h64):
         name, tensors, meta = fn()
         save_file({k: v.detach().contiguous() for k, v in tensors.items()},
                   os.path.join(GOLDEN_DIR, name + ".safetensors"))
         with open(os.path.join(GOLDEN_DIR, name + ".json"), "w") as f:
             json.dump(meta, f, indent=1)
         print("wrote", name, sum(v.numel() for v in tensors.values()), "values")
+
+
+
+
+TRF_H64 = dict(B=3, L=12, caplens=[12, 7, 9], V=50, E=48, d=64, ff=32, H=1, layers=2, S=2, seed=55)
+
+
+def gen_transformer_h64():
+    """Head dim 64 (the HIP attention kernel's tile); params regenerated from the recipe at test time."""
+    cfg = TRF_H64
+    dec = _transformer_decoder(cfg)
+    enc, caps, caplens = _inputs(cfg)
+    r = transformer_loss(dec, enc, caps, caplens)
+    r["loss"].backward()
+    grads = _grads(dec)
+    tr = _train_module(False)
+    tr.wordMap = word_map(cfg["V"])
+    dec2 = _transformer_decoder(cfg)
+    (loss_avg, top5, _, _), post = _run_ref_train_step(tr, dec2, enc, caps, caplens, False)
+    t = dict(enc=enc, caps=caps, caplens=caplens, predictions=r["scores"].detach(), loss=r["loss"].detach().view(1),
+             ref_step_loss=torch.tensor([loss_avg]), ref_step_top5=torch.tensor([top5]))
+    t.update(grads)
+    t.update(post)
+    meta = dict(cfg=cfg, decode_lengths=r["dls"], source="transformerDecoder.py:88-108; train.py:240-302",
+                note="params: tests/golden_util.make_params(named_shapes, cfg.seed); not stored")
+    return "transformer_tf_h64", t, meta
 
 
 if __name__ == "__main__":
