@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
 
@@ -147,7 +148,7 @@ def main():
     torch.manual_seed(42 + rank)
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
     enc, dec = build(cfg, device)
-    trainer = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm")
+    trainer = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm", graph=not args.no_graph)
     B = cfg["batch"]
     batches = [synthetic_batch(B, rank, i, device) for i in range(4)]
     for i in range(args.warmup):

@@ -46,6 +46,8 @@ class MhaDesc(ctypes.Structure):
 # name -> argtypes  (every entry point declared in include/imgcap_abi.h)
 _SIGS = {
     "imgcap_version": [],
+    "imgcap_set_seed_counter": [c_void_p],
+    "imgcap_stochastic_depth_scales": [c_int, c_int, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p],
     "imgcap_gemm": [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                     c_int64, c_void_p, c_int64, c_int64, c_int, ctypes.POINTER(Epilogue), c_void_p],
     "imgcap_transpose": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p],

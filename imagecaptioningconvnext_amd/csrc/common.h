@@ -50,6 +50,34 @@ DEV void store_from_f(void* p, long i, int dtype, float v) {
   if (dtype == IMGCAP_F32) ((float*)p)[i] = v; else ((bf16*)p)[i] = (bf16)v;
 }
 
+// G consecutive elements as floats; one 16-byte access when G*sizeof(T) == 16 (caller
+// guarantees alignment), element-wise otherwise.
+template <typename T, int G>
+DEV void ld_g(const T* __restrict__ p, float (&v)[G]) {
+  if constexpr (G * sizeof(T) == 16) {
+    const uint4 u = *(const uint4*)p;
+    const T* e = (const T*)&u;
+#pragma unroll
+    for (int j = 0; j < G; ++j) v[j] = to_f(e[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < G; ++j) v[j] = to_f(p[j]);
+  }
+}
+template <typename T, int G>
+DEV void st_g(T* __restrict__ p, const float (&v)[G]) {
+  if constexpr (G * sizeof(T) == 16) {
+    uint4 u;
+    T* e = (T*)&u;
+#pragma unroll
+    for (int j = 0; j < G; ++j) e[j] = from_f<T>(v[j]);
+    *(uint4*)p = u;
+  } else {
+#pragma unroll
+    for (int j = 0; j < G; ++j) p[j] = from_f<T>(v[j]);
+  }
+}
+
 // ---- wave / block reductions (wave64) --------------------------------------------------
 DEV float wave_sum(float v) {
 #pragma unroll
@@ -83,6 +111,13 @@ DEV uint32_t hash3(uint64_t seed, uint32_t stream, uint64_t idx) {
   x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
   x ^= x >> 33;
   return (uint32_t)x;
+}
+// Optional device-resident step counter (imgcap_set_seed_counter).  When set, every mask seed
+// is mixed with *ctr at kernel run time, so a captured HIP graph draws fresh masks on each
+// replay while the seeds baked into its kernel arguments stay fixed.
+extern const uint64_t* g_seed_ctr;
+DEV uint64_t eff_seed(uint64_t seed, const uint64_t* ctr) {
+  return ctr ? seed ^ ((*ctr + 1) * 0x2545F4914F6CDD1Dull) : seed;
 }
 // keep iff u >= p ; returns scale 1/(1-p) or 0
 DEV float dropout_scale(uint64_t seed, uint32_t stream, uint64_t idx, float p) {

@@ -308,9 +308,26 @@ static int launch_dw(int B, int H, int W, int C, const void* x, const float* w, 
   return 0;
 }
 
+__global__ void sd_scales_kernel(int n, int B, const float* __restrict__ probs, uint64_t seed0,
+                                 const uint64_t* seed_ctr, uint32_t sid, float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  out[i] = dropout_scale(eff_seed(seed0, seed_ctr), sid, (uint64_t)i, probs[i / B]);
+}
+
 }  // namespace imgcap
 
 using namespace imgcap;
+
+extern "C" int imgcap_stochastic_depth_scales(int nblocks, int B, const float* probs, uint64_t seed,
+                                              uint32_t drop_stream, float* out, void* stream) {
+  const int n = nblocks * B;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(sd_scales_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, B, probs, seed,
+                     g_seed_ctr, drop_stream, out);
+  IMGCAP_CHECK_LAUNCH("imgcap_stochastic_depth_scales");
+  return 0;
+}
 
 extern "C" int imgcap_convnext_stem(int dtype, int B, int H, int W, int C0, const float* images, const float* w,
                                     const float* bias, const float* ln_w, const float* ln_b, void* out, void* stream) {

@@ -47,7 +47,9 @@ template <typename T>
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(int n, int dim, const int64_t* __restrict__ ids,
                                                             const float* __restrict__ table,
                                                             const float* __restrict__ pe, int L, float p,
-                                                            uint64_t seed, uint32_t sid, T* __restrict__ out) {
+                                                            uint64_t seed0, const uint64_t* seed_ctr, uint32_t sid,
+                                                            T* __restrict__ out) {
+  const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
   const long total = (long)n * dim;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
     const long r = e / dim;
@@ -60,8 +62,10 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(int n, int dim, cons
 
 template <typename T>
 __global__ __launch_bounds__(256) void embedding_bwd_kernel(int n, int dim, const int64_t* __restrict__ ids,
-                                                            const T* __restrict__ dout, float p, uint64_t seed,
-                                                            uint32_t sid, float* __restrict__ dtable) {
+                                                            const T* __restrict__ dout, float p, uint64_t seed0,
+                                                            const uint64_t* seed_ctr, uint32_t sid,
+                                                            float* __restrict__ dtable) {
+  const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
   const long total = (long)n * dim;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
     const long r = e / dim;
@@ -82,8 +86,9 @@ __global__ void fill_kernel(long n, float v, T* __restrict__ x) {
 }
 
 template <typename T>
-__global__ void dropout_kernel(long n, const T* __restrict__ x, float p, uint64_t seed, uint32_t sid,
-                               T* __restrict__ y) {
+__global__ void dropout_kernel(long n, const T* __restrict__ x, float p, uint64_t seed0, const uint64_t* seed_ctr,
+                               uint32_t sid, T* __restrict__ y) {
+  const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     y[i] = from_f<T>(to_f(x[i]) * dropout_scale(seed, sid, i, p));
 }
@@ -155,10 +160,10 @@ extern "C" int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* id
   const long total = (long)n * dim;
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(embedding_fwd_kernel<bf16>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
-                       table, pe, L, drop_p, seed, drop_stream, (bf16*)out);
+                       table, pe, L, drop_p, seed, g_seed_ctr, drop_stream, (bf16*)out);
   else
     hipLaunchKernelGGL(embedding_fwd_kernel<float>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
-                       table, pe, L, drop_p, seed, drop_stream, (float*)out);
+                       table, pe, L, drop_p, seed, g_seed_ctr, drop_stream, (float*)out);
   IMGCAP_CHECK_LAUNCH("imgcap_embedding_fwd");
   return 0;
 }
@@ -169,10 +174,10 @@ extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* id
   const long total = (long)n * dim;
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(embedding_bwd_kernel<bf16>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
-                       (const bf16*)dout, drop_p, seed, drop_stream, dtable);
+                       (const bf16*)dout, drop_p, seed, g_seed_ctr, drop_stream, dtable);
   else
     hipLaunchKernelGGL(embedding_bwd_kernel<float>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
-                       (const float*)dout, drop_p, seed, drop_stream, dtable);
+                       (const float*)dout, drop_p, seed, g_seed_ctr, drop_stream, dtable);
   IMGCAP_CHECK_LAUNCH("imgcap_embedding_bwd");
   return 0;
 }
@@ -182,10 +187,10 @@ extern "C" int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint
   if (n == 0) return 0;
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(dropout_kernel<bf16>, grid_for(n), dim3(256), 0, (hipStream_t)stream, (long)n, (const bf16*)x,
-                       p, seed, drop_stream, (bf16*)y);
+                       p, seed, g_seed_ctr, drop_stream, (bf16*)y);
   else
     hipLaunchKernelGGL(dropout_kernel<float>, grid_for(n), dim3(256), 0, (hipStream_t)stream, (long)n,
-                       (const float*)x, p, seed, drop_stream, (float*)y);
+                       (const float*)x, p, seed, g_seed_ctr, drop_stream, (float*)y);
   IMGCAP_CHECK_LAUNCH("imgcap_dropout");
   return 0;
 }

@@ -17,6 +17,8 @@
 // skinny kernel (M <= 64, A and B k-major): the LSTM recurrence GEMMs at M = batch.  Each
 //   block owns 16 output columns; its 8 waves split K and stream A/B fragments straight from
 //   global into registers (no LDS round trip, no barriers in the loop), then reduce in LDS.
+#include <algorithm>
+
 #include "common.h"
 
 namespace imgcap {
@@ -189,150 +191,7 @@ DEV void epilogue_from_lds(const imgcap_epilogue& ep, const float* tile, int LDT
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// tiled kernel
-template <typename T, int BM, int BN>
-struct GemmCfg {
-  static constexpr int VEC = 16 / sizeof(T);
-  static constexpr int BK = 32;
-  static constexpr int LDK = BK + VEC;  // +16 bytes per LDS row
-  static constexpr int TM = BM / 2 / 16;
-  static constexpr int TN = BN / 2 / 16;
-  static constexpr int A_VECS = BM * BK / VEC / 256;
-  static constexpr int B_VECS = BN * BK / VEC / 256;
-  static constexpr int STAGE_BYTES = (BM + BN) * LDK * (int)sizeof(T);
-  static constexpr int EPI_ROWS = BM / 2;   // one wave-row's worth of output per epilogue pass
-  static constexpr int LDT = BN + 4;
-  static constexpr int EPI_BYTES = EPI_ROWS * LDT * 4;
-  static constexpr int SMEM = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
-  static_assert(A_VECS >= 1 && B_VECS >= 1, "tile too small for 256 threads");
-};
-
-// Load one operand tile (ROWS x BK) into registers.  KMAJ: element (r,k) at P[r*ld + k].
-template <typename T, int ROWS, int BK, int NV, bool KMAJ>
-DEV void tile_load(uint4 (&reg)[NV], const T* __restrict__ P, long ld, int r0, int k0, int R, int K) {
-  constexpr int VEC = 16 / sizeof(T);
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int v = tid + i * 256;
-    int r, k;
-    if (KMAJ) { r = v / (BK / VEC); k = (v % (BK / VEC)) * VEC; }
-    else      { k = v / (ROWS / VEC); r = (v % (ROWS / VEC)) * VEC; }
-    const int gr = r0 + r, gk = k0 + k;
-    const int cr = gr < R ? gr : R - 1;  // clamped (always-valid) address
-    const int ck = gk < K ? gk : K - 1;
-    const uint4 x = KMAJ ? *(const uint4*)(P + (long)cr * ld + (ck / VEC) * VEC)
-                         : *(const uint4*)(P + (long)ck * ld + (cr / VEC) * VEC);
-    const bool ok = KMAJ ? (gr < R && gk < K) : (gk < K && gr < R);
-    reg[i] = ok ? x : make_uint4(0u, 0u, 0u, 0u);
-    if (KMAJ && gk + VEC > K) reg[i] = mask_tail<T>(reg[i], K - gk);
-  }
-}
-
-template <typename T, int ROWS, int BK, int LDK, int NV, bool KMAJ>
-DEV void tile_store(T* S, const uint4 (&reg)[NV]) {
-  constexpr int VEC = 16 / sizeof(T);
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int v = tid + i * 256;
-    if (KMAJ) {
-      const int r = v / (BK / VEC), k = (v % (BK / VEC)) * VEC;
-      *(uint4*)(S + r * LDK + k) = reg[i];
-    } else {
-      const int k = v / (ROWS / VEC), r = (v % (ROWS / VEC)) * VEC;
-      const uint32_t w[4] = {reg[i].x, reg[i].y, reg[i].z, reg[i].w};
-      if (sizeof(T) == 2) {
-        unsigned short* s16 = (unsigned short*)S;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          s16[(r + j) * LDK + k] = (unsigned short)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
-      } else {
-        uint32_t* s32 = (uint32_t*)S;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s32[(r + j) * LDK + k] = w[j];
-      }
-    }
-  }
-}
-
-template <typename T, int BM, int BN, bool AK, bool BKM>
-__global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long lda, long sA,
-                                                   const T* __restrict__ B, long ldb, long sB,
-                                                   void* __restrict__ C, long ldc, long sC,
-                                                   int M, int N, int K, imgcap_epilogue ep, int vec_ok) {
-  using G = GemmCfg<T, BM, BN>;
-  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
-  T* As = (T*)smem;
-  T* Bs = As + BM * G::LDK;
-
-  const int bz = blockIdx.z;
-  A += bz * sA;
-  B += bz * sB;
-  const long cbase = (long)bz * sC;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int rb = wm * (BM / 2), cb = wn * (BN / 2);
-
-  f32x4 acc[G::TM][G::TN];
-#pragma unroll
-  for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  uint4 ra[G::A_VECS], rbv[G::B_VECS];
-  tile_load<T, BM, G::BK, G::A_VECS, AK>(ra, A, lda, m0, 0, M, K);
-  tile_load<T, BN, G::BK, G::B_VECS, BKM>(rbv, B, ldb, n0, 0, N, K);
-  tile_store<T, BM, G::BK, G::LDK, G::A_VECS, AK>(As, ra);
-  tile_store<T, BN, G::BK, G::LDK, G::B_VECS, BKM>(Bs, rbv);
-  __syncthreads();
-
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
-  const int nk = (K + G::BK - 1) / G::BK;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      tile_load<T, BM, G::BK, G::A_VECS, AK>(ra, A, lda, m0, (kt + 1) * G::BK, M, K);
-      tile_load<T, BN, G::BK, G::B_VECS, BKM>(rbv, B, ldb, n0, (kt + 1) * G::BK, N, K);
-    }
-    Frag<T> af[G::TM], bfr[G::TN];
-#pragma unroll
-    for (int i = 0; i < G::TM; ++i) af[i] = lds_frag<T>(As + (rb + i * 16 + fr) * G::LDK + fk);
-#pragma unroll
-    for (int j = 0; j < G::TN; ++j) bfr[j] = lds_frag<T>(Bs + (cb + j * 16 + fr) * G::LDK + fk);
-#pragma unroll
-    for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < G::TN; ++j) mma(acc[i][j], af[i], bfr[j]);
-    __syncthreads();
-    if (more) {
-      tile_store<T, BM, G::BK, G::LDK, G::A_VECS, AK>(As, ra);
-      tile_store<T, BN, G::BK, G::LDK, G::B_VECS, BKM>(Bs, rbv);
-      __syncthreads();
-    }
-  }
-
-  // epilogue: two passes of BM/2 rows (one wave-row each) through LDS
-  float* tile = (float*)smem;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    if (wm == pass) {
-#pragma unroll
-      for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-        for (int j = 0; j < G::TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            tile[(i * 16 + 4 * (lane >> 4) + r) * G::LDT + cb + j * 16 + fr] = acc[i][j][r];
-    }
-    __syncthreads();
-    epilogue_from_lds<BN>(ep, tile, G::LDT, G::EPI_ROWS, m0 + pass * G::EPI_ROWS, n0, M, N, C, ldc, cbase,
-                          vec_ok != 0);
-    __syncthreads();
-  }
-}
+#include "gemm_tiled.h"
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
@@ -363,8 +222,10 @@ template <typename T, int MT, int SW, int DEPTH>
 __global__ __launch_bounds__(64 * SW) void gemm_skinny_kernel(const T* __restrict__ A, long lda,
                                                               const T* __restrict__ B, long ldb,
                                                               void* __restrict__ C, long ldc, int M, int N, int K,
-                                                              imgcap_epilogue ep, int vec_ok) {
+                                                              imgcap_epilogue ep, int vec_ok,
+                                                              const uint64_t* seed_ctr) {
   constexpr int H = SkinnyLd<T>::H;
+  if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
   constexpr int LDT = 16 + 4;
   __shared__ __attribute__((aligned(16))) float part[SW][MT * 16][LDT];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -424,26 +285,6 @@ __global__ __launch_bounds__(64 * SW) void gemm_skinny_kernel(const T* __restric
   epilogue_from_lds<16>(ep, &part[0][0][0], LDT, MT * 16, 0, n0, M, N, C, ldc, 0, vec_ok != 0);
 }
 
-// ---------------------------------------------------------------------------------------
-template <typename T, int BM, int BN>
-static int launch_tiled(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
-                        long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
-                        int vec_ok, hipStream_t st) {
-  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
-  const T* a = (const T*)A;
-  const T* b = (const T*)B;
-#define L_(AKV, BKV)                                                                                       \
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, AKV, BKV>), grid, dim3(256), 0, st, a, lda, sA, b, ldb, sB, C, ldc, \
-                     sC, M, N, K, ep, vec_ok)
-  if (ak && bk) L_(true, true);
-  else if (ak && !bk) L_(true, false);
-  else if (!ak && bk) L_(false, true);
-  else L_(false, false);
-#undef L_
-  IMGCAP_CHECK_LAUNCH("imgcap_gemm");
-  return 0;
-}
-
 template <typename T>
 static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
                          long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
@@ -455,7 +296,7 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
     const T* b = (const T*)B;
 #define SK_(MT, SW, DEPTH)                                                                                   \
   hipLaunchKernelGGL((gemm_skinny_kernel<T, MT, SW, DEPTH>), dim3(blocks), dim3(64 * SW), 0, st, a, lda, b, ldb, C, \
-                     ldc, M, N, K, ep, vec_ok)
+                     ldc, M, N, K, ep, vec_ok, g_seed_ctr)
     constexpr bool F32 = sizeof(T) == 4;
     if (M <= 32) {
       if (wide) SK_(2, 16, F32 ? 2 : 4); else SK_(2, 8, F32 ? 2 : 8);
@@ -468,39 +309,36 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
   }
   const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   if (tiles128 < 512)
-    return launch_tiled<T, 64, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
-  return launch_tiled<T, 128, 128>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
+    return launch_tiled<T, 64, 64, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
+  return launch_tiled<T, 128, 128, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
 }
 
 // bias-gradient style column sums: out[c] = beta*out[c] + sum_r x[r, c].
-// Block = 64 columns (8 vectors of 8) x 32 row lanes; fixed-order LDS reduction (deterministic).
+// Block = 64 columns (8 vectors of 8) x 32 row lanes over the row slice blockIdx.y of
+// gridDim.y; fixed-order LDS reduction.  With one slice the block writes out directly; with
+// several, each writes its partial row of ws and colsum_reduce_kernel adds the slices in
+// order — deterministic either way, and enough blocks to fill the chip for narrow outputs.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(int rows, int cols, const T* __restrict__ x, long ld,
-                                                     float* __restrict__ out, float beta, int vec_ok) {
+                                                     float* __restrict__ out, float beta, int vec_ok,
+                                                     int rows_per_slice) {
   __shared__ float red[32][65];
   const int cv = threadIdx.x & 7, rl = threadIdx.x >> 3;
   const int c0 = blockIdx.x * 64 + cv * 8;
+  const int r_beg = blockIdx.y * rows_per_slice, r_end = min(rows, r_beg + rows_per_slice);
   float s[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = 0.f;
   if (vec_ok && c0 + 8 <= cols) {
-    for (int r = rl; r < rows; r += 32) {
+    for (int r = r_beg + rl; r < r_end; r += 32) {
       float v[8];
-      const T* p = x + (long)r * ld + c0;
-      if (sizeof(T) == 2) {
-        const bf16x8 q = *(const bf16x8*)p;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (float)q[j];
-      } else {
-        const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
-      }
+      ld_g<T, 16 / sizeof(T)>(x + (long)r * ld + c0, *(float(*)[16 / sizeof(T)])v);
+      if constexpr (sizeof(T) == 4) ld_g<T, 4>(x + (long)r * ld + c0 + 4, *(float(*)[4])(v + 4));
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] += v[j];
     }
   } else {
-    for (int r = rl; r < rows; r += 32)
+    for (int r = r_beg + rl; r < r_end; r += 32)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (c0 + j < cols) s[j] += to_f(x[(long)r * ld + c0 + j]);
@@ -512,8 +350,20 @@ __global__ __launch_bounds__(256) void colsum_kernel(int rows, int cols, const T
     const int c = blockIdx.x * 64 + threadIdx.x;
     float t = 0.f;
     for (int i = 0; i < 32; ++i) t += red[i][threadIdx.x];
-    if (c < cols) out[c] = (beta != 0.f ? beta * out[c] : 0.f) + t;
+    if (c < cols) {
+      if (gridDim.y == 1) out[c] = (beta != 0.f ? beta * out[c] : 0.f) + t;
+      else out[(long)blockIdx.y * cols + c] = t;
+    }
   }
+}
+
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(int cols, int slices, const float* __restrict__ ws,
+                                                            float* __restrict__ out, float beta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float t = 0.f;
+  for (int y = 0; y < slices; ++y) t += ws[(long)y * cols + c];
+  out[c] = (beta != 0.f ? beta * out[c] : 0.f) + t;
 }
 
 // out[c][r] = in[r][c] (2-D transpose through an LDS tile; weights -> k-major copies)
@@ -567,17 +417,46 @@ extern "C" int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, 
                               batch, *epi, vec_ok, st);
 }
 
+namespace {
+// Row-slice partials of imgcap_colsum.  Grown on demand (first at the warm-up step, before any
+// graph capture); one buffer per process, used by one stream at a time.
+float* g_colsum_ws = nullptr;
+size_t g_colsum_ws_bytes = 0;
+}  // namespace
+
 extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64_t ldx, float* out, float beta,
                              void* stream) {
   if (cols == 0) return 0;
-  dim3 grid((cols + 63) / 64);
+  const int cblocks = (cols + 63) / 64;
+  // slices: ~512 blocks in total, >= 64 rows each, at most 64 slices
+  int slices = std::min(std::min(64, (512 + cblocks - 1) / cblocks), std::max(1, rows / 64));
+  const int rps = (rows + slices - 1) / std::max(slices, 1);
+  slices = rows > 0 ? (rows + rps - 1) / rps : 1;
+  float* dst = out;
+  if (slices > 1) {
+    const size_t need = (size_t)slices * cols * sizeof(float);
+    if (need > g_colsum_ws_bytes) {
+      if (g_colsum_ws) (void)hipFree(g_colsum_ws);
+      g_colsum_ws = nullptr;
+      g_colsum_ws_bytes = 0;
+      const size_t bytes = std::max(need, (size_t)4 << 20);
+      if (hipMalloc(&g_colsum_ws, bytes) != hipSuccess) return fail(IMGCAP_EINVAL, "imgcap_colsum: workspace");
+      g_colsum_ws_bytes = bytes;
+    }
+    dst = g_colsum_ws;
+  }
+  const dim3 grid(cblocks, slices);
   const int vec_ok = aligned16(x) && ldx % 8 == 0;
+  hipStream_t st = (hipStream_t)stream;
   if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const bf16*)x, ldx,
-                       out, beta, vec_ok);
+    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, (const bf16*)x, ldx, dst, beta,
+                       vec_ok, std::max(rps, 1));
   else
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const float*)x,
-                       ldx, out, beta, vec_ok);
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, rows, cols, (const float*)x, ldx, dst, beta,
+                       vec_ok, std::max(rps, 1));
+  if (slices > 1)
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, cols, slices, dst, out,
+                       beta);
   IMGCAP_CHECK_LAUNCH("imgcap_colsum");
   return 0;
 }

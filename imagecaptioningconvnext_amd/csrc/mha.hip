@@ -105,7 +105,8 @@ DEV bool key_masked(const imgcap_mha_desc& d, int b, int i, int j) {
 
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void mha_fwd_kernel(imgcap_mha_desc d) {
+__global__ __launch_bounds__(256) void mha_fwd_kernel(imgcap_mha_desc d, const uint64_t* seed_ctr) {
+  if (d.drop_p > 0.f) d.seed = eff_seed(d.seed, seed_ctr);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int LD = Img<T>::LD;
   T* Qs = (T*)smem;
@@ -180,7 +181,8 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(imgcap_mha_desc d) {
 
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void mha_bwd_kernel(imgcap_mha_desc d) {
+__global__ __launch_bounds__(256) void mha_bwd_kernel(imgcap_mha_desc d, const uint64_t* seed_ctr) {
+  if (d.drop_p > 0.f) d.seed = eff_seed(d.seed, seed_ctr);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int LD = Img<T>::LD;
   constexpr int NE = Img<T>::ELEMS;
@@ -317,10 +319,10 @@ extern "C" int imgcap_mha_fwd(const imgcap_mha_desc* d, void* stream) {
   const dim3 grid(d->B * d->H);
   if (d->dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(mha_fwd_kernel<bf16>, grid, dim3(256), 3 * Img<bf16>::ELEMS * sizeof(bf16),
-                       (hipStream_t)stream, *d);
+                       (hipStream_t)stream, *d, g_seed_ctr);
   else
     hipLaunchKernelGGL(mha_fwd_kernel<float>, grid, dim3(256), 3 * Img<float>::ELEMS * sizeof(float),
-                       (hipStream_t)stream, *d);
+                       (hipStream_t)stream, *d, g_seed_ctr);
   IMGCAP_CHECK_LAUNCH("imgcap_mha_fwd");
   return 0;
 }
@@ -339,10 +341,10 @@ extern "C" int imgcap_mha_bwd(const imgcap_mha_desc* d, void* stream) {
   }
   if (d->dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(mha_bwd_kernel<bf16>, grid, dim3(256), 6 * Img<bf16>::ELEMS * sizeof(bf16),
-                       (hipStream_t)stream, *d);
+                       (hipStream_t)stream, *d, g_seed_ctr);
   else
     hipLaunchKernelGGL(mha_bwd_kernel<float>, grid, dim3(256), 6 * Img<float>::ELEMS * sizeof(float),
-                       (hipStream_t)stream, *d);
+                       (hipStream_t)stream, *d, g_seed_ctr);
   IMGCAP_CHECK_LAUNCH("imgcap_mha_bwd");
   return 0;
 }

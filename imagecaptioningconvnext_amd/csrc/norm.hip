@@ -1,113 +1,153 @@
 // Row LayerNorm of a (dropout-)residual sum: the post-norm blocks of
 // nn.TransformerDecoderLayer (transformerDecoder.py:82,104): x = LN(x + dropout(sublayer(x))).
-// One wave per row (cols <= 64*16); the row stays in registers between the two variance
-// passes, so HBM traffic is one read of each input and one write of s and y.
+// One wave per row (cols <= 1024); a lane owns granules of G consecutive columns (16-byte
+// accesses when the row pitch allows), and the row stays in registers between the mean and
+// variance passes, so HBM traffic is one read of each input and one write of s and y.
+#include <algorithm>
+#include <initializer_list>
+
 #include "common.h"
 
 namespace imgcap {
 
-constexpr int LN_MAXV = 16;  // values per lane -> cols <= 1024
+constexpr int LN_MAXC = 1024;
 
-template <typename T>
+template <typename T, int G>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(int rows, int cols, const T* __restrict__ x,
-                                                         const T* __restrict__ r, float p, uint64_t seed,
-                                                         uint32_t stream_id, const float* __restrict__ g,
-                                                         const float* __restrict__ b, float eps, T* __restrict__ s_out,
-                                                         T* __restrict__ y, float* __restrict__ mean_o,
-                                                         float* __restrict__ rstd_o) {
+                                                         const T* __restrict__ r, float p, uint64_t seed0,
+                                                         const uint64_t* seed_ctr, uint32_t stream_id,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         float eps, T* __restrict__ s_out, T* __restrict__ y,
+                                                         float* __restrict__ mean_o, float* __restrict__ rstd_o) {
+  constexpr int MAXJ = LN_MAXC / (64 * G);
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
-  float v[LN_MAXV];
+  const uint64_t seed = (r && p > 0.f) ? eff_seed(seed0, seed_ctr) : seed0;
+  float v[MAXJ][G];
   float sum = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = 0.f;
-    if (c < cols) {
-      const long idx = (long)row * cols + c;
-      float t = to_f(x[idx]);
-      if (r) t += to_f(r[idx]) * dropout_scale(seed, stream_id, idx, p);
-      if (s_out) s_out[idx] = from_f<T>(t);
-      t = to_f(from_f<T>(t));  // LN sees exactly the stored s (bwd recomputes from it)
-      v[i] = t;
-      sum += t;
+  for (int j = 0; j < MAXJ; ++j) {
+    const int c0 = G * (lane + 64 * j);
+#pragma unroll
+    for (int e = 0; e < G; ++e) v[j][e] = 0.f;
+    if (c0 < cols) {
+      const long idx = (long)row * cols + c0;
+      float xv[G];
+      ld_g<T, G>(x + idx, xv);
+      if (r) {
+        float rv[G];
+        ld_g<T, G>(r + idx, rv);
+#pragma unroll
+        for (int e = 0; e < G; ++e) xv[e] += rv[e] * dropout_scale(seed, stream_id, idx + e, p);
+      }
+      if (s_out) st_g<T, G>(s_out + idx, xv);
+#pragma unroll
+      for (int e = 0; e < G; ++e) {
+        v[j][e] = to_f(from_f<T>(xv[e]));  // LN sees exactly the stored s (bwd recomputes from it)
+        sum += v[j][e];
+      }
     }
   }
   const float mean = wave_sum(sum) / cols;
   float sq = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
-    const int c = lane + 64 * i;
-    if (c < cols) { const float d = v[i] - mean; sq += d * d; }
-  }
+  for (int j = 0; j < MAXJ; ++j)
+    if (G * (lane + 64 * j) < cols)
+#pragma unroll
+      for (int e = 0; e < G; ++e) { const float d = v[j][e] - mean; sq += d * d; }
   const float rstd = rsqrtf(wave_sum(sq) / cols + eps);
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
-    const int c = lane + 64 * i;
-    if (c < cols) y[(long)row * cols + c] = from_f<T>((v[i] - mean) * rstd * g[c] + b[c]);
+  for (int j = 0; j < MAXJ; ++j) {
+    const int c0 = G * (lane + 64 * j);
+    if (c0 < cols) {
+      float o[G];
+#pragma unroll
+      for (int e = 0; e < G; ++e) o[e] = (v[j][e] - mean) * rstd * g[c0 + e] + b[c0 + e];
+      st_g<T, G>(y + (long)row * cols + c0, o);
+    }
   }
   if (lane == 0) { mean_o[row] = mean; rstd_o[row] = rstd; }
 }
 
-template <typename T>
+// dS = LN backward of dy; dx = dS; dr = dS * dropmask.  Each wave walks rows_per_wave rows;
+// dgamma/dbeta partials are summed over the block's waves in LDS in a fixed order and added
+// to the output with one atomic per column per block (grid sized to ~2 blocks per CU).
+template <typename T, int G>
 __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                          const T* __restrict__ s, const float* __restrict__ mean_i,
                                                          const float* __restrict__ rstd_i, const float* __restrict__ g,
-                                                         float p, uint64_t seed, uint32_t stream_id, T* __restrict__ dx,
-                                                         T* __restrict__ dr, float* __restrict__ dg,
-                                                         float* __restrict__ db, int rows_per_block) {
-  // each block: rows_per_block rows, 4 waves; dgamma/dbeta partials reduced in LDS then one
-  // atomic per column per block
-  __shared__ float pg[1024], pb[1024];
-  for (int c = threadIdx.x; c < cols; c += 256) { pg[c] = 0.f; pb[c] = 0.f; }
-  __syncthreads();
+                                                         float p, uint64_t seed0, const uint64_t* seed_ctr,
+                                                         uint32_t stream_id, T* __restrict__ dx, T* __restrict__ dr,
+                                                         float* __restrict__ dg, float* __restrict__ db,
+                                                         int rows_per_wave) {
+  constexpr int MAXJ = LN_MAXC / (64 * G);
+  __shared__ float part[2][4][LN_MAXC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float lg[LN_MAXV], lb[LN_MAXV];
+  const uint64_t seed = (dr && p > 0.f) ? eff_seed(seed0, seed_ctr) : seed0;
+  float lg[MAXJ][G], lb[MAXJ][G];
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) { lg[i] = 0.f; lb[i] = 0.f; }
-  const int r_end = min(rows, (blockIdx.x + 1) * rows_per_block);
-  for (int row = blockIdx.x * rows_per_block + w; row < r_end; row += 4) {
+  for (int j = 0; j < MAXJ; ++j)
+#pragma unroll
+    for (int e = 0; e < G; ++e) { lg[j][e] = 0.f; lb[j][e] = 0.f; }
+  const int r0 = (blockIdx.x * 4 + w) * rows_per_wave;
+  const int r_end = min(rows, r0 + rows_per_wave);
+  for (int row = r0; row < r_end; ++row) {
     const float mean = mean_i[row], rstd = rstd_i[row];
-    float xh[LN_MAXV], gdy[LN_MAXV];
+    float xh[MAXJ][G], gdy[MAXJ][G];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      const int c = lane + 64 * i;
-      xh[i] = 0.f; gdy[i] = 0.f;
-      if (c < cols) {
-        const long idx = (long)row * cols + c;
-        const float d = to_f(dy[idx]);
-        xh[i] = (to_f(s[idx]) - mean) * rstd;
-        gdy[i] = d * g[c];
-        lg[i] += d * xh[i];
-        lb[i] += d;
-        s1 += gdy[i];
-        s2 += gdy[i] * xh[i];
+    for (int j = 0; j < MAXJ; ++j) {
+      const int c0 = G * (lane + 64 * j);
+#pragma unroll
+      for (int e = 0; e < G; ++e) { xh[j][e] = 0.f; gdy[j][e] = 0.f; }
+      if (c0 < cols) {
+        const long idx = (long)row * cols + c0;
+        float dv[G], sv[G];
+        ld_g<T, G>(dy + idx, dv);
+        ld_g<T, G>(s + idx, sv);
+#pragma unroll
+        for (int e = 0; e < G; ++e) {
+          xh[j][e] = (sv[e] - mean) * rstd;
+          gdy[j][e] = dv[e] * g[c0 + e];
+          lg[j][e] += dv[e] * xh[j][e];
+          lb[j][e] += dv[e];
+          s1 += gdy[j][e];
+          s2 += gdy[j][e] * xh[j][e];
+        }
       }
     }
     s1 = wave_sum(s1) / cols;
     s2 = wave_sum(s2) / cols;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < cols) {
-        const long idx = (long)row * cols + c;
-        const float d = rstd * (gdy[i] - s1 - xh[i] * s2);
-        dx[idx] = from_f<T>(d);
-        if (dr) dr[idx] = from_f<T>(d * dropout_scale(seed, stream_id, idx, p));
+    for (int j = 0; j < MAXJ; ++j) {
+      const int c0 = G * (lane + 64 * j);
+      if (c0 < cols) {
+        const long idx = (long)row * cols + c0;
+        float d[G];
+#pragma unroll
+        for (int e = 0; e < G; ++e) d[e] = rstd * (gdy[j][e] - s1 - xh[j][e] * s2);
+        st_g<T, G>(dx + idx, d);
+        if (dr) {
+#pragma unroll
+          for (int e = 0; e < G; ++e) d[e] *= dropout_scale(seed, stream_id, idx + e, p);
+          st_g<T, G>(dr + idx, d);
+        }
       }
     }
   }
+  if (!dg && !db) return;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
-    const int c = lane + 64 * i;
-    if (c < cols) { atomicAdd(&pg[c], lg[i]); atomicAdd(&pb[c], lb[i]); }
+  for (int j = 0; j < MAXJ; ++j) {
+    const int c0 = G * (lane + 64 * j);
+    if (c0 < cols)
+#pragma unroll
+      for (int e = 0; e < G; ++e) { part[0][w][c0 + e] = lg[j][e]; part[1][w][c0 + e] = lb[j][e]; }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < cols; c += 256) {
-    if (dg) atomicAdd(&dg[c], pg[c]);
-    if (db) atomicAdd(&db[c], pb[c]);
+    if (dg) atomicAdd(&dg[c], ((part[0][0][c] + part[0][1][c]) + part[0][2][c]) + part[0][3][c]);
+    if (db) atomicAdd(&db[c], ((part[1][0][c] + part[1][1][c]) + part[1][2][c]) + part[1][3][c]);
   }
 }
 
@@ -115,19 +155,33 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, con
 
 using namespace imgcap;
 
+namespace {
+// granule: 16-byte accesses when the row pitch and every operand allow it, else scalar
+template <typename T>
+bool vec_rows(int cols, std::initializer_list<const void*> ptrs) {
+  if ((cols * sizeof(T)) % 16 != 0) return false;
+  for (const void* q : ptrs)
+    if (q && !aligned16(q)) return false;
+  return true;
+}
+}  // namespace
+
 extern "C" int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const void* x, const void* r, float drop_p,
                                         uint64_t seed, uint32_t drop_stream, const float* gamma, const float* beta,
                                         float eps, void* s_out, void* y, float* mean, float* rstd, void* stream) {
-  IMGCAP_REQUIRE(cols > 0 && cols <= 64 * LN_MAXV, "imgcap_add_layernorm_fwd: cols must be in (0, 1024]");
+  IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_fwd: cols must be in (0, 1024]");
   if (rows == 0) return 0;
   dim3 grid((rows + 3) / 4);
-  if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(add_ln_fwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const bf16*)x,
-                       (const bf16*)r, drop_p, seed, drop_stream, gamma, beta, eps, (bf16*)s_out, (bf16*)y, mean, rstd);
-  else
-    hipLaunchKernelGGL(add_ln_fwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const float*)x,
-                       (const float*)r, drop_p, seed, drop_stream, gamma, beta, eps, (float*)s_out, (float*)y, mean,
-                       rstd);
+  hipStream_t st = (hipStream_t)stream;
+#define LNF_(T, G)                                                                                              \
+  hipLaunchKernelGGL((add_ln_fwd_kernel<T, G>), grid, dim3(256), 0, st, rows, cols, (const T*)x, (const T*)r,    \
+                     drop_p, seed, g_seed_ctr, drop_stream, gamma, beta, eps, (T*)s_out, (T*)y, mean, rstd)
+  if (dtype == IMGCAP_BF16) {
+    if (vec_rows<bf16>(cols, {x, r, s_out, y})) LNF_(bf16, 8); else LNF_(bf16, 1);
+  } else {
+    if (vec_rows<float>(cols, {x, r, s_out, y})) LNF_(float, 4); else LNF_(float, 1);
+  }
+#undef LNF_
   IMGCAP_CHECK_LAUNCH("imgcap_add_layernorm_fwd");
   return 0;
 }
@@ -136,18 +190,20 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
                                         const float* mean, const float* rstd, const float* gamma, float drop_p,
                                         uint64_t seed, uint32_t drop_stream, void* dx, void* dr, float* dgamma,
                                         float* dbeta, void* stream) {
-  IMGCAP_REQUIRE(cols > 0 && cols <= 64 * LN_MAXV, "imgcap_add_layernorm_bwd: cols must be in (0, 1024]");
+  IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_bwd: cols must be in (0, 1024]");
   if (rows == 0) return 0;
-  const int rpb = 64;
-  dim3 grid((rows + rpb - 1) / rpb);
-  if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(add_ln_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const bf16*)dy,
-                       (const bf16*)s, mean, rstd, gamma, drop_p, seed, drop_stream, (bf16*)dx, (bf16*)dr, dgamma,
-                       dbeta, rpb);
-  else
-    hipLaunchKernelGGL(add_ln_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
-                       (const float*)dy, (const float*)s, mean, rstd, gamma, drop_p, seed, drop_stream, (float*)dx,
-                       (float*)dr, dgamma, dbeta, rpb);
+  const int rpw = std::max(1, (rows + 4 * 512 - 1) / (4 * 512));  // ~512 blocks of 4 waves
+  dim3 grid((rows + 4 * rpw - 1) / (4 * rpw));
+  hipStream_t st = (hipStream_t)stream;
+#define LNB_(T, G)                                                                                              \
+  hipLaunchKernelGGL((add_ln_bwd_kernel<T, G>), grid, dim3(256), 0, st, rows, cols, (const T*)dy, (const T*)s,   \
+                     mean, rstd, gamma, drop_p, seed, g_seed_ctr, drop_stream, (T*)dx, (T*)dr, dgamma, dbeta, rpw)
+  if (dtype == IMGCAP_BF16) {
+    if (vec_rows<bf16>(cols, {dy, s, dx, dr})) LNB_(bf16, 8); else LNB_(bf16, 1);
+  } else {
+    if (vec_rows<float>(cols, {dy, s, dx, dr})) LNB_(float, 4); else LNB_(float, 1);
+  }
+#undef LNB_
   IMGCAP_CHECK_LAUNCH("imgcap_add_layernorm_bwd");
   return 0;
 }

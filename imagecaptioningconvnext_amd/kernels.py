@@ -220,3 +220,20 @@ def transpose(x, out=None):
     _abi.call("imgcap_transpose", dt(x), rows, cols, x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0),
               stream())
     return out
+
+
+def set_seed_counter(counter):
+    """Mix the device int64 scalar ``counter`` into every mask seed (None = off); see
+    imgcap_set_seed_counter.  The tensor must outlive every launch that used it."""
+    if counter is not None:
+        _check_dev(counter)
+        if counter.dtype != torch.int64 or counter.numel() != 1:
+            raise ValueError("seed counter must be a one-element int64 tensor")
+    _abi.call("imgcap_set_seed_counter", ptr(counter))
+
+
+def stochastic_depth_scales(probs, B, seed, drop_stream, out):
+    _check_dev(probs, out)
+    _abi.call("imgcap_stochastic_depth_scales", probs.numel(), B, probs.data_ptr(), seed, drop_stream,
+              out.data_ptr(), stream())
+    return out

@@ -28,6 +28,9 @@ VARIANTS = {
 }
 
 
+SD_STREAM = 7  # RNG stream id of the encoder's stochastic-depth draws
+
+
 class _LayerNorm2d(nn.LayerNorm):
     """Parameter holder with torchvision's LayerNorm2d names (weight, bias), eps 1e-6."""
 
@@ -143,14 +146,17 @@ class Encoder(nn.Module):
         return pk
 
     def _sd_scales(self, B, device):
-        """StochasticDepth(p, "row") per-sample scales keep/(1-p) for every block (train mode)."""
-        probs = [blk.sd_prob for s in range(4) for blk in self.convnext[1 + 2 * s]]
-        g = torch.Generator(device=device)
-        g.manual_seed(self.sd_seed)
+        """StochasticDepth(p, "row") per-sample scales keep/(1-p) for every block (train mode),
+        drawn on the device by the counter RNG (no host sync; graph-capturable)."""
+        pk = self._pack()
+        if "sd_probs" not in pk:
+            probs = [blk.sd_prob for s in range(4) for blk in self.convnext[1 + 2 * s]]
+            pk["sd_probs"] = torch.tensor(probs, device=device, dtype=torch.float32)
+        probs = pk["sd_probs"]
+        out = torch.empty(probs.numel(), B, device=device, dtype=torch.float32)
+        K.stochastic_depth_scales(probs, B, self.sd_seed, SD_STREAM, out)
         self.sd_seed += 1
-        u = torch.rand(len(probs), B, device=device, generator=g)
-        p = torch.tensor(probs, device=device).view(-1, 1)
-        return torch.where(u >= p, 1.0 / (1.0 - p), torch.zeros_like(u)).contiguous()
+        return out
 
     def forward(self, images):
         """encoder.py:23-27.  images [B,3,H,W] (f32, on GPU) -> [B, s, s, E] NHWC, compute dtype."""

@@ -8,14 +8,23 @@ Per step, exactly the reference's work:
   clip_gradient (clamp +-5) + Adam step (one fused kernel)                    :284-291 / :387-394
   loss/token/top-5 metrics (reduceLossAndTokens + accuracy all-reduces,
   fused into one 3-float all-reduce; read back lazily, no per-step host sync) :396-403
+
+With ``graph=True`` the encoder + decoder forward/backward (several hundred kernel launches,
+most of them small on the LSTM recurrence) is captured once into a HIP graph and replayed
+per step; the batch is copied into the graph's static input buffers first.  Dropout and
+stochastic-depth masks stay fresh per replay through the device step counter
+(imgcap_set_seed_counter) bumped inside the graph.  The all-reduce and the Adam step (whose
+bias correction depends on the host step count) run eagerly after the replay.
 """
 import torch
 import torch.distributed as dist
 
+from . import kernels as K
+
 
 class TeacherForcedTrainer:
     def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, grad_clip=5.0, alphaC=1.0, pad_id=0,
-                 process_group=None):
+                 process_group=None, graph=False):
         self.encoder = encoder
         self.decoder = decoder
         self.lstm = lstm
@@ -27,6 +36,8 @@ class TeacherForcedTrainer:
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.eng = decoder.engine()
         self._metric_log = []
+        self.graph = graph
+        self._graph = None
         if self.world > 1:
             # DDP construction broadcasts rank 0's parameters (trainMultiGPU.py:233); the encoder is
             # broadcast too because its weights are randomly initialised here (SURVEY.md §7 v)
@@ -35,7 +46,7 @@ class TeacherForcedTrainer:
             for p in encoder.parameters():
                 dist.broadcast(p.data, 0, group=process_group)
 
-    def step(self, imgs, caps, caplens):
+    def _fwd_bwd(self, imgs, caps, caplens):
         self.encoder.train()
         self.decoder.train()
         with torch.no_grad():
@@ -45,11 +56,43 @@ class TeacherForcedTrainer:
         else:
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
         self.eng.backward(s)
+        return s["metrics"]
+
+    def _capture(self, imgs, caps, caplens, warmup=2):
+        dev = imgs.device
+        self._seed_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        K.set_seed_counter(self._seed_ctr)
+        self._inputs = (imgs.clone(), caps.clone(), caplens.clone())
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # first-touch allocations and one-time kernel setup
+            for _ in range(warmup):
+                self._fwd_bwd(*self._inputs)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._seed_ctr.add_(1)
+            self._metrics = self._fwd_bwd(*self._inputs)
+        self._graph = g
+
+    def step(self, imgs, caps, caplens):
+        if not self.graph:
+            m = self._fwd_bwd(imgs, caps, caplens)
+        else:
+            if self._graph is None:
+                self._capture(imgs, caps, caplens)
+            for dst, src in zip(self._inputs, (imgs, caps, caplens)):
+                if dst.shape != src.shape:
+                    raise ValueError("graph mode needs a fixed batch shape; got %s, captured %s"
+                                     % (tuple(src.shape), tuple(dst.shape)))
+                if dst.data_ptr() != src.data_ptr():
+                    dst.copy_(src, non_blocking=True)
+            self._graph.replay()
+            m = self._metrics
         fp = self.eng.fp
         if self.world > 1:
             dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
         fp.adam_step(self.decoder_lr, self.grad_clip, grad_div=float(self.world))
-        m = s["metrics"]
         red = torch.stack([m[0] * m[1], m[1], m[2]])
         if self.world > 1:
             dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)

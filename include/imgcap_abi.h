@@ -31,6 +31,13 @@ enum { IMGCAP_ACT_NONE = 0, IMGCAP_ACT_GELU = 1, IMGCAP_ACT_RELU = 2 };
 const char* imgcap_last_error_string(void);
 int imgcap_version(void);
 
+/* Device-resident step counter mixed into every dropout / stochastic-depth seed at kernel
+ * run time: mask = f(seed ^ g(*counter), stream, index).  Lets a captured HIP graph draw new
+ * masks on each replay (the counter is bumped by a node inside the graph) while the seeds in
+ * its kernel arguments stay fixed.  NULL (the default) = seeds used as given.  Process-wide;
+ * read at launch-enqueue time, so set it before capturing. */
+int imgcap_set_seed_counter(const uint64_t* counter);
+
 /* ---------------------------------------------------------------------------------------
  * GEMM with fused epilogue (MFMA: bf16 16x16x32 / f32 16x16x4).
  *   acc[m,n] = sum_k A(m,k) * B(k,n)
@@ -112,6 +119,11 @@ int imgcap_ln_patchify2(int dtype, int B, int H, int W, int C, const void* x, co
 /* AdaptiveAvgPool2d((OH,OW)) on NHWC (encoder.py:20,25) */
 int imgcap_adaptive_pool_nhwc(int dtype, int B, int H, int W, int C, int OH, int OW,
                               const void* x, void* out, void* stream);
+/* StochasticDepth(p_i, "row") per-sample scales of every CNBlock (torchvision convnext,
+ * train mode; encoder.py:18 builds it): out[i*B + b] = keep ? 1/(1-p_i) : 0, keep drawn from
+ * the counter RNG (seed, drop_stream, index i*B+b).  probs: device fp32 [nblocks]. */
+int imgcap_stochastic_depth_scales(int nblocks, int B, const float* probs, uint64_t seed,
+                                   uint32_t drop_stream, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Token embedding (+ dropout, + positional encoding) — decoder.py:119,

@@ -1,0 +1,77 @@
+"""Fused train step (train.py:251-299): eager launches vs HIP-graph replay, and the device
+seed counter that keeps dropout / stochastic-depth masks fresh across replays."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _models(dev, decoder, dropout, sd_off):
+    from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
+    torch.manual_seed(5)
+    enc = Encoder(variant="tiny", compute_dtype=torch.float32)
+    enc.fine_tune(False)
+    if sd_off:
+        for m in enc.modules():
+            if hasattr(m, "sd_prob"):
+                m.sd_prob = 0.0
+    if decoder == "lstm":
+        dec = DecoderWithAttention(attention_dim=64, embed_dim=64, decoder_dim=64, vocab_size=120, device=dev,
+                                   encoder_dim=768, dropout=dropout, compute_dtype=torch.float32)
+    else:
+        dec = TransformerDecoder(embed_dim=128, decoder_dim=128, vocab_size=120, maxLen=20, device=dev,
+                                 wordMap=None, pretrained_embeddings_path=None, fine_tune_embeddings=True,
+                                 dropout=dropout, encoder_dim=768, num_heads=2, num_layers=2,
+                                 compute_dtype=torch.float32)
+    return enc.to(dev), dec.to(dev)
+
+
+def _batch(dev, i, B=4, L=20, V=120):
+    g = torch.Generator().manual_seed(100 + i)
+    img = torch.randn(B, 3, 64, 64, generator=g)
+    caps = torch.randint(1, V - 2, (B, L), generator=g)
+    caps[:, 0] = V - 2
+    lens = torch.tensor([L, 15, 11, 7])[:B]
+    for b in range(B):
+        caps[b, lens[b] - 1] = V - 1
+        caps[b, lens[b]:] = 0
+    return img.to(dev), caps.to(dev), lens.view(B, 1).to(dev)
+
+
+@pytest.mark.parametrize("decoder", ["lstm", "transformer"])
+def test_graph_replay_matches_eager(hip_device, decoder):
+    from imagecaptioningconvnext_amd import kernels as K
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    runs = []
+    for graph in (False, True):
+        enc, dec = _models(hip_device, decoder, dropout=0.0, sd_off=True)
+        tr = TeacherForcedTrainer(enc, dec, lstm=decoder == "lstm", graph=graph)
+        for i in range(3):
+            tr.step(*_batch(hip_device, i))
+        runs.append((tr.drain_metrics(), tr.eng.fp.flat.clone()))
+        K.set_seed_counter(None)
+    (m_e, p_e), (m_g, p_g) = runs
+    for a, b in zip(m_e, m_g):
+        assert abs(a[0] - b[0]) < 1e-5 * abs(a[0]) and a[1] == b[1] and abs(a[2] - b[2]) < 1e-3
+    torch.testing.assert_close(p_g, p_e, rtol=1e-5, atol=1e-6)
+
+
+def test_graph_replays_draw_fresh_masks(hip_device):
+    from imagecaptioningconvnext_amd import kernels as K
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    enc, dec = _models(hip_device, "lstm", dropout=0.5, sd_off=False)
+    tr = TeacherForcedTrainer(enc, dec, lstm=True, graph=True, decoder_lr=0.0)
+    x = _batch(hip_device, 0)
+    for _ in range(3):
+        tr.step(*x)
+    losses = [m[0] for m in tr.drain_metrics()]
+    # lr 0: the only thing that changes between replays is the dropout / drop-path masks
+    assert len(set(losses)) == 3, losses
+    # the same counter value reproduces the same masks
+    tr._seed_ctr.fill_(0)
+    tr.step(*x)
+    again = tr.drain_metrics()[0][0]
+    assert again == losses[0]
+    K.set_seed_counter(None)

@@ -1,0 +1,82 @@
+"""Kernel microbenchmarks at the bench step's shapes (GPU box): python tools/microbench.py [group]
+
+Times each launch with HIP events over back-to-back repetitions on random data and prints
+achieved TFLOP/s or GB/s.  Used to iterate on kernel variants; numbers quoted in DESIGN.md.
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
+from imagecaptioningconvnext_amd.roofline import time_launch  # noqa: E402
+
+dev = torch.device("cuda:0")
+bf = torch.bfloat16
+
+
+def gemm_case(name, M, N, Kd, ta=False, tb=True, act=0, out_dtype=bf, reps=30):
+    r8 = lambda x: (x + 7) // 8 * 8  # noqa: E731  (16-byte row pitch, as the engines allocate)
+    a = torch.randn(Kd, r8(M), device=dev).to(bf)[:, :M] if ta else torch.randn(M, r8(Kd), device=dev).to(bf)[:, :Kd]
+    b = torch.randn(N, r8(Kd), device=dev).to(bf)[:, :Kd] if tb else torch.randn(Kd, r8(N), device=dev).to(bf)[:, :N]
+    out = torch.empty(M, N, device=dev, dtype=out_dtype)
+    t = time_launch(lambda: K.gemm(a, b, trans_a=ta, trans_b=tb, out=out, act=act), reps=reps)
+    tf = 2.0 * M * N * Kd / t / 1e12
+    print(f"{name:46s} M={M:6d} N={N:5d} K={Kd:5d} {'T' if ta else 'N'}{'T' if tb else 'N'}  "
+          f"{t * 1e6:8.1f} us  {tf:7.1f} TFLOP/s")
+
+
+def gemms():
+    B = 32
+    gemm_case("enc s1 pw1 (C->4C, GELU)", B * 3136, 384, 96, act=K.ACT_GELU)
+    gemm_case("enc s1 pw2 (4C->C)", B * 3136, 96, 384)
+    gemm_case("enc s3 pw1", B * 196, 1536, 384, act=K.ACT_GELU)
+    gemm_case("enc s3 pw2", B * 196, 384, 1536)
+    gemm_case("fc logits", 1632, 9490, 512)
+    gemm_case("fc dW (TN)", 9490, 512, 1632, ta=True, tb=False, out_dtype=torch.float32)
+    gemm_case("fc dX (NN)", 1632, 512, 9490, tb=False)
+    gemm_case("trf in_proj (B=64)", 3328, 1536, 512)
+    gemm_case("trf in_proj dW (TN)", 1536, 512, 3328, ta=True, tb=False, out_dtype=torch.float32)
+    gemm_case("trf in_proj dX (NN)", 3328, 512, 1536, tb=False)
+    gemm_case("trf ffn (B=64)", 3328, 512, 512)
+    gemm_case("big square", 4096, 4096, 4096)
+    gemm_case("lstm G1 (skinny)", 32, 3328, 512, out_dtype=torch.float32)
+    gemm_case("lstm G2 (skinny)", 32, 2048, 768, out_dtype=torch.float32)
+    gemm_case("lstm dz (skinny)", 32, 768, 2048, out_dtype=torch.float32)
+    gemm_case("lstm dh (skinny)", 32, 512, 3328, out_dtype=torch.float32)
+
+
+def misc():
+    B = 32
+    for (H, C) in ((56, 96), (28, 192), (14, 384), (7, 768)):
+        x = torch.randn(B, H, H, C, device=dev).to(bf)
+        y = torch.empty_like(x)
+        w = torch.randn(49, C, device=dev)
+        b = torch.randn(C, device=dev)
+        t = time_launch(lambda: K.dwconv7_ln(x, w, b, b, b, y))
+        gbs = 2 * x.numel() * 2 / t / 1e9
+        print(f"dwconv7_ln B={B} H={H} C={C}: {t * 1e6:8.1f} us {gbs:8.1f} GB/s")
+    for rows, cols in ((3328, 512), (1632, 9490), (3328, 1536)):
+        x = torch.randn(rows, cols, device=dev).to(bf)
+        o = torch.empty(cols, device=dev)
+        t = time_launch(lambda: K.colsum(x, o))
+        print(f"colsum {rows}x{cols}: {t * 1e6:8.1f} us {x.numel() * 2 / t / 1e9:8.1f} GB/s")
+    rows, cols = 3328, 512
+    x = torch.randn(rows, cols, device=dev).to(bf)
+    g = torch.randn(cols, device=dev)
+    s = torch.empty_like(x)
+    y, mu, rs = K.add_layernorm(x, x, g, g, 1e-5, s_out=s)
+    dg = torch.zeros(cols, device=dev)
+    t = time_launch(lambda: K.add_layernorm(x, x, g, g, 1e-5, s_out=s))
+    print(f"add_ln fwd {rows}x{cols}: {t * 1e6:8.1f} us")
+    t = time_launch(lambda: K.add_layernorm_bwd(x, s, mu, rs, g, dg, dg, dr=y))
+    print(f"add_ln bwd {rows}x{cols}: {t * 1e6:8.1f} us")
+
+
+if __name__ == "__main__":
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "gemm"):
+        gemms()
+    if which in ("all", "misc"):
+        misc()
