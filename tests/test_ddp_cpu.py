@@ -1,0 +1,9 @@
+"""World-size-2 gloo run of the trainer's DDP path on CPU (trainMultiGPU.py:339-420): rank-0
+weight broadcast, SUM all-reduce of the flat gradient with the 1/world mean folded into the
+Adam step, fused metric all-reduce -- checked against the reference's own 2-rank run
+(tests/golden/ddp2_lstm, produced by trainMultiGPU.trainWithTeacherForcing under gloo DDP)."""
+import ddp_util
+
+
+def test_trainer_ddp2_matches_reference_trainMultiGPU(tmp_path):
+    ddp_util.check(ddp_util.run("oracle", tmp_path))

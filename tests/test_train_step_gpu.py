@@ -55,7 +55,10 @@ def test_graph_replay_matches_eager(hip_device, decoder):
     (m_e, p_e), (m_g, p_g) = runs
     for a, b in zip(m_e, m_g):
         assert abs(a[0] - b[0]) < 1e-5 * abs(a[0]) and a[1] == b[1] and abs(a[2] - b[2]) < 1e-3
-    torch.testing.assert_close(p_g, p_e, rtol=1e-5, atol=1e-6)
+    # bias / LayerNorm-affine / embedding gradients are reduced with float atomics (order varies
+    # run to run), and Adam's early steps amplify ULP-level gradient differences on entries with
+    # near-zero gradient: agree to 5% of one lr=1e-4 step
+    torch.testing.assert_close(p_g, p_e, rtol=1e-5, atol=5e-6)
 
 
 def test_graph_replays_draw_fresh_masks(hip_device):
@@ -75,3 +78,10 @@ def test_graph_replays_draw_fresh_masks(hip_device):
     again = tr.drain_metrics()[0][0]
     assert again == losses[0]
     K.set_seed_counter(None)
+
+
+def test_trainer_ddp2_hip_matches_reference_trainMultiGPU(hip_device, tmp_path):
+    """Two ranks (gloo, sharing the one GPU) through the HIP engine vs the reference's 2-rank
+    trainMultiGPU step (tests/golden/ddp2_lstm)."""
+    import ddp_util
+    ddp_util.check(ddp_util.run("hip", tmp_path))
