@@ -24,14 +24,16 @@ class Epilogue(ctypes.Structure):
         ("alpha", c_float), ("beta", c_float), ("drop_p", c_float), ("aux_scale", c_float),
         ("act", ctypes.c_int32), ("c_dtype", ctypes.c_int32), ("rows_per_scale", ctypes.c_int32),
         ("drop_stream", c_uint32),
+        ("split_k", ctypes.c_int32),
     ]
 
 
 class LstmDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("dtype", "B", "P", "E", "A", "D", "M", "T")] + [
         (n, c_void_p) for n in ("w_hcat", "b_hcat", "w_ih", "w_f", "enc", "att1", "xe", "c0", "dl", "g1", "alphas",
-                                "awe", "zs", "gates", "cs", "hs", "hprev", "g2", "w_ihz_t", "w_hcat_t", "dhs", "dalpha",
-                                "dcat", "dz", "dh", "dc", "de", "datt1", "dwf", "dbea")]
+                                "awe", "zs", "gates", "cs", "hs", "hprev", "w_zh_t", "w_att_t", "dhs", "dalpha",
+                                "dcat", "dz", "ws_y", "y_cnt", "dh", "dc", "de", "datt1", "dwf", "dbea")] + [
+        ("x_slices", ctypes.c_int32), ("y_slices", ctypes.c_int32)]
 
 
 class MhaDesc(ctypes.Structure):
@@ -47,6 +49,7 @@ class MhaDesc(ctypes.Structure):
 _SIGS = {
     "imgcap_version": [],
     "imgcap_set_seed_counter": [c_void_p],
+    "imgcap_cnblock_mlp": [c_int, c_int] + [c_void_p] * 7 + [c_int, c_void_p, c_void_p],
     "imgcap_stochastic_depth_scales": [c_int, c_int, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p],
     "imgcap_gemm": [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                     c_int64, c_void_p, c_int64, c_int64, c_int, ctypes.POINTER(Epilogue), c_void_p],

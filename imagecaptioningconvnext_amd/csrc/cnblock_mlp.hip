@@ -1,0 +1,262 @@
+// Fused ConvNeXt block MLP (torchvision CNBlock, reached via encoder.py:18-24):
+//   x[m, :] += gamma * sd[m / rows_per_sample] * (GELU(z[m, :] W1^T + b1) W2^T + b2)
+// with z = LN(dwconv7(x)) (dwconv7_ln), W1 [4C, C], W2 [C, 4C] (nn.Linear weights), bf16.
+// The 4C-wide hidden activation never leaves the chip: the block walks the hidden dimension
+// in chunks of HC, computing H = GELU(Z W1c^T + b1c) and immediately accumulating
+// O += H W2c^T; HBM traffic per row is z + x read and x written (6C bytes) instead of the
+// unfused 6C + 16C (hidden written by Linear1 and read back by Linear2).
+//
+// Block = 4 waves, BM rows; wave w owns rows [w*BM/4, +BM/4) of BOTH GEMMs, so its hidden
+// chunk goes accumulator -> LDS (per-wave region, layout change C-fragment -> A-fragment) ->
+// MFMA without a block barrier.  The Z rows of a wave stay in registers as A fragments for
+// the whole chunk loop; the W1/W2 chunks are shared by the 4 waves through a double-buffered
+// LDS stage (global loads of chunk i+1 in flight under chunk i's MFMAs).  Epilogue: fp32
+// tile through LDS, 8 columns per thread (16-byte residual loads and stores).
+#include "mfma.h"
+
+namespace imgcap {
+
+#ifndef MLP_GELU
+#define MLP_GELU 0
+#endif
+#ifndef MLP_TAG
+#define MLP_TAG "erf"
+#endif
+// GELU of the hidden activation.  MLP_GELU (kernel-variant experiments, tools/kbench): 0 =
+// erf form (torch nn.GELU default), 1 = identity (timing only), 2 = fast erf.
+DEV float mlp_gelu(float v) {
+#if MLP_GELU == 1
+  return v;
+#elif MLP_GELU == 2
+  return gelu_fast(v);
+#else
+  return gelu_erf(v);
+#endif
+}
+
+template <int C, int BM, int HC, bool ZL>
+struct MlpCfg {
+  static constexpr int WR = BM / 4;           // rows per wave
+  static constexpr int TM = WR / 16;
+  static constexpr int TN1 = HC / 16;         // hidden-chunk fragments per wave
+  static constexpr int TN2 = C / 16;          // output fragments per wave
+  static constexpr int KS1 = C / 32;          // k-steps of GEMM1
+  static constexpr int KS2 = HC / 32;         // k-steps of GEMM2
+  static constexpr int LD1 = C + 8;           // W1c image [HC][C] row stride (bf16)
+  static constexpr int LD2 = HC + 8;          // W2c image [C][HC]
+  static constexpr int LDH = HC + 8;          // per-wave hidden image [WR][HC]
+  static constexpr int BUFE = HC * LD1 + C * LD2;
+  static constexpr int HE = WR * LDH;
+  static constexpr int V1 = HC * C / 8 / 256;  // 16-byte vectors per thread per W1 chunk
+  static constexpr int V2 = C * HC / 8 / 256;
+  static constexpr int LDO = C + 4;            // fp32 epilogue image row stride
+  static constexpr int LDZ = C + 8;           // Z image [BM][C] (ZL: A fragments read from LDS)
+  static constexpr int ZE = ZL ? BM * LDZ : 0;
+  static constexpr int STAGE_BYTES = (BUFE + 4 * HE + ZE) * 2;
+  static constexpr int EPI_BYTES = BM * LDO * 4;
+  static constexpr int SMEM = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  static_assert(WR % 16 == 0 && C % 32 == 0 && HC % 32 == 0, "tile shape");
+  static_assert(V1 * 8 * 256 == HC * C && V2 * 8 * 256 == C * HC, "chunk must split evenly over 256 threads");
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+};
+
+// weight chunk staging: W1 rows [h0, h0+HC) -> image [HC][C]; W2 columns [h0, h0+HC) ->
+// image [C][HC]; one chunk in flight in registers while the previous one is consumed
+template <int C, int HC, int V1, int V2>
+DEV void mlp_load(uint4 (&r1)[V1], uint4 (&r2)[V2], const bf16* __restrict__ w1, const bf16* __restrict__ w2,
+                  int h0) {
+#pragma unroll
+  for (int i = 0; i < V1; ++i) {
+    const int v = threadIdx.x + i * 256, r = v / (C / 8), c = (v % (C / 8)) * 8;
+    r1[i] = *(const uint4*)(w1 + (long)(h0 + r) * C + c);
+  }
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    const int v = threadIdx.x + i * 256, n = v / (HC / 8), c = (v % (HC / 8)) * 8;
+    r2[i] = *(const uint4*)(w2 + (long)n * (4 * C) + h0 + c);
+  }
+}
+template <int C, int HC, int LD1, int LD2, int V1, int V2>
+DEV void mlp_store(bf16* buf, const uint4 (&r1)[V1], const uint4 (&r2)[V2]) {
+#pragma unroll
+  for (int i = 0; i < V1; ++i) {
+    const int v = threadIdx.x + i * 256, r = v / (C / 8), c = (v % (C / 8)) * 8;
+    *(uint4*)(buf + r * LD1 + c) = r1[i];
+  }
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    const int v = threadIdx.x + i * 256, n = v / (HC / 8), c = (v % (HC / 8)) * 8;
+    *(uint4*)(buf + HC * LD1 + n * LD2 + c) = r2[i];
+  }
+}
+
+template <int C, int BM, int HC, bool ZL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cnblock_mlp_kernel(int M, const bf16* __restrict__ z,
+                                                          const bf16* __restrict__ w1, const float* __restrict__ b1,
+                                                          const bf16* __restrict__ w2, const float* __restrict__ b2,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ sd, int rows_per_sample,
+                                                          bf16* __restrict__ x) {
+  using G = MlpCfg<C, BM, HC, ZL>;
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  bf16* wbuf = (bf16*)smem;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16* hbuf = wbuf + G::BUFE + w * G::HE;
+  bf16* zimg = wbuf + G::BUFE + 4 * G::HE;  // ZL only
+  const int m0 = blockIdx.x * BM;
+  const int wr0 = m0 + w * G::WR;
+
+  // this wave's Z rows as A fragments (row fr of each 16-row slab, k = 8*fq..): kept in
+  // registers for the whole chunk loop, or (ZL, wide C) staged once into an LDS image
+  constexpr int ZR = ZL ? 1 : G::TM, ZK = ZL ? 1 : G::KS1;
+  bf16x8 zf[ZR][ZK];
+  if constexpr (ZL) {
+    for (int v = threadIdx.x; v < BM * (C / 8); v += 256) {
+      const int r = v / (C / 8), c = (v % (C / 8)) * 8;
+      const int row = m0 + r;
+      const uint4 u = *(const uint4*)(z + (long)(row < M ? row : 0) * C + c);
+      *(uint4*)(zimg + r * G::LDZ + c) = row < M ? u : make_uint4(0u, 0u, 0u, 0u);
+    }
+  } else {
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm) {
+      const int row = wr0 + tm * 16 + fr;
+      const bool ok = row < M;
+      const bf16* zp = z + (long)(ok ? row : 0) * C + 8 * fq;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const uint4 u = *(const uint4*)(zp + ks * 32);
+        zf[tm][ks] = __builtin_bit_cast(bf16x8, ok ? u : make_uint4(0u, 0u, 0u, 0u));
+      }
+    }
+  }
+  f32x4 acc2[G::TM][G::TN2];
+#pragma unroll
+  for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < G::TN2; ++tn) acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 r1[G::V1], r2[G::V2];
+  mlp_load<C, HC>(r1, r2, w1, w2, 0);
+  mlp_store<C, HC, G::LD1, G::LD2>(wbuf, r1, r2);
+  __syncthreads();  // (also publishes the Z image)
+
+  constexpr int NCH = 4 * C / HC;
+  for (int ch = 0; ch < NCH; ++ch) {
+    const bf16* cur = wbuf;
+    // unconditional (the last iteration re-loads chunk 0, never stored to a live buffer):
+    // a conditional load would make the compiler keep r1/r2 in scratch across the branch
+    mlp_load<C, HC>(r1, r2, w1, w2, ((ch + 1) % NCH) * HC);
+    // GEMM1: H[WR, HC] = Z W1c^T
+    f32x4 acc1[G::TM][G::TN1];
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < G::TN1; ++tn) acc1[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+#pragma unroll
+      for (int tn = 0; tn < G::TN1; ++tn) {
+        const bf16x8 bfr = *(const bf16x8*)(cur + (tn * 16 + fr) * G::LD1 + ks * 32 + 8 * fq);
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) {
+          bf16x8 za;
+          if constexpr (ZL)
+            za = *(const bf16x8*)(zimg + (w * G::WR + tm * 16 + fr) * G::LDZ + ks * 32 + 8 * fq);
+          else
+            za = zf[tm < ZR ? tm : 0][ks < ZK ? ks : 0];
+          acc1[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(za, bfr, acc1[tm][tn], 0, 0, 0);
+        }
+      }
+    }
+    // bias + GELU -> bf16 hidden chunk in this wave's LDS image
+    const int h0 = ch * HC;
+#pragma unroll
+    for (int tn = 0; tn < G::TN1; ++tn) {
+      const float bb = b1[h0 + tn * 16 + fr];
+#pragma unroll
+      for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          hbuf[(tm * 16 + 4 * fq + r) * G::LDH + tn * 16 + fr] = (bf16)mlp_gelu(acc1[tm][tn][r] + bb);
+    }
+    // GEMM2: O[WR, C] += H W2c^T   (the hidden image is written and read by this wave only)
+    const bf16* w2c = cur + HC * G::LD1;
+#pragma unroll
+    for (int ks = 0; ks < G::KS2; ++ks) {
+      bf16x8 hf[G::TM];
+#pragma unroll
+      for (int tm = 0; tm < G::TM; ++tm) hf[tm] = *(const bf16x8*)(hbuf + (tm * 16 + fr) * G::LDH + ks * 32 + 8 * fq);
+#pragma unroll
+      for (int tn = 0; tn < G::TN2; ++tn) {
+        const bf16x8 bfr = *(const bf16x8*)(w2c + (tn * 16 + fr) * G::LD2 + ks * 32 + 8 * fq);
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+          acc2[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[tm], bfr, acc2[tm][tn], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done with the staged chunk
+    mlp_store<C, HC, G::LD1, G::LD2>(wbuf, r1, r2);
+    __syncthreads();
+  }
+
+  // epilogue: fp32 tile through LDS, then x += gamma * sd * (o + b2) on 8-column vectors
+  float* tile = (float*)smem;
+#pragma unroll
+  for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < G::TN2; ++tn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        tile[(w * G::WR + tm * 16 + 4 * fq + r) * G::LDO + tn * 16 + fr] = acc2[tm][tn][r];
+  __syncthreads();
+  constexpr int NV = C / 8;
+  for (int e = threadIdx.x; e < BM * NV; e += 256) {
+    const int r = e / NV, c = (e % NV) * 8;
+    const int m = m0 + r;
+    if (m >= M) continue;
+    const float s = sd ? sd[m / rows_per_sample] : 1.f;
+    bf16* xp = x + (long)m * C + c;
+    const bf16x8 xv = *(const bf16x8*)xp;
+    const f32x4 t0 = *(const f32x4*)(tile + r * G::LDO + c), t1 = *(const f32x4*)(tile + r * G::LDO + c + 4);
+    const f32x4 g0 = *(const f32x4*)(gamma + c), g1 = *(const f32x4*)(gamma + c + 4);
+    const f32x4 c0 = *(const f32x4*)(b2 + c), c1 = *(const f32x4*)(b2 + c + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (bf16)((float)xv[j] + (t0[j] + c0[j]) * g0[j] * s);
+      o[j + 4] = (bf16)((float)xv[j + 4] + (t1[j] + c1[j]) * g1[j] * s);
+    }
+    *(bf16x8*)xp = o;
+  }
+}
+
+}  // namespace imgcap
+
+using namespace imgcap;
+
+extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const void* w1, const float* b1, const void* w2,
+                                  const float* b2, const float* gamma, const float* sd, int rows_per_sample, void* x,
+                                  void* stream) {
+  if (M == 0) return 0;
+  IMGCAP_REQUIRE(aligned16(z) && aligned16(w1) && aligned16(w2) && aligned16(x) && aligned16(b1) &&
+                     aligned16(b2) && aligned16(gamma),
+                 "imgcap_cnblock_mlp: operands must be 16-byte aligned");
+  IMGCAP_REQUIRE(sd == nullptr || rows_per_sample > 0, "imgcap_cnblock_mlp: rows_per_sample");
+  hipStream_t st = (hipStream_t)stream;
+#define MLP_(CC, BM, HC, ZL)                                                                                 \
+  hipLaunchKernelGGL((cnblock_mlp_kernel<CC, BM, HC, ZL>), dim3((M + BM - 1) / BM), dim3(256), 0, st, M,         \
+                     (const bf16*)z, (const bf16*)w1, b1, (const bf16*)w2, b2, gamma, sd, rows_per_sample, \
+                     (bf16*)x)
+  switch (C) {
+    case 96: MLP_(96, 128, 64, false); break;
+    case 128: MLP_(128, 128, 64, false); break;
+    case 192: MLP_(192, 128, 32, false); break;
+    case 384: MLP_(384, 64, 32, true); break;
+    default: return fail(IMGCAP_EUNSUPPORTED, "imgcap_cnblock_mlp: C must be 96, 128, 192 or 384");
+  }
+#undef MLP_
+  IMGCAP_CHECK_LAUNCH("imgcap_cnblock_mlp");
+  return 0;
+}

@@ -21,6 +21,8 @@ namespace imgcap {
 // ---- error plumbing (host) -------------------------------------------------------------
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
+// process-wide device scratch of at least `bytes` (NULL on allocation failure); see abi.cpp
+void* workspace(size_t bytes);
 
 #define IMGCAP_CHECK_LAUNCH(what)                                                   \
   do {                                                                             \
@@ -127,6 +129,15 @@ DEV float dropout_scale(uint64_t seed, uint32_t stream, uint64_t idx, float p) {
 }
 
 DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// erf-form GELU with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, below the bf16
+// rounding of the result): one exp and one reciprocal instead of the library erff
+DEV float gelu_fast(float x) {
+  const float u = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.f + 0.3275911f * u);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float e = 1.f - poly * __expf(-u * u);  // erf(|x|/sqrt 2)
+  return 0.5f * x * (1.f + copysignf(e, x));
+}
 DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
 }  // namespace imgcap

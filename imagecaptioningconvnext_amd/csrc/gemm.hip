@@ -20,59 +20,9 @@
 #include <algorithm>
 
 #include "common.h"
+#include "mfma.h"
 
 namespace imgcap {
-
-template <typename T> struct Frag;
-template <> struct Frag<bf16> { bf16x8 v; };
-template <> struct Frag<float> { f32x4 lo, hi; };
-
-DEV void mma(f32x4& acc, const Frag<bf16>& a, const Frag<bf16>& b) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc, 0, 0, 0);
-}
-DEV void mma(f32x4& acc, const Frag<float>& a, const Frag<float>& b) {
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[kk], b.lo[kk], acc, 0, 0, 0);
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[kk], b.hi[kk], acc, 0, 0, 0);
-}
-
-template <typename T> DEV Frag<T> frag_from(const uint4& lo, const uint4& hi);
-template <> DEV Frag<bf16> frag_from<bf16>(const uint4& lo, const uint4&) {
-  Frag<bf16> f;
-  f.v = __builtin_bit_cast(bf16x8, lo);
-  return f;
-}
-template <> DEV Frag<float> frag_from<float>(const uint4& lo, const uint4& hi) {
-  Frag<float> f;
-  f.lo = __builtin_bit_cast(f32x4, lo);
-  f.hi = __builtin_bit_cast(f32x4, hi);
-  return f;
-}
-
-template <typename T> DEV Frag<T> lds_frag(const T* p);
-template <> DEV Frag<bf16> lds_frag<bf16>(const bf16* p) { Frag<bf16> f; f.v = *(const bf16x8*)p; return f; }
-template <> DEV Frag<float> lds_frag<float>(const float* p) {
-  Frag<float> f; f.lo = *(const f32x4*)p; f.hi = *(const f32x4*)(p + 4); return f;
-}
-
-// zero the elements of a 16-byte vector whose index >= nvalid (0..VEC); word-wise, in registers
-template <typename T>
-DEV uint4 mask_tail(uint4 v, int nvalid) {
-  constexpr int EPW = 4 / sizeof(T);  // elements per 32-bit word
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e0 = i * EPW;
-    if (EPW == 1) {
-      if (e0 >= nvalid) w[i] = 0u;
-    } else {
-      if (e0 >= nvalid) w[i] = 0u;
-      else if (e0 + 1 >= nvalid) w[i] &= 0xFFFFu;
-    }
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
 
 // ---------------------------------------------------------------------------------------
 // epilogue on 8 consecutive columns of one row (n0 .. n0+7), all in range and 16-B aligned
@@ -191,104 +141,68 @@ DEV void epilogue_from_lds(const imgcap_epilogue& ep, const float* tile, int LDT
   }
 }
 
+// split-K partial tile -> its slice of the workspace P[z][M][N] (row pitch N, plain stores)
+template <int BN>
+DEV void partial_from_lds(const float* tile, int LDT, int rows, int m_base, int n_base, int M, int N,
+                          float* P) {
+  constexpr int NV = BN / 4;
+  const bool vec = (N & 3) == 0;
+  for (int e = threadIdx.x; e < rows * NV; e += blockDim.x) {
+    const int r = e / NV, c4 = (e % NV) * 4;
+    const int m = m_base + r, n = n_base + c4;
+    if (m >= M || n >= N) continue;
+    const f32x4 v = *(const f32x4*)(tile + r * LDT + c4);
+    float* dst = P + (long)m * N + n;
+    if (vec) {
+      *(f32x4*)dst = v;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j < N) dst[j] = v[j];
+    }
+  }
+}
+
+// C[m, n] = alpha * sum_z P[z][m][n] + beta * C[m, n]   (fixed slice order: deterministic)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S, const float* __restrict__ P,
+                                                            float* __restrict__ C, long ldc, float alpha,
+                                                            float beta) {
+  const long total = (long)M * N;
+  const long plane = total;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    float t = 0.f;
+    for (int z = 0; z < S; ++z) t += P[z * plane + i];
+    const int m = (int)(i / N), n = (int)(i % N);
+    float* c = C + (long)m * ldc + n;
+    *c = alpha * t + (beta != 0.f ? beta * *c : 0.f);
+  }
+}
+
 #include "gemm_tiled.h"
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
 // SW waves split K; each wave issues the loads of up to DEPTH k-steps at once (one memory
 // round trip per chunk), fragments go straight from global memory to the MFMAs.
-template <typename T> struct SkinnyLd {
-  static constexpr int H = sizeof(T) == 4 ? 2 : 1;  // 16-byte vectors per 8-element fragment
-};
-
-template <typename T>
-DEV void skinny_load(uint4 (&dst)[SkinnyLd<T>::H], const T* row, int k0, int K, bool row_ok) {
-  constexpr int H = SkinnyLd<T>::H;
-  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-  const bool kin = row_ok && k0 < K;
-  const int ck = kin ? k0 : 0;
-  dst[0] = *(const uint4*)(row + ck);
-  if (H == 2) dst[H - 1] = (ck + 4 < K) ? *(const uint4*)(row + ck + 4) : zero;
-  if (!kin) {
-#pragma unroll
-    for (int h = 0; h < H; ++h) dst[h] = zero;
-  } else if (k0 + 8 > K) {
-    dst[0] = mask_tail<T>(dst[0], K - k0);
-    if (H == 2) dst[H - 1] = mask_tail<T>(dst[H - 1], K - k0 - 4);
-  }
-}
-
 template <typename T, int MT, int SW, int DEPTH>
 __global__ __launch_bounds__(64 * SW) void gemm_skinny_kernel(const T* __restrict__ A, long lda,
                                                               const T* __restrict__ B, long ldb,
                                                               void* __restrict__ C, long ldc, int M, int N, int K,
                                                               imgcap_epilogue ep, int vec_ok,
                                                               const uint64_t* seed_ctr) {
-  constexpr int H = SkinnyLd<T>::H;
   if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
-  constexpr int LDT = 16 + 4;
-  __shared__ __attribute__((aligned(16))) float part[SW][MT * 16][LDT];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(16))) float part[SW][MT * 16][SKINNY_LDT];
   const int n0 = blockIdx.x * 16;
-  const int fr = lane & 15, fk = 8 * (lane >> 4);
-  const int nks = (K + 31) / 32;
-  const int per = (nks + SW - 1) / SW;
-  const int ks0 = w * per, ks1 = min(nks, ks0 + per);
-  const T* arow[MT];
-  bool aok[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) {
-    const int m = t * 16 + fr;
-    aok[t] = m < M;
-    arow[t] = A + (long)(aok[t] ? m : 0) * lda;
-  }
-  const int n = n0 + fr;
+  const int n = n0 + (threadIdx.x & 15);
   const bool bok = n < N;
-  const T* brow = B + (long)(bok ? n : N - 1) * ldb;
-  f32x4 acc[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int base = ks0; base < ks1; base += DEPTH) {
-    const int cnt = min(DEPTH, ks1 - base);
-    uint4 ar[DEPTH][MT][H], br[DEPTH][H];
-#pragma unroll
-    for (int i = 0; i < DEPTH; ++i) {
-      if (i < cnt) {
-        const int k0 = (base + i) * 32 + fk;
-        skinny_load<T>(br[i], brow, k0, K, bok);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) skinny_load<T>(ar[i][t], arow[t], k0, K, aok[t]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < DEPTH; ++i) {
-      if (i < cnt) {
-        const Frag<T> fb = frag_from<T>(br[i][0], br[i][H - 1]);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) mma(acc[t], frag_from<T>(ar[i][t][0], ar[i][t][H - 1]), fb);
-      }
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < MT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) part[w][t * 16 + 4 * (lane >> 4) + r][fr] = acc[t][r];
-  __syncthreads();
-  for (int e = threadIdx.x; e < MT * 16 * 16; e += 64 * SW) {
-    const int r = e / 16, c = e % 16;
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < SW; ++q) s += part[q][r][c];
-    part[0][r][c] = s;
-  }
-  __syncthreads();
-  epilogue_from_lds<16>(ep, &part[0][0][0], LDT, MT * 16, 0, n0, M, N, C, ldc, 0, vec_ok != 0);
+  skinny_tile<T, MT, SW, DEPTH>(A, lda, M, B + (long)(bok ? n : N - 1) * ldb, bok, K, part);
+  epilogue_from_lds<16>(ep, &part[0][0][0], SKINNY_LDT, MT * 16, 0, n0, M, N, C, ldc, 0, vec_ok != 0);
 }
 
 template <typename T>
 static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
                          long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
-                         int vec_ok, hipStream_t st) {
+                         int vec_ok, hipStream_t st, int split) {
   if (M <= 64 && ak && bk && batch == 1) {
     const int blocks = (N + 15) / 16;
     const bool wide = blocks < 96;  // few column blocks: split K over 16 waves instead of 8
@@ -297,17 +211,37 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
 #define SK_(MT, SW, DEPTH)                                                                                   \
   hipLaunchKernelGGL((gemm_skinny_kernel<T, MT, SW, DEPTH>), dim3(blocks), dim3(64 * SW), 0, st, a, lda, b, ldb, C, \
                      ldc, M, N, K, ep, vec_ok, g_seed_ctr)
+    // DEPTH = the wave's k-step count rounded up to a power of two (all loads of a wave in one
+    // round trip); capped by registers (fp32 fragments are twice as wide)
+    const int per = ((K + 31) / 32 + (wide ? 16 : 8) - 1) / (wide ? 16 : 8);
+    const int depth = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : 8;
     constexpr bool F32 = sizeof(T) == 4;
+#define SK_W(MT, SW)                                              \
+  do {                                                            \
+    if (depth <= 1) SK_(MT, SW, 1);                               \
+    else if (F32 || depth <= 2) SK_(MT, SW, 2);                   \
+    else if (depth <= 4 || MT == 4) SK_(MT, SW, (F32 ? 2 : 4));   \
+    else SK_(MT, SW, (F32 || MT == 4 ? 2 : 8));                   \
+  } while (0)
     if (M <= 32) {
-      if (wide) SK_(2, 16, F32 ? 2 : 4); else SK_(2, 8, F32 ? 2 : 8);
+      if (wide) SK_W(2, 16); else SK_W(2, 8);
     } else {
-      if (wide) SK_(4, 16, 2); else SK_(4, 8, F32 ? 2 : 4);
+      if (wide) SK_W(4, 16); else SK_W(4, 8);
     }
+#undef SK_W
 #undef SK_
     IMGCAP_CHECK_LAUNCH("imgcap_gemm(skinny)");
     return 0;
   }
   const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
+  if (split != 1) {
+    // long-K reductions into a small fp32 output (weight gradients): 128x128 tiles, K sliced
+    // so that the grid reaches ~2 blocks per CU with >= 4 k-tiles per slice
+    if (split < 0) split = (int)std::max(1L, std::min({512 / std::max(tiles128, 1L), (long)K / 256, 32L}));
+    if (split > 1)
+      return launch_tiled<T, 128, 128, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, 1, ep, vec_ok, st,
+                                           split);
+  }
   if (tiles128 < 512)
     return launch_tiled<T, 64, 64, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
   return launch_tiled<T, 128, 128, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
@@ -409,20 +343,20 @@ extern "C" int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, 
   const bool vec_ok = aligned16(C) && ldc % 8 == 0 && strideC % 8 == 0 &&
                       (epi->res == nullptr || (aligned16(epi->res) && epi->ldr % 8 == 0)) &&
                       (epi->aux == nullptr || epi->ldaux % 8 == 0);
+  int split = 1;
+  if (epi->split_k != 0 && epi->split_k != 1) {
+    IMGCAP_REQUIRE(epi->c_dtype == IMGCAP_F32 && batch == 1 && !epi->bias && !epi->colscale && !epi->rowscale &&
+                       !epi->res && !epi->aux && epi->act == IMGCAP_ACT_NONE && epi->drop_p == 0.f,
+                   "imgcap_gemm: split_k needs an fp32 C = alpha*A.B + beta*C (no other epilogue, batch 1)");
+    split = epi->split_k;
+  }
   hipStream_t st = (hipStream_t)stream;
   if (dtype == IMGCAP_BF16)
     return gemm_dispatch<bf16>(a_kmajor, b_kmajor, M, N, K, A, lda, strideA, B, ldb, strideB, C, ldc, strideC,
-                               batch, *epi, vec_ok, st);
+                               batch, *epi, vec_ok, st, split);
   return gemm_dispatch<float>(a_kmajor, b_kmajor, M, N, K, A, lda, strideA, B, ldb, strideB, C, ldc, strideC,
-                              batch, *epi, vec_ok, st);
+                              batch, *epi, vec_ok, st, split);
 }
-
-namespace {
-// Row-slice partials of imgcap_colsum.  Grown on demand (first at the warm-up step, before any
-// graph capture); one buffer per process, used by one stream at a time.
-float* g_colsum_ws = nullptr;
-size_t g_colsum_ws_bytes = 0;
-}  // namespace
 
 extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64_t ldx, float* out, float beta,
                              void* stream) {
@@ -434,16 +368,8 @@ extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64
   slices = rows > 0 ? (rows + rps - 1) / rps : 1;
   float* dst = out;
   if (slices > 1) {
-    const size_t need = (size_t)slices * cols * sizeof(float);
-    if (need > g_colsum_ws_bytes) {
-      if (g_colsum_ws) (void)hipFree(g_colsum_ws);
-      g_colsum_ws = nullptr;
-      g_colsum_ws_bytes = 0;
-      const size_t bytes = std::max(need, (size_t)4 << 20);
-      if (hipMalloc(&g_colsum_ws, bytes) != hipSuccess) return fail(IMGCAP_EINVAL, "imgcap_colsum: workspace");
-      g_colsum_ws_bytes = bytes;
-    }
-    dst = g_colsum_ws;
+    dst = (float*)workspace((size_t)slices * cols * sizeof(float));
+    if (!dst) return fail(IMGCAP_EINVAL, "imgcap_colsum: workspace allocation failed");
   }
   const dim3 grid(cblocks, slices);
   const int vec_ok = aligned16(x) && ldx % 8 == 0;

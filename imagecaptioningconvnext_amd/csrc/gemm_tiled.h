@@ -123,14 +123,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long
                                                    const T* __restrict__ B, long ldb, long sB,
                                                    void* __restrict__ C, long ldc, long sC,
                                                    int M, int N, int K, imgcap_epilogue ep, int vec_ok,
-                                                   const uint64_t* seed_ctr) {
+                                                   const uint64_t* seed_ctr, int kslice) {
   using G = GemmCfg<T, BM, BN, BK, AK, BKM>;
   if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   T* As = (T*)smem;
   T* Bs = As + G::A_ELEMS;
 
-  const int bz = blockIdx.z;
+  // grid.z = batch entries, or K slices (kslice > 0: slice z covers k in [z*kslice, +kslice)
+  // and stores its partial tile into plane z of the fp32 workspace C = P[z][M][N])
+  const int bz = kslice ? 0 : blockIdx.z;
+  const int kt0 = kslice ? blockIdx.z * (kslice / BK) : 0;
   A += bz * sA;
   B += bz * sB;
   const long cbase = (long)bz * sC;
@@ -148,14 +151,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long
     for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[G::A_VECS], rbv[G::B_VECS];
-  tile_load<T, BM, BK, G::A_VECS, AK>(ra, A, lda, m0, 0, M, K);
-  tile_load<T, BN, BK, G::B_VECS, BKM>(rbv, B, ldb, n0, 0, N, K);
+  tile_load<T, BM, BK, G::A_VECS, AK>(ra, A, lda, m0, kt0 * BK, M, K);
+  tile_load<T, BN, BK, G::B_VECS, BKM>(rbv, B, ldb, n0, kt0 * BK, N, K);
   tile_store<T, BM, BK, G::A_VECS, AK, G::LDK, G::LDA_T>(As, ra);
   tile_store<T, BN, BK, G::B_VECS, BKM, G::LDK, G::LDB_T>(Bs, rbv);
   __syncthreads();
 
-  const int nk = (K + BK - 1) / BK;
-  for (int kt = 0; kt < nk; ++kt) {
+  const int nk = kslice ? min((K + BK - 1) / BK, kt0 + kslice / BK) : (K + BK - 1) / BK;
+  for (int kt = kt0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) {
       tile_load<T, BM, BK, G::A_VECS, AK>(ra, A, lda, m0, (kt + 1) * BK, M, K);
@@ -196,8 +199,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long
             tile[(i * 16 + 4 * (lane >> 4) + r) * G::LDT + cb + j * 16 + fr] = acc[i][j][r];
     }
     __syncthreads();
-    epilogue_from_lds<BN>(ep, tile, G::LDT, G::EPI_ROWS, m0 + pass * G::EPI_ROWS, n0, M, N, C, ldc, cbase,
-                          vec_ok != 0);
+    if (kslice)
+      partial_from_lds<BN>(tile, G::LDT, G::EPI_ROWS, m0 + pass * G::EPI_ROWS, n0, M, N,
+                           (float*)C + (long)blockIdx.z * M * N);
+    else
+      epilogue_from_lds<BN>(ep, tile, G::LDT, G::EPI_ROWS, m0 + pass * G::EPI_ROWS, n0, M, N, C, ldc, cbase,
+                            vec_ok != 0);
     __syncthreads();
   }
 }
@@ -205,18 +212,33 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, long
 template <typename T, int BM, int BN, int BK>
 static int launch_tiled(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
                         long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
-                        int vec_ok, hipStream_t st) {
-  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
+                        int vec_ok, hipStream_t st, int split = 1) {
+  // split > 1 (batch == 1): K cut into `split` BK-aligned slices, one grid.z layer each, whose
+  // partial products go to workspace planes; splitk_reduce_kernel then finishes C
+  const int kslice = split > 1 ? ((K + split - 1) / split + BK - 1) / BK * BK : 0;
+  const int zdim = split > 1 ? (K + kslice - 1) / kslice : batch;
+  void* Cout = C;
+  if (split > 1) {
+    C = workspace((size_t)zdim * M * N * sizeof(float));
+    if (!C) return fail(IMGCAP_EINVAL, "imgcap_gemm: split-K workspace allocation failed");
+  }
+  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, zdim);
   const T* a = (const T*)A;
   const T* b = (const T*)B;
 #define L_(AKV, BKV)                                                                                             \
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, BK, AKV, BKV>), grid, dim3(256), 0, st, a, lda, sA, b, ldb, sB, C, ldc, \
-                     sC, M, N, K, ep, vec_ok, g_seed_ctr)
+                     sC, M, N, K, ep, vec_ok, g_seed_ctr, kslice)
   if (ak && bk) L_(true, true);
   else if (ak && !bk) L_(true, false);
   else if (!ak && bk) L_(false, true);
   else L_(false, false);
 #undef L_
+  if (split > 1) {
+    const long total = (long)M * N;
+    const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, N, zdim, (const float*)C,
+                       (float*)Cout, ldc, ep.alpha, ep.beta);
+  }
   IMGCAP_CHECK_LAUNCH("imgcap_gemm");
   return 0;
 }

@@ -15,10 +15,19 @@
 //   * backward keeps only the recurrent chain in the loop: the encoder_att / full_att weight
 //     gradients are summed over t in ONE pass afterwards (attn_param_grad_kernel), from the
 //     saved softmax-input gradients de[b,t,p]
-// Per step (forward): skinny GEMM(h->g1) -> attn_fwd -> skinny GEMM(z->g2) -> cell_fwd.
-// Backward: cell_bwd -> skinny GEMM(dgates->dz) -> attn_bwd -> skinny GEMM(dcat->dh), with
-// the weights pre-transposed (w_ihz_t, w_hcat_t) so every step GEMM is k-major x k-major.
-#include "common.h"
+// Per step, three launches each way:
+//   forward : skinny GEMM h_{t-1} -> g1 = [att2 | gate_pre | hh]
+//             -> attn_fwd (scores, softmax, context, sigmoid gate)
+//             -> gate_cell_fwd (z_t W_ih[:, M:]^T with the four gates of 4 units per 16-column
+//                block, LSTMCell pointwise in the epilogue)
+//   backward: x_partial (dgates_t . [W_ih[:, M:] | W_hh], K split over the grid into slabs)
+//             -> attn_bwd (sums the dz slabs) -> dh_cell (dh_{t-1} = [d att2 | d gate_pre] .
+//                [W_da; W_fb] + the W_hh slabs, K split over the grid, last-arriving block per
+//                column tile reduces and runs the LSTMCell backward of step t-1 in the epilogue)
+// with the weights pre-transposed so every step GEMM is k-major x k-major.
+#include <algorithm>
+
+#include "mfma.h"
 
 namespace imgcap {
 
@@ -93,61 +102,147 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
   }
 }
 
-// ---- forward LSTMCell pointwise (torch gate order i, f, g, o) --------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void cell_fwd_kernel(imgcap_lstm_desc d, int t) {
-  const int D = d.D, Tn = d.T;
-  const int W3 = d.A + d.E + 4 * D;
-  const long n = (long)d.B * D;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const int b = (int)(e / D), j = (int)(e % D);
+// ---- forward: input GEMM of the attention half + LSTMCell (torch gate order i, f, g, o) ----
+// Block x owns units 4x..4x+3: its 16 columns are gate q = c/4 of unit 4x + c%4 (B row
+// q*D + unit of W_ih[:, M:]), so all four gates of a unit meet in one block's tile.
+// Rows go in groups of RG = 32 (blockIdx.y).
+constexpr int RG = 32;
+constexpr int RG_MT = RG / 16;
+template <typename T, int SW, int DEPTH>
+__global__ __launch_bounds__(64 * SW) void gate_cell_fwd_kernel(imgcap_lstm_desc d, int t) {
+  __shared__ __attribute__((aligned(16))) float part[SW][RG][SKINNY_LDT];
+  const int D = d.D, E = d.E, Tn = d.T;
+  const int W3 = d.A + E + 4 * D;
+  const int r0 = blockIdx.y * RG, rows = min(RG, d.B - r0);
+  const int c = threadIdx.x & 15;
+  const T* brow = (const T*)d.w_ih + (long)((c >> 2) * D + blockIdx.x * 4 + (c & 3)) * (d.M + E) + d.M;
+  skinny_tile<T, RG_MT, SW, DEPTH>((const T*)d.zs + ((long)r0 * Tn + t) * E, (long)Tn * E, rows, brow, true, E,
+                                   part);
+  for (int e = threadIdx.x; e < rows * 4; e += 64 * SW) {
+    const int b = r0 + (e >> 2), jj = e & 3, j = blockIdx.x * 4 + jj;
     const long bt = (long)b * Tn + t;
     const float* xe = d.xe + bt * 4 * D;
-    const float* hh = d.g1 + bt * W3 + d.A + d.E;
-    const float* g2 = d.g2 + (long)b * 4 * D;
-    const float gi = sigmoidf_(xe[j] + hh[j] + g2[j]);
-    const float gf = sigmoidf_(xe[D + j] + hh[D + j] + g2[D + j]);
-    const float gg = tanhf(xe[2 * D + j] + hh[2 * D + j] + g2[2 * D + j]);
-    const float go = sigmoidf_(xe[3 * D + j] + hh[3 * D + j] + g2[3 * D + j]);
+    const float* hh = d.g1 + bt * W3 + d.A + E;
+    float g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[q] = part[0][b - r0][q * 4 + jj] + xe[q * D + j] + hh[q * D + j];
+    const float gi = sigmoidf_(g[0]), gf = sigmoidf_(g[1]), gg = tanhf(g[2]), go = sigmoidf_(g[3]);
     const float cp = t == 0 ? d.c0[(long)b * D + j] : d.cs[(bt - 1) * D + j];
-    const float c = gf * cp + gi * gg;
-    const float h = go * tanhf(c);
+    const float cn = gf * cp + gi * gg;
+    const float h = go * tanhf(cn);
     float* ga = d.gates + bt * 4 * D;
     ga[j] = gi; ga[D + j] = gf; ga[2 * D + j] = gg; ga[3 * D + j] = go;
-    d.cs[bt * D + j] = c;
+    d.cs[bt * D + j] = cn;
     ((T*)d.hs)[bt * D + j] = from_f<T>(h);
     if (t + 1 < Tn) ((T*)d.hprev)[(bt + 1) * D + j] = from_f<T>(h);
   }
 }
 
-// ---- backward LSTMCell pointwise -----------------------------------------------------
+// LSTMCell backward of one (row, unit) at step t given dL/dh_t from the later steps (dh_next,
+// without the fc term) and the carried dL/dc_t in d.dc; writes d gates_preact into dcat and
+// the carry dL/dc_{t-1}.  Rows past their decode length contribute nothing.
 template <typename T>
-__global__ __launch_bounds__(256) void cell_bwd_kernel(imgcap_lstm_desc d, int t) {
+DEV void cell_bwd_point(const imgcap_lstm_desc& d, int t, int b, int j, float dh_next, bool has_next) {
   const int D = d.D, Tn = d.T;
   const int W3 = d.A + d.E + 4 * D;
-  const long n = (long)d.B * D;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const int b = (int)(e / D), j = (int)(e % D);
-    const long bt = (long)b * Tn + t;
-    T* dg = (T*)d.dcat + bt * W3 + d.A + d.E;
-    if (t >= d.dl[b]) {
-      dg[j] = dg[D + j] = dg[2 * D + j] = dg[3 * D + j] = from_f<T>(0.f);
-      d.dc[e] = 0.f;
-      continue;
+  const long bt = (long)b * Tn + t;
+  const long e = (long)b * D + j;
+  T* dg = (T*)d.dcat + bt * W3 + d.A + d.E;
+  if (t >= d.dl[b]) {
+    dg[j] = dg[D + j] = dg[2 * D + j] = dg[3 * D + j] = from_f<T>(0.f);
+    d.dc[e] = 0.f;
+    return;
+  }
+  const float dh = to_f(((const T*)d.dhs)[bt * D + j]) + (has_next ? dh_next : 0.f);
+  const float* ga = d.gates + bt * 4 * D;
+  const float gi = ga[j], gf = ga[D + j], gg = ga[2 * D + j], go = ga[3 * D + j];
+  const float c = d.cs[bt * D + j];
+  const float cp = t == 0 ? d.c0[e] : d.cs[(bt - 1) * D + j];
+  const float tc = tanhf(c);
+  const float dct = (has_next ? d.dc[e] : 0.f) + dh * go * (1.f - tc * tc);
+  dg[j] = from_f<T>(dct * gg * gi * (1.f - gi));
+  dg[D + j] = from_f<T>(dct * cp * gf * (1.f - gf));
+  dg[2 * D + j] = from_f<T>(dct * gi * (1.f - gg * gg));
+  dg[3 * D + j] = from_f<T>(dh * tc * go * (1.f - go));
+  d.dc[e] = dct * gf;
+}
+
+// ---- backward: LSTMCell of the last step (no carry from later steps) ------------------
+template <typename T>
+__global__ __launch_bounds__(256) void cell_bwd_last_kernel(imgcap_lstm_desc d) {
+  const long n = (long)d.B * d.D;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256)
+    cell_bwd_point<T>(d, d.T - 1, (int)(e / d.D), (int)(e % d.D), 0.f, false);
+}
+
+// ---- backward: dgates_t . [W_ih[:, M:] | W_hh]  -> K-slice partial slabs ----------------
+// grid (ceil((E+D)/16), x_slices, row groups); slab z = d.dz[z][B][E + D]: columns < E are
+// dL/dz_t, the rest the W_hh part of dL/dh_{t-1}.  Consumers add the slabs.
+template <typename T, int SW, int DEPTH>
+__global__ __launch_bounds__(64 * SW) void x_partial_kernel(imgcap_lstm_desc d, int t, int kslice) {
+  __shared__ __attribute__((aligned(16))) float part[SW][RG][SKINNY_LDT];
+  const int r0 = blockIdx.z * RG, rows = min(RG, d.B - r0);
+  const int D = d.D, E = d.E, NX = E + D, K4 = 4 * D;
+  const int W3 = d.A + E + K4;
+  const int k0 = blockIdx.y * kslice, klen = min(K4 - k0, kslice);
+  const int n0 = blockIdx.x * 16, n = n0 + (threadIdx.x & 15);
+  const bool bok = n < NX;
+  const T* A = (const T*)d.dcat + ((long)r0 * d.T + t) * W3 + d.A + E + k0;
+  const T* brow = (const T*)d.w_zh_t + (long)(bok ? n : 0) * K4 + k0;
+  skinny_tile<T, RG_MT, SW, DEPTH>(A, (long)d.T * W3, rows, brow, bok, klen, part);
+  float* slab = d.dz + ((long)blockIdx.y * d.B + r0) * NX;
+  for (int e = threadIdx.x; e < rows * 16; e += 64 * SW) {
+    const int r = e >> 4, c = e & 15;
+    if (n0 + c < NX) slab[(long)r * NX + n0 + c] = part[0][r][c];
+  }
+}
+
+// ---- backward: dh_{t-1} = [d att2 | d gate_pre]_t . [W_da; W_fb] + W_hh slabs, then the
+// LSTMCell backward of step t-1 (t >= 1) or dL/dh0 (t == 0).  grid (D/16, y_slices, row
+// groups): each block publishes its K-slice tile; the last arriving block of a column tile (agent-scope
+// release/acquire around a relaxed ticket, cdna_hip_programming.md §5 "Projection GEMM",
+// item 2) sums the slabs in slice order and runs the epilogue.  y_cnt returns to 0.
+template <typename T, int SW, int DEPTH>
+__global__ __launch_bounds__(64 * SW) void dh_cell_kernel(imgcap_lstm_desc d, int t, int kslice) {
+  __shared__ __attribute__((aligned(16))) float part[SW][RG][SKINNY_LDT];
+  __shared__ int is_last;
+  const int D = d.D, E = d.E, KY = d.A + E, NX = E + D;
+  const int W3 = KY + 4 * D;
+  const int ntile = gridDim.x, S = gridDim.y;
+  const int r0 = blockIdx.z * RG, rows = min(RG, d.B - r0);
+  const int tile = blockIdx.z * ntile + blockIdx.x;  // counter / slab index of (row group, columns)
+  const int k0 = blockIdx.y * kslice, klen = min(KY - k0, kslice);
+  const int n0 = blockIdx.x * 16, n = n0 + (threadIdx.x & 15);
+  const T* A = (const T*)d.dcat + ((long)r0 * d.T + t) * W3 + k0;
+  const T* brow = (const T*)d.w_att_t + (long)n * KY + k0;
+  skinny_tile<T, RG_MT, SW, DEPTH>(A, (long)d.T * W3, rows, brow, true, klen, part);
+  constexpr int TILE = RG * 16;
+  const long ntiles = (long)ntile * gridDim.z;
+  float* slab = d.ws_y + ((long)blockIdx.y * ntiles + tile) * TILE;
+  for (int e = threadIdx.x; e < TILE; e += 64 * SW) slab[e] = part[0][e >> 4][e & 15];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ticket = __hip_atomic_fetch_add(d.y_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = ticket == S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(d.y_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const bool last = t + 1 >= Tn;  // no carry into the last step
-    const float dh = to_f(((const T*)d.dhs)[bt * D + j]) + (last ? 0.f : d.dh[e]);
-    const float* ga = d.gates + bt * 4 * D;
-    const float gi = ga[j], gf = ga[D + j], gg = ga[2 * D + j], go = ga[3 * D + j];
-    const float c = d.cs[bt * D + j];
-    const float cp = t == 0 ? d.c0[e] : d.cs[(bt - 1) * D + j];
-    const float tc = tanhf(c);
-    const float dct = (last ? 0.f : d.dc[e]) + dh * go * (1.f - tc * tc);
-    dg[j] = from_f<T>(dct * gg * gi * (1.f - gi));
-    dg[D + j] = from_f<T>(dct * cp * gf * (1.f - gf));
-    dg[2 * D + j] = from_f<T>(dct * gi * (1.f - gg * gg));
-    dg[3 * D + j] = from_f<T>(dh * tc * go * (1.f - go));
-    d.dc[e] = dct * gf;
+    is_last = last;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  for (int e = threadIdx.x; e < rows * 16; e += 64 * SW) {
+    const int b = r0 + (e >> 4), j = n0 + (e & 15);
+    float dh = 0.f;
+    for (int z = 0; z < S; ++z) dh += d.ws_y[((long)z * ntiles + tile) * TILE + e];
+    for (int z = 0; z < d.x_slices; ++z) dh += d.dz[((long)z * d.B + b) * NX + E + j];
+    if (t == 0) d.dh[(long)b * D + j] = dh;
+    else cell_bwd_point<T>(d, t - 1, b, j, dh, true);
   }
 }
 
@@ -170,12 +265,14 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
   float* dal = al + MAXP;        // [MAXP]
   float* part = dal + MAXP;      // [2][A]
   const float* g1 = d.g1 + bt * W3;
-  const float* dz = d.dz + (long)b * E;
+  const int NX = E + d.D;
   const float* awe = d.awe + bt * E;
   for (int e = threadIdx.x; e < E; e += ATT_THREADS) {
+    float dz = 0.f;  // dL/dz_t = sum of the x_partial slabs
+    for (int z = 0; z < d.x_slices; ++z) dz += d.dz[((long)z * d.B + b) * NX + e];
     const float s = sigmoidf_(g1[A + e]);
-    dawe[e] = dz[e] * s;
-    dcat[A + e] = from_f<T>(dz[e] * awe[e] * s * (1.f - s));  // d gate_pre
+    dawe[e] = dz * s;
+    dcat[A + e] = from_f<T>(dz * awe[e] * s * (1.f - s));  // d gate_pre
   }
   if (threadIdx.x < P) al[threadIdx.x] = d.alphas[bt * P + threadIdx.x];
   __syncthreads();
@@ -307,50 +404,68 @@ static imgcap_epilogue f32_epi(const float* bias) {
   return ep;
 }
 
+// SW waves per block and DEPTH k-steps per load round: DEPTH = the wave's k-step count
+// rounded up to a power of two (fp32 fragments are twice as wide: at most 2)
+static int depth_for(int klen, int sw, bool f32) {
+  const int per = ((klen + 31) / 32 + sw - 1) / sw;
+  const int dpt = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 ? 4 : 8;
+  return f32 ? std::min(dpt, 2) : dpt;
+}
+
+#define LSTM_DEPTH_SWITCH(dpt, KERNEL, SW, ...)                                      \
+  do {                                                                               \
+    if ((dpt) <= 1) hipLaunchKernelGGL((KERNEL<T, SW, 1>), __VA_ARGS__);             \
+    else if ((dpt) <= 2) hipLaunchKernelGGL((KERNEL<T, SW, 2>), __VA_ARGS__);        \
+    else if ((dpt) <= 4) hipLaunchKernelGGL((KERNEL<T, SW, (F32 ? 2 : 4)>), __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<T, SW, (F32 ? 2 : 8)>), __VA_ARGS__);            \
+  } while (0)
+
 template <typename T>
 static int lstm_fwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
+  constexpr bool F32 = sizeof(T) == 4;
   const int W3 = d.A + d.E + 4 * d.D;
   const int ct = d.dtype;
-  const imgcap_epilogue e1 = f32_epi(d.b_hcat), e2 = f32_epi(nullptr);
+  const int nrg = (d.B + RG - 1) / RG;
+  const imgcap_epilogue e1 = f32_epi(d.b_hcat);
+  const int dpt_g = depth_for(d.E, 8, F32);
   for (int t = 0; t < d.T; ++t) {
     int rc = imgcap_gemm(ct, 1, 1, d.B, W3, d.D, (const T*)d.hprev + (long)t * d.D, (long)d.T * d.D, 0, d.w_hcat,
                          d.D, 0, d.g1 + (long)t * W3, (long)d.T * W3, 0, 1, &e1, st);
     if (rc) return rc;
     hipLaunchKernelGGL(attn_fwd_kernel<T>, dim3(d.B), dim3(ATT_THREADS), 0, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm attn_fwd");
-    rc = imgcap_gemm(ct, 1, 1, d.B, 4 * d.D, d.E, (const T*)d.zs + (long)t * d.E, (long)d.T * d.E, 0,
-                     (const T*)d.w_ih + d.M, d.M + d.E, 0, d.g2, 4 * d.D, 0, 1, &e2, st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(cell_fwd_kernel<T>, pw_grid((long)d.B * d.D), dim3(256), 0, st, d, t);
-    IMGCAP_CHECK_LAUNCH("lstm cell_fwd");
+    LSTM_DEPTH_SWITCH(dpt_g, gate_cell_fwd_kernel, 8, dim3(d.D / 4, nrg), dim3(512), 0, st, d, t);
+    IMGCAP_CHECK_LAUNCH("lstm gate_cell_fwd");
   }
   return 0;
 }
 
 template <typename T>
 static int lstm_bwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
-  const int W3 = d.A + d.E + 4 * d.D;
-  const int ct = d.dtype;
-  const imgcap_epilogue ep = f32_epi(nullptr);
+  constexpr bool F32 = sizeof(T) == 4;
+  const int nrg = (d.B + RG - 1) / RG;
+  const int NX = d.E + d.D, K4 = 4 * d.D, KY = d.A + d.E;
+  const int kx = ((K4 + d.x_slices - 1) / d.x_slices + 31) / 32 * 32;
+  const int ky = ((KY + d.y_slices - 1) / d.y_slices + 31) / 32 * 32;
+  const int sx = (K4 + kx - 1) / kx, sy = (KY + ky - 1) / ky;  // non-empty slices
+  const int dpt_x = depth_for(kx, 8, F32), dpt_y = depth_for(ky, 4, F32);
   const size_t shm = (d.E + 2 * MAXP + 2 * d.A) * sizeof(float);
+  imgcap_lstm_desc dd = d;
+  dd.x_slices = sx;
+  dd.y_slices = sy;
+  hipLaunchKernelGGL(cell_bwd_last_kernel<T>, pw_grid((long)d.B * d.D), dim3(256), 0, st, dd);
+  IMGCAP_CHECK_LAUNCH("lstm cell_bwd_last");
   for (int t = d.T - 1; t >= 0; --t) {
-    hipLaunchKernelGGL(cell_bwd_kernel<T>, pw_grid((long)d.B * d.D), dim3(256), 0, st, d, t);
-    IMGCAP_CHECK_LAUNCH("lstm cell_bwd");
-    // dz = dgates_t . W_ih[:, M:]      (w_ihz_t = W_ih[:, M:]^T, [E][4D])
-    int rc = imgcap_gemm(ct, 1, 1, d.B, d.E, 4 * d.D, (const T*)d.dcat + (long)t * W3 + d.A + d.E, (long)d.T * W3,
-                         0, d.w_ihz_t, 4 * d.D, 0, d.dz, d.E, 0, 1, &ep, st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(attn_bwd_kernel<T>, dim3(d.B), dim3(ATT_THREADS), shm, st, d, t);
+    LSTM_DEPTH_SWITCH(dpt_x, x_partial_kernel, 8, dim3((NX + 15) / 16, sx, nrg), dim3(512), 0, st, dd, t, kx);
+    IMGCAP_CHECK_LAUNCH("lstm x_partial");
+    hipLaunchKernelGGL(attn_bwd_kernel<T>, dim3(d.B), dim3(ATT_THREADS), shm, st, dd, t);
     IMGCAP_CHECK_LAUNCH("lstm attn_bwd");
-    // dh_{t-1} = [d att2 | d gate_pre | d gates] . W_hcat    (w_hcat_t = W_hcat^T, [D][W3]);
-    // at t = 0 this is dL/dh0
-    rc = imgcap_gemm(ct, 1, 1, d.B, d.D, W3, (const T*)d.dcat + (long)t * W3, (long)d.T * W3, 0, d.w_hcat_t, W3, 0,
-                     d.dh, d.D, 0, 1, &ep, st);
-    if (rc) return rc;
+    LSTM_DEPTH_SWITCH(dpt_y, dh_cell_kernel, 4, dim3(d.D / 16, sy, nrg), dim3(256), 0, st, dd, t, ky);
+    IMGCAP_CHECK_LAUNCH("lstm dh_cell");
   }
   const size_t shm2 = (size_t)d.T * PCH * sizeof(float);
   const int thr = d.A >= 512 ? 512 : ((d.A + 63) / 64) * 64;
-  hipLaunchKernelGGL(attn_param_grad_kernel<T>, dim3((d.P + PCH - 1) / PCH, d.B), dim3(thr), shm2, st, d);
+  hipLaunchKernelGGL(attn_param_grad_kernel<T>, dim3((d.P + PCH - 1) / PCH, d.B), dim3(thr), shm2, st, dd);
   IMGCAP_CHECK_LAUNCH("lstm attn_param_grad");
   return 0;
 }
@@ -359,7 +474,7 @@ static int check_desc(const imgcap_lstm_desc* d) {
   IMGCAP_REQUIRE(d != nullptr, "lstm desc NULL");
   IMGCAP_REQUIRE(d->dtype == IMGCAP_F32 || d->dtype == IMGCAP_BF16, "lstm: dtype");
   IMGCAP_REQUIRE(d->B > 0 && d->T > 0 && d->P > 0 && d->P <= MAXP, "lstm: need 0 < P <= 64");
-  IMGCAP_REQUIRE(d->E % 8 == 0 && d->A % 8 == 0 && d->D % 8 == 0 && d->M % 8 == 0, "lstm: dims % 8");
+  IMGCAP_REQUIRE(d->E % 8 == 0 && d->A % 8 == 0 && d->M % 8 == 0 && d->D % 16 == 0, "lstm: E, A, M % 8, D % 16");
   return 0;
 }
 
@@ -377,7 +492,10 @@ extern "C" int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream) {
   if (int rc = check_desc(d)) return rc;
   IMGCAP_REQUIRE((d->E + 2 * MAXP + 2 * d->A) * 4 <= 65536, "lstm bwd: E/A too large for LDS");
   IMGCAP_REQUIRE((size_t)d->T * PCH * 4 <= 65536, "lstm bwd: T too large for LDS");
-  IMGCAP_REQUIRE(d->w_ihz_t && d->w_hcat_t && d->de && d->dbea, "lstm bwd: transposed weights / de / dbea needed");
+  IMGCAP_REQUIRE(d->w_zh_t && d->w_att_t && d->de && d->dbea && d->ws_y && d->y_cnt,
+                 "lstm bwd: transposed weights / de / dbea / ws_y / y_cnt needed");
+  IMGCAP_REQUIRE(d->x_slices >= 1 && d->x_slices <= 16 && d->y_slices >= 1 && d->y_slices <= 16,
+                 "lstm bwd: x_slices, y_slices in [1, 16]");
   if (d->dtype == IMGCAP_BF16) return lstm_bwd_impl<bf16>(*d, (hipStream_t)stream);
   return lstm_bwd_impl<float>(*d, (hipStream_t)stream);
 }

@@ -43,11 +43,12 @@ def _ld(t, trans):
 
 def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None, bias=None, act=ACT_NONE, alpha=1.0,
          beta=0.0, res=None, aux=None, aux_scale=1.0, colscale=None, rowscale=None, rows_per_scale=1, drop_p=0.0,
-         seed=0, drop_stream=0, drop_ld=None, M=None, N=None, K=None):
+         seed=0, drop_stream=0, drop_ld=None, M=None, N=None, K=None, split_k=0):
     """out[M,N] = epilogue(op(a) @ op(b)); op(x) = x.T if trans else x (torch semantics).
 
     ``a``/``b`` are 2-D views (unit inner stride).  With trans_b=True, b is an nn.Linear
-    weight [N, K] and the call is ``a @ b.T``.
+    weight [N, K] and the call is ``a @ b.T``.  split_k (-1 = auto) slices K across the grid
+    for long-K fp32 products ``out = alpha * a @ b + beta * out`` (no other epilogue).
     """
     _check_dev(a, b, out, bias, res, aux)
     if a.dtype != b.dtype:
@@ -81,6 +82,7 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None, bias=N
     ep.seed = seed
     ep.drop_stream = drop_stream
     ep.drop_ld = N if drop_ld is None else drop_ld
+    ep.split_k = split_k
     _abi.call("imgcap_gemm", dt(a), 0 if trans_a else 1, 1 if trans_b else 0, M, N, K,
               a.data_ptr(), _ld(a, trans_a), 0, b.data_ptr(), _ld(b, trans_b), 0,
               out.data_ptr(), out.stride(0), 0, 1, ctypes.byref(ep), stream())
@@ -89,7 +91,7 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None, bias=N
 
 def gemm_raw(dtype, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, C, ldc, c_dtype, *, batch=1, sA=0, sB=0, sC=0,
              bias=None, act=ACT_NONE, alpha=1.0, beta=0.0, rowscale=None, rows_per_scale=1, drop_p=0.0, seed=0,
-             drop_stream=0, drop_ld=0):
+             drop_stream=0, drop_ld=0, split_k=0):
     """Pointer-level GEMM for strided / batched operand views."""
     ep = Epilogue()
     ep.bias = bias
@@ -103,6 +105,7 @@ def gemm_raw(dtype, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, C, ldc, c_dtype
     ep.seed = seed
     ep.drop_stream = drop_stream
     ep.drop_ld = drop_ld
+    ep.split_k = split_k
     _abi.call("imgcap_gemm", dtype, a_kmajor, b_kmajor, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch,
               ctypes.byref(ep), stream())
 
@@ -230,6 +233,18 @@ def set_seed_counter(counter):
         if counter.dtype != torch.int64 or counter.numel() != 1:
             raise ValueError("seed counter must be a one-element int64 tensor")
     _abi.call("imgcap_set_seed_counter", ptr(counter))
+
+
+CNBLOCK_MLP_CHANNELS = (96, 128, 192, 384)
+
+
+def cnblock_mlp(z, w1, b1, w2, b2, gamma, x, sd=None, rows_per_sample=1):
+    """x += gamma * sd * (GELU(z W1^T + b1) W2^T + b2), hidden on chip (bf16; x updated in place)."""
+    _check_dev(z, w1, w2, x)
+    M, C = x.shape
+    _abi.call("imgcap_cnblock_mlp", M, C, z.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+              gamma.data_ptr(), ptr(sd), rows_per_sample, x.data_ptr(), stream())
+    return x
 
 
 def stochastic_depth_scales(probs, B, seed, drop_stream, out):

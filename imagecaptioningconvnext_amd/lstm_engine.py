@@ -18,6 +18,10 @@ from . import _abi
 from . import kernels as K
 from .flat import FlatParams
 
+# weight gradients: long-K fp32 products into the gradient buffer, K sliced over the
+# grid (imgcap_epilogue.split_k)
+DW = dict(split_k=-1)
+
 _STREAM_DROPOUT_H = 11  # dropout stream id for fc(dropout(h)) (decoder.py:144)
 
 
@@ -49,6 +53,12 @@ class LstmEngine:
         self.Vpad = (self.V + 7) // 8 * 8
         self.seed = 1234
         self.step_id = 0
+        self._y_cnt = None
+
+    # K-slices of the backward step GEMMs (imgcap_lstm_desc.x_slices / y_slices): enough blocks
+    # to cover the CUs at batch 32 with D = 512 (x: 80 column tiles x 3, y: 32 x 8)
+    X_SLICES = 3
+    Y_SLICES = 8
 
     # ---------------------------------------------------------------------------------------
     def weights(self):
@@ -114,12 +124,11 @@ class LstmEngine:
         gates = torch.empty(B, T, 4 * D, **f32)
         cs = torch.empty(B, T, D, **f32)
         hs = torch.empty(B, T, D, **ctd)
-        g2 = torch.empty(B, 4 * D, **f32)
         d = _abi.LstmDesc()
         d.dtype, d.B, d.P, d.E, d.A, d.D, d.M, d.T = K.dt(emb), B, P, E, A, D, M, T
         for k, v in dict(w_hcat=w["hcat"], b_hcat=w["bhcat"], w_ih=w["wih"], w_f=w["wf"], enc=enc_s, att1=att1,
                          xe=xe, c0=c0, dl=dl, g1=g1, alphas=alphas, awe=awe, zs=zs, gates=gates, cs=cs, hs=hs,
-                         hprev=hprev, g2=g2).items():
+                         hprev=hprev).items():
             setattr(d, k, v.data_ptr())
         _abi.call("imgcap_lstm_tf_fwd", ctypes.byref(d), K.stream())
         # ---- fc(dropout(h)) over all B*T rows (decoder.py:144) ----------------------------------
@@ -128,7 +137,7 @@ class LstmEngine:
             hd = K.dropout(hd, p_drop, s["seed"], _STREAM_DROPOUT_H)
         tmask = torch.arange(T, device=dev).view(1, T) < dl.view(B, 1)
         s.update(enc_s=enc_s, ids=ids, emb=emb, mean=mean, att1=att1, xe=xe, c0=c0, g1=g1, alphas=alphas, awe=awe,
-                 zs=zs, gates=gates, cs=cs, hs=hs, hprev=hprev, g2=g2, hd=hd, tmask=tmask, desc=d)
+                 zs=zs, gates=gates, cs=cs, hs=hs, hprev=hprev, hd=hd, tmask=tmask, desc=d)
         if loss:
             logits = torch.empty(B * T, self.Vpad, **ctd)
             K.gemm(hd, w["wfc"], trans_b=True, bias=w["bfc"], out=logits, N=V)
@@ -178,44 +187,53 @@ class LstmEngine:
             dalpha = s["dalpha"]
         BT = B * T
         # fc: dW_fc = dlogits^T hd ; db_fc = colsum ; dh = (dlogits W_fc) * dropmask
-        K.gemm(dlogits, s["hd"], trans_a=True, out=_G.g("fc.weight"), M=V)
+        K.gemm(dlogits, s["hd"], trans_a=True, out=_G.g("fc.weight"), M=V, **DW)
         K.colsum(dlogits, _G.g("fc.bias"), cols=V)
         dhs = K.gemm(dlogits, w["wfc"], K=V, drop_p=s["p_drop"], seed=s["seed"], drop_stream=_STREAM_DROPOUT_H,
                      drop_ld=D)
         f32 = dict(device=dev, dtype=torch.float32)
         dcat = torch.empty(B, T, W3, device=dev, dtype=ct)
-        dz, dh, dc = torch.empty(B, E, **f32), torch.empty(B, D, **f32), torch.empty(B, D, **f32)
+        xs, ys = self.X_SLICES, self.Y_SLICES
+        nrg = (B + 31) // 32
+        dz = torch.empty(xs, B, E + D, **f32)                    # K-slice slabs of the step GEMMs
+        ws_y = torch.empty(ys * nrg * (D // 16) * 512, **f32)
+        if self._y_cnt is None or self._y_cnt.numel() < nrg * (D // 16) or self._y_cnt.device != dev:
+            self._y_cnt = torch.zeros(nrg * (D // 16), device=dev, dtype=torch.int32)  # left at 0 by the kernel
+        dh, dc = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
         de = torch.empty(B, T, P, **f32)
         datt1 = torch.empty(B * P, A, device=dev, dtype=ct)
         npc = (P + 6) // 7  # pixel chunks of attn_param_grad_kernel
         dwf, dbea = torch.empty(B * npc, A, **f32), torch.empty(B * npc, A, **f32)
-        # k-major copies of the two weights the backward recurrence multiplies by
-        wihz_t = K.transpose(w["wih"][:, M:])            # [E, 4D]
-        whcat_t = K.transpose(w["hcat"])                 # [D, W3]
+        # k-major copies of the weights the backward recurrence multiplies by
+        wzh_t = torch.empty(E + D, 4 * D, device=dev, dtype=ct)   # [W_ih[:, M:] | W_hh]^T
+        K.transpose(w["wih"][:, M:], out=wzh_t[:E])
+        K.transpose(w["hcat"][A + E:], out=wzh_t[E:])
+        watt_t = K.transpose(w["hcat"][:A + E])                    # [D, A + E] = [W_da; W_fb]^T
         d = s["desc"]
-        for k, v in dict(w_ihz_t=wihz_t, w_hcat_t=whcat_t, dhs=dhs, dalpha=dalpha, dcat=dcat, dz=dz, dh=dh, dc=dc,
-                         de=de, datt1=datt1, dwf=dwf, dbea=dbea).items():
+        for k, v in dict(w_zh_t=wzh_t, w_att_t=watt_t, dhs=dhs, dalpha=dalpha, dcat=dcat, dz=dz, ws_y=ws_y,
+                         y_cnt=self._y_cnt, dh=dh, dc=dc, de=de, datt1=datt1, dwf=dwf, dbea=dbea).items():
             setattr(d, k, K.ptr(v))
+        d.x_slices, d.y_slices = xs, ys
         _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream())
         dc2 = dcat.view(BT, W3)
         dgates = dc2[:, A + E:]
         # W_hcat / b_hcat grads (batched over all B*T rows)
-        K.gemm(dc2, s["hprev"].view(BT, D), trans_a=True, out=_G.g("attention.decoder_att.weight", (W3, D), W3 * D))
+        K.gemm(dc2, s["hprev"].view(BT, D), trans_a=True, out=_G.g("attention.decoder_att.weight", (W3, D), W3 * D), **DW)
         K.colsum(dc2, _G.g("attention.decoder_att.bias", (W3,), W3))
         # LSTMCell weight_ih (emb half | attention half), bias_ih
         gwih = _G.g("decode_step.weight_ih")
-        K.gemm(dgates, s["emb"], trans_a=True, out=gwih[:, :M], M=4 * D)
-        K.gemm(dgates, s["zs"].view(BT, E), trans_a=True, out=gwih[:, M:], M=4 * D)
+        K.gemm(dgates, s["emb"], trans_a=True, out=gwih[:, :M], M=4 * D, **DW)
+        K.gemm(dgates, s["zs"].view(BT, E), trans_a=True, out=gwih[:, M:], M=4 * D, **DW)
         K.colsum(dgates, _G.g("decode_step.bias_ih"))
         # embedding: d_emb = dgates W_ih[:, :M]  -> scatter-add rows
         demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
         K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
         # init_h / init_c from dh0, dc0
         dinit = torch.cat([dh, dc], dim=1).to(ct)
-        K.gemm(dinit, s["mean"], trans_a=True, out=_G.g("init_h.weight", (2 * D, E), 2 * D * E))
+        K.gemm(dinit, s["mean"], trans_a=True, out=_G.g("init_h.weight", (2 * D, E), 2 * D * E), **DW)
         K.colsum(dinit, _G.g("init_h.bias", (2 * D,), 2 * D))
         # encoder_att from the time-summed d att1
-        K.gemm(datt1, s["enc_s"].view(B * P, E), trans_a=True, out=_G.g("attention.encoder_att.weight"))
+        K.gemm(datt1, s["enc_s"].view(B * P, E), trans_a=True, out=_G.g("attention.encoder_att.weight"), **DW)
         K.colsum(dbea, _G.g("attention.encoder_att.bias"))
         K.colsum(dwf, _G.g("attention.full_att.weight", (A,)))
         # full_att.bias: exactly zero gradient (softmax is shift-invariant) -> left at 0

@@ -179,14 +179,20 @@ class Encoder(nn.Module):
             _, h, w, C = x.shape
             M = B * h * w
             z = torch.empty_like(x)
-            hid = torch.empty(M, 4 * C, device=dev, dtype=ct)
+            hid = None if (ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS) else \
+                torch.empty(M, 4 * C, device=dev, dtype=ct)
             x2 = x.view(M, C)
+            fused = ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS
             for blk in blocks:
                 K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], z)
-                K.gemm(z.view(M, C), blk["w1"], trans_b=True, bias=blk["b1"], act=K.ACT_GELU, out=hid)
                 rs = sd[bid] if (sd is not None and blk["sd"] > 0) else None
-                K.gemm(hid, blk["w2"], trans_b=True, bias=blk["b2"], colscale=blk["gamma"], rowscale=rs,
-                       rows_per_scale=h * w, res=x2, out=x2)
+                if fused:  # Linear -> GELU -> Linear -> layer_scale -> drop path -> residual, hidden on chip
+                    K.cnblock_mlp(z.view(M, C), blk["w1"], blk["b1"], blk["w2"], blk["b2"], blk["gamma"], x2,
+                                  sd=rs, rows_per_sample=h * w)
+                else:
+                    K.gemm(z.view(M, C), blk["w1"], trans_b=True, bias=blk["b1"], act=K.ACT_GELU, out=hid)
+                    K.gemm(hid, blk["w2"], trans_b=True, bias=blk["b2"], colscale=blk["gamma"], rowscale=rs,
+                           rows_per_scale=h * w, res=x2, out=x2)
                 bid += 1
             if down is not None:
                 patches = torch.empty(B * (h // 2) * (w // 2), 4 * C, device=dev, dtype=ct)

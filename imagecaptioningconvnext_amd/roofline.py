@@ -14,14 +14,30 @@ PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0
 
 
-def time_launch(fn, reps=50, warm=5):
+def time_launch(fn, reps=50, warm=5, graph=True):
+    """Seconds per launch of ``fn``, HIP events around ``reps`` back-to-back launches.  With
+    graph=True the launches are captured into one HIP graph and replayed, so host launch cost
+    (~10 us per ctypes call) does not hide short kernels -- the per-launch figure then matches
+    the kernel durations rocprofv3 reports for the step (which also replays a graph)."""
     for _ in range(warm):
         fn()
+    torch.cuda.synchronize()
+    g = None
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(st)
-    for _ in range(reps):
-        fn()
+    if g is not None:
+        g.replay()
+    else:
+        for _ in range(reps):
+            fn()
     b.record(st)
     b.synchronize()
     return a.elapsed_time(b) / reps * 1e-3  # seconds per launch

@@ -19,6 +19,10 @@ from . import _abi
 from . import kernels as K
 from .flat import FlatParams
 
+# weight gradients: long-K fp32 products into the gradient buffer, K sliced over the
+# grid (imgcap_epilogue.split_k)
+DW = dict(split_k=-1)
+
 # dropout stream ids (each site gets its own counter-based mask stream)
 _S_EMB = 1
 
@@ -178,7 +182,7 @@ class TransformerEngine:
         if dlogits is None:
             dlogits = torch.empty(BL, self.Vpad, device=dev, dtype=ct)
             K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
-        K.gemm(dlogits, s["xL"], trans_a=True, out=G("fc_out.weight"), M=V)
+        K.gemm(dlogits, s["xL"], trans_a=True, out=G("fc_out.weight"), M=V, **DW)
         K.colsum(dlogits, G("fc_out.bias"), cols=V)
         dx = K.gemm(dlogits, fp.w("fc_out.weight"), K=V)                    # [BL, d]
         dmem = torch.zeros(BP, d, device=dev, dtype=torch.float32)
@@ -191,10 +195,10 @@ class TransformerEngine:
                                       G(lw("norm3.weight")), G(lw("norm3.bias")), drop_p=p, seed=seed,
                                       drop_stream=_s(i, 5), dr=dy3)
             # y3 = hdn W2^T + b2 ; hdn = drop(relu(x2 W1^T + b1))
-            K.gemm(dy3, st["hdn"], trans_a=True, out=G(lw("linear2.weight")))
+            K.gemm(dy3, st["hdn"], trans_a=True, out=G(lw("linear2.weight")), **DW)
             K.colsum(dy3, G(lw("linear2.bias")))
             dpre = K.gemm(dy3, fp.w(lw("linear2.weight")), aux=st["hdn"], aux_scale=1.0 / (1.0 - p))
-            K.gemm(dpre, st["x2"], trans_a=True, out=G(lw("linear1.weight")))
+            K.gemm(dpre, st["x2"], trans_a=True, out=G(lw("linear1.weight")), **DW)
             K.colsum(dpre, G(lw("linear1.bias")))
             K.gemm(dpre, fp.w(lw("linear1.weight")), out=ds3, beta=1.0)      # dx2 = ds3 + dpre W1
             # x2 = LN2(x1 + drop(y2))
@@ -202,7 +206,7 @@ class TransformerEngine:
             ds2 = K.add_layernorm_bwd(ds3, st["s2"], st["mu2"], st["rs2"], fp.f32(lw("norm2.weight")),
                                       G(lw("norm2.weight")), G(lw("norm2.bias")), drop_p=p, seed=seed,
                                       drop_stream=_s(i, 3), dr=dy2)
-            K.gemm(dy2, st["o2"], trans_a=True, out=G(lw("multihead_attn.out_proj.weight")))
+            K.gemm(dy2, st["o2"], trans_a=True, out=G(lw("multihead_attn.out_proj.weight")), **DW)
             K.colsum(dy2, G(lw("multihead_attn.out_proj.bias")))
             do2 = K.gemm(dy2, fp.w(lw("multihead_attn.out_proj.weight")))
             dq2 = torch.empty(BL, d, device=dev, dtype=ct)
@@ -214,9 +218,9 @@ class TransformerEngine:
             gw = G(lw("multihead_attn.in_proj_weight"))
             gb = G(lw("multihead_attn.in_proj_bias"))
             wq = fp.w(lw("multihead_attn.in_proj_weight"))
-            K.gemm(dq2, st["x1"], trans_a=True, out=gw[:d])
+            K.gemm(dq2, st["x1"], trans_a=True, out=gw[:d], **DW)
             K.colsum(dq2, gb[:d])
-            K.gemm(dkv2, s["mem"], trans_a=True, out=gw[d:])
+            K.gemm(dkv2, s["mem"], trans_a=True, out=gw[d:], **DW)
             K.colsum(dkv2, gb[d:])
             K.gemm(dkv2, wq[d:], out=dmem, beta=1.0)                          # dmem += dkv2 W_kv
             K.gemm(dq2, wq[:d], out=ds2, beta=1.0)                            # dx1 = ds2 + dq2 W_q
@@ -225,7 +229,7 @@ class TransformerEngine:
             ds1 = K.add_layernorm_bwd(ds2, st["s1"], st["mu1"], st["rs1"], fp.f32(lw("norm1.weight")),
                                       G(lw("norm1.weight")), G(lw("norm1.bias")), drop_p=p, seed=seed,
                                       drop_stream=_s(i, 1), dr=dy)
-            K.gemm(dy, st["o"], trans_a=True, out=G(lw("self_attn.out_proj.weight")))
+            K.gemm(dy, st["o"], trans_a=True, out=G(lw("self_attn.out_proj.weight")), **DW)
             K.colsum(dy, G(lw("self_attn.out_proj.bias")))
             do = K.gemm(dy, fp.w(lw("self_attn.out_proj.weight")))
             dqkv = torch.empty(BL, 3 * d, device=dev, dtype=ct)
@@ -234,7 +238,7 @@ class TransformerEngine:
                       o=None, ldo=d, lse=st["lse1"], causal=True, key_ids=s["key_ids"], pad_id=s["pad_id"], p=p,
                       seed=seed, sid=_s(i, 0), dout=do, lddo=d, dq=dqkv, lddq=3 * d, dk=dqkv[:, d:], lddk=3 * d,
                       dv=dqkv[:, 2 * d:], lddv=3 * d, bwd=True)
-            K.gemm(dqkv, st["x"], trans_a=True, out=G(lw("self_attn.in_proj_weight")))
+            K.gemm(dqkv, st["x"], trans_a=True, out=G(lw("self_attn.in_proj_weight")), **DW)
             K.colsum(dqkv, G(lw("self_attn.in_proj_bias")))
             K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
             dx = ds1
@@ -243,7 +247,7 @@ class TransformerEngine:
         denc = None
         if self.has_proj:
             dmem_c = dmem.to(ct)
-            K.gemm(dmem_c, s["enc"].view(BP, self.E), trans_a=True, out=G("encoder_proj.weight"))
+            K.gemm(dmem_c, s["enc"].view(BP, self.E), trans_a=True, out=G("encoder_proj.weight"), **DW)
             K.colsum(dmem, G("encoder_proj.bias"))
             if want_denc:
                 denc = K.gemm(dmem_c, fp.w("encoder_proj.weight")).view(B, P, self.E)

@@ -68,6 +68,10 @@ typedef struct imgcap_epilogue {
   int32_t c_dtype;
   int32_t rows_per_scale;
   uint32_t drop_stream;
+  int32_t split_k;         /* 0/1: off.  n > 1: K split n ways, -1: library picks n.  Only for
+                              fp32 C = alpha*A.B + beta*C (no other epilogue, batch 1): slices
+                              write fp32 partials to library scratch, a second kernel adds them
+                              in fixed order (deterministic) */
 } imgcap_epilogue;
 
 int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
@@ -119,6 +123,14 @@ int imgcap_ln_patchify2(int dtype, int B, int H, int W, int C, const void* x, co
 /* AdaptiveAvgPool2d((OH,OW)) on NHWC (encoder.py:20,25) */
 int imgcap_adaptive_pool_nhwc(int dtype, int B, int H, int W, int C, int OH, int OW,
                               const void* x, void* out, void* stream);
+/* Fused ConvNeXt CNBlock MLP, bf16 (torchvision CNBlock via encoder.py:18):
+ *   x[m, :] += gamma * sd[m / rows_per_sample] * (GELU(z[m, :] W1^T + b1) W2^T + b2)
+ * z = dwconv7_ln output [M, C]; w1 [4C, C], w2 [C, 4C] (nn.Linear weights); gamma = layer_scale;
+ * sd = per-sample stochastic-depth scales or NULL.  The 4C hidden stays on chip.
+ * C in {96, 128, 192, 384} (IMGCAP_EUNSUPPORTED otherwise: use the two-GEMM form). */
+int imgcap_cnblock_mlp(int M, int C, const void* z, const void* w1, const float* b1, const void* w2,
+                       const float* b2, const float* gamma, const float* sd, int rows_per_sample, void* x,
+                       void* stream);
 /* StochasticDepth(p_i, "row") per-sample scales of every CNBlock (torchvision convnext,
  * train mode; encoder.py:18 builds it): out[i*B + b] = keep ? 1/(1-p_i) : 0, keep drawn from
  * the counter RNG (seed, drop_stream, index i*B+b).  probs: device fp32 [nblocks]. */
@@ -160,12 +172,17 @@ int imgcap_clamp_adam(int64_t n, float* param, const float* grad, float* m, floa
 
 /* ---------------------------------------------------------------------------------------
  * LSTM + soft-attention decoder, teacher forced (decoder.py:104-148, Attention 60-66,
- * LSTMCell at :141).  One call enqueues all T steps (4 kernels per step).  Batch-major
- * buffers [B, T, .]; rows sorted by decode length (decoder.py:114); W3 = A + E + 4D.
- * fwd requires: hprev[:,0,:] = h0, c0, xe = emb_t W_ih[:, :M]^T + b_ih + b_hh, att1.
- * bwd requires: the saved forward buffers, dhs (dL/dh_t from fc), dalpha, transposed weights;
- * produces dcat (= per-step [d att2 | d gate_pre | d gates_preact]) for the weight-gradient
- * GEMMs, dh/dc (= dL/dh0, dL/dc0), datt1 (sum over t of dL/datt1) and dwf / dbea partials.
+ * LSTMCell at :141).  One call enqueues all T steps (3 kernels per step each way).
+ * Batch-major buffers [B, T, .]; rows sorted by decode length (decoder.py:114);
+ * W3 = A + E + 4D.
+ * fwd requires: hprev[:,0,:] = h0, c0, xe = emb_t W_ih[:, :M]^T + b_ih, att1
+ *   (b_hh rides in b_hcat).
+ * bwd requires: the saved forward buffers, dhs (dL/dh_t from fc), dalpha, the transposed
+ * weights; produces dcat (= per-step [d att2 | d gate_pre | d gates_preact]) for the
+ * weight-gradient GEMMs, dh/dc (= dL/dh0, dL/dc0), datt1 (sum over t of dL/datt1) and the
+ * dwf / dbea partials.  Step GEMMs with long K are split over the grid: x_slices K-slices of
+ * dgates . [W_ih[:, M:] | W_hh] into the dz slabs, y_slices of [d att2 | d gate_pre] .
+ * [W_da; W_fb] into ws_y, reduced in-kernel by the last arriving block (y_cnt counters).
  * -------------------------------------------------------------------------------------- */
 typedef struct imgcap_lstm_desc {
   int32_t dtype, B, P, E, A, D, M, T;
@@ -178,7 +195,7 @@ typedef struct imgcap_lstm_desc {
   const float* xe;      /* [B, T, 4D] emb W_ih[:, :M]^T + b_ih      */
   const float* c0;      /* [B, D]                                   */
   const int32_t* dl;    /* [B] decode lengths (sorted, device)      */
-  float* g1;            /* [B, T, W3] saved                         */
+  float* g1;            /* [B, T, W3] saved [att2 | gate_pre | hh]  */
   float* alphas;        /* [B, T, P]  output (0 where t >= dl[b])   */
   float* awe;           /* [B, T, E]  saved attention context       */
   void* zs;             /* [B, T, E]  gate * context (LSTM input)   */
@@ -186,19 +203,22 @@ typedef struct imgcap_lstm_desc {
   float* cs;            /* [B, T, D]                                */
   void* hs;             /* [B, T, D]  h_t                           */
   void* hprev;          /* [B, T, D]  h_{t-1}; slot 0 = h0          */
-  float* g2;            /* [B, 4D] workspace                        */
-  const void* w_ihz_t;  /* [E, 4D]  = W_ih[:, M:]^T   (bwd)         */
-  const void* w_hcat_t; /* [D, W3]  = W_hcat^T        (bwd)         */
+  const void* w_zh_t;   /* [E + D, 4D] = [W_ih[:, M:] | W_hh]^T (bwd) */
+  const void* w_att_t;  /* [D, A + E]  = [W_da; W_fb]^T        (bwd) */
   const void* dhs;      /* [B, T, D]  bwd input                     */
   const float* dalpha;  /* [B, T, P]  bwd input dL/dalpha or NULL   */
   void* dcat;           /* [B, T, W3] bwd output                    */
-  float* dz;            /* [B, E] workspace                         */
+  float* dz;            /* [x_slices, B, E + D] workspace (slabs)   */
+  float* ws_y;          /* [y_slices, ceil(B/32) * D/16, 512] workspace */
+  int32_t* y_cnt;       /* [ceil(B/32) * D/16] zero-initialised counters (left at 0) */
   float* dh;            /* [B, D] out: dL/dh0                       */
   float* dc;            /* [B, D] out: dL/dc0                       */
   float* de;            /* [B, T, P] workspace: dL/d(attention score) */
   void* datt1;          /* [B, P, A] out: sum_t dL/datt1 (dtype)    */
   float* dwf;           /* [B*ceil(P/7), A] out: partials of dL/dw_f  */
   float* dbea;          /* [B*ceil(P/7), A] out: partials of dL/db_ea */
+  int32_t x_slices;     /* 1..16 */
+  int32_t y_slices;     /* 1..16 */
 } imgcap_lstm_desc;
 
 int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream);

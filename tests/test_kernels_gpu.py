@@ -39,6 +39,28 @@ def test_gemm_layouts(hip_device, dtype, tol, ta, tb, M, N, Kd):
     assert _rel(out.cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("split", [-1, 3, 7])
+@pytest.mark.parametrize("M,N,Kd,ta,tb", [(512, 1536, 3328, True, False), (300, 260, 1000, True, False),
+                                          (130, 200, 4100, False, True), (96, 520, 777, True, True)])
+def test_gemm_split_k_accumulate(hip_device, dtype, tol, split, M, N, Kd, ta, tb):
+    """Weight-gradient form: out = alpha*A.B + beta*out with K sliced over the grid."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + Kd)
+    a = torch.randn(M, Kd, generator=g)
+    b = torch.randn(Kd, N, generator=g)
+    c0 = torch.randn(M, N, generator=g)
+    ref = c0 + (a.to(dtype).float() @ b.to(dtype).float()) * 0.5
+    ad = _padded(a.t() if ta else a, hip_device, dtype)
+    bd = _padded(b.t() if tb else b, hip_device, dtype)
+    out = _padded(c0, hip_device, torch.float32)
+    K.gemm(ad, bd, trans_a=ta, trans_b=tb, out=out, alpha=0.5, beta=1.0, split_k=split)
+    assert _rel(out.cpu(), ref) < tol
+    o2 = K.gemm(ad, bd, trans_a=ta, trans_b=tb, out=out.clone(), split_k=split)
+    assert _rel(o2.cpu(), (ref - c0) * 2) < tol
+    with pytest.raises(RuntimeError):
+        K.gemm(ad, bd, trans_a=ta, trans_b=tb, out=out, bias=torch.zeros(N, device=hip_device), split_k=split)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
 def test_gemm_epilogues(hip_device, dtype, tol):
     torch.manual_seed(0)
@@ -75,11 +97,12 @@ def test_gemm_epilogues(hip_device, dtype, tol):
     assert _rel(o1.cpu()[kept], 2 * base[kept]) < tol
 
 
-def test_colsum(hip_device):
-    x = torch.randn(1000, 77)
-    out = torch.zeros(77, device=hip_device)
-    K.colsum(x.to(hip_device), out)
-    assert _rel(out.cpu(), x.sum(0)) < 1e-6
+@pytest.mark.parametrize("rows,cols", [(1000, 77), (3328, 512), (1632, 9490), (40, 64), (0, 16)])
+def test_colsum(hip_device, rows, cols):
+    x = torch.randn(rows, cols)
+    out = torch.ones(cols, device=hip_device)
+    K.colsum(x.to(hip_device), out, beta=0.5)
+    assert _rel(out.cpu(), x.sum(0) + 0.5) < 1e-6
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
@@ -235,3 +258,26 @@ def test_transpose(hip_device):
         view = x[:, 8:72]
         out = K.transpose(view)
         assert torch.equal(out.cpu(), view.cpu().t())
+
+
+@pytest.mark.parametrize("C,M", [(96, 1000), (128, 300), (192, 520), (384, 130)])
+@pytest.mark.parametrize("with_sd", [False, True])
+def test_cnblock_mlp_fused(hip_device, C, M, with_sd):
+    """Fused CNBlock MLP vs torch: x + gamma*sd*(GELU(z W1^T + b1) W2^T + b2), hidden in bf16."""
+    g = torch.Generator(device="cpu").manual_seed(C + M)
+    z = torch.randn(M, C, generator=g).bfloat16()
+    x = torch.randn(M, C, generator=g).bfloat16()
+    w1 = (torch.randn(4 * C, C, generator=g) / math.sqrt(C)).bfloat16()
+    w2 = (torch.randn(C, 4 * C, generator=g) / math.sqrt(4 * C)).bfloat16()
+    b1, b2, gamma = (torch.randn(n, generator=g) for n in (4 * C, C, C))
+    rps = 49
+    sd = (torch.rand((M + rps - 1) // rps, generator=g) > 0.3).float() / 0.7 if with_sd else None
+    hid = F.gelu(z.float() @ w1.float().t() + b1).bfloat16().float()
+    delta = (hid @ w2.float().t() + b2) * gamma
+    if with_sd:
+        delta = delta * sd.repeat_interleave(rps)[:M].view(M, 1)
+    xd = x.to(hip_device)
+    dev = lambda t: None if t is None else t.to(hip_device)  # noqa: E731
+    K.cnblock_mlp(dev(z), dev(w1), dev(b1), dev(w2), dev(b2), dev(gamma), xd, sd=dev(sd), rows_per_sample=rps)
+    got = xd.cpu().float() - x.float()
+    assert _rel(got, delta) < 2e-2

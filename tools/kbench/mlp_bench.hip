@@ -1,0 +1,37 @@
+// Standalone timing of cnblock_mlp_kernel variants (GPU box): hipcc -O3 --offload-arch=gfx950
+// -DMLP_GELU=<0|1|2> ... ; prints us per launch for the Tiny stage shapes.
+#include <cstdio>
+#include <vector>
+#include "../../imagecaptioningconvnext_amd/csrc/cnblock_mlp.hip"
+#include "../../imagecaptioningconvnext_amd/csrc/abi.cpp"
+
+int main() {
+  const int B = 32;
+  const int shapes[3][2] = {{56, 96}, {28, 192}, {14, 384}};
+  for (auto& sh : shapes) {
+    const int H = sh[0], C = sh[1];
+    const int M = B * H * H;
+    bf16 *z, *x, *w1, *w2;
+    float *b1, *b2, *g;
+    hipMalloc(&z, (size_t)M * C * 2); hipMalloc(&x, (size_t)M * C * 2);
+    hipMalloc(&w1, (size_t)4 * C * C * 2); hipMalloc(&w2, (size_t)4 * C * C * 2);
+    hipMalloc(&b1, 4 * C * 4); hipMalloc(&b2, C * 4); hipMalloc(&g, C * 4);
+    hipMemset(z, 0, (size_t)M * C * 2); hipMemset(x, 0, (size_t)M * C * 2);
+    hipMemset(w1, 0, (size_t)4 * C * C * 2); hipMemset(w2, 0, (size_t)4 * C * C * 2);
+    hipMemset(b1, 0, 4 * C * 4); hipMemset(b2, 0, C * 4); hipMemset(g, 0, C * 4);
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    for (int i = 0; i < 3; ++i) imgcap_cnblock_mlp(M, C, z, w1, b1, w2, b2, g, nullptr, 1, x, nullptr);
+    hipEventRecord(a);
+    const int reps = 20;
+    for (int i = 0; i < reps; ++i) imgcap_cnblock_mlp(M, C, z, w1, b1, w2, b2, g, nullptr, 1, x, nullptr);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    const double us = ms * 1e3 / reps, fl = 2.0 * 2 * M * C * 4.0 * C;
+    printf("variant %s C=%4d M=%6d: %8.1f us %7.1f TFLOP/s\n", MLP_TAG, C, M, us, fl / us / 1e6);
+    hipFree(z); hipFree(x); hipFree(w1); hipFree(w2); hipFree(b1); hipFree(b2); hipFree(g);
+  }
+  return 0;
+}

@@ -16,13 +16,16 @@ dev = torch.device("cuda:0")
 bf = torch.bfloat16
 
 
-def gemm_case(name, M, N, Kd, ta=False, tb=True, act=0, out_dtype=bf, reps=30):
+def gemm_case(name, M, N, Kd, ta=False, tb=True, act=0, out_dtype=bf, reps=30, split_k=0):
     r8 = lambda x: (x + 7) // 8 * 8  # noqa: E731  (16-byte row pitch, as the engines allocate)
     a = torch.randn(Kd, r8(M), device=dev).to(bf)[:, :M] if ta else torch.randn(M, r8(Kd), device=dev).to(bf)[:, :Kd]
     b = torch.randn(N, r8(Kd), device=dev).to(bf)[:, :Kd] if tb else torch.randn(Kd, r8(N), device=dev).to(bf)[:, :N]
     out = torch.empty(M, N, device=dev, dtype=out_dtype)
-    t = time_launch(lambda: K.gemm(a, b, trans_a=ta, trans_b=tb, out=out, act=act), reps=reps)
+    beta = 0.0
+    t = time_launch(lambda: K.gemm(a, b, trans_a=ta, trans_b=tb, out=out, act=act, beta=beta, split_k=split_k),
+                    reps=reps)
     tf = 2.0 * M * N * Kd / t / 1e12
+    name = name + (f" split={split_k}" if split_k else "")
     print(f"{name:46s} M={M:6d} N={N:5d} K={Kd:5d} {'T' if ta else 'N'}{'T' if tb else 'N'}  "
           f"{t * 1e6:8.1f} us  {tf:7.1f} TFLOP/s")
 
@@ -38,6 +41,10 @@ def gemms():
     gemm_case("fc dX (NN)", 1632, 512, 9490, tb=False)
     gemm_case("trf in_proj (B=64)", 3328, 1536, 512)
     gemm_case("trf in_proj dW (TN)", 1536, 512, 3328, ta=True, tb=False, out_dtype=torch.float32)
+    for sk in (0, -1, 4, 8):
+        gemm_case("trf in_proj dW (TN)", 1536, 512, 3328, ta=True, tb=False, out_dtype=torch.float32, split_k=sk)
+        gemm_case("trf ff dW (TN)", 512, 512, 3328, ta=True, tb=False, out_dtype=torch.float32, split_k=sk)
+        gemm_case("fc dW (TN) C3", 9490, 512, 3328, ta=True, tb=False, out_dtype=torch.float32, split_k=sk)
     gemm_case("trf in_proj dX (NN)", 3328, 512, 1536, tb=False)
     gemm_case("trf ffn (B=64)", 3328, 512, 512)
     gemm_case("big square", 4096, 4096, 4096)
@@ -45,6 +52,28 @@ def gemms():
     gemm_case("lstm G2 (skinny)", 32, 2048, 768, out_dtype=torch.float32)
     gemm_case("lstm dz (skinny)", 32, 768, 2048, out_dtype=torch.float32)
     gemm_case("lstm dh (skinny)", 32, 512, 3328, out_dtype=torch.float32)
+
+
+def mlp():
+    """Fused CNBlock MLP vs the two-GEMM form at the Tiny stage shapes (B=32)."""
+    B = 32
+    for (H, C) in ((56, 96), (28, 192), (14, 384)):
+        M = B * H * H
+        z = torch.randn(M, C, device=dev).to(bf)
+        x = torch.randn(M, C, device=dev).to(bf)
+        w1 = (torch.randn(4 * C, C, device=dev) / C ** 0.5).to(bf)
+        w2 = (torch.randn(C, 4 * C, device=dev) / (4 * C) ** 0.5).to(bf)
+        b1, b2, gm = torch.randn(4 * C, device=dev), torch.randn(C, device=dev), torch.randn(C, device=dev) * 1e-3
+        hid = torch.empty(M, 4 * C, device=dev, dtype=bf)
+        flops = 2.0 * 2 * M * C * 4 * C
+        t = time_launch(lambda: K.cnblock_mlp(z, w1, b1, w2, b2, gm, x), reps=20)
+        print(f"cnblock_mlp fused  M={M:6d} C={C:4d}: {t * 1e6:8.1f} us {flops / t / 1e12:7.1f} TFLOP/s")
+
+        def unfused():
+            K.gemm(z, w1, trans_b=True, bias=b1, act=K.ACT_GELU, out=hid)
+            K.gemm(hid, w2, trans_b=True, bias=b2, colscale=gm, res=x, out=x)
+        t = time_launch(unfused, reps=20)
+        print(f"cnblock_mlp 2-GEMM M={M:6d} C={C:4d}: {t * 1e6:8.1f} us {flops / t / 1e12:7.1f} TFLOP/s")
 
 
 def misc():
@@ -80,3 +109,5 @@ if __name__ == "__main__":
         gemms()
     if which in ("all", "misc"):
         misc()
+    if which in ("all", "mlp"):
+        mlp()
