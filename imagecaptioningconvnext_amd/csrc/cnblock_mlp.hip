@@ -22,6 +22,18 @@ namespace imgcap {
 #ifndef MLP_TAG
 #define MLP_TAG "erf"
 #endif
+#ifndef MLP96_BM
+#define MLP96_BM 128
+#endif
+#ifndef MLP96_WPE
+#define MLP96_WPE 2
+#endif
+#ifndef MLP192_BM
+#define MLP192_BM 64
+#endif
+#ifndef MLP192_WPE
+#define MLP192_WPE 2
+#endif
 // GELU of the hidden activation.  MLP_GELU (kernel-variant experiments, tools/kbench): 0 =
 // erf form (torch nn.GELU default), 1 = identity (timing only), 2 = fast erf.
 DEV float mlp_gelu(float v) {
@@ -90,8 +102,10 @@ DEV void mlp_store(bf16* buf, const uint4 (&r1)[V1], const uint4 (&r2)[V2]) {
   }
 }
 
-template <int C, int BM, int HC, bool ZL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cnblock_mlp_kernel(int M, const bf16* __restrict__ z,
+// WPE: waves per SIMD the register budget must allow (1 = up to 512 registers per lane, 2 = 256:
+// two resident blocks per CU, one block's prologue/epilogue latency under the other's MFMAs)
+template <int C, int BM, int HC, bool ZL, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void cnblock_mlp_kernel(int M, const bf16* __restrict__ z,
                                                           const bf16* __restrict__ w1, const float* __restrict__ b1,
                                                           const bf16* __restrict__ w2, const float* __restrict__ b2,
                                                           const float* __restrict__ gamma,
@@ -176,10 +190,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int tn = 0; tn < G::TN1; ++tn) {
       const float bb = b1[h0 + tn * 16 + fr];
 #pragma unroll
-      for (int tm = 0; tm < G::TM; ++tm)
+      for (int tm = 0; tm < G::TM; ++tm) {
+        bf16* hp = hbuf + (tm * 16 + 4 * fq) * G::LDH + tn * 16 + fr;
+#if MLP_GELU == 2
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          hbuf[(tm * 16 + 4 * fq + r) * G::LDH + tn * 16 + fr] = (bf16)mlp_gelu(acc1[tm][tn][r] + bb);
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 gv = gelu_fast2(f32x2{acc1[tm][tn][r] + bb, acc1[tm][tn][r + 1] + bb});
+          hp[r * G::LDH] = (bf16)gv[0];
+          hp[(r + 1) * G::LDH] = (bf16)gv[1];
+        }
+#else
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hp[r * G::LDH] = (bf16)mlp_gelu(acc1[tm][tn][r] + bb);
+#endif
+      }
     }
     // GEMM2: O[WR, C] += H W2c^T   (the hidden image is written and read by this wave only)
     const bf16* w2c = cur + HC * G::LD1;
@@ -245,16 +269,15 @@ extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const void* w1, c
                  "imgcap_cnblock_mlp: operands must be 16-byte aligned");
   IMGCAP_REQUIRE(sd == nullptr || rows_per_sample > 0, "imgcap_cnblock_mlp: rows_per_sample");
   hipStream_t st = (hipStream_t)stream;
-#define MLP_(CC, BM, HC, ZL)                                                                                 \
-  hipLaunchKernelGGL((cnblock_mlp_kernel<CC, BM, HC, ZL>), dim3((M + BM - 1) / BM), dim3(256), 0, st, M,         \
+#define MLP_(CC, BM, HC, ZL, WPE)                                                                            \
+  hipLaunchKernelGGL((cnblock_mlp_kernel<CC, BM, HC, ZL, WPE>), dim3((M + BM - 1) / BM), dim3(256), 0, st, M,         \
                      (const bf16*)z, (const bf16*)w1, b1, (const bf16*)w2, b2, gamma, sd, rows_per_sample, \
                      (bf16*)x)
   switch (C) {
-    case 96: MLP_(96, 128, 64, false); break;
-    case 128: MLP_(128, 128, 64, false); break;
-    case 192: MLP_(192, 128, 32, false); break;
-    case 384: MLP_(384, 64, 32, true); break;
-    default: return fail(IMGCAP_EUNSUPPORTED, "imgcap_cnblock_mlp: C must be 96, 128, 192 or 384");
+    case 96: MLP_(96, MLP96_BM, 64, false, MLP96_WPE); break;
+    case 128: MLP_(128, 128, 64, false, 1); break;
+    case 192: MLP_(192, MLP192_BM, 32, false, MLP192_WPE); break;
+    default: return fail(IMGCAP_EUNSUPPORTED, "imgcap_cnblock_mlp: C must be 96, 128 or 192");
   }
 #undef MLP_
   IMGCAP_CHECK_LAUNCH("imgcap_cnblock_mlp");

@@ -18,6 +18,7 @@
 //   block owns 16 output columns; its 8 waves split K and stream A/B fragments straight from
 //   global into registers (no LDS round trip, no barriers in the loop), then reduce in LDS.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "mfma.h"
@@ -179,6 +180,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 }
 
 #include "gemm_tiled.h"
+#include "gemm_glds.h"
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
@@ -234,6 +236,46 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
     return 0;
   }
   const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
+  if constexpr (sizeof(T) == 2) {
+    static const bool glds_on = [] {
+      const char* e = getenv("IMGCAP_GEMM_GLDS");  // A/B switch for kernel benchmarks
+      return !(e && e[0] == '0');
+    }();
+    if (glds_on && batch == 1 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && K >= 64) {
+      // split-K (weight gradients): enough blocks for ~2 per CU, >= 4 k-tiles per slice
+      int sk = 1;
+      if (split < 0) sk = (int)std::max(1L, std::min({512 / std::max(tiles128, 1L), (long)(K / 256), 32L}));
+      else if (split > 1) sk = split;
+      if (sk > 1 || tiles128 >= 128) {
+        const int kslice = sk > 1 ? ((K + sk - 1) / sk + 63) / 64 * 64 : 0;
+        const int zdim = sk > 1 ? (K + kslice - 1) / kslice : 1;
+        void* Cdst = C;
+        if (sk > 1) {
+          Cdst = workspace((size_t)zdim * M * N * sizeof(float));
+          if (!Cdst) return fail(IMGCAP_EINVAL, "imgcap_gemm: split-K workspace allocation failed");
+        }
+        dim3 grid((N + 127) / 128, (M + 127) / 128, zdim);
+        const bf16* a = (const bf16*)A;
+        const bf16* b = (const bf16*)B;
+#define GL_(AKV, BKV)                                                                                              \
+  hipLaunchKernelGGL((gemm_glds_kernel<128, 128, AKV, BKV>), grid, dim3(256), 0, st, a, lda, b, ldb, Cdst, ldc, M, N, \
+                     K, ep, vec_ok, g_seed_ctr, kslice)
+        if (ak && bk) GL_(true, true);
+        else if (ak) GL_(true, false);
+        else if (bk) GL_(false, true);
+        else GL_(false, false);
+#undef GL_
+        if (sk > 1) {
+          const long total = (long)M * N;
+          const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
+          hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, N, zdim, (const float*)Cdst,
+                             (float*)C, ldc, ep.alpha, ep.beta);
+        }
+        IMGCAP_CHECK_LAUNCH("imgcap_gemm(glds)");
+        return 0;
+      }
+    }
+  }
   if (split != 1) {
     // long-K reductions into a small fp32 output (weight gradients): 128x128 tiles, K sliced
     // so that the grid reaches ~2 blocks per CU with >= 4 k-tiles per slice

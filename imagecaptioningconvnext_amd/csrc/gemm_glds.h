@@ -1,0 +1,175 @@
+// 128x128x64 bf16 GEMM tile with LDS-DMA staging — included by gemm.hip.
+//
+// Every operand layout (k-major: nn.Linear forward; m/n-major: the weight-gradient and
+// input-gradient forms) with K % 64 == 0 — the bulk of the encoder / decoder projections and
+// their backward.  Each k-tile of A and B (128 rows x 64 k = 16 KiB each) is copied
+// global -> LDS by global_load_lds_dwordx4 (no VGPR staging, cdna_hip_programming.md §5
+// "Async global->LDS copy"), 4 per operand per thread, into a lane-linear image whose 16-byte
+// slots are XOR-swizzled on the SOURCE address; fragment reads apply the same involution
+// (ds_read_b128 for k-major images, hardware-transposed ds_read_b64_tr_b16 for m/n-major).  Two stages: the DMA of tile k+1 is in
+// flight while tile k is multiplied (counted s_waitcnt vmcnt + raw s_barrier, never a
+// vmcnt(0) in the loop).  Without staging registers the kernel fits two waves per SIMD, so
+// two blocks share a CU and one block's prologue / epilogue hides under the other's MFMAs.
+// Rows past M / N read a clamped valid row (their outputs are masked in the epilogue); a K
+// tail (K % 64 != 0) is zeroed in LDS after its DMA lands.  With kslice > 0, grid.z walks K
+// slices and each block stores its fp32 partial tile into workspace plane z (split-K).
+
+// One operand's 64-deep k-tile -> its LDS image by LDS-DMA, 16-byte slots lane-linear per
+// wave-instruction (1 KiB = 64 slots), swizzle applied on the source address:
+//   k-major ([rows][K] in memory): image [ROWS][8 slots of 8 k]; slot c of row r at c ^ (r & 7)
+//   m/n-major ([K][rows]):          image [64 k][ROWS/8 slots of 8 rows]; slot c of k-row kr at
+//                                   c ^ tr_swz(kr), read back transposed by ds_read_b64_tr_b16
+DEV int tr_swz(int kr) { return 2 * ((kr & 3) | (((kr >> 3) & 1) << 2)); }
+
+template <int ROWS, bool KMAJ>
+DEV void glds_issue_op(const bf16* __restrict__ P, long ld, int r0, int R, int k0, int K, char* img, int w,
+                       int lane) {
+  constexpr int PER = ROWS * 8 / 256;  // 16-byte slots per thread
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int p0 = (j * 4 + w) * 64;  // first slot of this wave-instruction
+    const int p = p0 + lane;
+    const bf16* src;
+    if constexpr (KMAJ) {
+      const int r = p >> 3, c = (p & 7) ^ (r & 7);
+      src = P + (long)min(r0 + r, R - 1) * ld + min(k0 + c * 8, K - 8);  // k >= K: zeroed after landing
+    } else {
+      constexpr int SL = ROWS / 8;
+      const int kr = p / SL, c = (p % SL) ^ tr_swz(kr);
+      const int col = min(r0 + c * 8, ((R - 1) >> 3) << 3);  // past-the-end slots re-read a valid one
+      src = P + (long)min(k0 + kr, K - 1) * ld + col;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(img + p0 * 16), 16,
+                                     0, 0);
+  }
+}
+
+// Zero this thread's slots of a k-tile that lie past K (K % 64 != 0 tail; K % 8 == 0).
+template <int ROWS, bool KMAJ>
+DEV void glds_zero_tail(int k0, int K, char* img, int w, int lane) {
+  constexpr int PER = ROWS * 8 / 256;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int p = (j * 4 + w) * 64 + lane;
+    int k;
+    if constexpr (KMAJ) {
+      const int r = p >> 3;
+      k = k0 + ((p & 7) ^ (r & 7)) * 8;
+    } else {
+      k = k0 + p / (ROWS / 8);
+    }
+    if (k >= K) *(uint4*)(img + p * 16) = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+typedef short glds_v4s16 __attribute__((ext_vector_type(4)));
+typedef short glds_v8s16 __attribute__((ext_vector_type(8)));
+
+// A-/B-operand fragment (row row0 + lane&15, k = 32*kk + 8*(lane>>4) + 0..7)
+template <int ROWS, bool KMAJ>
+DEV bf16x8 glds_frag_op(const char* img, int row0, int kk, int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (KMAJ) {
+    const int r = row0 + fr, c = kk * 4 + fq;
+    return *(const bf16x8*)(img + ((r << 3) + (c ^ (r & 7))) * 16);
+  } else {
+    // lane 4q+p of a 16-lane group: k-row 32kk + 8g + q (+4 for the upper half), columns
+    // row0 + 4p .. +3; the hardware transpose hands lane i column i of the 4 k-rows
+    const int q = fr >> 2, p = fr & 3, g = fq;
+    const int kr = kk * 32 + 8 * g + q;
+    const int col = row0 + 4 * p;
+    const int byte_lo = kr * (ROWS * 2) + (((col >> 3) ^ tr_swz(kr)) << 4) + ((col & 7) << 1);
+    const int byte_hi = (kr + 4) * (ROWS * 2) + (((col >> 3) ^ tr_swz(kr + 4)) << 4) + ((col & 7) << 1);
+    typedef __attribute__((address_space(3))) glds_v4s16 lds_v4s16;
+    const glds_v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(img + byte_lo));
+    const glds_v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(img + byte_hi));
+    const glds_v8s16 all = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, all);
+  }
+}
+
+template <int BM, int BN, bool AK, bool BKM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_glds_kernel(
+    const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, void* __restrict__ C, long ldc,
+    int M, int N, int K, imgcap_epilogue ep, int vec_ok, const uint64_t* seed_ctr, int kslice) {
+  constexpr int TILE_A = BM * 64 * 2, TILE_B = BN * 64 * 2, STAGE = TILE_A + TILE_B;
+  constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 fragments per wave (2 x 2 waves)
+  constexpr int LDT = BN + 4, EPI_ROWS = BM / 2;
+  static_assert(EPI_ROWS * LDT * 4 <= 2 * STAGE, "epilogue tile fits the stages");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
+  int bx, by;
+  xcd_remap(bx, by);
+  const int m0 = by * BM, n0 = bx * BN;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int rb = wm * (BM / 2), cb = wn * (BN / 2);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // k-tiles [kt0, nk): the whole K, or slice blockIdx.z of a split-K launch (kslice % 64 == 0)
+  const int kt0 = kslice ? blockIdx.z * (kslice / 64) : 0;
+  const int nk = kslice ? min((K + 63) / 64, kt0 + kslice / 64) : (K + 63) / 64;
+  glds_issue_op<BM, AK>(A, lda, m0, M, kt0 * 64, K, smem, w, lane);
+  glds_issue_op<BN, BKM>(B, ldb, n0, N, kt0 * 64, K, smem + TILE_A, w, lane);
+  for (int kt = kt0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * STAGE;
+      glds_issue_op<BM, AK>(A, lda, m0, M, (kt + 1) * 64, K, nxt, w, lane);
+      glds_issue_op<BN, BKM>(B, ldb, n0, N, (kt + 1) * 64, K, nxt + TILE_A, w, lane);
+      // this thread's copies of tile kt are the older half of its outstanding DMA
+      if constexpr (BM * 8 / 256 + BN * 8 / 256 == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if ((kt + 1) * 64 > K) {  // K tail: clear the slots past K that this thread's DMA filled
+        glds_zero_tail<BM, AK>(kt * 64, K, cur, w, lane);
+        glds_zero_tail<BN, BKM>(kt * 64, K, cur + TILE_A, w, lane);
+      }
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's part of tile kt is in LDS
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = glds_frag_op<BM, AK>(cur, rb + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag_op<BN, BKM>(cur + TILE_A, cb + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone is done reading `cur` before its refill
+    asm volatile("" ::: "memory");
+  }
+
+  float* tile = (float*)smem;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tile[(i * 16 + 4 * fq + r) * LDT + cb + j * 16 + fr] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (kslice)
+      partial_from_lds<BN>(tile, LDT, EPI_ROWS, m0 + pass * EPI_ROWS, n0, M, N, (float*)C + (long)blockIdx.z * M * N);
+    else
+      epilogue_from_lds<BN>(ep, tile, LDT, EPI_ROWS, m0 + pass * EPI_ROWS, n0, M, N, C, ldc, 0, vec_ok != 0);
+    __syncthreads();
+  }
+}

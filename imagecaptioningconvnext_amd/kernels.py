@@ -235,7 +235,7 @@ def set_seed_counter(counter):
     _abi.call("imgcap_set_seed_counter", ptr(counter))
 
 
-CNBLOCK_MLP_CHANNELS = (96, 128, 192, 384)
+CNBLOCK_MLP_CHANNELS = (96, 128, 192)
 
 
 def cnblock_mlp(z, w1, b1, w2, b2, gamma, x, sd=None, rows_per_sample=1):

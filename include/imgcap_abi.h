@@ -127,7 +127,8 @@ int imgcap_adaptive_pool_nhwc(int dtype, int B, int H, int W, int C, int OH, int
  *   x[m, :] += gamma * sd[m / rows_per_sample] * (GELU(z[m, :] W1^T + b1) W2^T + b2)
  * z = dwconv7_ln output [M, C]; w1 [4C, C], w2 [C, 4C] (nn.Linear weights); gamma = layer_scale;
  * sd = per-sample stochastic-depth scales or NULL.  The 4C hidden stays on chip.
- * C in {96, 128, 192, 384} (IMGCAP_EUNSUPPORTED otherwise: use the two-GEMM form). */
+ * C in {96, 128, 192} (IMGCAP_EUNSUPPORTED otherwise: the wide, short stages run faster as two
+ * GEMMs with full-chip parallelism). */
 int imgcap_cnblock_mlp(int M, int C, const void* z, const void* w1, const float* b1, const void* w2,
                        const float* b2, const float* gamma, const float* sd, int rows_per_sample, void* x,
                        void* stream);
