@@ -164,18 +164,19 @@ DEV void partial_from_lds(const float* tile, int LDT, int rows, int m_base, int 
   }
 }
 
-// C[m, n] = alpha * sum_z P[z][m][n] + beta * C[m, n]   (fixed slice order: deterministic)
+// C[m, n] = epilogue(sum_z P[z][m][n])  (fixed slice order: deterministic; the full epilogue
+// of imgcap_gemm -- bias, activation, dropout, scales, residual, beta -- runs here)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S, const float* __restrict__ P,
-                                                            float* __restrict__ C, long ldc, float alpha,
-                                                            float beta) {
+                                                            void* __restrict__ C, long ldc, imgcap_epilogue ep,
+                                                            const uint64_t* seed_ctr) {
+  if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
   const long total = (long)M * N;
   const long plane = total;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     float t = 0.f;
     for (int z = 0; z < S; ++z) t += P[z * plane + i];
     const int m = (int)(i / N), n = (int)(i % N);
-    float* c = C + (long)m * ldc + n;
-    *c = alpha * t + (beta != 0.f ? beta * *c : 0.f);
+    epi_scalar(ep, C, (long)m * ldc + n, m, n, t);
   }
 }
 
@@ -241,11 +242,15 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       const char* e = getenv("IMGCAP_GEMM_GLDS");  // A/B switch for kernel benchmarks
       return !(e && e[0] == '0');
     }();
-    if (glds_on && batch == 1 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && K >= 64) {
-      // split-K (weight gradients): enough blocks for ~2 per CU, >= 4 k-tiles per slice
+    if (glds_on && batch == 1 && lda % 8 == 0 && ldb % 8 == 0 && K >= 64) {
+      // split-K: requested (weight gradients, -1 = auto) or, for grids too small to fill the chip
+      // with a long K, chosen here; partial tiles go to scratch and the reduce kernel applies the
+      // epilogue.  Auto: ~2 blocks per CU, >= 4 k-tiles per slice.
       int sk = 1;
-      if (split < 0) sk = (int)std::max(1L, std::min({512 / std::max(tiles128, 1L), (long)(K / 256), 32L}));
-      else if (split > 1) sk = split;
+      if (split < 0 || (split == 1 && tiles128 < 96 && K >= 2048))
+        sk = (int)std::max(1L, std::min({512 / std::max(tiles128, 1L), (long)(K / 256), 32L}));
+      else if (split > 1)
+        sk = split;
       if (sk > 1 || tiles128 >= 128) {
         const int kslice = sk > 1 ? ((K + sk - 1) / sk + 63) / 64 * 64 : 0;
         const int zdim = sk > 1 ? (K + kslice - 1) / kslice : 1;
@@ -268,8 +273,8 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
         if (sk > 1) {
           const long total = (long)M * N;
           const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
-          hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, N, zdim, (const float*)Cdst,
-                             (float*)C, ldc, ep.alpha, ep.beta);
+          hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, N, zdim, (const float*)Cdst, C,
+                             ldc, ep, g_seed_ctr);
         }
         IMGCAP_CHECK_LAUNCH("imgcap_gemm(glds)");
         return 0;

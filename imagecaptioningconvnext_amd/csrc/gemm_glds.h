@@ -32,7 +32,8 @@ DEV void glds_issue_op(const bf16* __restrict__ P, long ld, int r0, int R, int k
     const bf16* src;
     if constexpr (KMAJ) {
       const int r = p >> 3, c = (p & 7) ^ (r & 7);
-      src = P + (long)min(r0 + r, R - 1) * ld + min(k0 + c * 8, K - 8);  // k >= K: zeroed after landing
+      // slots at or past K re-read the last (8-aligned) slot of the row; zeroed after landing
+      src = P + (long)min(r0 + r, R - 1) * ld + min(k0 + c * 8, ((K - 1) >> 3) << 3);
     } else {
       constexpr int SL = ROWS / 8;
       const int kr = p / SL, c = (p % SL) ^ tr_swz(kr);
@@ -44,21 +45,23 @@ DEV void glds_issue_op(const bf16* __restrict__ P, long ld, int r0, int R, int k
   }
 }
 
-// Zero this thread's slots of a k-tile that lie past K (K % 64 != 0 tail; K % 8 == 0).
+// Zero what this thread's DMA put past K into a k-tile (K % 64 != 0): whole slots, and for
+// k-major images the elements >= K of the slot that straddles K.
 template <int ROWS, bool KMAJ>
 DEV void glds_zero_tail(int k0, int K, char* img, int w, int lane) {
   constexpr int PER = ROWS * 8 / 256;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int p = (j * 4 + w) * 64 + lane;
-    int k;
+    uint4* slot = (uint4*)(img + p * 16);
     if constexpr (KMAJ) {
       const int r = p >> 3;
-      k = k0 + ((p & 7) ^ (r & 7)) * 8;
+      const int k = k0 + ((p & 7) ^ (r & 7)) * 8;
+      if (k >= K) *slot = make_uint4(0u, 0u, 0u, 0u);
+      else if (k + 8 > K) *slot = mask_tail<bf16>(*slot, K - k);
     } else {
-      k = k0 + p / (ROWS / 8);
+      if (k0 + p / (ROWS / 8) >= K) *slot = make_uint4(0u, 0u, 0u, 0u);
     }
-    if (k >= K) *(uint4*)(img + p * 16) = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 
@@ -116,8 +119,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // k-tiles [kt0, nk): the whole K, or slice blockIdx.z of a split-K launch (kslice % 64 == 0)
   const int kt0 = kslice ? blockIdx.z * (kslice / 64) : 0;
   const int nk = kslice ? min((K + 63) / 64, kt0 + kslice / 64) : (K + 63) / 64;
-  glds_issue_op<BM, AK>(A, lda, m0, M, kt0 * 64, K, smem, w, lane);
-  glds_issue_op<BN, BKM>(B, ldb, n0, N, kt0 * 64, K, smem + TILE_A, w, lane);
+  glds_issue_op<BM, AK>(A, lda, m0, M, kt0 * 64, K, smem + (kt0 & 1) * STAGE, w, lane);
+  glds_issue_op<BN, BKM>(B, ldb, n0, N, kt0 * 64, K, smem + (kt0 & 1) * STAGE + TILE_A, w, lane);
   for (int kt = kt0; kt < nk; ++kt) {
     char* cur = smem + (kt & 1) * STAGE;
     if (kt + 1 < nk) {

@@ -236,8 +236,8 @@ static int launch_tiled(int ak, int bk, int M, int N, int K, const void* A, long
   if (split > 1) {
     const long total = (long)M * N;
     const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, N, zdim, (const float*)C,
-                       (float*)Cout, ldc, ep.alpha, ep.beta);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, N, zdim, (const float*)C, Cout, ldc,
+                       ep, g_seed_ctr);
   }
   IMGCAP_CHECK_LAUNCH("imgcap_gemm");
   return 0;

@@ -26,7 +26,8 @@ def _rel(a, b):
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,Kd", [(37, 50, 72), (32, 3328, 512), (64, 200, 136), (300, 260, 1000), (1030, 520, 96),
                                      (5, 50, 20), (17, 33, 40), (64, 100, 1000), (1, 16, 8), (130, 9490, 40),
-                                     (1500, 1800, 192), (4100, 520, 256), (1500, 1800, 200), (2100, 1100, 584)])
+                                     (1500, 1800, 192), (4100, 520, 256), (1500, 1800, 200), (2100, 1100, 584),
+                                     (1600, 2000, 1001), (300, 520, 9490)])
 def test_gemm_layouts(hip_device, dtype, tol, ta, tb, M, N, Kd):
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
     a = torch.randn(M, Kd, generator=g)
@@ -60,6 +61,28 @@ def test_gemm_split_k_accumulate(hip_device, dtype, tol, split, M, N, Kd, ta, tb
     assert _rel(o2.cpu(), (ref - c0) * 2) < tol
     with pytest.raises(RuntimeError):
         K.gemm(ad, bd, trans_a=ta, trans_b=tb, out=out, bias=torch.zeros(N, device=hip_device), split_k=split)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 1e-2)])
+def test_gemm_auto_split_with_epilogue(hip_device, dtype, tol):
+    """Small grid + long K takes the split-K path unasked; the reduce applies the whole epilogue
+    (bias, ReLU, dropout, bf16 out) -- the decoder's fc dX shape (K = vocab)."""
+    g = torch.Generator(device="cpu").manual_seed(9)
+    M, N, Kd = 400, 256, 9490
+    a = torch.randn(M, Kd, generator=g)
+    w = torch.randn(Kd, N, generator=g) / math.sqrt(Kd)
+    bias = torch.randn(N, generator=g)
+    ad, wd = _padded(a, hip_device, dtype), _padded(w, hip_device, dtype)
+    o = K.gemm(ad, wd, bias=bias.to(hip_device), act=K.ACT_RELU, out_dtype=torch.float32)
+    ref = torch.relu(a.to(dtype).float() @ w.to(dtype).float() + bias)
+    assert _rel(o.cpu(), ref) < tol
+    d1 = K.gemm(ad, wd, drop_p=0.5, seed=3, drop_stream=2, out_dtype=torch.bfloat16)
+    d2 = K.gemm(ad, wd, drop_p=0.5, seed=3, drop_stream=2, out_dtype=torch.bfloat16)
+    assert torch.equal(d1, d2)
+    base = a.to(dtype).float() @ w.to(dtype).float()
+    kept = d1.cpu().float() != 0
+    assert 0.4 < kept.float().mean().item() < 0.6
+    assert _rel(d1.cpu().float()[kept], 2 * base[kept]) < tol
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
