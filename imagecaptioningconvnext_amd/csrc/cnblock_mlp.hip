@@ -1,6 +1,7 @@
 // Fused ConvNeXt block MLP (torchvision CNBlock, reached via encoder.py:18-24):
 //   x[m, :] += gamma * sd[m / rows_per_sample] * (GELU(z[m, :] W1^T + b1) W2^T + b2)
-// with z = LN(dwconv7(x)) (dwconv7_ln), W1 [4C, C], W2 [C, 4C] (nn.Linear weights), bf16.
+// with z = LN(y), y = dwconv7(x) (the LayerNorm runs in this kernel's prologue when ln_w is
+// given, else z is taken as already normalised), W1 [4C, C], W2 [C, 4C] (nn.Linear), bf16.
 // The 4C-wide hidden activation never leaves the chip: the block walks the hidden dimension
 // in chunks of HC, computing H = GELU(Z W1c^T + b1c) and immediately accumulating
 // O += H W2c^T; HBM traffic per row is z + x read and x written (6C bytes) instead of the
@@ -110,7 +111,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
                                                           const bf16* __restrict__ w2, const float* __restrict__ b2,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ sd, int rows_per_sample,
-                                                          bf16* __restrict__ x) {
+                                                          const float* __restrict__ lnw,
+                                                          const float* __restrict__ lnb, bf16* __restrict__ x) {
   using G = MlpCfg<C, BM, HC, ZL>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   bf16* wbuf = (bf16*)smem;
@@ -142,6 +144,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       for (int ks = 0; ks < G::KS1; ++ks) {
         const uint4 u = *(const uint4*)(zp + ks * 32);
         zf[tm][ks] = __builtin_bit_cast(bf16x8, ok ? u : make_uint4(0u, 0u, 0u, 0u));
+      }
+    }
+    if (lnw) {
+      // z = LayerNorm(y) (torchvision LayerNorm2d, eps 1e-6), two-pass in fp32: row fr's C values
+      // sit in lanes fr, fr+16, fr+32, fr+48; the result is rounded to bf16 like a stored z
+#pragma unroll
+      for (int tm = 0; tm < G::TM; ++tm) {
+        float s = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s += (float)zf[tm][ks][j];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const float mean = s * (1.f / C);
+        float q = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { const float dd = (float)zf[tm][ks][j] - mean; q += dd * dd; }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        const float rstd = rsqrtf(q * (1.f / C) + 1e-6f);
+#pragma unroll
+        for (int ks = 0; ks < G::KS1; ++ks) {
+          const int k = ks * 32 + 8 * fq;
+          const f32x4 g0 = *(const f32x4*)(lnw + k), g1 = *(const f32x4*)(lnw + k + 4);
+          const f32x4 c0 = *(const f32x4*)(lnb + k), c1 = *(const f32x4*)(lnb + k + 4);
+          const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+          const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) zf[tm][ks][j] = (bf16)(((float)zf[tm][ks][j] - mean) * rstd * gg[j] + cc[j]);
+        }
       }
     }
   }
@@ -260,19 +295,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 
 using namespace imgcap;
 
-extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const void* w1, const float* b1, const void* w2,
-                                  const float* b2, const float* gamma, const float* sd, int rows_per_sample, void* x,
-                                  void* stream) {
+extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const float* ln_w, const float* ln_b, const void* w1,
+                                  const float* b1, const void* w2, const float* b2, const float* gamma, const float* sd,
+                                  int rows_per_sample, void* x, void* stream) {
   if (M == 0) return 0;
   IMGCAP_REQUIRE(aligned16(z) && aligned16(w1) && aligned16(w2) && aligned16(x) && aligned16(b1) &&
                      aligned16(b2) && aligned16(gamma),
                  "imgcap_cnblock_mlp: operands must be 16-byte aligned");
   IMGCAP_REQUIRE(sd == nullptr || rows_per_sample > 0, "imgcap_cnblock_mlp: rows_per_sample");
+  IMGCAP_REQUIRE((ln_w == nullptr) == (ln_b == nullptr) && (ln_w == nullptr || (aligned16(ln_w) && aligned16(ln_b))),
+                 "imgcap_cnblock_mlp: ln_w / ln_b");
   hipStream_t st = (hipStream_t)stream;
 #define MLP_(CC, BM, HC, ZL, WPE)                                                                            \
   hipLaunchKernelGGL((cnblock_mlp_kernel<CC, BM, HC, ZL, WPE>), dim3((M + BM - 1) / BM), dim3(256), 0, st, M,         \
-                     (const bf16*)z, (const bf16*)w1, b1, (const bf16*)w2, b2, gamma, sd, rows_per_sample, \
-                     (bf16*)x)
+                     (const bf16*)z, (const bf16*)w1, b1, (const bf16*)w2, b2, gamma, sd, rows_per_sample, ln_w, \
+                     ln_b, (bf16*)x)
   switch (C) {
     case 96: MLP_(96, MLP96_BM, 64, false, MLP96_WPE); break;
     case 128: MLP_(128, 128, 64, false, 1); break;

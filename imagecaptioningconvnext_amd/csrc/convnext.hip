@@ -235,6 +235,109 @@ __global__ __launch_bounds__(256) void dwconv7_ln_kernel(int B, int H, int W, in
 }
 
 // ---------------------------------------------------------------------------------------
+// Depthwise 7x7 conv (+bias), no LayerNorm (the consumer normalises: the fused CNBlock MLP
+// in its prologue, or add_layernorm for the two-GEMM stages).  Without the cross-channel LN
+// the work tiles over channels: block = 4 waves = 32 channels (wave w: channels 8w..8w+7 of
+// the tile, so its 49x8 weights are wave-uniform scalar loads) x TR output rows of the
+// flattened [B*H] row sequence x the full width; lane = one row x PW consecutive pixels.
+// The (TR+6) x (W+6) x 32 input patch (zero halo) is staged once into LDS with 16-byte
+// coalesced loads; each lane then slides a PW+6 register window along its row for each of
+// the 7 kernel rows (rows of another image than the lane's are skipped: image boundaries
+// inside a tile).  fp32 accumulation, packed two channels per FMA.
+// LDS layout: 16-byte slots; pixel px of patch row r at slot r*RS + 4*px + px/PW (one gap slot
+// after every PW pixels), slot s of the pixel = its channels 8s..8s+7.  A wave reads slot wv of
+// pixel g*PW + q across its lanes (groups g, rows lr): 4*PW + 1 is odd, so the GW groups of a
+// row land in distinct bank groups, and RS = 16/GW (mod 16) interleaves successive rows into
+// the remaining ones -- each 16-lane pass of a ds_read_b128 is conflict-free.
+constexpr int DW_CT = 32;  // channels per block
+template <typename T, int PW>
+__global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C, const T* __restrict__ x,
+                                                      const float* __restrict__ w, const float* __restrict__ bias,
+                                                      T* __restrict__ y, int TR, int RS) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  constexpr int VE = 16 / sizeof(T);   // elements per 16-byte vector
+  constexpr int NV = DW_CT / VE;       // 16-byte vectors per pixel in the tile (4 bf16, 8 f32)
+  constexpr int SPP = DW_CT * 2 / 16;  // 16-byte slots per pixel in the LDS image: bf16 layout
+  static_assert(sizeof(T) == 2 || sizeof(T) == 4, "dtype");
+  const int WP = W + 6;                // padded row width (pixels)
+  const long R = (long)B * H;
+  const long r0 = (long)blockIdx.x * TR;
+  const int cb = blockIdx.y * DW_CT;
+  uint4* img = (uint4*)dsm;
+  // slot of (patch row r, padded pixel px, 16-byte part s); fp32 pixels use 2x the slots
+  auto slot = [&](int r, int px, int s) { return r * RS + (SPP * px + px / PW) * (NV / SPP) + s; };
+  // ---- stage the input patch (rows r0-3 .. r0+TR+2 of the flattened sequence) ----
+  const int tot = (TR + 6) * WP * NV;
+  for (int i = threadIdx.x; i < tot; i += 256) {
+    const int v = i % NV, px = i / NV;
+    const int pc = px % WP, pr = px / WP;
+    const long gr = r0 - 3 + pr;
+    const int gw = pc - 3;
+    uint4 val = make_uint4(0u, 0u, 0u, 0u);
+    if (gr >= 0 && gr < R && gw >= 0 && gw < W) val = *(const uint4*)(x + ((gr * W) + gw) * C + cb + v * VE);
+    img[slot(pr, pc, v)] = val;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = cb + wv * 8;      // this wave's 8 channels
+  const int GW = W / PW;           // pixel groups per row
+  const int lr = lane / GW, g = lane % GW;
+  const long orow = r0 + lr;
+  if (lr >= TR || orow >= R) return;
+  const int h = (int)(orow % H);
+  const int w0 = g * PW;
+  f32x2 acc[PW][4];
+  {
+    const f32x4 b0 = *(const f32x4*)(bias + c0), b1 = *(const f32x4*)(bias + c0 + 4);
+#pragma unroll
+    for (int p = 0; p < PW; ++p) {
+      acc[p][0] = f32x2{b0[0], b0[1]}; acc[p][1] = f32x2{b0[2], b0[3]};
+      acc[p][2] = f32x2{b1[0], b1[1]}; acc[p][3] = f32x2{b1[2], b1[3]};
+    }
+  }
+  for (int kh = 0; kh < 7; ++kh) {
+    const int ih = h + kh - 3;
+    if (ih < 0 || ih >= H) continue;  // outside this lane's image (zero padding)
+    f32x2 win[PW + 6][4];
+#pragma unroll
+    for (int q = 0; q < PW + 6; ++q) {
+      float v[8];
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8 u = __builtin_bit_cast(bf16x8, img[slot(lr + kh, w0 + q, wv)]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (float)u[j];
+      } else {
+        const f32x4 a = __builtin_bit_cast(f32x4, img[slot(lr + kh, w0 + q, 2 * wv)]);
+        const f32x4 b = __builtin_bit_cast(f32x4, img[slot(lr + kh, w0 + q, 2 * wv + 1)]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) win[q][j] = f32x2{v[2 * j], v[2 * j + 1]};
+    }
+#pragma unroll
+    for (int kw = 0; kw < 7; ++kw) {
+      const float* wp = w + (kh * 7 + kw) * C + c0;
+      const f32x4 wa = *(const f32x4*)wp, wb = *(const f32x4*)(wp + 4);
+      const f32x2 wt[4] = {f32x2{wa[0], wa[1]}, f32x2{wa[2], wa[3]}, f32x2{wb[0], wb[1]}, f32x2{wb[2], wb[3]}};
+#pragma unroll
+      for (int p = 0; p < PW; ++p)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[p][j] = win[p + kw][j] * wt[j] + acc[p][j];
+    }
+  }
+  T* out = y + (orow * W + w0) * C + c0;
+#pragma unroll
+  for (int p = 0; p < PW; ++p) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[2 * j] = acc[p][j][0]; o[2 * j + 1] = acc[p][j][1]; }
+    V8<T>::store(out + (long)p * C, o);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // LayerNorm2d + 2x2/s2 patch gather: one wave per input pixel.
 template <typename T>
 __global__ __launch_bounds__(256) void ln_patchify2_kernel(int B, int H, int W, int C, const T* __restrict__ x,
@@ -318,6 +421,48 @@ __global__ void sd_scales_kernel(int n, int B, const float* __restrict__ probs, 
 }  // namespace imgcap
 
 using namespace imgcap;
+
+namespace {
+template <typename T>
+int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
+                   hipStream_t st) {
+  // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups
+  const int PW = W % 7 == 0 ? 7 : W % 8 == 0 ? 8 : W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 1;
+  const int GW = W / PW, TR = 64 / GW;
+  const long R = (long)B * H;
+  // row stride in 16-byte slots (see dwconv7_kernel): >= the row's slots, = 16/GW (mod 16)
+  const int mult = sizeof(T) / 2;  // fp32 pixels take twice the slots
+  const int base = (4 * (W + 6) + (W + 5) / PW + 1) * mult;
+  const int target = (GW == 1 || GW == 2 || GW == 4 || GW == 8 || GW == 16) ? (16 / GW) % 16 : 1;
+  int RS = base;
+  while (RS % 16 != target) ++RS;
+  const size_t shm = (size_t)(TR + 6) * RS * 16;
+  dim3 grid((unsigned)((R + TR - 1) / TR), C / DW_CT);
+#define DW_(P)                                                                                                  \
+  hipLaunchKernelGGL((dwconv7_kernel<T, P>), grid, dim3(256), shm, st, B, H, W, C, (const T*)x, w, bias, (T*)y, TR, \
+                     RS)
+  switch (PW) {
+    case 8: DW_(8); break;
+    case 7: DW_(7); break;
+    case 4: DW_(4); break;
+    case 2: DW_(2); break;
+    default: DW_(1); break;
+  }
+#undef DW_
+  IMGCAP_CHECK_LAUNCH("imgcap_dwconv7");
+  return 0;
+}
+}  // namespace
+
+extern "C" int imgcap_dwconv7(int dtype, int B, int H, int W, int C, const void* x, const float* w,
+                              const float* bias, void* y, void* stream) {
+  IMGCAP_REQUIRE(C % DW_CT == 0, "imgcap_dwconv7: C must be a multiple of 32");
+  IMGCAP_REQUIRE(W >= 1 && W <= 64, "imgcap_dwconv7: W must be in [1, 64]");
+  IMGCAP_REQUIRE(aligned16(x) && aligned16(y) && aligned16(w) && aligned16(bias), "imgcap_dwconv7: alignment");
+  if ((long)B * H == 0) return 0;
+  if (dtype == IMGCAP_BF16) return dwconv7_launch<bf16>(B, H, W, C, x, w, bias, y, (hipStream_t)stream);
+  return dwconv7_launch<float>(B, H, W, C, x, w, bias, y, (hipStream_t)stream);
+}
 
 extern "C" int imgcap_stochastic_depth_scales(int nblocks, int B, const float* probs, uint64_t seed,
                                               uint32_t drop_stream, float* out, void* stream) {

@@ -10,7 +10,7 @@
 
 namespace imgcap {
 
-constexpr int LN_MAXC = 1024;
+constexpr int LN_MAXC = 2048;
 
 template <typename T, int G>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(int rows, int cols, const T* __restrict__ x,
@@ -169,7 +169,7 @@ bool vec_rows(int cols, std::initializer_list<const void*> ptrs) {
 extern "C" int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const void* x, const void* r, float drop_p,
                                         uint64_t seed, uint32_t drop_stream, const float* gamma, const float* beta,
                                         float eps, void* s_out, void* y, float* mean, float* rstd, void* stream) {
-  IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_fwd: cols must be in (0, 1024]");
+  IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_fwd: cols must be in (0, 2048]");
   if (rows == 0) return 0;
   dim3 grid((rows + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
@@ -190,7 +190,7 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
                                         const float* mean, const float* rstd, const float* gamma, float drop_p,
                                         uint64_t seed, uint32_t drop_stream, void* dx, void* dr, float* dgamma,
                                         float* dbeta, void* stream) {
-  IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_bwd: cols must be in (0, 1024]");
+  IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_bwd: cols must be in (0, 2048]");
   if (rows == 0) return 0;
   const int rpw = std::max(1, (rows + 4 * 512 - 1) / (4 * 512));  // ~512 blocks of 4 waves
   dim3 grid((rows + 4 * rpw - 1) / (4 * rpw));

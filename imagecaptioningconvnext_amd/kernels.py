@@ -191,6 +191,15 @@ def convnext_stem(images, w, bias, ln_w, ln_b, out):
     return out
 
 
+def dwconv7(x, w49, bias, out):
+    """Depthwise 7x7 + bias (NHWC), no LayerNorm."""
+    B, H, W, C = x.shape
+    _check_dev(x, out)
+    _abi.call("imgcap_dwconv7", dt(x), B, H, W, C, x.data_ptr(), w49.data_ptr(), bias.data_ptr(), out.data_ptr(),
+              stream())
+    return out
+
+
 def dwconv7_ln(x, w49, bias, ln_w, ln_b, out):
     B, H, W, C = x.shape
     _abi.call("imgcap_dwconv7_ln", dt(x), B, H, W, C, x.data_ptr(), w49.data_ptr(), bias.data_ptr(),
@@ -238,12 +247,13 @@ def set_seed_counter(counter):
 CNBLOCK_MLP_CHANNELS = (96, 128, 192)
 
 
-def cnblock_mlp(z, w1, b1, w2, b2, gamma, x, sd=None, rows_per_sample=1):
-    """x += gamma * sd * (GELU(z W1^T + b1) W2^T + b2), hidden on chip (bf16; x updated in place)."""
+def cnblock_mlp(z, w1, b1, w2, b2, gamma, x, sd=None, rows_per_sample=1, ln_w=None, ln_b=None):
+    """x += gamma * sd * (GELU(LN(z) W1^T + b1) W2^T + b2), hidden on chip (bf16; x updated in
+    place).  With ln_w/ln_b the LayerNorm (eps 1e-6) is applied to z in the kernel."""
     _check_dev(z, w1, w2, x)
     M, C = x.shape
-    _abi.call("imgcap_cnblock_mlp", M, C, z.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
-              gamma.data_ptr(), ptr(sd), rows_per_sample, x.data_ptr(), stream())
+    _abi.call("imgcap_cnblock_mlp", M, C, z.data_ptr(), ptr(ln_w), ptr(ln_b), w1.data_ptr(), b1.data_ptr(),
+              w2.data_ptr(), b2.data_ptr(), gamma.data_ptr(), ptr(sd), rows_per_sample, x.data_ptr(), stream())
     return x
 
 

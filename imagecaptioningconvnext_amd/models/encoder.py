@@ -179,18 +179,29 @@ class Encoder(nn.Module):
             _, h, w, C = x.shape
             M = B * h * w
             z = torch.empty_like(x)
-            hid = None if (ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS) else \
-                torch.empty(M, 4 * C, device=dev, dtype=ct)
+            hid = zn = None
+            if not (ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS):
+                hid = torch.empty(M, 4 * C, device=dev, dtype=ct)
+                zn = torch.empty(M, C, device=dev, dtype=ct)
             x2 = x.view(M, C)
             fused = ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS
             for blk in blocks:
-                K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], z)
                 rs = sd[bid] if (sd is not None and blk["sd"] > 0) else None
-                if fused:  # Linear -> GELU -> Linear -> layer_scale -> drop path -> residual, hidden on chip
+                if w <= 64:  # channel-tiled depthwise; LayerNorm applied by the consumer
+                    K.dwconv7(x, blk["w49"], blk["dwb"], z)
+                    ln = (blk["lnw"], blk["lnb"])
+                else:        # wide images: row kernel with the LayerNorm fused
+                    K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], z)
+                    ln = (None, None)
+                if fused:  # LN -> Linear -> GELU -> Linear -> layer_scale -> drop path -> residual, on chip
                     K.cnblock_mlp(z.view(M, C), blk["w1"], blk["b1"], blk["w2"], blk["b2"], blk["gamma"], x2,
-                                  sd=rs, rows_per_sample=h * w)
+                                  sd=rs, rows_per_sample=h * w, ln_w=ln[0], ln_b=ln[1])
                 else:
-                    K.gemm(z.view(M, C), blk["w1"], trans_b=True, bias=blk["b1"], act=K.ACT_GELU, out=hid)
+                    zn2 = z.view(M, C)
+                    if ln[0] is not None:
+                        K.add_layernorm(zn2, None, ln[0], ln[1], 1e-6, y=zn)
+                        zn2 = zn
+                    K.gemm(zn2, blk["w1"], trans_b=True, bias=blk["b1"], act=K.ACT_GELU, out=hid)
                     K.gemm(hid, blk["w2"], trans_b=True, bias=blk["b2"], colscale=blk["gamma"], rowscale=rs,
                            rows_per_scale=h * w, res=x2, out=x2)
                 bid += 1

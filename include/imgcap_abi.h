@@ -113,6 +113,11 @@ int imgcap_convnext_stem(int dtype, int B, int H, int W, int C0, const float* im
                          const float* w, const float* bias, const float* ln_w, const float* ln_b,
                          void* out, void* stream);
 /* CNBlock head: depthwise 7x7 (pad 3, bias) + LayerNorm(C, eps 1e-6).  w: f32 [49][C]. */
+/* Depthwise 7x7 conv + bias only, y [B,H,W,C] (the LayerNorm is applied by the consumer:
+ * imgcap_cnblock_mlp's prologue or imgcap_add_layernorm_fwd).  C % 32 == 0, W <= 64.
+ * w [49][C] (tap-major), fp32. */
+int imgcap_dwconv7(int dtype, int B, int H, int W, int C, const void* x, const float* w, const float* bias,
+                   void* y, void* stream);
 int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const void* x, const float* w,
                       const float* bias, const float* ln_w, const float* ln_b, void* out,
                       void* stream);
@@ -125,13 +130,14 @@ int imgcap_adaptive_pool_nhwc(int dtype, int B, int H, int W, int C, int OH, int
                               const void* x, void* out, void* stream);
 /* Fused ConvNeXt CNBlock MLP, bf16 (torchvision CNBlock via encoder.py:18):
  *   x[m, :] += gamma * sd[m / rows_per_sample] * (GELU(z[m, :] W1^T + b1) W2^T + b2)
- * z = dwconv7_ln output [M, C]; w1 [4C, C], w2 [C, 4C] (nn.Linear weights); gamma = layer_scale;
- * sd = per-sample stochastic-depth scales or NULL.  The 4C hidden stays on chip.
+ * z = LayerNorm(y; ln_w, ln_b, eps 1e-6) of the dwconv7 output y [M, C] (or z = y when ln_w is
+ * NULL); w1 [4C, C], w2 [C, 4C] (nn.Linear weights); gamma = layer_scale; sd = per-sample
+ * stochastic-depth scales or NULL.  The 4C hidden stays on chip.
  * C in {96, 128, 192} (IMGCAP_EUNSUPPORTED otherwise: the wide, short stages run faster as two
  * GEMMs with full-chip parallelism). */
-int imgcap_cnblock_mlp(int M, int C, const void* z, const void* w1, const float* b1, const void* w2,
-                       const float* b2, const float* gamma, const float* sd, int rows_per_sample, void* x,
-                       void* stream);
+int imgcap_cnblock_mlp(int M, int C, const void* y, const float* ln_w, const float* ln_b, const void* w1,
+                       const float* b1, const void* w2, const float* b2, const float* gamma, const float* sd,
+                       int rows_per_sample, void* x, void* stream);
 /* StochasticDepth(p_i, "row") per-sample scales of every CNBlock (torchvision convnext,
  * train mode; encoder.py:18 builds it): out[i*B + b] = keep ? 1/(1-p_i) : 0, keep drawn from
  * the counter RNG (seed, drop_stream, index i*B+b).  probs: device fp32 [nblocks]. */

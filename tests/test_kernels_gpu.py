@@ -235,6 +235,41 @@ def test_dwconv7_ln(hip_device, dtype, tol, H, C):
     assert _rel(out.cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,H,C", [(3, 56, 96), (2, 28, 192), (3, 14, 384), (5, 7, 768), (2, 8, 256), (3, 16, 128), (3, 4, 64), (2, 12, 96), (3, 2, 32),
+                                   (1, 64, 32), (4, 32, 1536)])
+def test_dwconv7(hip_device, dtype, tol, B, H, C):
+    """Depthwise 7x7 + bias (no LN), tiles spanning image boundaries in the flattened rows."""
+    torch.manual_seed(B * H + C)
+    x = torch.randn(B, H, H, C)
+    w = torch.randn(C, 1, 7, 7) * 0.2
+    bias = torch.randn(C)
+    xin = x.to(dtype).float()
+    ref = F.conv2d(xin.permute(0, 3, 1, 2), w, bias, padding=3, groups=C).permute(0, 2, 3, 1)
+    w49 = w.view(C, 49).t().contiguous().to(hip_device)
+    out = torch.empty(B, H, H, C, dtype=dtype, device=hip_device)
+    K.dwconv7(x.to(hip_device, dtype), w49, bias.to(hip_device), out)
+    assert _rel(out.cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("C,M", [(96, 700), (192, 300)])
+def test_cnblock_mlp_with_layernorm(hip_device, C, M):
+    """LN (eps 1e-6) in the MLP prologue == LN kernel then MLP (z rounded to bf16 either way)."""
+    g = torch.Generator(device="cpu").manual_seed(C)
+    y = (torch.randn(M, C, generator=g) * 3 + 1).bfloat16()
+    x = torch.randn(M, C, generator=g).bfloat16()
+    w1 = (torch.randn(4 * C, C, generator=g) / math.sqrt(C)).bfloat16()
+    w2 = (torch.randn(C, 4 * C, generator=g) / math.sqrt(4 * C)).bfloat16()
+    b1, b2, gamma, lw, lb = (torch.randn(n, generator=g) for n in (4 * C, C, C, C, C))
+    z = F.layer_norm(y.float(), (C,), lw, lb, 1e-6).bfloat16().float()
+    hid = F.gelu(z @ w1.float().t() + b1).bfloat16().float()
+    delta = (hid @ w2.float().t() + b2) * gamma
+    d = lambda t: t.to(hip_device)  # noqa: E731
+    xd = d(x)
+    K.cnblock_mlp(d(y), d(w1), d(b1), d(w2), d(b2), d(gamma), xd, ln_w=d(lw), ln_b=d(lb))
+    assert _rel(xd.cpu().float() - x.float(), delta) < 2e-2
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("C0,HW", [(96, 224), (128, 224), (192, 256)])
 def test_stem(hip_device, dtype, tol, C0, HW):

@@ -86,6 +86,8 @@ def misc():
         t = time_launch(lambda: K.dwconv7_ln(x, w, b, b, b, y))
         gbs = 2 * x.numel() * 2 / t / 1e9
         print(f"dwconv7_ln B={B} H={H} C={C}: {t * 1e6:8.1f} us {gbs:8.1f} GB/s")
+        t = time_launch(lambda: K.dwconv7(x, w, b, y))
+        print(f"dwconv7    B={B} H={H} C={C}: {t * 1e6:8.1f} us {2 * x.numel() * 2 / t / 1e9:8.1f} GB/s")
     for rows, cols in ((3328, 512), (1632, 9490), (3328, 1536)):
         x = torch.randn(rows, cols, device=dev).to(bf)
         o = torch.empty(cols, device=dev)
@@ -111,3 +113,12 @@ if __name__ == "__main__":
         misc()
     if which in ("all", "mlp"):
         mlp()
+    if which == "mlpdw":  # short run for PMC collection: s1 shapes only
+        B, H, C = 32, 56, 96
+        x = torch.randn(B, H, H, C, device=dev).to(bf)
+        y = torch.empty_like(x)
+        w = torch.randn(49, C, device=dev)
+        b = torch.randn(C, device=dev)
+        for _ in range(5):
+            K.dwconv7(x, w, b, y)
+        torch.cuda.synchronize()
