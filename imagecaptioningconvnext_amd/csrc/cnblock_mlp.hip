@@ -23,6 +23,9 @@ namespace imgcap {
 #ifndef MLP_TAG
 #define MLP_TAG "erf"
 #endif
+#ifndef MLP_EPI_BATCH
+#define MLP_EPI_BATCH 0
+#endif
 #ifndef MLP96_BM
 #define MLP96_BM 128
 #endif
@@ -261,6 +264,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   }
 
   // epilogue: fp32 tile through LDS, then x += gamma * sd * (o + b2) on 8-column vectors
+  constexpr int NV = C / 8;
+  constexpr int NIT = BM * NV / 256;
+  static_assert(NIT * 256 == BM * NV, "epilogue split");
   float* tile = (float*)smem;
 #pragma unroll
   for (int tm = 0; tm < G::TM; ++tm)
@@ -270,14 +276,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       for (int r = 0; r < 4; ++r)
         tile[(w * G::WR + tm * 16 + 4 * fq + r) * G::LDO + tn * 16 + fr] = acc2[tm][tn][r];
   __syncthreads();
-  constexpr int NV = C / 8;
-  for (int e = threadIdx.x; e < BM * NV; e += 256) {
-    const int r = e / NV, c = (e % NV) * 8;
+#if MLP_EPI_BATCH
+  // residual rows of all NIT iterations loaded at once (one memory round trip)
+  bf16x8 xres[NIT];
+#pragma unroll
+  for (int u = 0; u < NIT; ++u) {
+    const int e = threadIdx.x + u * 256, r = e / NV, c = (e % NV) * 8;
+    xres[u] = *(const bf16x8*)(x + (long)min(m0 + r, M - 1) * C + c);
+  }
+#endif
+#pragma unroll
+  for (int u = 0; u < NIT; ++u) {
+    const int e = threadIdx.x + u * 256, r = e / NV, c = (e % NV) * 8;
     const int m = m0 + r;
     if (m >= M) continue;
+#if MLP_EPI_BATCH
+    const bf16x8 xv = xres[u];
+#else
+    const bf16x8 xv = *(const bf16x8*)(x + (long)m * C + c);
+#endif
     const float s = sd ? sd[m / rows_per_sample] : 1.f;
-    bf16* xp = x + (long)m * C + c;
-    const bf16x8 xv = *(const bf16x8*)xp;
     const f32x4 t0 = *(const f32x4*)(tile + r * G::LDO + c), t1 = *(const f32x4*)(tile + r * G::LDO + c + 4);
     const f32x4 g0 = *(const f32x4*)(gamma + c), g1 = *(const f32x4*)(gamma + c + 4);
     const f32x4 c0 = *(const f32x4*)(b2 + c), c1 = *(const f32x4*)(b2 + c + 4);
@@ -287,7 +305,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       o[j] = (bf16)((float)xv[j] + (t0[j] + c0[j]) * g0[j] * s);
       o[j + 4] = (bf16)((float)xv[j + 4] + (t1[j] + c1[j]) * g1[j] * s);
     }
-    *(bf16x8*)xp = o;
+    *(bf16x8*)(x + (long)m * C + c) = o;
   }
 }
 

@@ -267,15 +267,32 @@ __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C
   // slot of (patch row r, padded pixel px, 16-byte part s); fp32 pixels use 2x the slots
   auto slot = [&](int r, int px, int s) { return r * RS + (SPP * px + px / PW) * (NV / SPP) + s; };
   // ---- stage the input patch (rows r0-3 .. r0+TR+2 of the flattened sequence) ----
+  // batches of 8 loads per thread in flight (clamped address + zero select, no branches around
+  // the loads), then their LDS stores: a couple of memory round trips per block
   const int tot = (TR + 6) * WP * NV;
-  for (int i = threadIdx.x; i < tot; i += 256) {
-    const int v = i % NV, px = i / NV;
-    const int pc = px % WP, pr = px / WP;
-    const long gr = r0 - 3 + pr;
-    const int gw = pc - 3;
-    uint4 val = make_uint4(0u, 0u, 0u, 0u);
-    if (gr >= 0 && gr < R && gw >= 0 && gw < W) val = *(const uint4*)(x + ((gr * W) + gw) * C + cb + v * VE);
-    img[slot(pr, pc, v)] = val;
+  constexpr int BATCH = 8;
+  for (int i0 = 0; i0 < tot; i0 += 256 * BATCH) {
+    uint4 val[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int i = i0 + u * 256 + threadIdx.x;
+      const int v = i % NV, px = i / NV;
+      const int pc = px % WP, pr = px / WP;
+      const long gr = r0 - 3 + pr;
+      const int gw = pc - 3;
+      const bool ok = i < tot && gr >= 0 && gr < R && gw >= 0 && gw < W;
+      const long src = ok ? ((gr * W) + gw) * C + cb + v * VE : 0;
+      const uint4 ld = *(const uint4*)(x + src);
+      val[u] = ok ? ld : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int i = i0 + u * 256 + threadIdx.x;
+      if (i < tot) {
+        const int v = i % NV, px = i / NV;
+        img[slot(px / WP, px % WP, v)] = val[u];
+      }
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -298,6 +315,16 @@ __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C
   }
   for (int kh = 0; kh < 7; ++kh) {
     const int ih = h + kh - 3;
+    // the 7 taps of this kernel row for the wave's 8 channels: wave-uniform, loaded in one batch
+    // (scalar loads) ahead of the window, so the taps cost one load round trip per row
+    f32x2 wt[7][4];
+#pragma unroll
+    for (int kw = 0; kw < 7; ++kw) {
+      const float* wp = w + (kh * 7 + kw) * C + c0;
+      const f32x4 wa = *(const f32x4*)wp, wb = *(const f32x4*)(wp + 4);
+      wt[kw][0] = f32x2{wa[0], wa[1]}; wt[kw][1] = f32x2{wa[2], wa[3]};
+      wt[kw][2] = f32x2{wb[0], wb[1]}; wt[kw][3] = f32x2{wb[2], wb[3]};
+    }
     if (ih < 0 || ih >= H) continue;  // outside this lane's image (zero padding)
     f32x2 win[PW + 6][4];
 #pragma unroll
@@ -317,15 +344,11 @@ __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C
       for (int j = 0; j < 4; ++j) win[q][j] = f32x2{v[2 * j], v[2 * j + 1]};
     }
 #pragma unroll
-    for (int kw = 0; kw < 7; ++kw) {
-      const float* wp = w + (kh * 7 + kw) * C + c0;
-      const f32x4 wa = *(const f32x4*)wp, wb = *(const f32x4*)(wp + 4);
-      const f32x2 wt[4] = {f32x2{wa[0], wa[1]}, f32x2{wa[2], wa[3]}, f32x2{wb[0], wb[1]}, f32x2{wb[2], wb[3]}};
+    for (int kw = 0; kw < 7; ++kw)
 #pragma unroll
       for (int p = 0; p < PW; ++p)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[p][j] = win[p + kw][j] * wt[j] + acc[p][j];
-    }
+        for (int j = 0; j < 4; ++j) acc[p][j] = win[p + kw][j] * wt[kw][j] + acc[p][j];
   }
   T* out = y + (orow * W + w0) * C + c0;
 #pragma unroll

@@ -22,13 +22,13 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     // clocks ramp up under sustained load: ~0.3 s of warm-up, then the best of 5 timed runs
-    for (int i = 0; i < 2000; ++i) imgcap_cnblock_mlp(M, C, z, w1, b1, w2, b2, g, nullptr, 1, x, nullptr);
+    for (int i = 0; i < 2000; ++i) imgcap_cnblock_mlp(M, C, z, nullptr, nullptr, w1, b1, w2, b2, g, nullptr, 1, x, nullptr);
     hipDeviceSynchronize();
     const int reps = 50;
     float best = 1e30f;
     for (int rep = 0; rep < 5; ++rep) {
       hipEventRecord(a);
-      for (int i = 0; i < reps; ++i) imgcap_cnblock_mlp(M, C, z, w1, b1, w2, b2, g, nullptr, 1, x, nullptr);
+      for (int i = 0; i < reps; ++i) imgcap_cnblock_mlp(M, C, z, nullptr, nullptr, w1, b1, w2, b2, g, nullptr, 1, x, nullptr);
       hipEventRecord(b);
       hipEventSynchronize(b);
       float ms;
