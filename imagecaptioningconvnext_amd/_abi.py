@@ -49,6 +49,7 @@ class MhaDesc(ctypes.Structure):
 _SIGS = {
     "imgcap_version": [],
     "imgcap_set_seed_counter": [c_void_p],
+    "imgcap_gemm_plan": [c_int] * 6 + [c_int64, c_int64, c_int, c_int, c_void_p],
     "imgcap_dwconv7": [c_int] * 5 + [c_void_p] * 5,
     "imgcap_cnblock_mlp": [c_int, c_int] + [c_void_p] * 9 + [c_int, c_void_p, c_void_p],
     "imgcap_stochastic_depth_scales": [c_int, c_int, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p],

@@ -202,11 +202,48 @@ __global__ __launch_bounds__(64 * SW) void gemm_skinny_kernel(const T* __restric
   epilogue_from_lds<16>(ep, &part[0][0][0], SKINNY_LDT, MT * 16, 0, n0, M, N, C, ldc, 0, vec_ok != 0);
 }
 
+// Which kernel serves a GEMM (also answered to callers by imgcap_gemm_plan)
+struct GemmPlan {
+  int kind;   // IMGCAP_GEMM_*
+  int split;  // K slices (1 = none)
+};
+
+static bool glds_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("IMGCAP_GEMM_GLDS");  // A/B switch for kernel benchmarks
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, long lda, long ldb, int batch, int split) {
+  if (M <= 64 && ak && bk && batch == 1) return {IMGCAP_GEMM_SKINNY, 1};
+  const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
+  const auto auto_split = [&] {
+    return (int)std::max(1L, std::min({512 / std::max(tiles128, 1L), (long)(K / 256), 32L}));
+  };
+  if (bf16_op && glds_enabled() && batch == 1 && lda % 8 == 0 && ldb % 8 == 0 && K >= 64) {
+    // split-K: requested (weight gradients, -1 = auto) or, for grids too small to fill the chip
+    // with a long K, chosen here; partial tiles go to scratch and the reduce kernel applies the
+    // epilogue.  Auto: ~2 blocks per CU, >= 4 k-tiles per slice.
+    int sk = 1;
+    if (split < 0 || (split == 1 && tiles128 < 96 && K >= 2048)) sk = auto_split();
+    else if (split > 1) sk = split;
+    if (sk > 1 || tiles128 >= 128) return {IMGCAP_GEMM_GLDS, sk};
+  }
+  if (split != 1) {
+    const int sk = split < 0 ? auto_split() : split;
+    if (sk > 1) return {IMGCAP_GEMM_TILED128, sk};
+  }
+  return {tiles128 < 512 ? IMGCAP_GEMM_TILED64 : IMGCAP_GEMM_TILED128, 1};
+}
+
 template <typename T>
 static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
                          long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
                          int vec_ok, hipStream_t st, int split) {
-  if (M <= 64 && ak && bk && batch == 1) {
+  const GemmPlan plan = gemm_plan(sizeof(T) == 2, ak, bk, M, N, K, lda, ldb, batch, split);
+  if (plan.kind == IMGCAP_GEMM_SKINNY) {
     const int blocks = (N + 15) / 16;
     const bool wide = blocks < 96;  // few column blocks: split K over 16 waves instead of 8
     const T* a = (const T*)A;
@@ -236,60 +273,41 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
     IMGCAP_CHECK_LAUNCH("imgcap_gemm(skinny)");
     return 0;
   }
-  const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   if constexpr (sizeof(T) == 2) {
-    static const bool glds_on = [] {
-      const char* e = getenv("IMGCAP_GEMM_GLDS");  // A/B switch for kernel benchmarks
-      return !(e && e[0] == '0');
-    }();
-    if (glds_on && batch == 1 && lda % 8 == 0 && ldb % 8 == 0 && K >= 64) {
-      // split-K: requested (weight gradients, -1 = auto) or, for grids too small to fill the chip
-      // with a long K, chosen here; partial tiles go to scratch and the reduce kernel applies the
-      // epilogue.  Auto: ~2 blocks per CU, >= 4 k-tiles per slice.
-      int sk = 1;
-      if (split < 0 || (split == 1 && tiles128 < 96 && K >= 2048))
-        sk = (int)std::max(1L, std::min({512 / std::max(tiles128, 1L), (long)(K / 256), 32L}));
-      else if (split > 1)
-        sk = split;
-      if (sk > 1 || tiles128 >= 128) {
-        const int kslice = sk > 1 ? ((K + sk - 1) / sk + 63) / 64 * 64 : 0;
-        const int zdim = sk > 1 ? (K + kslice - 1) / kslice : 1;
-        void* Cdst = C;
-        if (sk > 1) {
-          Cdst = workspace((size_t)zdim * M * N * sizeof(float));
-          if (!Cdst) return fail(IMGCAP_EINVAL, "imgcap_gemm: split-K workspace allocation failed");
-        }
-        dim3 grid((N + 127) / 128, (M + 127) / 128, zdim);
-        const bf16* a = (const bf16*)A;
-        const bf16* b = (const bf16*)B;
+    if (plan.kind == IMGCAP_GEMM_GLDS) {
+      const int sk = plan.split;
+      const int kslice = sk > 1 ? ((K + sk - 1) / sk + 63) / 64 * 64 : 0;
+      const int zdim = sk > 1 ? (K + kslice - 1) / kslice : 1;
+      void* Cdst = C;
+      if (sk > 1) {
+        Cdst = workspace((size_t)zdim * M * N * sizeof(float));
+        if (!Cdst) return fail(IMGCAP_EINVAL, "imgcap_gemm: split-K workspace allocation failed");
+      }
+      dim3 grid((N + 127) / 128, (M + 127) / 128, zdim);
+      const bf16* a = (const bf16*)A;
+      const bf16* b = (const bf16*)B;
 #define GL_(AKV, BKV)                                                                                              \
   hipLaunchKernelGGL((gemm_glds_kernel<128, 128, AKV, BKV>), grid, dim3(256), 0, st, a, lda, b, ldb, Cdst, ldc, M, N, \
                      K, ep, vec_ok, g_seed_ctr, kslice)
-        if (ak && bk) GL_(true, true);
-        else if (ak) GL_(true, false);
-        else if (bk) GL_(false, true);
-        else GL_(false, false);
+      if (ak && bk) GL_(true, true);
+      else if (ak) GL_(true, false);
+      else if (bk) GL_(false, true);
+      else GL_(false, false);
 #undef GL_
-        if (sk > 1) {
-          const long total = (long)M * N;
-          const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
-          hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, N, zdim, (const float*)Cdst, C,
-                             ldc, ep, g_seed_ctr);
-        }
-        IMGCAP_CHECK_LAUNCH("imgcap_gemm(glds)");
-        return 0;
+      if (sk > 1) {
+        const long total = (long)M * N;
+        const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, M, N, zdim, (const float*)Cdst, C,
+                           ldc, ep, g_seed_ctr);
       }
+      IMGCAP_CHECK_LAUNCH("imgcap_gemm(glds)");
+      return 0;
     }
   }
-  if (split != 1) {
-    // long-K reductions into a small fp32 output (weight gradients): 128x128 tiles, K sliced
-    // so that the grid reaches ~2 blocks per CU with >= 4 k-tiles per slice
-    if (split < 0) split = (int)std::max(1L, std::min({512 / std::max(tiles128, 1L), (long)K / 256, 32L}));
-    if (split > 1)
-      return launch_tiled<T, 128, 128, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, 1, ep, vec_ok, st,
-                                           split);
-  }
-  if (tiles128 < 512)
+  if (plan.kind == IMGCAP_GEMM_TILED128 && plan.split > 1)
+    return launch_tiled<T, 128, 128, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, 1, ep, vec_ok, st,
+                                         plan.split);
+  if (plan.kind == IMGCAP_GEMM_TILED64)
     return launch_tiled<T, 64, 64, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
   return launch_tiled<T, 128, 128, 64>(ak, bk, M, N, K, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, ep, vec_ok, st);
 }
@@ -403,6 +421,14 @@ extern "C" int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, 
                                batch, *epi, vec_ok, st, split);
   return gemm_dispatch<float>(a_kmajor, b_kmajor, M, N, K, A, lda, strideA, B, ldb, strideB, C, ldc, strideC,
                               batch, *epi, vec_ok, st, split);
+}
+
+extern "C" int imgcap_gemm_plan(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda, int64_t ldb,
+                                int batch, int split_k, int* splits) {
+  const GemmPlan p = gemm_plan(dtype == IMGCAP_BF16, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch,
+                               (split_k == 0 || split_k == 1) ? 1 : split_k);
+  if (splits) *splits = p.split;
+  return p.kind;
 }
 
 extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64_t ldx, float* out, float beta,

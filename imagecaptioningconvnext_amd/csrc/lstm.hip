@@ -47,9 +47,27 @@ template <> DEV void load8<float>(const float* p, float (&v)[8]) {
   for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
 }
 
-// ---- forward attention step: one block (16 waves) per batch row ------------------------
+// 8 consecutive elements kept as raw 16-byte words until used (1 word bf16, 2 words fp32)
+template <typename T> struct Raw8 { uint4 u[sizeof(T) / 2]; };
 template <typename T>
+DEV void raw_load(Raw8<T>& r, const T* p) {
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 2); ++i) r.u[i] = *(const uint4*)(p + i * (16 / sizeof(T)));
+}
+template <typename T>
+DEV void raw_to_f(const Raw8<T>& r, float (&x)[8]) { load8<T>((const T*)r.u, x); }
+
+// ---- forward attention step: one block (16 waves) per batch row ------------------------
+// Latency-bound (a few hundred KB per step spread over B blocks), so every global load the
+// block needs is issued up front, before any reduction:
+//   scores : wave w owns pixels p = w, w+16, ... (<= 4); lane l owns 8 attention units
+//            (att1 rows, att2 and w_f slices in registers)
+//   context: thread = (8-channel vector v of E, pixel group pg): pixels pg, pg + G, ...
+//            (<= MPP enc vectors in registers), partial sums reduced over pg in LDS
+template <typename T, int MPP>
 __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc d, int t) {
+  __shared__ float e_s[MAXP];
+  extern __shared__ __attribute__((aligned(16))) float part[];  // [G][E] context partials
   const int b = blockIdx.x;
   const int P = d.P, E = d.E, A = d.A, Tn = d.T;
   const int W3 = A + E + 4 * d.D;
@@ -58,44 +76,77 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
   const float* g1 = d.g1 + bt * W3;  // [att2 | gate_pre | hh]
   const T* att1 = (const T*)d.att1 + (long)b * P * A;
   const T* enc = (const T*)d.enc + (long)b * P * E;
-  __shared__ float e_s[MAXP];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // scores e_p = w_f . relu(att1_p + att2)   (full_att bias cancels in the softmax)
-  for (int p = w; p < P; p += ATT_WAVES) {
-    float s = 0.f;
-    for (int a = lane * 8; a < A; a += 512) {
-      float x[8];
-      load8<T>(att1 + (long)p * A + a, x);
-      const f32x4 g0 = *(const f32x4*)(g1 + a), g4 = *(const f32x4*)(g1 + a + 4);
-      const f32x4 w0 = *(const f32x4*)(d.w_f + a), w4 = *(const f32x4*)(d.w_f + a + 4);
+  const int NVE = E / 8, G = ATT_THREADS / NVE;
+  const int v = threadIdx.x % NVE, pg = threadIdx.x / NVE;
+  const bool ctx_thread = pg < G;
+  // ---- all loads ----
+  const int a0 = lane * 8;
+  const bool a_ok = a0 < A;
+  float att2[8], wf[8];
+  load8<float>(g1 + (a_ok ? a0 : 0), att2);
+  load8<float>(d.w_f + (a_ok ? a0 : 0), wf);
+  Raw8<T> a1[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s += w0[j] * fmaxf(x[j] + g0[j], 0.f);
-        s += w4[j] * fmaxf(x[j + 4] + g4[j], 0.f);
-      }
+  for (int i = 0; i < 4; ++i) {
+    const int p = w + i * ATT_WAVES;
+    raw_load(a1[i], att1 + (long)min(p, P - 1) * A + (a_ok ? a0 : 0));
+  }
+  Raw8<T> ev[MPP];
+#pragma unroll
+  for (int i = 0; i < MPP; ++i) {
+    const int p = pg + i * G;
+    raw_load(ev[i], enc + (long)min(p, P - 1) * E + v * 8);
+  }
+  // ---- scores e_p = w_f . relu(att1_p + att2)   (full_att bias cancels in the softmax) ----
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = w + i * ATT_WAVES;
+    float x[8];
+    raw_to_f(a1[i], x);
+    float sc = 0.f;
+    if (a_ok) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sc += wf[j] * fmaxf(x[j] + att2[j], 0.f);
     }
-    s = wave_sum(s);
-    if (lane == 0) e_s[p] = s;
+    sc = wave_sum(sc);
+    if (lane == 0 && p < P) e_s[p] = sc;
   }
   __syncthreads();
   if (w == 0) {
-    const float v = lane < P ? e_s[lane] : -INFINITY;
-    const float m = wave_max(v);
-    const float ex = lane < P ? __expf(v - m) : 0.f;
-    const float sum = wave_sum(ex);
-    const float al = ex / sum;
+    const float vv = lane < P ? e_s[lane] : -INFINITY;
+    const float m = wave_max(vv);
+    const float ex = lane < P ? __expf(vv - m) : 0.f;
+    const float al = ex / wave_sum(ex);
     if (lane < P) {
       e_s[lane] = al;
       d.alphas[bt * P + lane] = active ? al : 0.f;
     }
   }
   __syncthreads();
+  // ---- context partials over this thread's pixels ----
+  if (ctx_thread) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < MPP; ++i) {
+      const int p = pg + i * G;
+      if (p < P) {
+        float x[8];
+        raw_to_f(ev[i], x);
+        const float al = e_s[p];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += al * x[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[pg * E + v * 8 + j] = acc[j];
+  }
+  __syncthreads();
   T* zs = (T*)d.zs + bt * E;
   float* awe = d.awe + bt * E;
   for (int e = threadIdx.x; e < E; e += ATT_THREADS) {
     float s = 0.f;
-#pragma unroll 7
-    for (int p = 0; p < P; ++p) s += e_s[p] * to_f(enc[(long)p * E + e]);
+    for (int q = 0; q < G; ++q) s += part[q * E + e];
     const float gate = sigmoidf_(g1[A + e]);
     awe[e] = s;
     zs[e] = from_f<T>(gate * s);
@@ -247,7 +298,10 @@ __global__ __launch_bounds__(64 * SW) void dh_cell_kernel(imgcap_lstm_desc d, in
 }
 
 // ---- backward attention step: recurrent part only ---------------------------------------
-template <typename T>
+// Same load-everything-first structure as attn_fwd_kernel: the enc vectors (for d alpha =
+// enc . d awe), the att1 vectors (for d att2), the dz slabs, gate, context and alphas are all
+// requested before the first reduction; the reductions then run through LDS.
+template <typename T, int MPP>
 __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc d, int t) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x;
@@ -260,38 +314,83 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
     if (threadIdx.x < P) d.de[bt * P + threadIdx.x] = 0.f;
     return;
   }
-  float* dawe = sm;              // [E]
-  float* al = sm + E;            // [MAXP]
-  float* dal = al + MAXP;        // [MAXP]
-  float* part = dal + MAXP;      // [2][A]
+  const int NVE = E / 8, G = ATT_THREADS / NVE;
+  const int NVA = A / 8, GA = ATT_THREADS / NVA;
+  float* dawe = sm;                  // [E]
+  float* al = dawe + E;              // [MAXP]
+  float* dal = al + MAXP;            // [MAXP]
+  float* red = dal + MAXP;           // [P][NVE] d-alpha partials, then [GA][A] d-att2 partials
   const float* g1 = d.g1 + bt * W3;
   const int NX = E + d.D;
-  const float* awe = d.awe + bt * E;
-  for (int e = threadIdx.x; e < E; e += ATT_THREADS) {
-    float dz = 0.f;  // dL/dz_t = sum of the x_partial slabs
-    for (int z = 0; z < d.x_slices; ++z) dz += d.dz[((long)z * d.B + b) * NX + e];
-    const float s = sigmoidf_(g1[A + e]);
-    dawe[e] = dz * s;
-    dcat[A + e] = from_f<T>(dz * awe[e] * s * (1.f - s));  // d gate_pre
-  }
-  if (threadIdx.x < P) al[threadIdx.x] = d.alphas[bt * P + threadIdx.x];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const T* enc = (const T*)d.enc + (long)b * P * E;
-  for (int p = w; p < P; p += ATT_WAVES) {  // d alpha_p = enc_p . d awe  (+ reg/upstream term)
-    float s = 0.f;
-    for (int e = lane * 8; e < E; e += 512) {
-      float x[8];
-      load8<T>(enc + (long)p * E + e, x);
+  const T* att1 = (const T*)d.att1 + (long)b * P * A;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int v = tid % NVE, pg = tid / NVE;
+  const int va = tid % NVA, pga = tid / NVA;
+  // ---- all loads ----
+  Raw8<T> ev[MPP];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += x[j] * dawe[e + j];
+  for (int i = 0; i < MPP; ++i) raw_load(ev[i], enc + (long)min(pg + i * G, P - 1) * E + v * 8);
+  Raw8<T> av[MPP];
+#pragma unroll
+  for (int i = 0; i < MPP; ++i) raw_load(av[i], att1 + (long)min(pga + i * GA, P - 1) * A + va * 8);
+  float att2[8];
+  load8<float>(g1 + va * 8, att2);
+  float gate[8], awe[8], dz[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (pg == 0) {
+    load8<float>(g1 + A + v * 8, gate);
+    load8<float>(d.awe + bt * E + v * 8, awe);
+    for (int z = 0; z < d.x_slices; ++z) {  // dL/dz_t = sum of the x_partial slabs
+      float q[8];
+      load8<float>(d.dz + ((long)z * d.B + b) * NX + v * 8, q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dz[j] += q[j];
     }
+  }
+  float alpha_in = 0.f;
+  if (tid < P) alpha_in = d.alphas[bt * P + tid];
+  // ---- d awe = dz * sigmoid(gate), d gate_pre = dz * awe * s (1 - s) ----
+  if (pg == 0) {
+    float dg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = sigmoidf_(gate[j]);
+      dawe[v * 8 + j] = dz[j] * s;
+      dg[j] = dz[j] * awe[j] * s * (1.f - s);
+    }
+    st_g<T, 8>(dcat + A + v * 8, dg);
+  }
+  if (tid < P) al[tid] = alpha_in;
+  __syncthreads();
+  // ---- d alpha_p = enc_p . d awe (+ upstream) ----
+  if (pg < G) {
+    float dv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dv[j] = dawe[v * 8 + j];
+#pragma unroll
+    for (int i = 0; i < MPP; ++i) {
+      const int p = pg + i * G;
+      if (p < P) {
+        float x[8];
+        raw_to_f(ev[i], x);
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += x[j] * dv[j];
+        red[p * NVE + v] = s;
+      }
+    }
+  }
+  __syncthreads();
+  for (int p = w; p < P; p += ATT_WAVES) {
+    float s = 0.f;
+    for (int q = lane; q < NVE; q += 64) s += red[p * NVE + q];
     s = wave_sum(s);
-    if (lane == 0) dal[p] = s + (d.dalpha ? d.dalpha[bt * P + p] : 0.f);
+    if (lane == 0) dal[p] = s;
   }
   __syncthreads();
   if (w == 0) {  // softmax backward -> d score
-    const float a = lane < P ? al[lane] : 0.f, da = lane < P ? dal[lane] : 0.f;
+    const float a = lane < P ? al[lane] : 0.f;
+    const float da = lane < P ? dal[lane] + (d.dalpha ? d.dalpha[bt * P + lane] : 0.f) : 0.f;
     const float dot = wave_sum(a * da);
     if (lane < P) {
       const float de = a * (da - dot);
@@ -300,19 +399,29 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
     }
   }
   __syncthreads();
-  // d att2[a] = w_f[a] * sum_p de_p [att1[p,a] + att2[a] > 0]; two halves of p in parallel
-  const T* att1 = (const T*)d.att1 + (long)b * P * A;
-  const int half = threadIdx.x / 512, tid = threadIdx.x % 512;
-  const int p0 = half * ((P + 1) / 2), p1 = min(P, p0 + (P + 1) / 2);
-  for (int a = tid; a < A; a += 512) {
-    const float a2 = g1[a];
-    float s = 0.f;
-#pragma unroll 7
-    for (int p = p0; p < p1; ++p) s += (to_f(att1[(long)p * A + a]) + a2 > 0.f) ? dal[p] : 0.f;
-    part[half * A + a] = s;
+  // ---- d att2[a] = w_f[a] * sum_p de_p [att1[p,a] + att2[a] > 0] ----
+  if (pga < GA) {
+    float sacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < MPP; ++i) {
+      const int p = pga + i * GA;
+      if (p < P) {
+        float x[8];
+        raw_to_f(av[i], x);
+        const float de = dal[p];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sacc[j] += (x[j] + att2[j] > 0.f) ? de : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[pga * A + va * 8 + j] = sacc[j];
   }
   __syncthreads();
-  for (int a = threadIdx.x; a < A; a += ATT_THREADS) dcat[a] = from_f<T>((part[a] + part[A + a]) * d.w_f[a]);
+  for (int a = tid; a < A; a += ATT_THREADS) {
+    float s = 0.f;
+    for (int q = 0; q < GA; ++q) s += red[q * A + a];
+    dcat[a] = from_f<T>(s * d.w_f[a]);
+  }
 }
 
 // ---- attention parameter gradients, summed over all steps at once -----------------------
@@ -404,6 +513,17 @@ static imgcap_epilogue f32_epi(const float* bias) {
   return ep;
 }
 
+// pixels per thread of the attention kernels' (vector, pixel-group) mappings
+static int attn_mpp(const imgcap_lstm_desc& d) {
+  const int G = ATT_THREADS / (d.E / 8), GA = ATT_THREADS / (d.A / 8);
+  return std::max((d.P + G - 1) / G, (d.P + GA - 1) / GA);
+}
+static size_t attn_bwd_shm(const imgcap_lstm_desc& d) {
+  const int GA = ATT_THREADS / (d.A / 8);
+  const size_t red = std::max((size_t)d.P * (d.E / 8), (size_t)GA * d.A);
+  return (d.E + 2 * MAXP + red) * sizeof(float);
+}
+
 // SW waves per block and DEPTH k-steps per load round: DEPTH = the wave's k-step count
 // rounded up to a power of two (fp32 fragments are twice as wide: at most 2)
 static int depth_for(int klen, int sw, bool f32) {
@@ -428,11 +548,20 @@ static int lstm_fwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
   const int nrg = (d.B + RG - 1) / RG;
   const imgcap_epilogue e1 = f32_epi(d.b_hcat);
   const int dpt_g = depth_for(d.E, 8, F32);
+  const int mpp = attn_mpp(d);
+  const size_t shm_f = (size_t)(ATT_THREADS / (d.E / 8)) * d.E * sizeof(float);
   for (int t = 0; t < d.T; ++t) {
     int rc = imgcap_gemm(ct, 1, 1, d.B, W3, d.D, (const T*)d.hprev + (long)t * d.D, (long)d.T * d.D, 0, d.w_hcat,
                          d.D, 0, d.g1 + (long)t * W3, (long)d.T * W3, 0, 1, &e1, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(attn_fwd_kernel<T>, dim3(d.B), dim3(ATT_THREADS), 0, st, d, t);
+    if (mpp <= 4)
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 4>), dim3(d.B), dim3(ATT_THREADS), shm_f, st, d, t);
+    else if (mpp <= 5)
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 5>), dim3(d.B), dim3(ATT_THREADS), shm_f, st, d, t);
+    else if (mpp <= 8)
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 8>), dim3(d.B), dim3(ATT_THREADS), shm_f, st, d, t);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 16>), dim3(d.B), dim3(ATT_THREADS), shm_f, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm attn_fwd");
     LSTM_DEPTH_SWITCH(dpt_g, gate_cell_fwd_kernel, 8, dim3(d.D / 4, nrg), dim3(512), 0, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm gate_cell_fwd");
@@ -449,7 +578,8 @@ static int lstm_bwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
   const int ky = ((KY + d.y_slices - 1) / d.y_slices + 31) / 32 * 32;
   const int sx = (K4 + kx - 1) / kx, sy = (KY + ky - 1) / ky;  // non-empty slices
   const int dpt_x = depth_for(kx, 8, F32), dpt_y = depth_for(ky, 4, F32);
-  const size_t shm = (d.E + 2 * MAXP + 2 * d.A) * sizeof(float);
+  const size_t shm = attn_bwd_shm(d);
+  const int mpp = attn_mpp(d);
   imgcap_lstm_desc dd = d;
   dd.x_slices = sx;
   dd.y_slices = sy;
@@ -458,7 +588,14 @@ static int lstm_bwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
   for (int t = d.T - 1; t >= 0; --t) {
     LSTM_DEPTH_SWITCH(dpt_x, x_partial_kernel, 8, dim3((NX + 15) / 16, sx, nrg), dim3(512), 0, st, dd, t, kx);
     IMGCAP_CHECK_LAUNCH("lstm x_partial");
-    hipLaunchKernelGGL(attn_bwd_kernel<T>, dim3(d.B), dim3(ATT_THREADS), shm, st, dd, t);
+    if (mpp <= 4)
+      hipLaunchKernelGGL((attn_bwd_kernel<T, 4>), dim3(d.B), dim3(ATT_THREADS), shm, st, dd, t);
+    else if (mpp <= 5)
+      hipLaunchKernelGGL((attn_bwd_kernel<T, 5>), dim3(d.B), dim3(ATT_THREADS), shm, st, dd, t);
+    else if (mpp <= 8)
+      hipLaunchKernelGGL((attn_bwd_kernel<T, 8>), dim3(d.B), dim3(ATT_THREADS), shm, st, dd, t);
+    else
+      hipLaunchKernelGGL((attn_bwd_kernel<T, 16>), dim3(d.B), dim3(ATT_THREADS), shm, st, dd, t);
     IMGCAP_CHECK_LAUNCH("lstm attn_bwd");
     LSTM_DEPTH_SWITCH(dpt_y, dh_cell_kernel, 4, dim3(d.D / 16, sy, nrg), dim3(256), 0, st, dd, t, ky);
     IMGCAP_CHECK_LAUNCH("lstm dh_cell");
@@ -475,6 +612,10 @@ static int check_desc(const imgcap_lstm_desc* d) {
   IMGCAP_REQUIRE(d->dtype == IMGCAP_F32 || d->dtype == IMGCAP_BF16, "lstm: dtype");
   IMGCAP_REQUIRE(d->B > 0 && d->T > 0 && d->P > 0 && d->P <= MAXP, "lstm: need 0 < P <= 64");
   IMGCAP_REQUIRE(d->E % 8 == 0 && d->A % 8 == 0 && d->M % 8 == 0 && d->D % 16 == 0, "lstm: E, A, M % 8, D % 16");
+  IMGCAP_REQUIRE(d->A <= 512 && d->E <= 8 * ATT_THREADS, "lstm: attention_dim <= 512, encoder_dim <= 8192");
+  IMGCAP_REQUIRE(attn_mpp(*d) <= 16, "lstm: too many pixels per attention thread");
+  IMGCAP_REQUIRE((size_t)(ATT_THREADS / (d->E / 8)) * d->E * 4 <= 65536 && attn_bwd_shm(*d) <= 65536,
+                 "lstm: attention LDS budget");
   return 0;
 }
 
@@ -490,7 +631,6 @@ extern "C" int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream) {
 
 extern "C" int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream) {
   if (int rc = check_desc(d)) return rc;
-  IMGCAP_REQUIRE((d->E + 2 * MAXP + 2 * d->A) * 4 <= 65536, "lstm bwd: E/A too large for LDS");
   IMGCAP_REQUIRE((size_t)d->T * PCH * 4 <= 65536, "lstm bwd: T too large for LDS");
   IMGCAP_REQUIRE(d->w_zh_t && d->w_att_t && d->de && d->dbea && d->ws_y && d->y_cnt,
                  "lstm bwd: transposed weights / de / dbea / ws_y / y_cnt needed");

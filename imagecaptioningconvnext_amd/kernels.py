@@ -41,6 +41,23 @@ def _ld(t, trans):
     return t.stride(-2) if t.dim() >= 2 else t.shape[-1]
 
 
+_gemm_recorder = None
+
+
+def record_gemms(recorder):
+    """Collect every ``gemm`` call (a replayable closure + its shape) into ``recorder`` (a list),
+    or stop with None.  Used by the bench's roofline to re-time the step's GEMMs in isolation."""
+    global _gemm_recorder
+    _gemm_recorder = recorder
+
+
+def gemm_plan(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch=1, split_k=0):
+    """(kernel kind, K slices) imgcap_gemm picks for these operands (IMGCAP_GEMM_* ids)."""
+    sp = ctypes.c_int(1)
+    kind = _abi.lib().imgcap_gemm_plan(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch, split_k, ctypes.byref(sp))
+    return kind, sp.value
+
+
 def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None, bias=None, act=ACT_NONE, alpha=1.0,
          beta=0.0, res=None, aux=None, aux_scale=1.0, colscale=None, rowscale=None, rows_per_scale=1, drop_p=0.0,
          seed=0, drop_stream=0, drop_ld=None, M=None, N=None, K=None, split_k=0):
@@ -83,9 +100,14 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None, bias=N
     ep.drop_stream = drop_stream
     ep.drop_ld = N if drop_ld is None else drop_ld
     ep.split_k = split_k
-    _abi.call("imgcap_gemm", dt(a), 0 if trans_a else 1, 1 if trans_b else 0, M, N, K,
-              a.data_ptr(), _ld(a, trans_a), 0, b.data_ptr(), _ld(b, trans_b), 0,
-              out.data_ptr(), out.stride(0), 0, 1, ctypes.byref(ep), stream())
+    args = (dt(a), 0 if trans_a else 1, 1 if trans_b else 0, M, N, K, a.data_ptr(), _ld(a, trans_a), 0, b.data_ptr(),
+            _ld(b, trans_b), 0, out.data_ptr(), out.stride(0), 0, 1)
+    if _gemm_recorder is not None:
+        keep = (a, b, out, bias, res, aux, colscale, rowscale, ep)
+        _gemm_recorder.append(dict(M=M, N=N, K=K, dtype=args[0], ak=args[1], bk=args[2], lda=args[7], ldb=args[10],
+                                   split_k=split_k, keep=keep,
+                                   call=lambda: _abi.call("imgcap_gemm", *args, ctypes.byref(ep), stream())))
+    _abi.call("imgcap_gemm", *args, ctypes.byref(ep), stream())
     return out
 
 

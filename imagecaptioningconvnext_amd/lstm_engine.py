@@ -210,10 +210,12 @@ class LstmEngine:
         K.transpose(w["hcat"][A + E:], out=wzh_t[E:])
         watt_t = K.transpose(w["hcat"][:A + E])                    # [D, A + E] = [W_da; W_fb]^T
         d = s["desc"]
-        for k, v in dict(w_zh_t=wzh_t, w_att_t=watt_t, dhs=dhs, dalpha=dalpha, dcat=dcat, dz=dz, ws_y=ws_y,
-                         y_cnt=self._y_cnt, dh=dh, dc=dc, de=de, datt1=datt1, dwf=dwf, dbea=dbea).items():
+        bufs = dict(w_zh_t=wzh_t, w_att_t=watt_t, dhs=dhs, dalpha=dalpha, dcat=dcat, dz=dz, ws_y=ws_y,
+                    y_cnt=self._y_cnt, dh=dh, dc=dc, de=de, datt1=datt1, dwf=dwf, dbea=dbea)
+        for k, v in bufs.items():
             setattr(d, k, K.ptr(v))
         d.x_slices, d.y_slices = xs, ys
+        s["bwd_bufs"] = bufs  # the descriptor points into these: keep them alive as long as `s`
         _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream())
         dc2 = dcat.view(BT, W3)
         dgates = dc2[:, A + E:]

@@ -1,17 +1,31 @@
 """Live roofline of the bench step's dominant kernel (bench.py ``roofline`` field).
 
-Each candidate below replays ONE kernel launch of the step with the step's own shapes on the
-current HIP stream, timed with HIP events over ``reps`` back-to-back launches; its algorithmic
-traffic/work per launch is stated next to it.  The dominant kernel is the
-candidate with the largest (avg launch time x launches per step); its achieved rate is reported
-against the MI355X peak (HBM 8 TB/s, bf16 MFMA 2.5 PF/s dense).
+Candidates are timed on the current HIP stream with HIP events around back-to-back launches
+replayed from a HIP graph (so host launch cost does not hide short kernels), each with its
+algorithmic work per launch:
+
+  * every GEMM of one train step: the step runs once eagerly with ``kernels.record_gemms``
+    collecting each ``imgcap_gemm`` call; the calls are grouped by the kernel that serves them
+    (``imgcap_gemm_plan``: one group per kernel symbol, as rocprofv3 lists them) and each call
+    is re-timed in isolation.  Work = 2*M*N*K per call; a group's achieved rate is
+    sum(work) / sum(time), i.e. its average launch's work over its average launch duration.
+  * the fused ConvNeXt MLP (cnblock_mlp) per stage width: 2 * 2 * M * C * 4C per launch.
+  * the depthwise 7x7 per stage: HBM bytes = read x + write y (+ weights).
+
+The dominant kernel is the group with the largest time per step; its rate is reported against
+the MI355X peak (bf16 dense MFMA 2.5 PFLOP/s, HBM 8 TB/s; MI355X_MICROARCH.md).
 """
+import collections
+
 import torch
 
 from . import kernels as K
 
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0
+
+_KIND_NAME = {1: "gemm_skinny_kernel", 2: "gemm_kernel<64,64,64>", 3: "gemm_kernel<128,128,64>",
+              4: "gemm_glds_kernel<128,128>"}
 
 
 def time_launch(fn, reps=50, warm=5, graph=True):
@@ -43,67 +57,76 @@ def time_launch(fn, reps=50, warm=5, graph=True):
     return a.elapsed_time(b) / reps * 1e-3  # seconds per launch
 
 
-def _candidates_lstm(trainer, B, dev):
-    eng = trainer.eng
-    E, A, D, W3 = eng.E, eng.A, eng.D, eng.W3
-    w = eng.weights()
-    ct = eng.ct
-    es = 2 if ct == torch.bfloat16 else 4
-    h = torch.randn(B, D, device=dev).to(ct)
-    g1 = torch.empty(B, W3, device=dev)
-    cands = []
+def _gemm_groups(trainer, batch):
+    rec = []
+    K.record_gemms(rec)
+    try:
+        trainer._fwd_bwd(*batch)
+    finally:
+        K.record_gemms(None)
+    torch.cuda.synchronize()
+    groups = collections.OrderedDict()
+    for c in rec:
+        kind, splits = K.gemm_plan(c["dtype"], c["ak"], c["bk"], c["M"], c["N"], c["K"], c["lda"], c["ldb"], 1,
+                                   c["split_k"])
+        name = _KIND_NAME.get(kind, f"gemm kind {kind}")
+        if kind in (2, 3, 4):
+            name += f"<ak={c['ak']},bk={c['bk']}>" + (" (split-K)" if splits > 1 else "")
+        g = groups.setdefault(name, dict(name=name, calls=[], bound="mfma"))
+        g["calls"].append(c)
+    out = []
+    for g in groups.values():
+        t_tot, f_tot = 0.0, 0.0
+        for c in g["calls"]:
+            t_tot += time_launch(c["call"], reps=20, warm=2)
+            f_tot += 2.0 * c["M"] * c["N"] * c["K"]
+        n = len(g["calls"])
+        shapes = sorted({(c["M"], c["N"], c["K"]) for c in g["calls"]})
+        out.append(dict(name=g["name"], bound="mfma", per_step=n, t=t_tot / n, flops=f_tot / n,
+                        note=f"{n} launches/step, shapes (M,N,K) {shapes[:6]}{' ...' if len(shapes) > 6 else ''}"))
+    return out
 
-    def g1_gemm():
-        K.gemm(h, w["hcat"], trans_b=True, bias=w["bhcat"], out=g1)
 
-    cands.append(dict(name="gemm_skinny (LSTM step: h_{t-1} -> [att2|gate|hh])", fn=g1_gemm, per_step=51,
-                      bound="hbm", bytes=W3 * D * es + B * D * es + B * W3 * 4,
-                      note=f"M={B} N={W3} K={D}: weight stream W3*D*2 B + A + fp32 C per launch"))
-    return cands
-
-
-def _candidates_encoder(trainer, B, dev):
+def _encoder_groups(trainer, B, dev):
     enc = trainer.encoder
+    if enc.compute_dtype != torch.bfloat16:
+        return []
     pk = enc._pack()
-    blk = pk["stages"][0][0][0]
-    C = blk["w1"].shape[1]
-    Mrows = B * 56 * 56
-    z = torch.randn(Mrows, C, device=dev).to(enc.compute_dtype)
-    hid = torch.empty(Mrows, 4 * C, device=dev, dtype=enc.compute_dtype)
-    x = torch.randn(B, 56, 56, C, device=dev).to(enc.compute_dtype)
-    y = torch.empty_like(x)
-    cands = []
+    out = []
+    hw = 56
+    for st, (blocks, _) in enumerate(pk["stages"]):
+        blk = blocks[0]
+        C = blk["w1"].shape[1]
+        M = B * hw * hw
+        x = torch.randn(B, hw, hw, C, device=dev).to(torch.bfloat16)
+        y = torch.empty_like(x)
+        if C in K.CNBLOCK_MLP_CHANNELS:
+            x2 = x.view(M, C)
+            z = y.view(M, C)
 
-    def pw1():
-        K.gemm(z, blk["w1"], trans_b=True, bias=blk["b1"], act=K.ACT_GELU, out=hid)
-
-    cands.append(dict(name="gemm_kernel 128x128 (ConvNeXt stage-1 pointwise Linear C->4C + GELU)", fn=pw1,
-                      per_step=3, bound="mfma", flops=2 * Mrows * C * 4 * C,
-                      note=f"M={Mrows} N={4 * C} K={C}"))
-
-    def dw():
-        K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], y)
-
-    es = 2 if enc.compute_dtype == torch.bfloat16 else 4
-    cands.append(dict(name="dwconv7_ln (ConvNeXt stage-1 depthwise 7x7 + LayerNorm)", fn=dw, per_step=3,
-                      bound="hbm", bytes=2 * Mrows * C * es + 49 * C * 4,
-                      note=f"B*H*W={Mrows} C={C}: read x + write y"))
-    return cands
+            def mlp(blk=blk, z=z, x2=x2):
+                K.cnblock_mlp(z, blk["w1"], blk["b1"], blk["w2"], blk["b2"], blk["gamma"], x2, ln_w=blk["lnw"],
+                              ln_b=blk["lnb"])
+            out.append(dict(name=f"cnblock_mlp_kernel<{C}> (stage {st + 1} fused MLP)", bound="mfma",
+                            per_step=len(blocks), t=time_launch(mlp, reps=20), flops=2.0 * 2 * M * C * 4 * C,
+                            note=f"M={M} C={C}: LN + Linear C->4C + GELU + Linear 4C->C + scale + residual"))
+        if hw <= 64:
+            def dw(blk=blk, x=x, y=y):
+                K.dwconv7(x, blk["w49"], blk["dwb"], y)
+            out.append(dict(name=f"dwconv7_kernel (stage {st + 1}, C={C})", bound="hbm", per_step=len(blocks),
+                            t=time_launch(dw, reps=20), bytes=2.0 * M * C * 2 + 49 * C * 4,
+                            note=f"B*H*W={M} C={C}: read x + write y (bf16)"))
+        hw //= 2
+    return out
 
 
 def measure(cfg, trainer, batch):
     dev = batch[0].device
     B = batch[0].shape[0]
-    cands = _candidates_encoder(trainer, B, dev)
-    if cfg["decoder"] == "lstm":
-        cands += _candidates_lstm(trainer, B, dev)
-    best = None
+    cands = _gemm_groups(trainer, batch) + _encoder_groups(trainer, B, dev)
     for c in cands:
-        t = time_launch(c["fn"])
-        c["t"] = t
-        c["share"] = t * c["per_step"]
-        if best is None or c["share"] > best["share"]:
-            best = c
+        c["share"] = c["t"] * c["per_step"]
+    best = max(cands, key=lambda c: c["share"])
     t = best["t"]
     if best["bound"] == "hbm":
         achieved = best["bytes"] / t / 1e9
@@ -111,7 +134,8 @@ def measure(cfg, trainer, batch):
     else:
         achieved = best["flops"] / t / 1e12
         peak, unit = PEAK_BF16_TFLOPS, "TFLOP/s"
+    ranked = sorted(cands, key=lambda c: -c["share"])
     return {"bound": best["bound"], "achieved": round(achieved, 2), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": None, "kernel": best["name"],
             "avg_launch_us": round(t * 1e6, 2), "launches_per_step": best["per_step"], "shape": best["note"],
-            "others": {c["name"]: round(c["t"] * 1e6, 2) for c in cands if c is not best}}
+            "others_us_per_step": {c["name"]: round(c["share"] * 1e6, 1) for c in ranked[1:8]}}

@@ -81,6 +81,11 @@ int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                 const imgcap_epilogue* epi, void* stream);
 
 /* out[c, r] = in[r, c]  (weight transposes for the k-major skinny GEMMs) */
+/* Which kernel imgcap_gemm launches for these operands (diagnostics and the bench's roofline):
+ * returns one of IMGCAP_GEMM_*; *splits (if not NULL) = K slices (1 = none). */
+enum { IMGCAP_GEMM_SKINNY = 1, IMGCAP_GEMM_TILED64 = 2, IMGCAP_GEMM_TILED128 = 3, IMGCAP_GEMM_GLDS = 4 };
+int imgcap_gemm_plan(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda, int64_t ldb,
+                     int batch, int split_k, int* splits);
 int imgcap_transpose(int dtype, int rows, int cols, const void* in, int64_t ldi, void* out, int64_t ldo,
                      void* stream);
 

@@ -76,6 +76,29 @@ def mlp():
         print(f"cnblock_mlp 2-GEMM M={M:6d} C={C:4d}: {t * 1e6:8.1f} us {flops / t / 1e12:7.1f} TFLOP/s")
 
 
+def lstm():
+    """LSTM recurrence at the C2 shape (B=32, T=51, E=768, A=D=M=512): whole imgcap_lstm_tf_fwd /
+    _bwd launches (3 kernels per step each) replayed from a graph; per-step time = total / T."""
+    import ctypes
+    from imagecaptioningconvnext_amd import _abi
+    from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
+    B, L, V = 32, 52, 9490
+    dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=dev,
+                               encoder_dim=768, dropout=0.5, compute_dtype=bf).to(dev)
+    eng = dec.engine()
+    enc = torch.randn(B, 7, 7, 768, device=dev).to(bf)
+    caps = torch.randint(1, V - 3, (B, L), device=dev)
+    lens = torch.full((B, 1), L, device=dev, dtype=torch.long)
+    s = eng.forward(enc, caps, lens, fixed_T=True)
+    eng.backward(s)
+    d = s["desc"]
+    T = s["T"]
+    t = time_launch(lambda: _abi.call("imgcap_lstm_tf_fwd", ctypes.byref(d), K.stream()), reps=5, warm=2)
+    print(f"lstm fwd recurrence: {t * 1e6:8.1f} us total, {t * 1e6 / T:6.2f} us/step")
+    t = time_launch(lambda: _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream()), reps=5, warm=2)
+    print(f"lstm bwd recurrence: {t * 1e6:8.1f} us total, {t * 1e6 / T:6.2f} us/step")
+
+
 def misc():
     B = 32
     for (H, C) in ((56, 96), (28, 192), (14, 384), (7, 768)):
@@ -113,6 +136,8 @@ if __name__ == "__main__":
         misc()
     if which in ("all", "mlp"):
         mlp()
+    if which in ("all", "lstm"):
+        lstm()
     if which == "mlpdw":  # short run for PMC collection: s1 shapes only
         B, H, C = 32, 56, 96
         x = torch.randn(B, H, H, C, device=dev).to(bf)
