@@ -173,8 +173,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
   const long total = (long)M * N;
   const long plane = total;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    // slices added in order, loads issued 8 at a time
     float t = 0.f;
-    for (int z = 0; z < S; ++z) t += P[z * plane + i];
+    for (int z0 = 0; z0 < S; z0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = z0 + u < S ? P[(z0 + u) * plane + i] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t += v[u];
+    }
     const int m = (int)(i / N), n = (int)(i % N);
     epi_scalar(ep, C, (long)m * ldc + n, m, n, t);
   }
@@ -356,13 +363,32 @@ __global__ __launch_bounds__(256) void colsum_kernel(int rows, int cols, const T
   }
 }
 
+// Block = 32 columns x 8 slice groups: each thread adds the slices y = g, g+8, .. (loads issued
+// together, <= 8 per thread for <= 64 slices), then the 8 group sums of a column are added in
+// LDS in a fixed order.
 __global__ __launch_bounds__(256) void colsum_reduce_kernel(int cols, int slices, const float* __restrict__ ws,
                                                             float* __restrict__ out, float beta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  const int cc = c < cols ? c : 0;
+  float v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int y = g + 8 * u;
+    v[u] = y < slices ? ws[(long)y * cols + cc] : 0.f;
+  }
   float t = 0.f;
-  for (int y = 0; y < slices; ++y) t += ws[(long)y * cols + c];
-  out[c] = (beta != 0.f ? beta * out[c] : 0.f) + t;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) t += v[u];
+  red[g][cl] = t;
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += red[q][cl];
+    out[c] = (beta != 0.f ? beta * out[c] : 0.f) + s;
+  }
 }
 
 // out[c][r] = in[r][c] (2-D transpose through an LDS tile; weights -> k-major copies)
@@ -454,8 +480,7 @@ extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, rows, cols, (const float*)x, ldx, dst, beta,
                        vec_ok, std::max(rps, 1));
   if (slices > 1)
-    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, cols, slices, dst, out,
-                       beta);
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((cols + 31) / 32), dim3(256), 0, st, cols, slices, dst, out, beta);
   IMGCAP_CHECK_LAUNCH("imgcap_colsum");
   return 0;
 }

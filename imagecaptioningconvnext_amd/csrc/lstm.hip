@@ -167,18 +167,27 @@ __global__ __launch_bounds__(64 * SW) void gate_cell_fwd_kernel(imgcap_lstm_desc
   const int r0 = blockIdx.y * RG, rows = min(RG, d.B - r0);
   const int c = threadIdx.x & 15;
   const T* brow = (const T*)d.w_ih + (long)((c >> 2) * D + blockIdx.x * 4 + (c & 3)) * (d.M + E) + d.M;
-  skinny_tile<T, RG_MT, SW, DEPTH>((const T*)d.zs + ((long)r0 * Tn + t) * E, (long)Tn * E, rows, brow, true, E,
-                                   part);
-  for (int e = threadIdx.x; e < rows * 4; e += 64 * SW) {
-    const int b = r0 + (e >> 2), jj = e & 3, j = blockIdx.x * 4 + jj;
-    const long bt = (long)b * Tn + t;
+  // the cell's other inputs (x-part + hh-part of the gates, c_{t-1}) are loaded before the GEMM
+  // so their latency overlaps it; thread e < rows*4 owns (row e/4, unit 4*blockIdx.x + e%4)
+  const int e = threadIdx.x;
+  const bool cell_thread = e < rows * 4;
+  const int b = r0 + (cell_thread ? (e >> 2) : 0), jj = e & 3, j = blockIdx.x * 4 + jj;
+  const long bt = (long)b * Tn + t;
+  float pre[4], cp = 0.f;
+  if (cell_thread) {
     const float* xe = d.xe + bt * 4 * D;
     const float* hh = d.g1 + bt * W3 + d.A + E;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pre[q] = xe[q * D + j] + hh[q * D + j];
+    cp = t == 0 ? d.c0[(long)b * D + j] : d.cs[(bt - 1) * D + j];
+  }
+  skinny_tile<T, RG_MT, SW, DEPTH>((const T*)d.zs + ((long)r0 * Tn + t) * E, (long)Tn * E, rows, brow, true, E,
+                                   part);
+  if (cell_thread) {
     float g[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) g[q] = part[0][b - r0][q * 4 + jj] + xe[q * D + j] + hh[q * D + j];
+    for (int q = 0; q < 4; ++q) g[q] = part[0][b - r0][q * 4 + jj] + pre[q];
     const float gi = sigmoidf_(g[0]), gf = sigmoidf_(g[1]), gg = tanhf(g[2]), go = sigmoidf_(g[3]);
-    const float cp = t == 0 ? d.c0[(long)b * D + j] : d.cs[(bt - 1) * D + j];
     const float cn = gf * cp + gi * gg;
     const float h = go * tanhf(cn);
     float* ga = d.gates + bt * 4 * D;
@@ -191,31 +200,50 @@ __global__ __launch_bounds__(64 * SW) void gate_cell_fwd_kernel(imgcap_lstm_desc
 
 // LSTMCell backward of one (row, unit) at step t given dL/dh_t from the later steps (dh_next,
 // without the fc term) and the carried dL/dc_t in d.dc; writes d gates_preact into dcat and
-// the carry dL/dc_{t-1}.  Rows past their decode length contribute nothing.
+// the carry dL/dc_{t-1}.  Rows past their decode length contribute nothing.  The inputs are
+// gathered by cell_bwd_load (so a kernel can issue them early) and consumed by cell_bwd_apply.
+struct CellBwdIn {
+  float dhs, gi, gf, gg, go, c, cp, dc;
+  bool active;
+};
+
 template <typename T>
-DEV void cell_bwd_point(const imgcap_lstm_desc& d, int t, int b, int j, float dh_next, bool has_next) {
+DEV CellBwdIn cell_bwd_load(const imgcap_lstm_desc& d, int t, int b, int j) {
+  const int D = d.D, Tn = d.T;
+  const long bt = (long)b * Tn + t;
+  const long e = (long)b * D + j;
+  CellBwdIn in;
+  in.active = t < d.dl[b];
+  const float* ga = d.gates + bt * 4 * D;
+  in.dhs = to_f(((const T*)d.dhs)[bt * D + j]);
+  in.gi = ga[j]; in.gf = ga[D + j]; in.gg = ga[2 * D + j]; in.go = ga[3 * D + j];
+  in.c = d.cs[bt * D + j];
+  in.cp = t == 0 ? d.c0[e] : d.cs[(bt - 1) * D + j];
+  in.dc = d.dc[e];
+  return in;
+}
+
+template <typename T>
+DEV void cell_bwd_apply(const imgcap_lstm_desc& d, int t, int b, int j, const CellBwdIn& in, float dh_next,
+                        bool has_next) {
   const int D = d.D, Tn = d.T;
   const int W3 = d.A + d.E + 4 * D;
   const long bt = (long)b * Tn + t;
   const long e = (long)b * D + j;
   T* dg = (T*)d.dcat + bt * W3 + d.A + d.E;
-  if (t >= d.dl[b]) {
+  if (!in.active) {
     dg[j] = dg[D + j] = dg[2 * D + j] = dg[3 * D + j] = from_f<T>(0.f);
     d.dc[e] = 0.f;
     return;
   }
-  const float dh = to_f(((const T*)d.dhs)[bt * D + j]) + (has_next ? dh_next : 0.f);
-  const float* ga = d.gates + bt * 4 * D;
-  const float gi = ga[j], gf = ga[D + j], gg = ga[2 * D + j], go = ga[3 * D + j];
-  const float c = d.cs[bt * D + j];
-  const float cp = t == 0 ? d.c0[e] : d.cs[(bt - 1) * D + j];
-  const float tc = tanhf(c);
-  const float dct = (has_next ? d.dc[e] : 0.f) + dh * go * (1.f - tc * tc);
-  dg[j] = from_f<T>(dct * gg * gi * (1.f - gi));
-  dg[D + j] = from_f<T>(dct * cp * gf * (1.f - gf));
-  dg[2 * D + j] = from_f<T>(dct * gi * (1.f - gg * gg));
-  dg[3 * D + j] = from_f<T>(dh * tc * go * (1.f - go));
-  d.dc[e] = dct * gf;
+  const float dh = in.dhs + (has_next ? dh_next : 0.f);
+  const float tc = tanhf(in.c);
+  const float dct = (has_next ? in.dc : 0.f) + dh * in.go * (1.f - tc * tc);
+  dg[j] = from_f<T>(dct * in.gg * in.gi * (1.f - in.gi));
+  dg[D + j] = from_f<T>(dct * in.cp * in.gf * (1.f - in.gf));
+  dg[2 * D + j] = from_f<T>(dct * in.gi * (1.f - in.gg * in.gg));
+  dg[3 * D + j] = from_f<T>(dh * tc * in.go * (1.f - in.go));
+  d.dc[e] = dct * in.gf;
 }
 
 // ---- backward: LSTMCell of the last step (no carry from later steps) ------------------
@@ -223,7 +251,10 @@ template <typename T>
 __global__ __launch_bounds__(256) void cell_bwd_last_kernel(imgcap_lstm_desc d) {
   const long n = (long)d.B * d.D;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256)
-    cell_bwd_point<T>(d, d.T - 1, (int)(e / d.D), (int)(e % d.D), 0.f, false);
+  {
+    const int b = (int)(e / d.D), j = (int)(e % d.D);
+    cell_bwd_apply<T>(d, d.T - 1, b, j, cell_bwd_load<T>(d, d.T - 1, b, j), 0.f, false);
+  }
 }
 
 // ---- backward: dgates_t . [W_ih[:, M:] | W_hh]  -> K-slice partial slabs ----------------
@@ -266,6 +297,21 @@ __global__ __launch_bounds__(64 * SW) void dh_cell_kernel(imgcap_lstm_desc d, in
   const int n0 = blockIdx.x * 16, n = n0 + (threadIdx.x & 15);
   const T* A = (const T*)d.dcat + ((long)r0 * d.T + t) * W3 + k0;
   const T* brow = (const T*)d.w_att_t + (long)n * KY + k0;
+  // epilogue inputs requested before the GEMM (only the last-arriving block uses them, but the
+  // critical path is then the slab hand-off alone): W_hh part of dh from the x slabs and the
+  // cell-backward operands of step t-1, for this thread's (row, unit) items
+  constexpr int PER = RG * 16 / (64 * SW);
+  float xh[PER];
+  CellBwdIn cin[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + i * 64 * SW;
+    const int b = r0 + min(e >> 4, rows - 1), j = n0 + (e & 15);
+    float s = 0.f;
+    for (int z = 0; z < d.x_slices; ++z) s += d.dz[((long)z * d.B + b) * NX + E + j];
+    xh[i] = s;
+    if (t > 0) cin[i] = cell_bwd_load<T>(d, t - 1, b, j);
+  }
   skinny_tile<T, RG_MT, SW, DEPTH>(A, (long)d.T * W3, rows, brow, true, klen, part);
   constexpr int TILE = RG * 16;
   const long ntiles = (long)ntile * gridDim.z;
@@ -287,13 +333,16 @@ __global__ __launch_bounds__(64 * SW) void dh_cell_kernel(imgcap_lstm_desc d, in
   }
   __syncthreads();
   if (!is_last) return;
-  for (int e = threadIdx.x; e < rows * 16; e += 64 * SW) {
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + i * 64 * SW;
+    if (e >= rows * 16) continue;
     const int b = r0 + (e >> 4), j = n0 + (e & 15);
     float dh = 0.f;
     for (int z = 0; z < S; ++z) dh += d.ws_y[((long)z * ntiles + tile) * TILE + e];
-    for (int z = 0; z < d.x_slices; ++z) dh += d.dz[((long)z * d.B + b) * NX + E + j];
+    dh += xh[i];
     if (t == 0) d.dh[(long)b * D + j] = dh;
-    else cell_bwd_point<T>(d, t - 1, b, j, dh, true);
+    else cell_bwd_apply<T>(d, t - 1, b, j, cin[i], dh, true);
   }
 }
 

@@ -12,14 +12,14 @@ namespace imgcap {
 
 constexpr int LN_MAXC = 2048;
 
-template <typename T, int G>
+template <typename T, int G, int MAXC>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(int rows, int cols, const T* __restrict__ x,
                                                          const T* __restrict__ r, float p, uint64_t seed0,
                                                          const uint64_t* seed_ctr, uint32_t stream_id,
                                                          const float* __restrict__ g, const float* __restrict__ b,
                                                          float eps, T* __restrict__ s_out, T* __restrict__ y,
                                                          float* __restrict__ mean_o, float* __restrict__ rstd_o) {
-  constexpr int MAXJ = LN_MAXC / (64 * G);
+  constexpr int MAXJ = MAXC / (64 * G);
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(int rows, int cols, con
 // dS = LN backward of dy; dx = dS; dr = dS * dropmask.  Each wave walks rows_per_wave rows;
 // dgamma/dbeta partials are summed over the block's waves in LDS in a fixed order and added
 // to the output with one atomic per column per block (grid sized to ~2 blocks per CU).
-template <typename T, int G>
+template <typename T, int G, int MAXC>
 __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                          const T* __restrict__ s, const float* __restrict__ mean_i,
                                                          const float* __restrict__ rstd_i, const float* __restrict__ g,
@@ -81,8 +81,8 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, con
                                                          uint32_t stream_id, T* __restrict__ dx, T* __restrict__ dr,
                                                          float* __restrict__ dg, float* __restrict__ db,
                                                          int rows_per_wave) {
-  constexpr int MAXJ = LN_MAXC / (64 * G);
-  __shared__ float part[2][4][LN_MAXC];
+  constexpr int MAXJ = MAXC / (64 * G);
+  __shared__ float part[2][4][MAXC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t seed = (dr && p > 0.f) ? eff_seed(seed0, seed_ctr) : seed0;
   float lg[MAXJ][G], lb[MAXJ][G];
@@ -174,7 +174,11 @@ extern "C" int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const voi
   dim3 grid((rows + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
 #define LNF_(T, G)                                                                                              \
-  hipLaunchKernelGGL((add_ln_fwd_kernel<T, G>), grid, dim3(256), 0, st, rows, cols, (const T*)x, (const T*)r,    \
+  do {                                                                                                          \
+    if (cols <= 512) { LNF2_(T, G, 512); } else if (cols <= 1024) { LNF2_(T, G, 1024); } else { LNF2_(T, G, 2048); } \
+  } while (0)
+#define LNF2_(T, G, MC)                                                                                         \
+  hipLaunchKernelGGL((add_ln_fwd_kernel<T, G, MC>), grid, dim3(256), 0, st, rows, cols, (const T*)x, (const T*)r,    \
                      drop_p, seed, g_seed_ctr, drop_stream, gamma, beta, eps, (T*)s_out, (T*)y, mean, rstd)
   if (dtype == IMGCAP_BF16) {
     if (vec_rows<bf16>(cols, {x, r, s_out, y})) LNF_(bf16, 8); else LNF_(bf16, 1);
@@ -182,6 +186,7 @@ extern "C" int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const voi
     if (vec_rows<float>(cols, {x, r, s_out, y})) LNF_(float, 4); else LNF_(float, 1);
   }
 #undef LNF_
+#undef LNF2_
   IMGCAP_CHECK_LAUNCH("imgcap_add_layernorm_fwd");
   return 0;
 }
@@ -196,7 +201,11 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
   dim3 grid((rows + 4 * rpw - 1) / (4 * rpw));
   hipStream_t st = (hipStream_t)stream;
 #define LNB_(T, G)                                                                                              \
-  hipLaunchKernelGGL((add_ln_bwd_kernel<T, G>), grid, dim3(256), 0, st, rows, cols, (const T*)dy, (const T*)s,   \
+  do {                                                                                                          \
+    if (cols <= 512) { LNB2_(T, G, 512); } else if (cols <= 1024) { LNB2_(T, G, 1024); } else { LNB2_(T, G, 2048); } \
+  } while (0)
+#define LNB2_(T, G, MC)                                                                                         \
+  hipLaunchKernelGGL((add_ln_bwd_kernel<T, G, MC>), grid, dim3(256), 0, st, rows, cols, (const T*)dy, (const T*)s,   \
                      mean, rstd, gamma, drop_p, seed, g_seed_ctr, drop_stream, (T*)dx, (T*)dr, dgamma, dbeta, rpw)
   if (dtype == IMGCAP_BF16) {
     if (vec_rows<bf16>(cols, {dy, s, dx, dr})) LNB_(bf16, 8); else LNB_(bf16, 1);
@@ -204,6 +213,7 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
     if (vec_rows<float>(cols, {dy, s, dx, dr})) LNB_(float, 4); else LNB_(float, 1);
   }
 #undef LNB_
+#undef LNB2_
   IMGCAP_CHECK_LAUNCH("imgcap_add_layernorm_bwd");
   return 0;
 }

@@ -1,0 +1,140 @@
+"""Single-GPU teacher-forced training entry point with the reference's CLI (train.py:59-65).
+
+    python train.py --teacherForcing [--lstmDecoder] [--startingLayer 5] [--encoderLr 1e-4]
+                    [--encoder base|tiny|large] [--steps N] [--batchSize 32]
+
+Mirrors ``train.py``'s model construction (:37-57, :95-115) and ``trainWithTeacherForcing``
+(:240-302) on the MI355X path.  The COCO HDF5 pipeline (``CaptionDataset``) is outside this
+build's scope and its inputs are absent here, so batches are synthetic COCO-shaped tensors
+(224x224 images, length-52 captions, V = 9490) unless a loader is passed in.
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+# model / training parameters of the reference (train.py:37-57)
+embDim = 512
+attentionDim = 512
+decoderDim = 512
+dropout = 0.5
+maxLen = 52
+batchSize = 32
+decoderLr = 1e-4
+gradClip = 5.
+alphaC = 1.
+VOCAB = 9490  # len(wordMap) of the Karpathy COCO split, min_word_freq 5
+
+
+class AverageMeter:
+    """utils.py AverageMeter: running average of a metric."""
+
+    def __init__(self):
+        self.val = self.avg = self.sum = 0.0
+        self.count = 0
+
+    def update(self, val, n=1):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument('--checkpoint', type=str, default=None, help='Path to checkpoint file')
+    p.add_argument('--lstmDecoder', action='store_true', help='Use LSTM decoder instead of Transformer')
+    p.add_argument('--teacherForcing', action='store_true', help='Use teacher forcing training strategy')
+    p.add_argument('--startingLayer', type=int, default=5, help='Starting layer index for encoder fine-tuning')
+    p.add_argument('--encoderLr', type=float, default=1e-4, help='Learning rate for encoder if fine-tuning')
+    p.add_argument('--embeddingName', type=str, default=None, help='Pretrained embedding name from gensim')
+    # additions of this build
+    p.add_argument('--encoder', default='base', choices=['tiny', 'small', 'base', 'large'])
+    p.add_argument('--batchSize', type=int, default=batchSize)
+    p.add_argument('--steps', type=int, default=20, help='synthetic iterations per epoch')
+    p.add_argument('--epochs', type=int, default=1)
+    return p.parse_args(argv)
+
+
+def synthetic_loader(steps, B, device, rank=0, V=VOCAB, L=maxLen):
+    """COCO-shaped synthetic batches: normalised U[0,1) images, <start> w.. <end>."""
+    mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    for i in range(steps):
+        g = torch.Generator().manual_seed(1234 + 7919 * rank + i)
+        img = (torch.rand(B, 3, 224, 224, generator=g) - mean) / std
+        caps = torch.randint(1, V - 3, (B, L), generator=g)
+        caps[:, 0], caps[:, L - 1] = V - 2, V - 1
+        yield img.to(device), caps.to(device), torch.full((B, 1), L, dtype=torch.long, device=device)
+
+
+def build_models(args, device):
+    """train.py:100-115: decoder + Adam lr, frozen encoder (fine_tune(False))."""
+    from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
+    if args.embeddingName:
+        raise NotImplementedError("gensim pre-trained embeddings are outside the accelerated path")
+    encoder = Encoder(variant=args.encoder).to(device)
+    encoder.fine_tune(fine_tune=False)
+    E = encoder.encoder_dim
+    if args.lstmDecoder:
+        decoder = DecoderWithAttention(attention_dim=attentionDim, embed_dim=embDim, decoder_dim=decoderDim,
+                                       vocab_size=VOCAB, dropout=dropout, device=device, encoder_dim=E)
+    else:
+        decoder = TransformerDecoder(embed_dim=embDim, decoder_dim=decoderDim, vocab_size=VOCAB, maxLen=maxLen,
+                                     dropout=dropout, device=device, wordMap=None, pretrained_embeddings_path=None,
+                                     fine_tune_embeddings=True, encoder_dim=E)
+    if args.checkpoint:
+        ck = torch.load(args.checkpoint, map_location=device, weights_only=True)
+        encoder.load_state_dict(ck['encoder'])
+        decoder.load_state_dict(ck['decoder'])
+    return encoder, decoder.to(device)
+
+
+def trainWithTeacherForcing(trainDataLoader, encoder, decoder, trainer, epoch, lstm, log=print):
+    """train.py:240-302 on the fused MI355X step: returns (loss avg, top-5 avg, batch time avg,
+    data time avg) like the reference.  Metrics are read back once per epoch (no per-step sync)."""
+    encoder.train()
+    decoder.train()
+    batchTime, dataTime, losses, top5accs = AverageMeter(), AverageMeter(), AverageMeter(), AverageMeter()
+    start = time.time()
+    n = 0
+    for i, (imgs, caps, caplens) in enumerate(trainDataLoader):
+        dataTime.update(time.time() - start)
+        if i % 100 == 0:
+            log(f"TF, Epoch {epoch}, Batch {i + 1}", flush=True)
+        trainer.step(imgs, caps, caplens)
+        n += 1
+        batchTime.update(time.time() - start)
+        start = time.time()
+    torch.cuda.synchronize()
+    for loss, tokens, top5 in trainer.drain_metrics():
+        losses.update(loss, tokens)
+        top5accs.update(top5, tokens)
+    log(f"TF, Epoch {epoch}: Training Loss = {losses.avg:.4f}, Top-5 Accuracy = {top5accs.avg:.4f}", flush=True)
+    return losses.avg, top5accs.avg, batchTime.avg, dataTime.avg
+
+
+def main(argv=None):
+    args = parse(argv)
+    if not args.teacherForcing:
+        raise NotImplementedError("non-teacher-forced training is outside the accelerated path (SURVEY.md §8f)")
+    torch.manual_seed(42)
+    device = torch.device("cuda")
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    encoder, decoder = build_models(args, device)
+    trainer = TeacherForcedTrainer(encoder, decoder, lstm=args.lstmDecoder, decoder_lr=decoderLr, grad_clip=gradClip,
+                                   alphaC=alphaC, graph=True)
+    for epoch in range(args.epochs):
+        loader = synthetic_loader(args.steps, args.batchSize, device)
+        out = trainWithTeacherForcing(loader, encoder, decoder, trainer, epoch, args.lstmDecoder)
+        print(f"epoch {epoch}: loss {out[0]:.4f} top5 {out[1]:.2f} batch {out[2] * 1e3:.2f} ms", flush=True)
+
+
+if __name__ == '__main__':
+    main()
