@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libimgcap_hip.so")
 
 F32, BF16 = 0, 1
-ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU = 0, 1, 2, 3
 
 c_void_p, c_int, c_int64, c_float, c_uint64, c_uint32 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
                                                          ctypes.c_float, ctypes.c_uint64, ctypes.c_uint32)
@@ -33,7 +33,7 @@ class LstmDesc(ctypes.Structure):
         (n, c_void_p) for n in ("w_hcat", "b_hcat", "w_ih", "w_f", "enc", "att1", "xe", "c0", "dl", "g1", "alphas",
                                 "awe", "zs", "gates", "cs", "hs", "hprev", "w_zh_t", "w_att_t", "dhs", "dalpha",
                                 "dcat", "dz", "ws_y", "y_cnt", "dh", "dc", "de", "datt1", "dwf", "dbea")] + [
-        ("x_slices", ctypes.c_int32), ("y_slices", ctypes.c_int32)]
+        ("x_slices", ctypes.c_int32), ("y_slices", ctypes.c_int32), ("dawe", c_void_p)]
 
 
 class MhaDesc(ctypes.Structure):
@@ -65,7 +65,8 @@ _SIGS = {
                              c_void_p, c_void_p],
     "imgcap_dwconv7_ln": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p],
-    "imgcap_ln_patchify2": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_ln_patchify2": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                            c_void_p],
     "imgcap_adaptive_pool_nhwc": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "imgcap_embedding_fwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_float, c_uint64, c_uint32,
                              c_void_p, c_void_p],
@@ -86,6 +87,14 @@ _SIGS = {
     "imgcap_mean_mid": [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "imgcap_cast": [c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p],
     "imgcap_fill": [c_int, c_int64, c_float, c_void_p, c_void_p],
+    "imgcap_dwconv7_bwd_data": [c_int] * 5 + [c_void_p] * 5,
+    "imgcap_dwconv7_wgrad": [c_int] * 5 + [c_void_p] * 5,
+    "imgcap_layer_scale_grad": [c_int, c_int, c_int] + [c_void_p] * 10,
+    "imgcap_rowscale": [c_int, c_int64, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "imgcap_ln_patchify2_bwd": [c_int] * 5 + [c_void_p] * 3 + [c_int] + [c_void_p] * 4,
+    "imgcap_adaptive_pool_bwd_nhwc": [c_int] * 7 + [c_void_p] * 3,
+    "imgcap_lstm_denc": [c_int] * 4 + [c_void_p] * 6,
+    "imgcap_slice_reduce": [c_int64, c_int, c_void_p, c_int64, c_float, c_int64, c_void_p, c_void_p, c_void_p],
 }
 
 _lib = None

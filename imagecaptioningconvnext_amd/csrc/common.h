@@ -129,6 +129,10 @@ DEV float dropout_scale(uint64_t seed, uint32_t stream, uint64_t idx, float p) {
 }
 
 DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// d/dx of the erf-form GELU: Phi(x) + x phi(x)
+DEV float gelu_grad(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
 // erf-form GELU on two values at once, erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7,
 // far below the bf16 rounding of the result): packed-math polynomial (v_pk_fma_f32), native
 // v_rcp_f32 / v_exp_f32 -- roughly a third of the instructions of two library erff calls

@@ -253,7 +253,8 @@ constexpr int DW_CT = 32;  // channels per block
 template <typename T, int PW>
 __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C, const T* __restrict__ x,
                                                       const float* __restrict__ w, const float* __restrict__ bias,
-                                                      T* __restrict__ y, int TR, int RS) {
+                                                      T* __restrict__ y, int TR, int RS,
+                                                      const T* res, int flip) {
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   constexpr int VE = 16 / sizeof(T);   // elements per 16-byte vector
   constexpr int NV = DW_CT / VE;       // 16-byte vectors per pixel in the tile (4 bf16, 8 f32)
@@ -306,7 +307,8 @@ __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C
   const int w0 = g * PW;
   f32x2 acc[PW][4];
   {
-    const f32x4 b0 = *(const f32x4*)(bias + c0), b1 = *(const f32x4*)(bias + c0 + 4);
+    f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+    if (bias) { b0 = *(const f32x4*)(bias + c0); b1 = *(const f32x4*)(bias + c0 + 4); }
 #pragma unroll
     for (int p = 0; p < PW; ++p) {
       acc[p][0] = f32x2{b0[0], b0[1]}; acc[p][1] = f32x2{b0[2], b0[3]};
@@ -320,7 +322,8 @@ __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C
     f32x2 wt[7][4];
 #pragma unroll
     for (int kw = 0; kw < 7; ++kw) {
-      const float* wp = w + (kh * 7 + kw) * C + c0;
+      // flip: the transposed convolution of the backward pass (tap (kh,kw) -> (6-kh,6-kw))
+      const float* wp = w + (flip ? 48 - (kh * 7 + kw) : kh * 7 + kw) * C + c0;
       const f32x4 wa = *(const f32x4*)wp, wb = *(const f32x4*)(wp + 4);
       wt[kw][0] = f32x2{wa[0], wa[1]}; wt[kw][1] = f32x2{wa[2], wa[3]};
       wt[kw][2] = f32x2{wb[0], wb[1]}; wt[kw][3] = f32x2{wb[2], wb[3]};
@@ -356,6 +359,12 @@ __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C
     float o[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) { o[2 * j] = acc[p][j][0]; o[2 * j + 1] = acc[p][j][1]; }
+    if (res) {
+      float r[8];
+      V8<T>::load(res + (orow * W + w0 + p) * C + c0, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += r[j];
+    }
     V8<T>::store(out + (long)p * C, o);
   }
 }
@@ -365,7 +374,7 @@ __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C
 template <typename T>
 __global__ __launch_bounds__(256) void ln_patchify2_kernel(int B, int H, int W, int C, const T* __restrict__ x,
                                                            const float* __restrict__ lw, const float* __restrict__ lb,
-                                                           T* __restrict__ out) {
+                                                           T* __restrict__ out, int cmajor) {
   const long px = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (px >= (long)B * H * W) return;
@@ -390,11 +399,14 @@ __global__ __launch_bounds__(256) void ln_patchify2_kernel(int B, int H, int W, 
   const float rstd = rsqrtf(wave_sum(sq) / C + 1e-6f);
   const int HO = H / 2, WO = W / 2;
   const int oh = ih / 2, ow = iw / 2, kh = ih & 1, kw = iw & 1;
-  T* op = out + (((long)b * HO + oh) * WO + ow) * (4L * C) + (kh * 2 + kw) * C;
+  // patch row layout: (kh, kw, c) for the repacked frozen weights, or (c, kh, kw) = the torch
+  // Conv2d weight layout [2C][C][2][2] used directly when the downsample is trainable
+  T* op = out + (((long)b * HO + oh) * WO + ow) * (4L * C) + (cmajor ? kh * 2 + kw : (kh * 2 + kw) * C);
+  const int cs = cmajor ? 4 : 1;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int c = lane + 64 * i;
-    if (c < C) op[c] = from_f<T>((v[i] - mean) * rstd * lw[c] + lb[c]);
+    if (c < C) op[c * cs] = from_f<T>((v[i] - mean) * rstd * lw[c] + lb[c]);
   }
 }
 
@@ -448,7 +460,7 @@ using namespace imgcap;
 namespace {
 template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
-                   hipStream_t st) {
+                   hipStream_t st, const void* res = nullptr, int flip = 0) {
   // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups
   const int PW = W % 7 == 0 ? 7 : W % 8 == 0 ? 8 : W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 1;
   const int GW = W / PW, TR = 64 / GW;
@@ -463,7 +475,7 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
   dim3 grid((unsigned)((R + TR - 1) / TR), C / DW_CT);
 #define DW_(P)                                                                                                  \
   hipLaunchKernelGGL((dwconv7_kernel<T, P>), grid, dim3(256), shm, st, B, H, W, C, (const T*)x, w, bias, (T*)y, TR, \
-                     RS)
+                     RS, (const T*)res, flip)
   switch (PW) {
     case 8: DW_(8); break;
     case 7: DW_(7); break;
@@ -485,6 +497,20 @@ extern "C" int imgcap_dwconv7(int dtype, int B, int H, int W, int C, const void*
   if ((long)B * H == 0) return 0;
   if (dtype == IMGCAP_BF16) return dwconv7_launch<bf16>(B, H, W, C, x, w, bias, y, (hipStream_t)stream);
   return dwconv7_launch<float>(B, H, W, C, x, w, bias, y, (hipStream_t)stream);
+}
+
+extern "C" int imgcap_dwconv7_bwd_data(int dtype, int B, int H, int W, int C, const void* dz, const float* w,
+                                       const void* res, void* dx, void* stream) {
+  IMGCAP_REQUIRE(C % DW_CT == 0, "imgcap_dwconv7_bwd_data: C must be a multiple of 32");
+  IMGCAP_REQUIRE(W >= 1 && W <= 64, "imgcap_dwconv7_bwd_data: W must be in [1, 64]");
+  IMGCAP_REQUIRE(aligned16(dz) && aligned16(dx) && aligned16(w) && (!res || aligned16(res)),
+                 "imgcap_dwconv7_bwd_data: alignment");
+  // res may alias dx (each output element reads its own residual first); dz may not (neighbours)
+  IMGCAP_REQUIRE(dz != dx, "imgcap_dwconv7_bwd_data: dz and dx must differ");
+  if ((long)B * H == 0) return 0;
+  if (dtype == IMGCAP_BF16)
+    return dwconv7_launch<bf16>(B, H, W, C, dz, w, nullptr, dx, (hipStream_t)stream, res, 1);
+  return dwconv7_launch<float>(B, H, W, C, dz, w, nullptr, dx, (hipStream_t)stream, res, 1);
 }
 
 extern "C" int imgcap_stochastic_depth_scales(int nblocks, int B, const float* probs, uint64_t seed,
@@ -540,17 +566,17 @@ extern "C" int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const vo
 }
 
 extern "C" int imgcap_ln_patchify2(int dtype, int B, int H, int W, int C, const void* x, const float* ln_w,
-                                   const float* ln_b, void* out, void* stream) {
+                                   const float* ln_b, int cmajor, void* out, void* stream) {
   IMGCAP_REQUIRE(H % 2 == 0 && W % 2 == 0 && C <= 1536, "imgcap_ln_patchify2: bad shape");
   const long npx = (long)B * H * W;
   if (npx == 0) return 0;
   dim3 grid((unsigned)((npx + 3) / 4));
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(ln_patchify2_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, B, H, W, C,
-                       (const bf16*)x, ln_w, ln_b, (bf16*)out);
+                       (const bf16*)x, ln_w, ln_b, (bf16*)out, cmajor);
   else
     hipLaunchKernelGGL(ln_patchify2_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, B, H, W, C,
-                       (const float*)x, ln_w, ln_b, (float*)out);
+                       (const float*)x, ln_w, ln_b, (float*)out, cmajor);
   IMGCAP_CHECK_LAUNCH("imgcap_ln_patchify2");
   return 0;
 }

@@ -31,6 +31,31 @@ struct EpiFlags {
   bool bias, colscale, rowscale, res, aux, beta, drop;
 };
 
+DEV void load8_as_f(const void* p, long i, int dtype, float (&v)[8]) {
+  if (dtype == IMGCAP_BF16) {
+    const bf16x8 x = *(const bf16x8*)((const bf16*)p + i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+  } else {
+    const f32x4 a = *(const f32x4*)((const float*)p + i), b = *(const f32x4*)((const float*)p + i + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
+  }
+}
+// ACT_GELU with an aux operand: aux[m, n] = the pre-activation (c_dtype), written through
+DEV void store_pre8(const imgcap_epilogue& ep, int m, int n0, const float (&v)[8]) {
+  const long i = (long)m * ep.ldaux + n0;
+  if (ep.c_dtype == IMGCAP_BF16) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+    *(bf16x8*)((bf16*)ep.aux + i) = o;
+  } else {
+    *(f32x4*)((float*)ep.aux + i) = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)((float*)ep.aux + i + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+
 DEV void epi_vec8(const imgcap_epilogue& ep, const EpiFlags& f, void* C, long cidx, int m, int n0, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] *= ep.alpha;
@@ -40,6 +65,7 @@ DEV void epi_vec8(const imgcap_epilogue& ep, const EpiFlags& f, void* C, long ci
     for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[j + 4] += b1[j]; }
   }
   if (ep.act == IMGCAP_ACT_GELU) {
+    if (f.aux) store_pre8(ep, m, n0, v);  // pre-activation kept for the backward pass
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
   } else if (ep.act == IMGCAP_ACT_RELU) {
@@ -50,7 +76,12 @@ DEV void epi_vec8(const imgcap_epilogue& ep, const EpiFlags& f, void* C, long ci
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] *= dropout_scale(ep.seed, ep.drop_stream, (uint64_t)m * ep.drop_ld + n0 + j, ep.drop_p);
   }
-  if (f.aux) {
+  if (f.aux && ep.act == IMGCAP_ACT_DGELU) {
+    float hv[8];
+    load8_as_f(ep.aux, (long)m * ep.ldaux + n0, ep.c_dtype, hv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(hv[j]);
+  } else if (f.aux && ep.act != IMGCAP_ACT_GELU) {
     const long ai = (long)m * ep.ldaux + n0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = load_as_f(ep.aux, ai + j, ep.c_dtype) > 0.f ? v[j] * ep.aux_scale : 0.f;
@@ -103,10 +134,16 @@ DEV void epi_vec8(const imgcap_epilogue& ep, const EpiFlags& f, void* C, long ci
 DEV void epi_scalar(const imgcap_epilogue& ep, void* C, long cidx, int m, int n, float v) {
   v *= ep.alpha;
   if (ep.bias) v += ep.bias[n];
-  if (ep.act == IMGCAP_ACT_GELU) v = gelu_erf(v);
-  else if (ep.act == IMGCAP_ACT_RELU) v = fmaxf(v, 0.f);
+  if (ep.act == IMGCAP_ACT_GELU) {
+    if (ep.aux) store_from_f((void*)ep.aux, (long)m * ep.ldaux + n, ep.c_dtype, v);
+    v = gelu_erf(v);
+  } else if (ep.act == IMGCAP_ACT_RELU) {
+    v = fmaxf(v, 0.f);
+  }
   if (ep.drop_p > 0.f) v *= dropout_scale(ep.seed, ep.drop_stream, (uint64_t)m * ep.drop_ld + n, ep.drop_p);
-  if (ep.aux) v = load_as_f(ep.aux, (long)m * ep.ldaux + n, ep.c_dtype) > 0.f ? v * ep.aux_scale : 0.f;
+  if (ep.aux && ep.act == IMGCAP_ACT_DGELU) v *= gelu_grad(load_as_f(ep.aux, (long)m * ep.ldaux + n, ep.c_dtype));
+  else if (ep.aux && ep.act != IMGCAP_ACT_GELU)
+    v = load_as_f(ep.aux, (long)m * ep.ldaux + n, ep.c_dtype) > 0.f ? v * ep.aux_scale : 0.f;
   if (ep.colscale) v *= ep.colscale[n];
   if (ep.rowscale) v *= ep.rowscale[m / ep.rows_per_scale];
   if (ep.res) v += load_as_f(ep.res, (long)m * ep.ldr + n, ep.c_dtype);
@@ -433,7 +470,7 @@ extern "C" int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, 
   IMGCAP_REQUIRE(b_kmajor ? ldb >= K : ldb >= N, "imgcap_gemm: ldb too small");
   const bool vec_ok = aligned16(C) && ldc % 8 == 0 && strideC % 8 == 0 &&
                       (epi->res == nullptr || (aligned16(epi->res) && epi->ldr % 8 == 0)) &&
-                      (epi->aux == nullptr || epi->ldaux % 8 == 0);
+                      (epi->aux == nullptr || (aligned16(epi->aux) && epi->ldaux % 8 == 0));
   int split = 1;
   if (epi->split_k != 0 && epi->split_k != 1) {
     IMGCAP_REQUIRE(epi->c_dtype == IMGCAP_F32 && batch == 1 && !epi->bias && !epi->colscale && !epi->rowscale &&

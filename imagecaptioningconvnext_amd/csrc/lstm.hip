@@ -358,9 +358,12 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
   const int W3 = A + E + 4 * d.D;
   const long bt = (long)b * Tn + t;
   T* dcat = (T*)d.dcat + bt * W3;
+  float* dawe_o = d.dawe ? d.dawe + ((long)b * (Tn + 1) + t) * E : nullptr;
   if (t >= d.dl[b]) {
     for (int i = threadIdx.x; i < A + E; i += ATT_THREADS) dcat[i] = from_f<T>(0.f);
     if (threadIdx.x < P) d.de[bt * P + threadIdx.x] = 0.f;
+    if (dawe_o)
+      for (int i = threadIdx.x; i < E; i += ATT_THREADS) dawe_o[i] = 0.f;
     return;
   }
   const int NVE = E / 8, G = ATT_THREADS / NVE;
@@ -401,13 +404,16 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
   // ---- d awe = dz * sigmoid(gate), d gate_pre = dz * awe * s (1 - s) ----
   if (pg == 0) {
     float dg[8];
+    float da[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float s = sigmoidf_(gate[j]);
-      dawe[v * 8 + j] = dz[j] * s;
+      da[j] = dz[j] * s;
+      dawe[v * 8 + j] = da[j];
       dg[j] = dz[j] * awe[j] * s * (1.f - s);
     }
     st_g<T, 8>(dcat + A + v * 8, dg);
+    if (dawe_o) st_g<float, 8>(dawe_o + v * 8, da);
   }
   if (tid < P) al[tid] = alpha_in;
   __syncthreads();
@@ -527,6 +533,42 @@ __global__ __launch_bounds__(512) void attn_param_grad_kernel(imgcap_lstm_desc d
     d.dwf[((long)b * nc + c) * A + a] = swf;
     d.dbea[((long)b * nc + c) * A + a] = sb;
   }
+}
+
+// ---- gradient w.r.t. the encoder output (encoder fine-tuning) ----------------------------
+//   denc[sort_ind[b], p, e] = base[b, p, e] + sum_{t<T} alpha[b,t,p] dawe[b,t,e] + dawe[b,T,e] / P
+// base = datt1 . W_ea (the attention-projection path, one GEMM), dawe rows t < T = d context
+// per step (attn_bwd_kernel), row T = dL/d mean(enc) (init_h / init_c path).  Block = (batch
+// row, 256 channels); alpha[b] staged in LDS; each thread keeps its channel's P sums in
+// registers while t sweeps.
+constexpr int DENC_P = 64;
+__global__ __launch_bounds__(256) void lstm_denc_kernel(int T, int P, int E, const float* __restrict__ alphas,
+                                                        const float* __restrict__ dawe, const float* __restrict__ base,
+                                                        const int64_t* __restrict__ sort_ind,
+                                                        float* __restrict__ denc) {
+  extern __shared__ float al[];  // [T][P]
+  const int b = blockIdx.y;
+  for (int i = threadIdx.x; i < T * P; i += 256) al[i] = alphas[(long)b * T * P + i];
+  __syncthreads();
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= E) return;
+  float acc[DENC_P];
+  const float* dw = dawe + (long)b * (T + 1) * E + e;
+  const float m = dw[(long)T * E] / (float)P;
+#pragma unroll
+  for (int p = 0; p < DENC_P; ++p) acc[p] = m;
+  for (int t = 0; t < T; ++t) {
+    const float g = dw[(long)t * E];
+#pragma unroll
+    for (int p = 0; p < DENC_P; ++p)
+      if (p < P) acc[p] += al[t * P + p] * g;
+  }
+  const long ob = sort_ind ? sort_ind[b] : b;
+  const float* bs = base + (long)b * P * E + e;
+  float* o = denc + ob * P * E + e;
+#pragma unroll
+  for (int p = 0; p < DENC_P; ++p)
+    if (p < P) o[(long)p * E] = acc[p] + (base ? bs[(long)p * E] : 0.f);
 }
 
 // ---- doubly stochastic attention regularisation (train.py:269) --------------------------
@@ -694,5 +736,18 @@ extern "C" int imgcap_attn_reg(int B, int T, int P, const float* alphas, const i
   hipLaunchKernelGGL(attn_reg_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, T, P, alphas, dl, alphaC, dalpha,
                      reg_out);
   IMGCAP_CHECK_LAUNCH("imgcap_attn_reg");
+  return 0;
+}
+
+extern "C" int imgcap_lstm_denc(int B, int T, int P, int E, const float* alphas, const float* dawe, const float* base,
+                                const int64_t* sort_ind, float* denc, void* stream) {
+  IMGCAP_REQUIRE(P <= DENC_P, "imgcap_lstm_denc: P must be <= 64");
+  IMGCAP_REQUIRE(denc != base, "imgcap_lstm_denc: denc must not alias base (rows are permuted)");
+  if (B == 0 || E == 0) return 0;
+  const size_t shm = (size_t)T * P * sizeof(float);
+  IMGCAP_REQUIRE(shm <= 64 * 1024, "imgcap_lstm_denc: T*P too large");
+  hipLaunchKernelGGL(lstm_denc_kernel, dim3((E + 255) / 256, B), dim3(256), shm, (hipStream_t)stream, T, P, E, alphas,
+                     dawe, base, sort_ind, denc);
+  IMGCAP_CHECK_LAUNCH("imgcap_lstm_denc");
   return 0;
 }

@@ -71,16 +71,16 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(int rows, int cols, con
 }
 
 // dS = LN backward of dy; dx = dS; dr = dS * dropmask.  Each wave walks rows_per_wave rows;
-// dgamma/dbeta partials are summed over the block's waves in LDS in a fixed order and added
-// to the output with one atomic per column per block (grid sized to ~2 blocks per CU).
+// dgamma/dbeta partials are summed over the block's waves in LDS in a fixed order and written
+// as the block's slice row ws[block][2][cols]; imgcap_slice_reduce adds the slices in order
+// (deterministic; no same-address atomics, which serialised ~500 blocks per column before).
 template <typename T, int G, int MAXC>
 __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, const T* __restrict__ dy,
                                                          const T* __restrict__ s, const float* __restrict__ mean_i,
                                                          const float* __restrict__ rstd_i, const float* __restrict__ g,
                                                          float p, uint64_t seed0, const uint64_t* seed_ctr,
                                                          uint32_t stream_id, T* __restrict__ dx, T* __restrict__ dr,
-                                                         float* __restrict__ dg, float* __restrict__ db,
-                                                         int rows_per_wave) {
+                                                         float* __restrict__ ws, int rows_per_wave) {
   constexpr int MAXJ = MAXC / (64 * G);
   __shared__ float part[2][4][MAXC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, con
       }
     }
   }
-  if (!dg && !db) return;
+  if (!ws) return;
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) {
     const int c0 = G * (lane + 64 * j);
@@ -145,9 +145,10 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, con
       for (int e = 0; e < G; ++e) { part[0][w][c0 + e] = lg[j][e]; part[1][w][c0 + e] = lb[j][e]; }
   }
   __syncthreads();
+  float* out = ws + (long)blockIdx.x * 2 * cols;
   for (int c = threadIdx.x; c < cols; c += 256) {
-    if (dg) atomicAdd(&dg[c], ((part[0][0][c] + part[0][1][c]) + part[0][2][c]) + part[0][3][c]);
-    if (db) atomicAdd(&db[c], ((part[1][0][c] + part[1][1][c]) + part[1][2][c]) + part[1][3][c]);
+    out[c] = ((part[0][0][c] + part[0][1][c]) + part[0][2][c]) + part[0][3][c];
+    out[cols + c] = ((part[1][0][c] + part[1][1][c]) + part[1][2][c]) + part[1][3][c];
   }
 }
 
@@ -198,15 +199,21 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
   IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_bwd: cols must be in (0, 2048]");
   if (rows == 0) return 0;
   const int rpw = std::max(1, (rows + 4 * 512 - 1) / (4 * 512));  // ~512 blocks of 4 waves
-  dim3 grid((rows + 4 * rpw - 1) / (4 * rpw));
+  const int nblk = (rows + 4 * rpw - 1) / (4 * rpw);
+  dim3 grid(nblk);
   hipStream_t st = (hipStream_t)stream;
+  float* ws = nullptr;
+  if (dgamma || dbeta) {
+    ws = (float*)workspace((size_t)nblk * 2 * cols * sizeof(float));
+    if (!ws) return fail(IMGCAP_EINVAL, "imgcap_add_layernorm_bwd: workspace allocation failed");
+  }
 #define LNB_(T, G)                                                                                              \
   do {                                                                                                          \
     if (cols <= 512) { LNB2_(T, G, 512); } else if (cols <= 1024) { LNB2_(T, G, 1024); } else { LNB2_(T, G, 2048); } \
   } while (0)
 #define LNB2_(T, G, MC)                                                                                         \
   hipLaunchKernelGGL((add_ln_bwd_kernel<T, G, MC>), grid, dim3(256), 0, st, rows, cols, (const T*)dy, (const T*)s,   \
-                     mean, rstd, gamma, drop_p, seed, g_seed_ctr, drop_stream, (T*)dx, (T*)dr, dgamma, dbeta, rpw)
+                     mean, rstd, gamma, drop_p, seed, g_seed_ctr, drop_stream, (T*)dx, (T*)dr, ws, rpw)
   if (dtype == IMGCAP_BF16) {
     if (vec_rows<bf16>(cols, {dy, s, dx, dr})) LNB_(bf16, 8); else LNB_(bf16, 1);
   } else {
@@ -215,5 +222,8 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
 #undef LNB_
 #undef LNB2_
   IMGCAP_CHECK_LAUNCH("imgcap_add_layernorm_bwd");
+  if (dgamma && dbeta) return imgcap_slice_reduce(2L * cols, nblk, ws, 2L * cols, 1.f, cols, dgamma, dbeta, stream);
+  if (dgamma) return imgcap_slice_reduce(cols, nblk, ws, 2L * cols, 1.f, 0, dgamma, nullptr, stream);
+  if (dbeta) return imgcap_slice_reduce(cols, nblk, ws + cols, 2L * cols, 1.f, 0, dbeta, nullptr, stream);
   return 0;
 }

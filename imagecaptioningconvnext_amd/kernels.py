@@ -8,7 +8,7 @@ import ctypes
 import torch
 
 from . import _abi
-from ._abi import ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, Epilogue  # noqa: F401
+from ._abi import ACT_DGELU, ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, Epilogue  # noqa: F401
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -229,10 +229,10 @@ def dwconv7_ln(x, w49, bias, ln_w, ln_b, out):
     return out
 
 
-def ln_patchify2(x, ln_w, ln_b, out):
+def ln_patchify2(x, ln_w, ln_b, out, cmajor=False):
     B, H, W, C = x.shape
     _abi.call("imgcap_ln_patchify2", dt(x), B, H, W, C, x.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
-              out.data_ptr(), stream())
+              int(cmajor), out.data_ptr(), stream())
     return out
 
 
@@ -284,3 +284,48 @@ def stochastic_depth_scales(probs, B, seed, drop_stream, out):
     _abi.call("imgcap_stochastic_depth_scales", probs.numel(), B, probs.data_ptr(), seed, drop_stream,
               out.data_ptr(), stream())
     return out
+
+
+# ---- ConvNeXt backward (trainable encoder children) ----------------------------------------
+def dwconv7_bwd_data(dz, w49, out, res=None):
+    """out = res + dwconv7^T(dz) (flipped taps, no bias); w49 = forward weights [49][C]."""
+    B, H, W, C = dz.shape
+    _check_dev(dz, out)
+    _abi.call("imgcap_dwconv7_bwd_data", dt(dz), B, H, W, C, dz.data_ptr(), w49.data_ptr(), ptr(res),
+              out.data_ptr(), stream())
+    return out
+
+
+def dwconv7_wgrad(dz, x, dw, db):
+    """dw [C,1,7,7] / [C,49] fp32 and db [C] fp32 written (not accumulated)."""
+    B, H, W, C = dz.shape
+    _abi.call("imgcap_dwconv7_wgrad", dt(dz), B, H, W, C, dz.data_ptr(), x.data_ptr(), dw.data_ptr(),
+              db.data_ptr(), stream())
+
+
+def layer_scale_grad(G, w2, b2, gamma, cs, dw2, wg, dgamma, db2):
+    C, C4 = G.shape
+    _abi.call("imgcap_layer_scale_grad", dt(wg), C, C4, G.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+              gamma.data_ptr(), cs.data_ptr(), dw2.data_ptr(), wg.data_ptr(), dgamma.data_ptr(), db2.data_ptr(),
+              stream())
+
+
+def rowscale(x, s, rows_per_scale, out=None):
+    out = torch.empty_like(x) if out is None else out
+    rows, cols = x.shape
+    _abi.call("imgcap_rowscale", dt(x), rows, cols, x.data_ptr(), s.data_ptr(), rows_per_scale, out.data_ptr(),
+              stream())
+    return out
+
+
+def ln_patchify2_bwd(x, dpatches, ln_w, dx, dln_w, dln_b, cmajor=False):
+    B, H, W, C = x.shape
+    _abi.call("imgcap_ln_patchify2_bwd", dt(x), B, H, W, C, x.data_ptr(), dpatches.data_ptr(), ln_w.data_ptr(),
+              int(cmajor), dx.data_ptr(), dln_w.data_ptr(), dln_b.data_ptr(), stream())
+    return dx
+
+
+def adaptive_pool_bwd(dy, H, W, dx):
+    B, OH, OW, C = dy.shape
+    _abi.call("imgcap_adaptive_pool_bwd_nhwc", dt(dy), B, H, W, C, OH, OW, dy.data_ptr(), dx.data_ptr(), stream())
+    return dx

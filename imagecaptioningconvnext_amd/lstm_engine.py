@@ -165,10 +165,11 @@ class LstmEngine:
         return out.view(B, T, V)
 
     # ---------------------------------------------------------------------------------------
-    def backward(self, s, dlogits=None, dalpha=None, gbuf=None):
+    def backward(self, s, dlogits=None, dalpha=None, gbuf=None, want_denc=False):
         """Writes dL/dparams into ``gbuf`` (default: the flat grad buffer).  Default upstream:
         the fused loss of forward(loss=True); otherwise ``dlogits`` [B*T, V(pad)] (compute
-        dtype) and ``dalpha`` [B, T, P] (f32)."""
+        dtype) and ``dalpha`` [B, T, P] (f32).  want_denc: also dL/d encoder_out (fp32, the
+        caller's batch order) into s["denc"] -- encoder fine-tuning."""
         fp, ct = self.fp, self.ct
         gbuf = fp.grad if gbuf is None else gbuf
 
@@ -215,6 +216,9 @@ class LstmEngine:
         for k, v in bufs.items():
             setattr(d, k, K.ptr(v))
         d.x_slices, d.y_slices = xs, ys
+        dawe = torch.empty(B, T + 1, E, **f32) if want_denc else None
+        d.dawe = K.ptr(dawe)
+        bufs["dawe"] = dawe
         s["bwd_bufs"] = bufs  # the descriptor points into these: keep them alive as long as `s`
         _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream())
         dc2 = dcat.view(BT, W3)
@@ -239,4 +243,13 @@ class LstmEngine:
         K.colsum(dbea, _G.g("attention.encoder_att.bias"))
         K.colsum(dwf, _G.g("attention.full_att.weight", (A,)))
         # full_att.bias: exactly zero gradient (softmax is shift-invariant) -> left at 0
+        s["denc"] = None
+        if want_denc:
+            # decoder.py:61 (att1 = enc W_ea), :99-101 (mean -> init_h/c), :136 (context)
+            K.gemm(dinit, w["init"], out=dawe[:, T, :])                      # dL/d mean(enc)
+            base = K.gemm(datt1, w["wea"], out_dtype=torch.float32)         # [B*P, E]
+            denc = torch.empty(B, P, E, **f32)
+            _abi.call("imgcap_lstm_denc", B, T, P, E, s["alphas"].data_ptr(), dawe.data_ptr(), base.data_ptr(),
+                      s["sort_ind"].data_ptr(), denc.data_ptr(), K.stream())
+            s["denc"] = denc
         return gbuf

@@ -43,6 +43,7 @@ class _LstmTF(torch.autograd.Function):
         s = engine.forward(encoder_out, caps, caplens, fixed_T=False, loss=False)
         preds = engine.predictions(s)
         ctx.engine, ctx.s = engine, s
+        ctx.enc_shape, ctx.enc_dtype = encoder_out.shape, encoder_out.dtype
         ctx.mark_non_differentiable(s["caps_s"], s["sort_ind"])
         return preds, s["alphas"], s["caps_s"], s["sort_ind"]
 
@@ -54,13 +55,12 @@ class _LstmTF(torch.autograd.Function):
         mask = s["tmask"].reshape(-1, 1)
         dl[:, :V] = (dpred.reshape(B * T, V) * mask).to(eng.ct)
         da = None if dalpha is None else (dalpha * s["tmask"][..., None]).contiguous().float()
-        if encoder_out_needs_grad(ctx):
-            raise NotImplementedError("gradient w.r.t. encoder_out (encoder fine-tuning with the LSTM decoder) "
-                                      "is not built yet")
+        want = encoder_out_needs_grad(ctx)
         gbuf = torch.empty_like(eng.fp.grad)
-        eng.backward(s, dlogits=dl, dalpha=da, gbuf=gbuf)
+        eng.backward(s, dlogits=dl, dalpha=da, gbuf=gbuf, want_denc=want)
         grads = tuple(eng.fp.g(n, buf=gbuf) for n in eng.fp.params)
-        return (None, None, None, None) + grads
+        denc = s["denc"].view(ctx.enc_shape).to(ctx.enc_dtype) if want else None
+        return (None, denc, None, None) + grads
 
 
 class DecoderWithAttention(nn.Module):

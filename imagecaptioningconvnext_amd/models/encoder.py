@@ -10,8 +10,9 @@ initialised the torchvision way and ``variant`` selects tiny/base/large (BASELIN
 forward runs the NHWC trunk on the HIP kernels: stem (conv4x4+LN) -> per CNBlock
 dwconv7x7+LN -> MFMA GEMM (Linear C->4C, +bias, GELU) -> MFMA GEMM (Linear 4C->C, +bias,
 *layer_scale, *stochastic-depth, +residual, in place) -> downsample LN + 2x2 patch GEMM ->
-adaptive pool.  Only the frozen-encoder (no-grad) path is on the hot path of the configs run
-here; a trainable encoder output raises (fine-tuning backward is SURVEY.md §8 C5, next round).
+adaptive pool.  With trainable children (``fine_tune(True, startingLayer)``) the trainable
+suffix runs on encoder_engine.EncoderEngine (saved activations + HIP backward) and the output is
+differentiable; the frozen prefix always takes the fused fast path.
 """
 import math
 
@@ -84,6 +85,25 @@ def build_features(variant):
     return feats
 
 
+class _EncoderTrain(torch.autograd.Function):
+    """Differentiable encoder forward over the trainable children's parameters (FlatParams
+    order); backward = EncoderEngine.backward, handing autograd one grad view per parameter."""
+
+    @staticmethod
+    def forward(ctx, engine, images, *params):
+        feats, saved = engine.forward(images)
+        ctx.engine, ctx.saved = engine, saved
+        return feats
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        eng = ctx.engine
+        gbuf = torch.empty_like(eng.fp.grad)  # autograd accumulates the returned views into .grad
+        eng.backward(ctx.saved, dfeat, gbuf=gbuf)
+        grads = tuple(eng.fp.g(n, buf=gbuf) for n in eng.fp.params)
+        return (None, None) + grads
+
+
 class Encoder(nn.Module):
     def __init__(self, encoded_image_size=7, variant="base", compute_dtype=torch.bfloat16):
         super().__init__()
@@ -96,6 +116,7 @@ class Encoder(nn.Module):
         self.sd_seed = 0
         self._packed = None
         self._packed_key = None
+        self._engine = None
         self.fine_tune()
 
     def fine_tune(self, fine_tune=True, startingLayer=7):
@@ -158,33 +179,29 @@ class Encoder(nn.Module):
         self.sd_seed += 1
         return out
 
-    def forward(self, images):
-        """encoder.py:23-27.  images [B,3,H,W] (f32, on GPU) -> [B, s, s, E] NHWC, compute dtype."""
-        if any(p.requires_grad for p in self.convnext.parameters()) and torch.is_grad_enabled():
-            raise NotImplementedError("encoder fine-tuning backward (startingLayer < 8 with fine_tune=True) is not "
-                                      "built yet (SURVEY.md §8 C5); call fine_tune(False) or run under no_grad")
-        if not images.is_cuda:
-            raise RuntimeError("Encoder.forward runs on the HIP kernels only; move images to the GPU")
+    def _run_frozen(self, images, upto=8, sd=None):
+        """Stem + children [1, upto) of the trunk on the frozen fast path (no saved state).
+        Returns (x NHWC in the compute dtype, index of the next CNBlock for the SD scales)."""
         pk = self._pack()
         ct = self.compute_dtype
-        images = images.float().contiguous()
         B, _, H, W = images.shape
         dev = images.device
         C0 = pk["stem"][0].shape[0]
         x = torch.empty(B, H // 4, W // 4, C0, device=dev, dtype=ct)
         K.convnext_stem(images, *pk["stem"], x)
-        sd = self._sd_scales(B, dev) if self.training else None
         bid = 0
-        for blocks, down in pk["stages"]:
+        for st, (blocks, down) in enumerate(pk["stages"]):
+            if 1 + 2 * st >= upto:
+                break
             _, h, w, C = x.shape
             M = B * h * w
             z = torch.empty_like(x)
             hid = zn = None
-            if not (ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS):
+            fused = ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS
+            if not fused:
                 hid = torch.empty(M, 4 * C, device=dev, dtype=ct)
                 zn = torch.empty(M, C, device=dev, dtype=ct)
             x2 = x.view(M, C)
-            fused = ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS
             for blk in blocks:
                 rs = sd[bid] if (sd is not None and blk["sd"] > 0) else None
                 if w <= 64:  # channel-tiled depthwise; LayerNorm applied by the consumer
@@ -205,16 +222,43 @@ class Encoder(nn.Module):
                     K.gemm(hid, blk["w2"], trans_b=True, bias=blk["b2"], colscale=blk["gamma"], rowscale=rs,
                            rows_per_scale=h * w, res=x2, out=x2)
                 bid += 1
-            if down is not None:
+            if down is not None and 2 + 2 * st < upto:
                 patches = torch.empty(B * (h // 2) * (w // 2), 4 * C, device=dev, dtype=ct)
                 K.ln_patchify2(x, down["lnw"], down["lnb"], patches)
                 C2 = down["w"].shape[0]
                 x = torch.empty(B, h // 2, w // 2, C2, device=dev, dtype=ct)
                 K.gemm(patches, down["w"], trans_b=True, bias=down["b"], out=x.view(-1, C2))
+        return x, bid
+
+    def trainable(self):
+        return any(p.requires_grad for p in self.convnext.parameters())
+
+    def engine(self):
+        """HIP engine of the trainable children (rebuilt when fine_tune changes the set)."""
+        from ..encoder_engine import EncoderEngine
+        key = tuple(n for n, p in self.named_parameters() if p.requires_grad)
+        dev = next(self.convnext.parameters()).device
+        if self._engine is None or self._engine.key != key or not self._engine.fp.check_bound():
+            self._engine = EncoderEngine(self, dev)
+        return self._engine
+
+    def forward(self, images):
+        """encoder.py:23-27.  images [B,3,H,W] (f32, on GPU) -> [B, s, s, E] NHWC, compute dtype.
+        With trainable children (fine_tune) and grad enabled the output is differentiable:
+        backward runs the HIP encoder backward into the parameters' .grad."""
+        if not images.is_cuda:
+            raise RuntimeError("Encoder.forward runs on the HIP kernels only; move images to the GPU")
+        if self.trainable() and torch.is_grad_enabled():
+            eng = self.engine()
+            return _EncoderTrain.apply(eng, images, *eng.fp.params.values())
+        images = images.float().contiguous()
+        B = images.shape[0]
+        sd = self._sd_scales(B, images.device) if self.training else None
+        x, _ = self._run_frozen(images, 8, sd)
         s = self.enc_image_size
         if x.shape[1] == s and x.shape[2] == s:
             return x
-        out = torch.empty(B, s, s, x.shape[3], device=dev, dtype=ct)
+        out = torch.empty(B, s, s, x.shape[3], device=images.device, dtype=self.compute_dtype)
         return K.adaptive_pool(x, s, s, out)
 
     def macs_per_image(self, hw=224):

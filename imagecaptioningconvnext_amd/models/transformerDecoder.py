@@ -38,6 +38,7 @@ class _TransformerTF(torch.autograd.Function):
     def forward(ctx, engine, encoder_out, caps, caplens, key_ids, pad_id, *params):
         s = engine.forward(encoder_out, caps, caplens, key_ids=key_ids, pad_id=pad_id, loss=False)
         ctx.engine, ctx.s = engine, s
+        ctx.enc_shape, ctx.enc_dtype = encoder_out.shape, encoder_out.dtype
         return engine.predictions(s)
 
     @staticmethod
@@ -48,7 +49,7 @@ class _TransformerTF(torch.autograd.Function):
         dl[:, :V] = dpred.reshape(B * L, V).to(eng.ct)
         gbuf = torch.empty_like(eng.fp.grad)
         eng.backward(s, dlogits=dl, gbuf=gbuf, want_denc=bool(ctx.needs_input_grad[1]))
-        denc = s["denc"].to(dpred.dtype).view_as(s["enc"]) if s["denc"] is not None else None
+        denc = s["denc"].reshape(ctx.enc_shape).to(ctx.enc_dtype) if s["denc"] is not None else None
         grads = tuple(eng.fp.g(n, buf=gbuf) for n in eng.fp.params)
         return (None, denc, None, None, None, None) + grads
 

@@ -3,9 +3,9 @@
 Per step, exactly the reference's work:
   encoder(imgs) in train mode (frozen weights, stochastic depth active)      train.py:242,261
   decoder teacher-forced forward + packed CE (+ alpha reg for LSTM)          :262-276
-  zero_grad + backward                                                        :278-281
+  zero_grad + backward (into the fine-tuned encoder children too, if any)     :278-281
   DDP gradient averaging (one RCCL all-reduce over the flat grad buffer)      trainMultiGPU.py:233,384
-  clip_gradient (clamp +-5) + Adam step (one fused kernel)                    :284-291 / :387-394
+  clip_gradient (clamp +-5) + Adam step (one fused kernel per optimizer)      :284-291 / :387-394
   loss/token/top-5 metrics (reduceLossAndTokens + accuracy all-reduces,
   fused into one 3-float all-reduce; read back lazily, no per-step host sync) :396-403
 
@@ -23,12 +23,13 @@ from . import kernels as K
 
 
 class TeacherForcedTrainer:
-    def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, grad_clip=5.0, alphaC=1.0, pad_id=0,
-                 process_group=None, graph=False):
+    def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, encoder_lr=1e-4, grad_clip=5.0, alphaC=1.0,
+                 pad_id=0, process_group=None, graph=False):
         self.encoder = encoder
         self.decoder = decoder
         self.lstm = lstm
         self.decoder_lr = decoder_lr
+        self.encoder_lr = encoder_lr
         self.grad_clip = grad_clip
         self.alphaC = alphaC
         self.pad_id = pad_id
@@ -45,17 +46,26 @@ class TeacherForcedTrainer:
             self.eng.fp.refresh_shadow()
             for p in encoder.parameters():
                 dist.broadcast(p.data, 0, group=process_group)
+        # fine-tuned encoder children (Encoder.fine_tune, train.py:113-114): their own flat
+        # parameter/grad/Adam buffers, trained with encoder_lr after the same all-reduce
+        self.enc_eng = encoder.engine() if encoder.trainable() else None
 
     def _fwd_bwd(self, imgs, caps, caplens):
         self.encoder.train()
         self.decoder.train()
-        with torch.no_grad():
-            feats = self.encoder(imgs)
+        es = None
+        if self.enc_eng is not None:
+            feats, es = self.enc_eng.forward(imgs)
+        else:
+            with torch.no_grad():
+                feats = self.encoder(imgs)
         if self.lstm:
             s = self.eng.forward(feats, caps, caplens, fixed_T=True, alphaC=self.alphaC)
         else:
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
-        self.eng.backward(s)
+        self.eng.backward(s, want_denc=es is not None)
+        if es is not None:
+            self.enc_eng.backward(es, s["denc"].reshape(feats.shape))
         return s["metrics"]
 
     def _capture(self, imgs, caps, caplens, warmup=2):
@@ -93,6 +103,11 @@ class TeacherForcedTrainer:
         if self.world > 1:
             dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
         fp.adam_step(self.decoder_lr, self.grad_clip, grad_div=float(self.world))
+        if self.enc_eng is not None:
+            efp = self.enc_eng.fp
+            if self.world > 1:
+                dist.all_reduce(efp.grad, op=dist.ReduceOp.SUM, group=self.pg)
+            efp.adam_step(self.encoder_lr, self.grad_clip, grad_div=float(self.world))
         red = torch.stack([m[0] * m[1], m[1], m[2]])
         if self.world > 1:
             dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)

@@ -26,7 +26,9 @@ extern "C" {
 
 enum { IMGCAP_F32 = 0, IMGCAP_BF16 = 1 };
 enum { IMGCAP_OK = 0, IMGCAP_EINVAL = -1, IMGCAP_EUNSUPPORTED = -2 };
-enum { IMGCAP_ACT_NONE = 0, IMGCAP_ACT_GELU = 1, IMGCAP_ACT_RELU = 2 };
+/* ACT_GELU with an aux operand also writes the pre-activation to aux (the saved input of the
+ * backward pass); ACT_DGELU multiplies by GELU'(aux[m, n]) (aux = that saved pre-activation). */
+enum { IMGCAP_ACT_NONE = 0, IMGCAP_ACT_GELU = 1, IMGCAP_ACT_RELU = 2, IMGCAP_ACT_DGELU = 3 };
 
 const char* imgcap_last_error_string(void);
 int imgcap_version(void);
@@ -44,7 +46,8 @@ int imgcap_set_seed_counter(const uint64_t* counter);
  *   A(m,k) = A[m*lda + k] if a_kmajor else A[k*lda + m]
  *   B(k,n) = B[n*ldb + k] if b_kmajor else B[k*ldb + n]      (b_kmajor = nn.Linear weight [N][K])
  *   v = alpha*acc (+bias[n]) -> act -> dropout(p; seed,stream, index m*drop_ld+n)
- *       -> (*= aux[m,n] > 0 ? aux_scale : 0) -> (*= colscale[n]) -> (*= rowscale[m/rows_per_scale])
+ *       -> (*= aux[m,n] > 0 ? aux_scale : 0; or *= GELU'(aux[m,n]) for ACT_DGELU)
+ *       -> (*= colscale[n]) -> (*= rowscale[m/rows_per_scale])
  *       -> (+= res[m,n]) -> (+= beta*C[m,n]) -> C[m,n] (c_dtype)
  * Replaces every nn.Linear / 1x1-conv / patchify-conv / projection matmul on the path:
  * decoder.py:61-63,100-101,139-144; transformerDecoder.py:95,104,106; torchvision CNBlock
@@ -127,9 +130,10 @@ int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const void* x, cons
                       const float* bias, const float* ln_w, const float* ln_b, void* out,
                       void* stream);
 /* features[2,4,6] head: LayerNorm2d(C) then gather 2x2/s2 patches into rows
- * out[B*(H/2)*(W/2)][4C] ordered (kh, kw, c) (weights repacked to match). */
+ * out[B*(H/2)*(W/2)][4C] ordered (kh, kw, c) (weights repacked to match; cmajor = 0) or
+ * (c, kh, kw) (cmajor = 1: the torch Conv2d weight [2C][C][2][2] is the GEMM operand as is). */
 int imgcap_ln_patchify2(int dtype, int B, int H, int W, int C, const void* x, const float* ln_w,
-                        const float* ln_b, void* out, void* stream);
+                        const float* ln_b, int cmajor, void* out, void* stream);
 /* AdaptiveAvgPool2d((OH,OW)) on NHWC (encoder.py:20,25) */
 int imgcap_adaptive_pool_nhwc(int dtype, int B, int H, int W, int C, int OH, int OW,
                               const void* x, void* out, void* stream);
@@ -143,6 +147,42 @@ int imgcap_adaptive_pool_nhwc(int dtype, int B, int H, int W, int C, int OH, int
 int imgcap_cnblock_mlp(int M, int C, const void* y, const float* ln_w, const float* ln_b, const void* w1,
                        const float* b1, const void* w2, const float* b2, const float* gamma, const float* sd,
                        int rows_per_sample, void* x, void* stream);
+/* ---------------------------------------------------------------------------------------
+ * Backward of the trainable ConvNeXt children (Encoder.fine_tune, encoder.py:29-34; the
+ * encoder half of loss.backward() / encoderOptimizer.step() at train.py:278-290).
+ * -------------------------------------------------------------------------------------- */
+/* dx = res + dwconv7^T(dz): the depthwise 7x7 data gradient (the forward kernel with flipped
+ * taps, no bias).  w: the forward weights [49][C] (tap-major).  res may alias dx (or be NULL);
+ * dz may not. */
+int imgcap_dwconv7_bwd_data(int dtype, int B, int H, int W, int C, const void* dz, const float* w,
+                            const void* res, void* dx, void* stream);
+/* Depthwise weight / bias gradients: dw[c][kh*7+kw] = sum_{b,h,w} dz[b,h,w,c] *
+ * x[b,h+kh-3,w+kw-3,c] (zero padded), db[c] = sum dz[..., c]  (torch layout [C,1,7,7]; written,
+ * not accumulated; fixed-order reduction). */
+int imgcap_dwconv7_wgrad(int dtype, int B, int H, int W, int C, const void* dz, const void* x, float* dw,
+                         float* db, void* stream);
+/* Layer-scale backward of one CNBlock from G = (sd*dout)^T GELU(h)  [C][C4] fp32 and
+ * cs = colsum(sd*dout): dw2 = gamma*G, wg = gamma*w2 (dtype; operand of the d-hidden GEMM),
+ * dgamma = rowsum(w2*G) + b2*cs, db2 = gamma*cs. */
+int imgcap_layer_scale_grad(int dtype, int C, int C4, const float* G, const float* w2, const float* b2,
+                            const float* gamma, const float* cs, float* dw2, void* wg, float* dgamma,
+                            float* db2, void* stream);
+/* y[r, :] = x[r, :] * s[r / rows_per_scale]  (per-sample stochastic-depth scale; y may be x) */
+int imgcap_rowscale(int dtype, int64_t rows, int cols, const void* x, const float* s, int rows_per_scale,
+                    void* y, void* stream);
+/* Backward of imgcap_ln_patchify2 (features[2,4,6] LayerNorm2d + 2x2 patch gather): dpatches
+ * [B*(H/2)*(W/2)][4C] -> dx [B,H,W,C]; dln_w / dln_b written (statistics recomputed from x). */
+int imgcap_ln_patchify2_bwd(int dtype, int B, int H, int W, int C, const void* x, const void* dpatches,
+                            const float* ln_w, int cmajor, void* dx, float* dln_w, float* dln_b, void* stream);
+/* Backward of imgcap_adaptive_pool_nhwc (AdaptiveAvgPool2d, encoder.py:20,25). */
+int imgcap_adaptive_pool_bwd_nhwc(int dtype, int B, int H, int W, int C, int OH, int OW, const void* dy,
+                                  void* dx, void* stream);
+/* Fixed-order sum of `slices` partial rows ws[s*ld + i], i < n:
+ *   split == 0: out0[i] = beta*out0[i] + t_i;  split > 0: i >= split goes to out1[i - split];
+ *   split < 0:  depthwise layout i = c*50 + k -> out0[c*49 + k] (k < 49) / out1[c] (k = 49). */
+int imgcap_slice_reduce(int64_t n, int slices, const float* ws, int64_t ld, float beta, int64_t split,
+                        float* out0, float* out1, void* stream);
+
 /* StochasticDepth(p_i, "row") per-sample scales of every CNBlock (torchvision convnext,
  * train mode; encoder.py:18 builds it): out[i*B + b] = keep ? 1/(1-p_i) : 0, keep drawn from
  * the counter RNG (seed, drop_stream, index i*B+b).  probs: device fp32 [nblocks]. */
@@ -231,10 +271,18 @@ typedef struct imgcap_lstm_desc {
   float* dbea;          /* [B*ceil(P/7), A] out: partials of dL/db_ea */
   int32_t x_slices;     /* 1..16 */
   int32_t y_slices;     /* 1..16 */
+  float* dawe;          /* [B, T+1, E] out or NULL: dL/d(attention context) per step (rows t < T;
+                           row T is left to the caller) -- the encoder-gradient path */
 } imgcap_lstm_desc;
 
 int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream);
 int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream);
+/* dL/d encoder_out for encoder fine-tuning (the decoder.py:75-148 paths back into encoder_out):
+ *   denc[sort_ind[b], p, :] = base[b, p, :] + sum_{t<T} alphas[b,t,p] dawe[b,t,:] + dawe[b,T,:] / P
+ * base [B, P, E] fp32 = datt1 . W_ea (sorted order, may be NULL); dawe [B, T+1, E] fp32 as
+ * imgcap_lstm_desc.dawe with row T = dL/d mean(encoder_out); sort_ind NULL = identity; P <= 64. */
+int imgcap_lstm_denc(int B, int T, int P, int E, const float* alphas, const float* dawe, const float* base,
+                     const int64_t* sort_ind, float* denc, void* stream);
 /* train.py:269: reg = alphaC*mean_{b,p}(1-sum_t alpha)^2 -> *reg_out;
  * dalpha[b,t,p] = d reg / d alpha[b,t,p] (0 where t >= dl[b]) */
 int imgcap_attn_reg(int B, int T, int P, const float* alphas, const int32_t* dl, float alphaC, float* dalpha,

@@ -66,8 +66,9 @@ def mlp():
         b1, b2, gm = torch.randn(4 * C, device=dev), torch.randn(C, device=dev), torch.randn(C, device=dev) * 1e-3
         hid = torch.empty(M, 4 * C, device=dev, dtype=bf)
         flops = 2.0 * 2 * M * C * 4 * C
-        t = time_launch(lambda: K.cnblock_mlp(z, w1, b1, w2, b2, gm, x), reps=20)
-        print(f"cnblock_mlp fused  M={M:6d} C={C:4d}: {t * 1e6:8.1f} us {flops / t / 1e12:7.1f} TFLOP/s")
+        if C <= 192:
+            t = time_launch(lambda: K.cnblock_mlp(z, w1, b1, w2, b2, gm, x), reps=20)
+            print(f"cnblock_mlp fused  M={M:6d} C={C:4d}: {t * 1e6:8.1f} us {flops / t / 1e12:7.1f} TFLOP/s")
 
         def unfused():
             K.gemm(z, w1, trans_b=True, bias=b1, act=K.ACT_GELU, out=hid)
