@@ -30,6 +30,8 @@ CONFIGS = {
     "C2": dict(encoder="tiny", decoder="lstm", batch=32),
     "C3": dict(encoder="tiny", decoder="transformer", batch=64),
     "C4": dict(encoder="base", decoder="transformer", batch=32),
+    # ConvNeXt-Large + Transformer, encoder fine-tuned from startingLayer=7 (stage 4 trains)
+    "C5": dict(encoder="large", decoder="transformer", batch=64, starting_layer=7),
 }
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0       # HBM3E spec
@@ -65,7 +67,10 @@ def build(cfg, device):
     from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
     from imagecaptioningconvnext_amd.models.encoder import Encoder
     enc = Encoder(variant=cfg["encoder"], compute_dtype=torch.bfloat16).to(device)
-    enc.fine_tune(False)
+    if "starting_layer" in cfg:
+        enc.fine_tune(True, startingLayer=cfg["starting_layer"])
+    else:
+        enc.fine_tune(False)
     E = enc.encoder_dim
     if cfg["decoder"] == "lstm":
         dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=device,
@@ -79,8 +84,11 @@ def build(cfg, device):
 
 
 def flops_per_image(cfg, enc):
-    """Algorithmic FLOPs per image: frozen encoder fwd + 3x decoder fwd."""
+    """Algorithmic FLOPs per image: encoder fwd (+ 2x fwd for the fine-tuned
+    children's backward) + 3x decoder fwd."""
     enc_macs = enc.macs_per_image(224)
+    if "starting_layer" in cfg:
+        enc_macs += 2 * enc.macs_per_image(224, start=cfg["starting_layer"])
     T, E, A, D, M = CAPLEN - 1, enc.encoder_dim, 512, 512, 512
     if cfg["decoder"] == "lstm":
         P = 49
@@ -189,7 +197,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (224x224x3 U[0,1) ImageNet-normalised, random captions len 52), random-init weights",
-            "config": {"workload": f"{args.config}: ConvNeXt-{cfg['encoder'].capitalize()} (frozen) + "
+            "config": {"workload": f"{args.config}: ConvNeXt-{cfg['encoder'].capitalize()} "
+                                   f"({'fine-tuned from child %d' % cfg['starting_layer'] if 'starting_layer' in cfg else 'frozen'}) + "
                                    f"{'LSTM-attention' if cfg['decoder'] == 'lstm' else 'Transformer'} decoder, "
                                    f"teacher-forced train step",
                        "per_gpu_batch": B, "global_batch": B * world, "image": 224, "caption_len": CAPLEN,

@@ -261,14 +261,17 @@ class Encoder(nn.Module):
         out = torch.empty(B, s, s, x.shape[3], device=images.device, dtype=self.compute_dtype)
         return K.adaptive_pool(x, s, s, out)
 
-    def macs_per_image(self, hw=224):
+    def macs_per_image(self, hw=224, start=0):
+        """Multiply-accumulates per image of convnext.children()[start:] (all of them by default)."""
         chans, depths, _ = VARIANTS[self.variant]
         h = hw // 4
-        m = h * h * chans[0] * 48
+        m = h * h * chans[0] * 48 if start <= 0 else 0
         for st in range(4):
             C = chans[st]
-            m += depths[st] * (h * h * C * 49 + 2 * h * h * C * 4 * C)
+            if 1 + 2 * st >= start:
+                m += depths[st] * (h * h * C * 49 + 2 * h * h * C * 4 * C)
             if st < 3:
                 h //= 2
-                m += h * h * chans[st + 1] * 4 * C
+                if 2 + 2 * st >= start:
+                    m += h * h * chans[st + 1] * 4 * C
         return m

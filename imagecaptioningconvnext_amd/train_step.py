@@ -22,6 +22,12 @@ import torch.distributed as dist
 from . import kernels as K
 
 
+def _trainable(encoder):
+    """Encoder with fine-tuned children (any module exposing the Encoder surface)."""
+    fn = getattr(encoder, "trainable", None)
+    return bool(fn()) if callable(fn) else False
+
+
 class TeacherForcedTrainer:
     def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, encoder_lr=1e-4, grad_clip=5.0, alphaC=1.0,
                  pad_id=0, process_group=None, graph=False):
@@ -48,7 +54,14 @@ class TeacherForcedTrainer:
                 dist.broadcast(p.data, 0, group=process_group)
         # fine-tuned encoder children (Encoder.fine_tune, train.py:113-114): their own flat
         # parameter/grad/Adam buffers, trained with encoder_lr after the same all-reduce
-        self.enc_eng = encoder.engine() if encoder.trainable() else None
+        self.enc_eng = encoder.engine() if _trainable(encoder) else None
+
+    def enable_encoder_finetune(self, startingLayer):
+        """train.py:160-166: from this step on, children[startingLayer:] of the encoder train
+        with their own Adam (encoder_lr); the captured graph is rebuilt on the next step."""
+        self.encoder.fine_tune(fine_tune=True, startingLayer=startingLayer)
+        self.enc_eng = self.encoder.engine() if _trainable(self.encoder) else None
+        self._graph = None
 
     def _fwd_bwd(self, imgs, caps, caplens):
         self.encoder.train()
@@ -63,9 +76,11 @@ class TeacherForcedTrainer:
             s = self.eng.forward(feats, caps, caplens, fixed_T=True, alphaC=self.alphaC)
         else:
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
-        self.eng.backward(s, want_denc=es is not None)
         if es is not None:
+            self.eng.backward(s, want_denc=True)
             self.enc_eng.backward(es, s["denc"].reshape(feats.shape))
+        else:
+            self.eng.backward(s)
         return s["metrics"]
 
     def _capture(self, imgs, caps, caplens, warmup=2):

@@ -41,9 +41,14 @@ def main(argv=None):
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
     encoder, decoder = train.build_models(args, device)
     trainer = TeacherForcedTrainer(encoder, decoder, lstm=args.lstmDecoder, decoder_lr=train.decoderLr,
-                                   grad_clip=train.gradClip, alphaC=train.alphaC, graph=True)
+                                   encoder_lr=args.encoderLr, grad_clip=train.gradClip, alphaC=train.alphaC,
+                                   graph=True)
     log = print if rank == 0 else (lambda *a, **k: None)
     for epoch in range(args.epochs):
+        if epoch == args.fineTuneFromEpoch:  # trainMultiGPU.py: encoder fine-tuned (and DDP-averaged) from epoch 20
+            trainer.enable_encoder_finetune(args.startingLayer)
+            log(f"Fine-tuning encoder from epoch {epoch} onwards (starting from layer {args.startingLayer})",
+                flush=True)
         loader = train.synthetic_loader(args.steps, args.batchSize, device, rank=rank)
         out = train.trainWithTeacherForcing(loader, encoder, decoder, trainer, epoch, args.lstmDecoder, log=log)
         log(f"epoch {epoch}: global loss {out[0]:.4f} top5 {out[1]:.2f} batch {out[2] * 1e3:.2f} ms "
