@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libimgcap_hip.so")
+# IMGCAP_LIB: alternative build of the same library (the diagnostic stamps build of tools/)
+LIB_PATH = os.environ.get("IMGCAP_LIB") or os.path.join(_HERE, "libimgcap_hip.so")
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU = 0, 1, 2, 3
@@ -94,6 +95,7 @@ _SIGS = {
     "imgcap_ln_patchify2_bwd": [c_int] * 5 + [c_void_p] * 3 + [c_int] + [c_void_p] * 4,
     "imgcap_adaptive_pool_bwd_nhwc": [c_int] * 7 + [c_void_p] * 3,
     "imgcap_lstm_denc": [c_int] * 4 + [c_void_p] * 6,
+    "imgcap_gemm_set_policy": [c_int],
     "imgcap_slice_reduce": [c_int64, c_int, c_void_p, c_int64, c_float, c_int64, c_void_p, c_void_p, c_void_p],
 }
 

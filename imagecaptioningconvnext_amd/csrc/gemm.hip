@@ -67,7 +67,11 @@ DEV void epi_vec8(const imgcap_epilogue& ep, const EpiFlags& f, void* C, long ci
   if (ep.act == IMGCAP_ACT_GELU) {
     if (f.aux) store_pre8(ep, m, n0, v);  // pre-activation kept for the backward pass
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+    for (int j = 0; j < 8; j += 2) {  // erf by a 1.5e-7-accurate polynomial (common.h gelu_fast2)
+      const f32x2 g = gelu_fast2(f32x2{v[j], v[j + 1]});
+      v[j] = g[0];
+      v[j + 1] = g[1];
+    }
   } else if (ep.act == IMGCAP_ACT_RELU) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -136,7 +140,7 @@ DEV void epi_scalar(const imgcap_epilogue& ep, void* C, long cidx, int m, int n,
   if (ep.bias) v += ep.bias[n];
   if (ep.act == IMGCAP_ACT_GELU) {
     if (ep.aux) store_from_f((void*)ep.aux, (long)m * ep.ldaux + n, ep.c_dtype, v);
-    v = gelu_erf(v);
+    v = gelu_fast(v);
   } else if (ep.act == IMGCAP_ACT_RELU) {
     v = fmaxf(v, 0.f);
   }
@@ -175,6 +179,152 @@ DEV void epilogue_from_lds(const imgcap_epilogue& ep, const float* tile, int LDT
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (n + j < N) epi_scalar(ep, C, cidx + j, m, n + j, v[j]);
+    }
+  }
+}
+
+// 8 values of row m, columns n0..n0+7 (16-byte aligned, in range) of a c_dtype matrix
+struct Raw8v { uint4 a, b; };
+DEV Raw8v ld_row8(const void* p, long i, int dtype) {
+  Raw8v r;
+  if (dtype == IMGCAP_BF16) {
+    r.a = *(const uint4*)((const bf16*)p + i);
+    r.b = r.a;
+  } else {
+    r.a = *(const uint4*)((const float*)p + i);
+    r.b = *(const uint4*)((const float*)p + i + 4);
+  }
+  return r;
+}
+DEV void raw8_to_f(const Raw8v& r, int dtype, float (&v)[8]) {
+  if (dtype == IMGCAP_BF16) {
+    const bf16x8 x = __builtin_bit_cast(bf16x8, r.a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+  } else {
+    const f32x4 x = __builtin_bit_cast(f32x4, r.a), y = __builtin_bit_cast(f32x4, r.b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = x[j]; v[j + 4] = y[j]; }
+  }
+}
+
+// Fast epilogue of a fp32 tile staged in LDS (rows [0, ROWS) x [0, BN), row stride LDT) by a
+// block of NT threads: a thread owns one 8-column group (the same in every pass, so the
+// column operands -- bias, layer-scale -- are loaded once per call) and ROWS*BN/(8*NT) rows;
+// all of its LDS reads and global operand loads (residual, aux, C for beta, row scales) are
+// issued before the first use, so the pass costs one memory round trip instead of one per row.
+// Semantics = epi_vec8 / epi_scalar (imgcap_epilogue).
+// GAP: staged row r maps to output row m_base + r + (r >= ROWS/2 ? GAP : 0) (two row bands)
+template <int BN, int ROWS, int NT, int CH = 2, int GAP = 0>
+DEV void epilogue_tile(const imgcap_epilogue& ep, const float* tile, int LDT, int m_base, int n_base, int M, int N,
+                       void* C, long ldc, bool vec_ok) {
+  constexpr int NV = BN / 8, RPI = NT / NV, IT = ROWS / RPI;
+  static_assert(NT % NV == 0 && ROWS % RPI == 0 && IT % CH == 0, "epilogue_tile geometry");
+  const int c8 = (threadIdx.x % NV) * 8, rl = threadIdx.x / NV;
+  const int n = n_base + c8;
+  if (n >= N) return;
+  if (!(vec_ok && n + 8 <= N)) {  // ragged / unaligned column group: element-wise
+    for (int it = 0; it < IT; ++it) {
+      const int r = rl + it * RPI, m = m_base + r + (r >= ROWS / 2 ? GAP : 0);
+      if (m >= M) continue;
+      for (int j = 0; j < 8 && n + j < N; ++j) epi_scalar(ep, C, (long)m * ldc + n + j, m, n + j, tile[r * LDT + c8 + j]);
+    }
+    return;
+  }
+  const bool has_res = ep.res != nullptr, has_aux = ep.aux != nullptr, has_beta = ep.beta != 0.f;
+  const bool pre_gelu = has_aux && ep.act == IMGCAP_ACT_GELU;  // aux is an output then
+  float bias[8], cs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { bias[j] = 0.f; cs[j] = 1.f; }
+  if (ep.bias) {
+    const f32x4 b0 = *(const f32x4*)(ep.bias + n), b1 = *(const f32x4*)(ep.bias + n + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { bias[j] = b0[j]; bias[j + 4] = b1[j]; }
+  }
+  if (ep.colscale) {
+    const f32x4 s0 = *(const f32x4*)(ep.colscale + n), s1 = *(const f32x4*)(ep.colscale + n + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { cs[j] = s0[j]; cs[j + 4] = s1[j]; }
+  }
+#pragma unroll 1
+  for (int i0 = 0; i0 < IT; i0 += CH) {
+    float v[CH][8];
+    Raw8v resv[CH], auxv[CH], cv[CH];
+    float rsv[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {  // every load of the chunk first
+      const int r = rl + (i0 + u) * RPI;
+      const int m = min(m_base + r + (r >= ROWS / 2 ? GAP : 0), M - 1);
+      const float* t = tile + r * LDT + c8;
+      const f32x4 a = *(const f32x4*)t, b = *(const f32x4*)(t + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[u][j] = a[j]; v[u][j + 4] = b[j]; }
+      if (has_res) resv[u] = ld_row8(ep.res, (long)m * ep.ldr + n, ep.c_dtype);
+      if (has_aux && !pre_gelu) auxv[u] = ld_row8(ep.aux, (long)m * ep.ldaux + n, ep.c_dtype);
+      if (has_beta) cv[u] = ld_row8(C, (long)m * ldc + n, ep.c_dtype);
+      rsv[u] = ep.rowscale ? ep.rowscale[m / ep.rows_per_scale] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int r = rl + (i0 + u) * RPI;
+      const int m = m_base + r + (r >= ROWS / 2 ? GAP : 0);
+      if (m >= M) continue;
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = v[u][j] * ep.alpha + bias[j];
+      if (ep.act == IMGCAP_ACT_GELU) {
+        if (pre_gelu) store_pre8(ep, m, n, x);
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const f32x2 g = gelu_fast2(f32x2{x[j], x[j + 1]});
+          x[j] = g[0];
+          x[j + 1] = g[1];
+        }
+      } else if (ep.act == IMGCAP_ACT_RELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = fmaxf(x[j], 0.f);
+      }
+      if (ep.drop_p > 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          x[j] *= dropout_scale(ep.seed, ep.drop_stream, (uint64_t)m * ep.drop_ld + n + j, ep.drop_p);
+      }
+      if (has_aux && !pre_gelu) {
+        float a[8];
+        raw8_to_f(auxv[u], ep.c_dtype, a);
+        if (ep.act == IMGCAP_ACT_DGELU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] *= gelu_grad(a[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = a[j] > 0.f ? x[j] * ep.aux_scale : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] *= cs[j] * rsv[u];
+      if (has_res) {
+        float r[8];
+        raw8_to_f(resv[u], ep.c_dtype, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] += r[j];
+      }
+      if (has_beta) {
+        float o[8];
+        raw8_to_f(cv[u], ep.c_dtype, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] += ep.beta * o[j];
+      }
+      const long ci = (long)m * ldc + n;
+      if (ep.c_dtype == IMGCAP_BF16) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)x[j];
+        *(bf16x8*)((bf16*)C + ci) = o;
+      } else {
+        float* cp = (float*)C + ci;
+        *(f32x4*)cp = f32x4{x[0], x[1], x[2], x[3]};
+        *(f32x4*)(cp + 4) = f32x4{x[4], x[5], x[6], x[7]};
+      }
     }
   }
 }
@@ -226,6 +376,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 
 #include "gemm_tiled.h"
 #include "gemm_glds.h"
+#include "gemm256.h"
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
@@ -260,20 +411,45 @@ static bool glds_enabled() {
   return on;
 }
 
+static int glds_stages() {
+  static const int s = [] {
+    const char* e = getenv("IMGCAP_GLDS_STAGES");  // A/B switch for kernel benchmarks
+    const int v = e ? atoi(e) : 2;
+    return v >= 2 && v <= 4 ? v : 2;
+  }();
+  return s;
+}
+
+// 256x256 tile (gemm256.h): 0 never, 1 wherever it applies, -1 by shape (default; the
+// IMGCAP_GEMM256 environment variable or imgcap_gemm_set_policy override it)
+static int g_gemm256_mode = [] {
+  const char* e = getenv("IMGCAP_GEMM256");
+  return e ? atoi(e) : -1;
+}();
+static int gemm256_mode() { return g_gemm256_mode; }
+
 static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, long lda, long ldb, int batch, int split) {
   if (M <= 64 && ak && bk && batch == 1) return {IMGCAP_GEMM_SKINNY, 1};
+  const int mode = gemm256_mode();
+  const bool glds_ok = bf16_op && glds_enabled() && mode != 5 && batch == 1 && lda % 8 == 0 && ldb % 8 == 0 && K >= 64;
+  if (glds_ok && split == 1) {
+    // the 256 tile wins only with >= ~1.5 rounds of tiles over the CUs and long K (measured:
+    // tools/microbench.py probe); below that the 2-blocks-per-CU 128 tile overlaps better
+    const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+    if ((mode >= 1 && mode <= 3) || (mode < 0 && tiles256 >= 384 && K >= 512)) return {IMGCAP_GEMM_GLDS256, 1};
+  }
   const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   const auto auto_split = [&] {
     return (int)std::max(1L, std::min({512 / std::max(tiles128, 1L), (long)(K / 256), 32L}));
   };
-  if (bf16_op && glds_enabled() && batch == 1 && lda % 8 == 0 && ldb % 8 == 0 && K >= 64) {
+  if (glds_ok) {
     // split-K: requested (weight gradients, -1 = auto) or, for grids too small to fill the chip
     // with a long K, chosen here; partial tiles go to scratch and the reduce kernel applies the
     // epilogue.  Auto: ~2 blocks per CU, >= 4 k-tiles per slice.
     int sk = 1;
-    if (split < 0 || (split == 1 && tiles128 < 96 && K >= 2048)) sk = auto_split();
+    if (split < 0 || (split == 1 && tiles128 < 256 && K >= 2048)) sk = auto_split();
     else if (split > 1) sk = split;
-    if (sk > 1 || tiles128 >= 128) return {IMGCAP_GEMM_GLDS, sk};
+    if (sk > 1 || tiles128 >= 128 || mode == 4) return {IMGCAP_GEMM_GLDS, sk};
   }
   if (split != 1) {
     const int sk = split < 0 ? auto_split() : split;
@@ -318,6 +494,29 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
     return 0;
   }
   if constexpr (sizeof(T) == 2) {
+    if (plan.kind == IMGCAP_GEMM_GLDS256) {
+      dim3 grid((N + 255) / 256, (M + 255) / 256);
+      const bf16* a = (const bf16*)A;
+      const bf16* b = (const bf16*)B;
+      const int var = gemm256_mode() >= 1 ? gemm256_mode() : 2;  // 1: BK 64 x 2 stages, 2: BK 32 x 4, 3: BK 32 x 3
+#define G256_V(AKV, BKV, BKT, SV)                                                                               \
+  hipLaunchKernelGGL((gemm256_kernel<BKT, SV, AKV, BKV>), grid, dim3(512), 0, st, a, lda, b, ldb, C, ldc, M, N, K, \
+                     ep, vec_ok, g_seed_ctr, 0)
+#define G256_(AKV, BKV)                       \
+  do {                                        \
+    if (var == 1) G256_V(AKV, BKV, 64, 2);    \
+    else if (var == 3) G256_V(AKV, BKV, 32, 3); \
+    else G256_V(AKV, BKV, 32, 4);             \
+  } while (0)
+      if (ak && bk) G256_(true, true);
+      else if (ak) G256_(true, false);
+      else if (bk) G256_(false, true);
+      else G256_(false, false);
+#undef G256_
+#undef G256_V
+      IMGCAP_CHECK_LAUNCH("imgcap_gemm(glds256)");
+      return 0;
+    }
     if (plan.kind == IMGCAP_GEMM_GLDS) {
       const int sk = plan.split;
       const int kslice = sk > 1 ? ((K + sk - 1) / sk + 63) / 64 * 64 : 0;
@@ -330,14 +529,22 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       dim3 grid((N + 127) / 128, (M + 127) / 128, zdim);
       const bf16* a = (const bf16*)A;
       const bf16* b = (const bf16*)B;
-#define GL_(AKV, BKV)                                                                                              \
-  hipLaunchKernelGGL((gemm_glds_kernel<128, 128, AKV, BKV>), grid, dim3(256), 0, st, a, lda, b, ldb, Cdst, ldc, M, N, \
-                     K, ep, vec_ok, g_seed_ctr, kslice)
+      const int S = glds_stages();
+#define GL_S(AKV, BKV, SV)                                                                                           \
+  hipLaunchKernelGGL((gemm_glds_kernel<128, 128, AKV, BKV, SV>), grid, dim3(256), 0, st, a, lda, b, ldb, Cdst, ldc, M, \
+                     N, K, ep, vec_ok, g_seed_ctr, kslice)
+#define GL_(AKV, BKV)              \
+  do {                             \
+    if (S == 4) GL_S(AKV, BKV, 4);  \
+    else if (S == 3) GL_S(AKV, BKV, 3); \
+    else GL_S(AKV, BKV, 2);        \
+  } while (0)
       if (ak && bk) GL_(true, true);
       else if (ak) GL_(true, false);
       else if (bk) GL_(false, true);
       else GL_(false, false);
 #undef GL_
+#undef GL_S
       if (sk > 1) {
         const long total = (long)M * N;
         const int blocks = (int)std::min<long>((total + 255) / 256, 2048);
@@ -535,3 +742,16 @@ extern "C" int imgcap_transpose(int dtype, int rows, int cols, const void* in, i
   IMGCAP_CHECK_LAUNCH("imgcap_transpose");
   return 0;
 }
+
+extern "C" int imgcap_gemm_set_policy(int glds256) {
+  IMGCAP_REQUIRE(glds256 >= -1 && glds256 <= 5, "imgcap_gemm_set_policy: -1..5");
+  g_gemm256_mode = glds256;
+  return 0;
+}
+
+#ifdef IMGCAP_STAMPS
+extern "C" int imgcap_debug_stamps(void* p) {
+  unsigned long long* v = (unsigned long long*)p;
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dev_stamps), &v, sizeof(v));
+}
+#endif

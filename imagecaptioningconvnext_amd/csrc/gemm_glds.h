@@ -91,15 +91,17 @@ DEV bf16x8 glds_frag_op(const char* img, int row0, int kk, int lane) {
   }
 }
 
-template <int BM, int BN, bool AK, bool BKM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_glds_kernel(
-    const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, void* __restrict__ C, long ldc,
-    int M, int N, int K, imgcap_epilogue ep, int vec_ok, const uint64_t* seed_ctr, int kslice) {
+template <int BM, int BN, bool AK, bool BKM, int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 : 1, S == 2 ? 2 : 1))) void
+gemm_glds_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, void* __restrict__ C,
+                 long ldc, int M, int N, int K, imgcap_epilogue ep, int vec_ok, const uint64_t* seed_ctr,
+                 int kslice) {
   constexpr int TILE_A = BM * 64 * 2, TILE_B = BN * 64 * 2, STAGE = TILE_A + TILE_B;
   constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 fragments per wave (2 x 2 waves)
   constexpr int LDT = BN + 4, EPI_ROWS = BM / 2;
-  static_assert(EPI_ROWS * LDT * 4 <= 2 * STAGE, "epilogue tile fits the stages");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int LPT = BM * 8 / 256 + BN * 8 / 256;  // LDS-DMA instructions per thread per k-tile
+  static_assert(EPI_ROWS * LDT * 4 <= S * STAGE, "epilogue tile fits the stages");
+  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
   if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
   int bx, by;
   xcd_remap(bx, by);
@@ -116,26 +118,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // k-tiles [kt0, nk): the whole K, or slice blockIdx.z of a split-K launch (kslice % 64 == 0)
+  // k-tiles [kt0, nk): the whole K, or slice blockIdx.z of a split-K launch (kslice % 64 == 0).
+  // S stages: tiles kt+1 .. kt+S-1 are in flight while tile kt is multiplied.
   const int kt0 = kslice ? blockIdx.z * (kslice / 64) : 0;
   const int nk = kslice ? min((K + 63) / 64, kt0 + kslice / 64) : (K + 63) / 64;
-  glds_issue_op<BM, AK>(A, lda, m0, M, kt0 * 64, K, smem + (kt0 & 1) * STAGE, w, lane);
-  glds_issue_op<BN, BKM>(B, ldb, n0, N, kt0 * 64, K, smem + (kt0 & 1) * STAGE + TILE_A, w, lane);
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i) {
+    if (kt0 + i < nk) {
+      char* st = smem + i * STAGE;
+      glds_issue_op<BM, AK>(A, lda, m0, M, (kt0 + i) * 64, K, st, w, lane);
+      glds_issue_op<BN, BKM>(B, ldb, n0, N, (kt0 + i) * 64, K, st + TILE_A, w, lane);
+    }
+  }
   for (int kt = kt0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * STAGE;
-      glds_issue_op<BM, AK>(A, lda, m0, M, (kt + 1) * 64, K, nxt, w, lane);
-      glds_issue_op<BN, BKM>(B, ldb, n0, N, (kt + 1) * 64, K, nxt + TILE_A, w, lane);
-      // this thread's copies of tile kt are the older half of its outstanding DMA
-      if constexpr (BM * 8 / 256 + BN * 8 / 256 == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
+    const int r = kt - kt0;
+    char* cur = smem + (r % S) * STAGE;
+    if (kt + S - 1 < nk) {
+      char* nxt = smem + ((r + S - 1) % S) * STAGE;
+      glds_issue_op<BM, AK>(A, lda, m0, M, (kt + S - 1) * 64, K, nxt, w, lane);
+      glds_issue_op<BN, BKM>(B, ldb, n0, N, (kt + S - 1) * 64, K, nxt + TILE_A, w, lane);
+    }
+    // this thread's copies of tile kt are older than the (newer tiles) x LPT still allowed out
+    const int newer = min(S - 1, nk - 1 - kt);
+    if (newer == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if ((kt + 1) * 64 > K) {  // K tail: clear the slots past K that this thread's DMA filled
         glds_zero_tail<BM, AK>(kt * 64, K, cur, w, lane);
         glds_zero_tail<BN, BKM>(kt * 64, K, cur + TILE_A, w, lane);
       }
+    } else if (newer == 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
+    } else if (newer == 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LPT) : "memory");
     }
     __builtin_amdgcn_s_barrier();  // every wave's part of tile kt is in LDS
     asm volatile("" ::: "memory");
@@ -172,7 +188,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (kslice)
       partial_from_lds<BN>(tile, LDT, EPI_ROWS, m0 + pass * EPI_ROWS, n0, M, N, (float*)C + (long)blockIdx.z * M * N);
     else
-      epilogue_from_lds<BN>(ep, tile, LDT, EPI_ROWS, m0 + pass * EPI_ROWS, n0, M, N, C, ldc, 0, vec_ok != 0);
+      epilogue_tile<BN, EPI_ROWS, 256>(ep, tile, LDT, m0 + pass * EPI_ROWS, n0, M, N, C, ldc, vec_ok != 0);
     __syncthreads();
   }
 }

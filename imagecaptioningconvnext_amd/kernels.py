@@ -51,6 +51,11 @@ def record_gemms(recorder):
     _gemm_recorder = recorder
 
 
+def gemm_set_policy(glds256):
+    """-1 by shape (default), 0 never, 1 always use the 256x256 GEMM tile where eligible."""
+    _abi.call("imgcap_gemm_set_policy", int(glds256))
+
+
 def gemm_plan(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch=1, split_k=0):
     """(kernel kind, K slices) imgcap_gemm picks for these operands (IMGCAP_GEMM_* ids)."""
     sp = ctypes.c_int(1)

@@ -25,7 +25,7 @@ PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0
 
 _KIND_NAME = {1: "gemm_skinny_kernel", 2: "gemm_kernel<64,64,64>", 3: "gemm_kernel<128,128,64>",
-              4: "gemm_glds_kernel<128,128>"}
+              4: "gemm_glds_kernel<128,128>", 5: "gemm256_kernel<256,256>"}
 
 
 def time_launch(fn, reps=50, warm=5, graph=True):
@@ -70,7 +70,7 @@ def _gemm_groups(trainer, batch):
         kind, splits = K.gemm_plan(c["dtype"], c["ak"], c["bk"], c["M"], c["N"], c["K"], c["lda"], c["ldb"], 1,
                                    c["split_k"])
         name = _KIND_NAME.get(kind, f"gemm kind {kind}")
-        if kind in (2, 3, 4):
+        if kind in (2, 3, 4, 5):
             name += f"<ak={c['ak']},bk={c['bk']}>" + (" (split-K)" if splits > 1 else "")
         g = groups.setdefault(name, dict(name=name, calls=[], bound="mfma"))
         g["calls"].append(c)

@@ -39,6 +39,14 @@ def test_gemm_layouts(hip_device, dtype, tol, ta, tb, M, N, Kd):
     if dtype == torch.bfloat16:
         ref = a.bfloat16().float() @ b.bfloat16().float()
     assert _rel(out.cpu(), ref) < tol
+    if dtype == torch.bfloat16:  # the same product on the 256x256 tile (forced) and on the others
+        for pol in (1, 2, 3, 0):
+            K.gemm_set_policy(pol)
+            try:
+                out = K.gemm(ad, bd, trans_a=ta, trans_b=tb, out_dtype=torch.float32)
+            finally:
+                K.gemm_set_policy(-1)
+            assert _rel(out.cpu(), ref) < tol, pol
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
@@ -86,7 +94,16 @@ def test_gemm_auto_split_with_epilogue(hip_device, dtype, tol):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
-def test_gemm_epilogues(hip_device, dtype, tol):
+@pytest.mark.parametrize("policy", [-1, 1, 2])
+def test_gemm_epilogues(hip_device, dtype, tol, policy):
+    K.gemm_set_policy(policy)
+    try:
+        _gemm_epilogues(hip_device, dtype, tol)
+    finally:
+        K.gemm_set_policy(-1)
+
+
+def _gemm_epilogues(hip_device, dtype, tol):
     torch.manual_seed(0)
     M, N, Kd = 196, 96, 384
     x = torch.randn(M, Kd)

@@ -54,6 +54,31 @@ def gemms():
     gemm_case("lstm dh (skinny)", 32, 512, 3328, out_dtype=torch.float32)
 
 
+def gemm_probe():
+    for pol in (0, 1):
+        K.gemm_set_policy(pol)
+        print(f"-- policy glds256={pol}")
+        _gemm_probe()
+    for pol in (-1, 4, 5):
+        K.gemm_set_policy(pol)
+        print(f"-- policy {pol}: step shapes")
+        gemms()
+    K.gemm_set_policy(-1)
+
+
+def _gemm_probe():
+    """Where the time of a 128x128-tile GEMM goes at the encoder shapes: epilogue variants and K."""
+    M, N = 6272, 1536
+    for Kd in (384, 768, 1536, 3072):
+        gemm_case("probe act=none bf16", M, N, Kd)
+    gemm_case("probe act=gelu bf16", M, N, 384, act=K.ACT_GELU)
+    gemm_case("probe act=none f32", M, N, 384, out_dtype=torch.float32)
+    for Mx in (1568, 3136, 12544, 25088):
+        gemm_case("probe M sweep", Mx, N, 384)
+    gemm_case("probe square 4096", 4096, 4096, 4096)
+    gemm_case("probe square 8192", 8192, 8192, 8192, reps=5)
+
+
 def mlp():
     """Fused CNBlock MLP vs the two-GEMM form at the Tiny stage shapes (B=32)."""
     B = 32
@@ -133,6 +158,8 @@ if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "gemm"):
         gemms()
+    if which == "probe":
+        gemm_probe()
     if which in ("all", "misc"):
         misc()
     if which in ("all", "mlp"):
@@ -148,3 +175,56 @@ if __name__ == "__main__":
         for _ in range(5):
             K.dwconv7(x, w, b, y)
         torch.cuda.synchronize()
+
+
+def overlap():
+    """LSTM recurrence (fwd + bwd) and the frozen Tiny encoder forward (B=32), alone and on two
+    streams captured into one graph: how much of the encoder hides under the recurrence."""
+    import ctypes
+    from imagecaptioningconvnext_amd import _abi
+    from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    B, L, V = 32, 52, 9490
+    dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=dev,
+                               encoder_dim=768, dropout=0.5, compute_dtype=bf).to(dev)
+    enc = Encoder(variant="tiny", compute_dtype=bf).to(dev)
+    enc.fine_tune(False)
+    enc.train()
+    img = torch.randn(B, 3, 224, 224, device=dev)
+    eng = dec.engine()
+    feats = torch.randn(B, 7, 7, 768, device=dev).to(bf)
+    caps = torch.randint(1, V - 3, (B, L), device=dev)
+    lens = torch.full((B, 1), L, device=dev, dtype=torch.long)
+    s = eng.forward(feats, caps, lens, fixed_T=True)
+    eng.backward(s)
+    d = s["desc"]
+
+    def rec():
+        _abi.call("imgcap_lstm_tf_fwd", ctypes.byref(d), K.stream())
+        _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream())
+
+    def encf():
+        with torch.no_grad():
+            enc(img)
+    side = torch.cuda.Stream()
+    hi = torch.cuda.Stream(priority=-1)
+
+    def both(main=None):
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            encf()
+        rec()
+        cur.wait_stream(side)
+    t_r = time_launch(rec, reps=3, warm=1)
+    t_e = time_launch(encf, reps=3, warm=1)
+    t_b = time_launch(both, reps=3, warm=1)
+    print(f"overlap: recurrence {t_r * 1e6:.0f} us, encoder {t_e * 1e6:.0f} us, sum {(t_r + t_e) * 1e6:.0f} us, "
+          f"two streams {t_b * 1e6:.0f} us")
+    with torch.cuda.stream(hi):
+        t_h = time_launch(both, reps=3, warm=1)
+    print(f"overlap (recurrence on a high-priority stream): {t_h * 1e6:.0f} us")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "overlap":
+    overlap()
