@@ -46,6 +46,12 @@ class MhaDesc(ctypes.Structure):
         ("dv", c_void_p), ("lddq", c_int64), ("lddk", c_int64), ("lddv", c_int64)]
 
 
+class ColsumItem(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("out", c_void_p), ("ld", c_int64), ("rows", ctypes.c_int32),
+                ("cols", ctypes.c_int32), ("dtype", ctypes.c_int32), ("vec_ok", ctypes.c_int32),
+                ("beta", c_float)]
+
+
 # name -> argtypes  (every entry point declared in include/imgcap_abi.h)
 _SIGS = {
     "imgcap_version": [],
@@ -96,6 +102,7 @@ _SIGS = {
     "imgcap_adaptive_pool_bwd_nhwc": [c_int] * 7 + [c_void_p] * 3,
     "imgcap_lstm_denc": [c_int] * 4 + [c_void_p] * 6,
     "imgcap_gemm_set_policy": [c_int],
+    "imgcap_colsum_multi": [c_int, c_void_p, c_void_p],
     "imgcap_slice_reduce": [c_int64, c_int, c_void_p, c_int64, c_float, c_int64, c_void_p, c_void_p, c_void_p],
 }
 

@@ -18,7 +18,7 @@
 namespace imgcap {
 
 #ifndef MLP_GELU
-#define MLP_GELU 0
+#define MLP_GELU 2  // packed polynomial erf (|err| <= 1.5e-7, common.h gelu_fast2); 0 = libm erff
 #endif
 #ifndef MLP_TAG
 #define MLP_TAG "erf"

@@ -370,10 +370,10 @@ extern "C" int imgcap_ln_patchify2_bwd(int dtype, int B, int H, int W, int C, co
   else
     hipLaunchKernelGGL(ln_patchify2_bwd_kernel<float>, dim3(blocks), dim3(256), shm, st, B, H, W, C, (const float*)x,
                        (const float*)dpatches, ln_w, (float*)dx, ws, ppw, cmajor);
-  hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((2 * C + 255) / 256)), dim3(256), 0, st, 2L * C, blocks,
-                     ws, 2L * C, 0.f, (long)C, dln_w, dln_b);
   IMGCAP_CHECK_LAUNCH("imgcap_ln_patchify2_bwd");
-  return 0;
+  imgcap_colsum_item it[2] = {{ws, dln_w, 2L * C, blocks, C, IMGCAP_F32, 0, 0.f},
+                              {ws + C, dln_b, 2L * C, blocks, C, IMGCAP_F32, 0, 0.f}};
+  return imgcap_colsum_multi(2, it, stream);
 }
 
 extern "C" int imgcap_adaptive_pool_bwd_nhwc(int dtype, int B, int H, int W, int C, int OH, int OW, const void* dy,

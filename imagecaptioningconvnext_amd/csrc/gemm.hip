@@ -436,7 +436,7 @@ static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, lon
     // the 256 tile wins only with >= ~1.5 rounds of tiles over the CUs and long K (measured:
     // tools/microbench.py probe); below that the 2-blocks-per-CU 128 tile overlaps better
     const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-    if ((mode >= 1 && mode <= 3) || (mode < 0 && tiles256 >= 384 && K >= 512)) return {IMGCAP_GEMM_GLDS256, 1};
+    if ((mode >= 1 && mode <= 3) || (mode < 0 && tiles256 >= 384 && K >= 1024)) return {IMGCAP_GEMM_GLDS256, 1};
   }
   const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   const auto auto_split = [&] {
@@ -498,7 +498,7 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       dim3 grid((N + 255) / 256, (M + 255) / 256);
       const bf16* a = (const bf16*)A;
       const bf16* b = (const bf16*)B;
-      const int var = gemm256_mode() >= 1 ? gemm256_mode() : 2;  // 1: BK 64 x 2 stages, 2: BK 32 x 4, 3: BK 32 x 3
+      const int var = gemm256_mode() >= 1 ? gemm256_mode() : 1;  // 1: BK 64 x 2 stages, 2: BK 32 x 4, 3: BK 32 x 3
 #define G256_V(AKV, BKV, BKT, SV)                                                                               \
   hipLaunchKernelGGL((gemm256_kernel<BKT, SV, AKV, BKV>), grid, dim3(512), 0, st, a, lda, b, ldb, C, ldc, M, N, K, \
                      ep, vec_ok, g_seed_ctr, 0)
@@ -635,6 +635,77 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(int cols, int slices
   }
 }
 
+// ---- many column sums in one launch (the bias gradients of a whole backward pass) ----------
+// Block = (item, 64-column group): 8 column vectors x 32 row lanes walk ALL rows of the item
+// (8 rows in flight per lane), fixed-order LDS reduction, out = beta*out + sum.
+constexpr int COLSUM_MAX_ITEMS = 64;
+struct ColsumBatch {
+  int n;
+  int first_block[COLSUM_MAX_ITEMS + 1];
+  imgcap_colsum_item it[COLSUM_MAX_ITEMS];
+};
+
+__global__ __launch_bounds__(256) void colsum_multi_kernel(ColsumBatch b) {
+  __shared__ float red[32][65];
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.first_block[k + 1]) ++k;
+  const imgcap_colsum_item& item = b.it[k];
+  const int cg = blockIdx.x - b.first_block[k];
+  const int cv = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = cg * 64 + cv * 8;
+  const bool vec = item.vec_ok && c0 + 8 <= item.cols;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (c0 < item.cols) {
+    constexpr int U = 8;  // rows in flight per lane
+    int r = rl;
+    if (item.dtype == IMGCAP_BF16) {
+      const bf16* x = (const bf16*)item.x;
+      for (; vec && r + 32 * (U - 1) < item.rows; r += 32 * U) {
+        bf16x8 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *(const bf16x8*)(x + (long)(r + 32 * u) * item.ld + c0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += (float)v[u][j];
+      }
+      for (; r < item.rows; r += 32)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (c0 + j < item.cols) s[j] += (float)x[(long)r * item.ld + c0 + j];
+    } else {
+      const float* x = (const float*)item.x;
+      for (; vec && r + 32 * (U - 1) < item.rows; r += 32 * U) {
+        f32x4 v[U][2];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          v[u][0] = *(const f32x4*)(x + (long)(r + 32 * u) * item.ld + c0);
+          v[u][1] = *(const f32x4*)(x + (long)(r + 32 * u) * item.ld + c0 + 4);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { s[j] += v[u][0][j]; s[j + 4] += v[u][1][j]; }
+      }
+      for (; r < item.rows; r += 32)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (c0 + j < item.cols) s[j] += x[(long)r * item.ld + c0 + j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cv * 8 + j] = s[j];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = cg * 64 + threadIdx.x;
+    float t = 0.f;
+    for (int i = 0; i < 32; ++i) t += red[i][threadIdx.x];
+    if (c < item.cols) item.out[c] = (item.beta != 0.f ? item.beta * item.out[c] : 0.f) + t;
+  }
+}
+
 // out[c][r] = in[r][c] (2-D transpose through an LDS tile; weights -> k-major copies)
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(int rows, int cols, const T* __restrict__ in, long ldi,
@@ -755,3 +826,23 @@ extern "C" int imgcap_debug_stamps(void* p) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_dev_stamps), &v, sizeof(v));
 }
 #endif
+
+extern "C" int imgcap_colsum_multi(int n, const imgcap_colsum_item* items, void* stream) {
+  IMGCAP_REQUIRE(n >= 0 && n <= COLSUM_MAX_ITEMS, "imgcap_colsum_multi: at most 64 items per call");
+  if (n == 0) return 0;
+  ColsumBatch b{};
+  b.n = n;
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    b.it[i] = items[i];
+    b.it[i].vec_ok = aligned16(items[i].x) && (items[i].dtype == IMGCAP_BF16 ? items[i].ld % 8 == 0
+                                                                               : items[i].ld % 4 == 0);
+    b.first_block[i] = blocks;
+    blocks += (items[i].cols + 63) / 64;
+  }
+  b.first_block[n] = blocks;
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(colsum_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
+  IMGCAP_CHECK_LAUNCH("imgcap_colsum_multi");
+  return 0;
+}

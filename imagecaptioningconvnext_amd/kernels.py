@@ -4,6 +4,7 @@ All functions enqueue on ``torch.cuda.current_stream()``; none allocates unless 
 return a fresh output.  Inputs must already live on the GPU; there is no CPU path.
 """
 import ctypes
+import os
 
 import torch
 
@@ -145,6 +146,29 @@ def colsum(x, out, beta=0.0, rows=None, cols=None, ld=None):
     return out
 
 
+class ColsumBatch:
+    """Deferred bias gradients: ``add`` records colsum(x) -> out (x kept alive), ``run`` issues
+    them as ONE imgcap_colsum_multi launch per 64 items (instead of 1-2 launches each)."""
+
+    def __init__(self):
+        self.items = []
+
+    def add(self, x, out, cols=None, rows=None, ld=None, beta=0.0):
+        _check_dev(x, out)
+        self.items.append((x, out, x.shape[0] if rows is None else rows, x.shape[1] if cols is None else cols,
+                           x.stride(0) if ld is None else ld, beta))
+
+    def run(self):
+        for i0 in range(0, len(self.items), 64):
+            chunk = self.items[i0:i0 + 64]
+            arr = (_abi.ColsumItem * len(chunk))()
+            for a, (x, out, rows, cols, ld, beta) in zip(arr, chunk):
+                a.x, a.out, a.ld, a.rows, a.cols, a.dtype, a.beta = x.data_ptr(), out.data_ptr(), ld, rows, cols, \
+                    dt(x), beta
+            _abi.call("imgcap_colsum_multi", len(chunk), ctypes.cast(arr, ctypes.c_void_p), stream())
+        self.items = []
+
+
 def add_layernorm(x, r, gamma, beta, eps, *, drop_p=0.0, seed=0, drop_stream=0, s_out=None, y=None):
     rows, cols = x.shape
     y = torch.empty_like(x) if y is None else y
@@ -271,7 +295,9 @@ def set_seed_counter(counter):
     _abi.call("imgcap_set_seed_counter", ptr(counter))
 
 
-CNBLOCK_MLP_CHANNELS = (96, 128, 192)
+# widths served by the fused CNBlock MLP kernel (the others run LN + two GEMMs); IMGCAP_FUSED_MLP_C
+# overrides for A/B runs ("96,128")
+CNBLOCK_MLP_CHANNELS = tuple(int(c) for c in os.environ.get("IMGCAP_FUSED_MLP_C", "96,128,192").split(",") if c)
 
 
 def cnblock_mlp(z, w1, b1, w2, b2, gamma, x, sd=None, rows_per_sample=1, ln_w=None, ln_b=None):

@@ -179,11 +179,12 @@ class TransformerEngine:
         BL, BP = B * L, B * P
         dev = s["xL"].device
         gbuf.zero_()
+        cb = K.ColsumBatch()  # every bias gradient, reduced in one launch at the end
         if dlogits is None:
             dlogits = torch.empty(BL, self.Vpad, device=dev, dtype=ct)
             K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
         K.gemm(dlogits, s["xL"], trans_a=True, out=G("fc_out.weight"), M=V, **DW)
-        K.colsum(dlogits, G("fc_out.bias"), cols=V)
+        cb.add(dlogits, G("fc_out.bias"), cols=V)
         dx = K.gemm(dlogits, fp.w("fc_out.weight"), K=V)                    # [BL, d]
         dmem = torch.zeros(BP, d, device=dev, dtype=torch.float32)
         for i in reversed(range(self.layers)):
@@ -196,10 +197,10 @@ class TransformerEngine:
                                       drop_stream=_s(i, 5), dr=dy3)
             # y3 = hdn W2^T + b2 ; hdn = drop(relu(x2 W1^T + b1))
             K.gemm(dy3, st["hdn"], trans_a=True, out=G(lw("linear2.weight")), **DW)
-            K.colsum(dy3, G(lw("linear2.bias")))
+            cb.add(dy3, G(lw("linear2.bias")))
             dpre = K.gemm(dy3, fp.w(lw("linear2.weight")), aux=st["hdn"], aux_scale=1.0 / (1.0 - p))
             K.gemm(dpre, st["x2"], trans_a=True, out=G(lw("linear1.weight")), **DW)
-            K.colsum(dpre, G(lw("linear1.bias")))
+            cb.add(dpre, G(lw("linear1.bias")))
             K.gemm(dpre, fp.w(lw("linear1.weight")), out=ds3, beta=1.0)      # dx2 = ds3 + dpre W1
             # x2 = LN2(x1 + drop(y2))
             dy2 = torch.empty_like(dx)
@@ -207,7 +208,7 @@ class TransformerEngine:
                                       G(lw("norm2.weight")), G(lw("norm2.bias")), drop_p=p, seed=seed,
                                       drop_stream=_s(i, 3), dr=dy2)
             K.gemm(dy2, st["o2"], trans_a=True, out=G(lw("multihead_attn.out_proj.weight")), **DW)
-            K.colsum(dy2, G(lw("multihead_attn.out_proj.bias")))
+            cb.add(dy2, G(lw("multihead_attn.out_proj.bias")))
             do2 = K.gemm(dy2, fp.w(lw("multihead_attn.out_proj.weight")))
             dq2 = torch.empty(BL, d, device=dev, dtype=ct)
             dkv2 = torch.empty(BP, 2 * d, device=dev, dtype=ct)
@@ -219,9 +220,9 @@ class TransformerEngine:
             gb = G(lw("multihead_attn.in_proj_bias"))
             wq = fp.w(lw("multihead_attn.in_proj_weight"))
             K.gemm(dq2, st["x1"], trans_a=True, out=gw[:d], **DW)
-            K.colsum(dq2, gb[:d])
+            cb.add(dq2, gb[:d])
             K.gemm(dkv2, s["mem"], trans_a=True, out=gw[d:], **DW)
-            K.colsum(dkv2, gb[d:])
+            cb.add(dkv2, gb[d:])
             K.gemm(dkv2, wq[d:], out=dmem, beta=1.0)                          # dmem += dkv2 W_kv
             K.gemm(dq2, wq[:d], out=ds2, beta=1.0)                            # dx1 = ds2 + dq2 W_q
             # x1 = LN1(x + drop(y))
@@ -230,7 +231,7 @@ class TransformerEngine:
                                       G(lw("norm1.weight")), G(lw("norm1.bias")), drop_p=p, seed=seed,
                                       drop_stream=_s(i, 1), dr=dy)
             K.gemm(dy, st["o"], trans_a=True, out=G(lw("self_attn.out_proj.weight")), **DW)
-            K.colsum(dy, G(lw("self_attn.out_proj.bias")))
+            cb.add(dy, G(lw("self_attn.out_proj.bias")))
             do = K.gemm(dy, fp.w(lw("self_attn.out_proj.weight")))
             dqkv = torch.empty(BL, 3 * d, device=dev, dtype=ct)
             qkv = st["qkv"]
@@ -239,7 +240,7 @@ class TransformerEngine:
                       seed=seed, sid=_s(i, 0), dout=do, lddo=d, dq=dqkv, lddq=3 * d, dk=dqkv[:, d:], lddk=3 * d,
                       dv=dqkv[:, 2 * d:], lddv=3 * d, bwd=True)
             K.gemm(dqkv, st["x"], trans_a=True, out=G(lw("self_attn.in_proj_weight")), **DW)
-            K.colsum(dqkv, G(lw("self_attn.in_proj_bias")))
+            cb.add(dqkv, G(lw("self_attn.in_proj_bias")))
             K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
             dx = ds1
         # embedding (dropout mask recomputed; PE has no parameters)
@@ -248,10 +249,11 @@ class TransformerEngine:
         if self.has_proj:
             dmem_c = dmem.to(ct)
             K.gemm(dmem_c, s["enc"].view(BP, self.E), trans_a=True, out=G("encoder_proj.weight"), **DW)
-            K.colsum(dmem, G("encoder_proj.bias"))
+            cb.add(dmem, G("encoder_proj.bias"))
             if want_denc:
                 denc = K.gemm(dmem_c, fp.w("encoder_proj.weight")).view(B, P, self.E)
         elif want_denc:
             denc = dmem.to(ct).view(B, P, d)
+        cb.run()
         s["denc"] = denc
         return gbuf

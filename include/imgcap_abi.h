@@ -99,6 +99,17 @@ int imgcap_gemm_set_policy(int glds256);
 int imgcap_transpose(int dtype, int rows, int cols, const void* in, int64_t ldi, void* out, int64_t ldo,
                      void* stream);
 
+/* Many column sums in one launch: out_i = beta_i*out_i + colsum(x_i)  (the bias gradients of a
+ * whole backward pass, deferred to its end; <= 64 items per call; vec_ok is set by the library) */
+typedef struct imgcap_colsum_item {
+  const void* x;      /* [rows, ld] of dtype */
+  float* out;         /* [cols] fp32 */
+  int64_t ld;
+  int32_t rows, cols, dtype, vec_ok;
+  float beta;
+} imgcap_colsum_item;
+int imgcap_colsum_multi(int n, const imgcap_colsum_item* items, void* stream);
+
 /* column sums of a [rows, cols] matrix into fp32 out[cols] (bias gradients); beta=1 accumulates */
 int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64_t ldx, float* out, float beta,
                   void* stream);
