@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run encoder and decoder of a step back to back (no two-stream overlap)")
     return ap.parse_args()
 
 
@@ -156,7 +158,11 @@ def main():
     torch.manual_seed(42 + rank)
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
     enc, dec = build(cfg, device)
-    trainer = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm", graph=not args.no_graph)
+    # frozen encoder: its forward for batch i+1 overlaps the decoder step of batch i (two
+    # streams in one graph); every timed step still does one encoder + one decoder pass
+    pipeline = not args.no_pipeline and "starting_layer" not in cfg
+    trainer = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm", graph=not args.no_graph,
+                                   pipeline=pipeline)
     B = cfg["batch"]
     batches = [synthetic_batch(B, rank, i, device) for i in range(4)]
     for i in range(args.warmup):
@@ -196,6 +202,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
+            "pipeline": "encoder(batch i+1) || decoder fwd/bwd(batch i), two HIP streams in one graph"
+                        if pipeline else "sequential",
             "data": "synthetic (224x224x3 U[0,1) ImageNet-normalised, random captions len 52), random-init weights",
             "config": {"workload": f"{args.config}: ConvNeXt-{cfg['encoder'].capitalize()} "
                                    f"({'fine-tuned from child %d' % cfg['starting_layer'] if 'starting_layer' in cfg else 'frozen'}) + "

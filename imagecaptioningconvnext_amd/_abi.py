@@ -102,6 +102,7 @@ _SIGS = {
     "imgcap_adaptive_pool_bwd_nhwc": [c_int] * 7 + [c_void_p] * 3,
     "imgcap_lstm_denc": [c_int] * 4 + [c_void_p] * 6,
     "imgcap_gemm_set_policy": [c_int],
+    "imgcap_workspace_slot": [c_int],
     "imgcap_colsum_multi": [c_int, c_void_p, c_void_p],
     "imgcap_slice_reduce": [c_int64, c_int, c_void_p, c_int64, c_float, c_int64, c_void_p, c_void_p, c_void_p],
 }

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <mutex>
 #include <vector>
 #include <string>
 
@@ -17,20 +18,34 @@ int fail(int code, const std::string& msg) {
 }
 const uint64_t* g_seed_ctr = nullptr;
 
-// Scratch for split reductions (GEMM split-K partials, colsum row slices).  Kernels on one
-// stream use it one after another.  A grown buffer never frees the old one: a captured HIP
-// graph may still reference it.
+// Scratch for split reductions (GEMM split-K partials, colsum / LayerNorm-gradient slices).
+// Two slots: work that may run concurrently on another stream (the trainer's encoder beside
+// the decoder) selects slot 1 with imgcap_workspace_slot; kernels of one slot run one after
+// another.  Grow-only (a captured HIP graph may reference a buffer, and no allocation may
+// happen during capture: warm-up runs size them), a grown buffer never frees the old one.
+struct Ws {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+static std::mutex g_ws_mu;
+static Ws g_ws[2];
 static std::vector<void*> g_ws_retired;
-static void* g_ws = nullptr;
-static size_t g_ws_bytes = 0;
-void* workspace(size_t bytes) {
-  if (bytes <= g_ws_bytes) return g_ws;
+static thread_local int g_ws_slot = 0;
+int set_workspace_slot(int slot) {
+  const int prev = g_ws_slot;
+  g_ws_slot = slot;
+  return prev;
+}
+void* workspace(size_t bytes, hipStream_t) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  Ws& w = g_ws[g_ws_slot];
+  if (bytes <= w.bytes) return w.p;
   size_t sz = std::max(bytes, (size_t)16 << 20);
   void* p = nullptr;
   if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
-  if (g_ws) g_ws_retired.push_back(g_ws);
-  g_ws = p;
-  g_ws_bytes = sz;
+  if (w.p) g_ws_retired.push_back(w.p);
+  w.p = p;
+  w.bytes = sz;
   return p;
 }
 }  // namespace imgcap
@@ -42,3 +57,9 @@ extern "C" int imgcap_set_seed_counter(const uint64_t* counter) {
 
 extern "C" const char* imgcap_last_error_string(void) { return imgcap::g_last_error.c_str(); }
 extern "C" int imgcap_version(void) { return 1; }
+
+extern "C" int imgcap_workspace_slot(int slot) {
+  if (slot < 0 || slot > 1) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_slot: 0 or 1");
+  imgcap::set_workspace_slot(slot);
+  return IMGCAP_OK;
+}

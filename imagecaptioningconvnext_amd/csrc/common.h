@@ -21,8 +21,9 @@ namespace imgcap {
 // ---- error plumbing (host) -------------------------------------------------------------
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
-// process-wide device scratch of at least `bytes` (NULL on allocation failure); see abi.cpp
-void* workspace(size_t bytes);
+// device scratch of at least `bytes` from the calling thread's current slot (NULL on
+// allocation failure); abi.cpp
+void* workspace(size_t bytes, hipStream_t stream);
 
 #define IMGCAP_CHECK_LAUNCH(what)                                                   \
   do {                                                                             \

@@ -302,7 +302,7 @@ extern "C" int imgcap_dwconv7_wgrad(int dtype, int B, int H, int W, int C, const
   const long waves_wanted = std::max<long>(1, std::min<long>(R, (512 / cblocks) * 4));
   const int rpw = (int)((R + waves_wanted - 1) / waves_wanted);
   const int slices = (int)((R + 4L * rpw - 1) / (4L * rpw));
-  float* ws = (float*)workspace((size_t)slices * C * 50 * sizeof(float));
+  float* ws = (float*)workspace((size_t)slices * C * 50 * sizeof(float), (hipStream_t)stream);
   if (!ws) return fail(IMGCAP_EINVAL, "imgcap_dwconv7_wgrad: workspace allocation failed");
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid(cblocks, slices);
@@ -360,7 +360,7 @@ extern "C" int imgcap_ln_patchify2_bwd(int dtype, int B, int H, int W, int C, co
   if (NPX == 0) return 0;
   const int ppw = (int)std::max<long>(1, (NPX + 4 * 512 - 1) / (4 * 512));
   const int blocks = (int)((NPX + 4L * ppw - 1) / (4L * ppw));
-  float* ws = (float*)workspace((size_t)blocks * 2 * C * sizeof(float));
+  float* ws = (float*)workspace((size_t)blocks * 2 * C * sizeof(float), (hipStream_t)stream);
   if (!ws) return fail(IMGCAP_EINVAL, "imgcap_ln_patchify2_bwd: workspace allocation failed");
   hipStream_t st = (hipStream_t)stream;
   const size_t shm = (size_t)8 * C * sizeof(float);

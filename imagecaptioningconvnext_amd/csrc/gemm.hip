@@ -523,7 +523,7 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       const int zdim = sk > 1 ? (K + kslice - 1) / kslice : 1;
       void* Cdst = C;
       if (sk > 1) {
-        Cdst = workspace((size_t)zdim * M * N * sizeof(float));
+        Cdst = workspace((size_t)zdim * M * N * sizeof(float), st);
         if (!Cdst) return fail(IMGCAP_EINVAL, "imgcap_gemm: split-K workspace allocation failed");
       }
       dim3 grid((N + 127) / 128, (M + 127) / 128, zdim);
@@ -782,7 +782,7 @@ extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64
   slices = rows > 0 ? (rows + rps - 1) / rps : 1;
   float* dst = out;
   if (slices > 1) {
-    dst = (float*)workspace((size_t)slices * cols * sizeof(float));
+    dst = (float*)workspace((size_t)slices * cols * sizeof(float), (hipStream_t)stream);
     if (!dst) return fail(IMGCAP_EINVAL, "imgcap_colsum: workspace allocation failed");
   }
   const dim3 grid(cblocks, slices);

@@ -219,7 +219,7 @@ static int launch_tiled(int ak, int bk, int M, int N, int K, const void* A, long
   const int zdim = split > 1 ? (K + kslice - 1) / kslice : batch;
   void* Cout = C;
   if (split > 1) {
-    C = workspace((size_t)zdim * M * N * sizeof(float));
+    C = workspace((size_t)zdim * M * N * sizeof(float), st);
     if (!C) return fail(IMGCAP_EINVAL, "imgcap_gemm: split-K workspace allocation failed");
   }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, zdim);

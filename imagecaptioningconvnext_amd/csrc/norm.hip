@@ -204,7 +204,7 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
   hipStream_t st = (hipStream_t)stream;
   float* ws = nullptr;
   if (dgamma || dbeta) {
-    ws = (float*)workspace((size_t)nblk * 2 * cols * sizeof(float));
+    ws = (float*)workspace((size_t)nblk * 2 * cols * sizeof(float), st);
     if (!ws) return fail(IMGCAP_EINVAL, "imgcap_add_layernorm_bwd: workspace allocation failed");
   }
 #define LNB_(T, G)                                                                                              \

@@ -52,6 +52,20 @@ def record_gemms(recorder):
     _gemm_recorder = recorder
 
 
+class workspace_slot:
+    """Context manager: library scratch slot 1 for work that runs beside slot-0 work on another
+    stream (imgcap_workspace_slot)."""
+
+    def __init__(self, slot=1):
+        self.slot = slot
+
+    def __enter__(self):
+        _abi.call("imgcap_workspace_slot", self.slot)
+
+    def __exit__(self, *a):
+        _abi.call("imgcap_workspace_slot", 0)
+
+
 def gemm_set_policy(glds256):
     """-1 by shape (default), 0 never, 1 always use the 256x256 GEMM tile where eligible."""
     _abi.call("imgcap_gemm_set_policy", int(glds256))

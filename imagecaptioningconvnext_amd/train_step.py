@@ -30,7 +30,7 @@ def _trainable(encoder):
 
 class TeacherForcedTrainer:
     def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, encoder_lr=1e-4, grad_clip=5.0, alphaC=1.0,
-                 pad_id=0, process_group=None, graph=False):
+                 pad_id=0, process_group=None, graph=False, pipeline=False):
         self.encoder = encoder
         self.decoder = decoder
         self.lstm = lstm
@@ -45,6 +45,12 @@ class TeacherForcedTrainer:
         self._metric_log = []
         self.graph = graph
         self._graph = None
+        # pipeline: the frozen encoder's forward of batch i runs on a second stream beside the
+        # decoder forward/backward of batch i-1 (the LSTM recurrence leaves most CUs idle);
+        # step(i) returns the metrics of batch i-1 and flush() finishes the last batch.  The
+        # parameter updates are exactly the sequential ones (the encoder is frozen).
+        self.pipeline = pipeline
+        self._pipe = None
         if self.world > 1:
             # DDP construction broadcasts rank 0's parameters (trainMultiGPU.py:233); the encoder is
             # broadcast too because its weights are randomly initialised here (SURVEY.md §7 v)
@@ -60,8 +66,15 @@ class TeacherForcedTrainer:
         """train.py:160-166: from this step on, children[startingLayer:] of the encoder train
         with their own Adam (encoder_lr); the captured graph is rebuilt on the next step."""
         self.encoder.fine_tune(fine_tune=True, startingLayer=startingLayer)
+        self.flush()
         self.enc_eng = self.encoder.engine() if _trainable(self.encoder) else None
         self._graph = None
+        self._pipe = None
+
+    def _encode(self, imgs):
+        self.encoder.train()
+        with torch.no_grad(), K.workspace_slot(1 if self.pipeline else 0):
+            return self.encoder(imgs)
 
     def _fwd_bwd(self, imgs, caps, caplens):
         self.encoder.train()
@@ -70,8 +83,11 @@ class TeacherForcedTrainer:
         if self.enc_eng is not None:
             feats, es = self.enc_eng.forward(imgs)
         else:
-            with torch.no_grad():
-                feats = self.encoder(imgs)
+            feats = self._encode(imgs)
+        return self._dec(feats, caps, caplens, es)
+
+    def _dec(self, feats, caps, caplens, es=None):
+        self.decoder.train()
         if self.lstm:
             s = self.eng.forward(feats, caps, caplens, fixed_T=True, alphaC=self.alphaC)
         else:
@@ -100,7 +116,94 @@ class TeacherForcedTrainer:
             self._metrics = self._fwd_bwd(*self._inputs)
         self._graph = g
 
+    # ---- encoder / decoder pipeline ------------------------------------------------------------
+    def _pipe_capture(self, imgs, caps, caplens, warmup=2):
+        dev = imgs.device
+        self._seed_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        K.set_seed_counter(self._seed_ctr)
+        side = torch.cuda.Stream(device=dev)
+        main = torch.cuda.current_stream(dev)
+        P = dict(side=side, i=0, img=imgs.clone(), caps=[caps.clone(), caps.clone()],
+                 lens=[caplens.clone(), caplens.clone()])
+        side.wait_stream(main)
+        with torch.cuda.stream(side):  # first-touch allocations and one-time kernel setup
+            for _ in range(warmup):
+                f = self._encode(P["img"])
+                self._dec(f, P["caps"][0], P["lens"][0])
+        main.wait_stream(side)
+        P["feats"] = [torch.empty_like(f), torch.empty_like(f)]
+        P["graphs"], P["metrics"] = [], []
+        pool = None
+        for k in (0, 1):  # graph k: encode the new batch into slot k, train on slot 1-k
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self._seed_ctr.add_(1)
+                cur = torch.cuda.current_stream(dev)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    P["feats"][k].copy_(self._encode(P["img"]))
+                m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k])
+                cur.wait_stream(side)
+            pool = g.pool()
+            P["graphs"].append(g)
+            P["metrics"].append(m)
+        self._pipe = P
+
+    def _pipe_step(self, imgs, caps, caplens):
+        """Returns the metrics tensor of the previous batch (None on the first call)."""
+        if not self.graph:
+            main = torch.cuda.current_stream()
+            if self._pipe is None:
+                self._pipe = dict(side=torch.cuda.Stream(device=imgs.device), pending=None)
+            P = self._pipe
+            P["side"].wait_stream(main)
+            with torch.cuda.stream(P["side"]):
+                feats = self._encode(imgs)
+            m = self._dec(*P["pending"]) if P["pending"] is not None else None
+            main.wait_stream(P["side"])
+            feats.record_stream(main)
+            P["pending"] = (feats, caps, caplens)
+            return m
+        if self._pipe is None:
+            self._pipe_capture(imgs, caps, caplens)
+        P = self._pipe
+        k = P["i"] % 2
+        for dst, src in ((P["img"], imgs), (P["caps"][k], caps), (P["lens"][k], caplens)):
+            if dst.shape != src.shape:
+                raise ValueError("graph mode needs a fixed batch shape; got %s, captured %s"
+                                 % (tuple(src.shape), tuple(dst.shape)))
+            dst.copy_(src, non_blocking=True)
+        m = None
+        if P["i"] == 0:
+            P["feats"][k].copy_(self._encode(P["img"]))
+        else:
+            P["graphs"][k].replay()
+            m = P["metrics"][k]
+        P["i"] += 1
+        return m
+
+    def flush(self):
+        """Pipeline mode: train on the last batch handed to step() (no-op otherwise)."""
+        P = self._pipe
+        if not self.pipeline or P is None:
+            return None
+        if not self.graph:
+            if P["pending"] is None:
+                return None
+            m = self._dec(*P["pending"])
+            P["pending"] = None
+        else:
+            if P["i"] == 0:
+                return None
+            j = (P["i"] - 1) % 2
+            m = self._dec(P["feats"][j], P["caps"][j], P["lens"][j])
+            P["i"] = 0
+        return self._update(m)
+
     def step(self, imgs, caps, caplens):
+        if self.pipeline and self.enc_eng is None:
+            m = self._pipe_step(imgs, caps, caplens)
+            return None if m is None else self._update(m)
         if not self.graph:
             m = self._fwd_bwd(imgs, caps, caplens)
         else:
@@ -114,6 +217,10 @@ class TeacherForcedTrainer:
                     dst.copy_(src, non_blocking=True)
             self._graph.replay()
             m = self._metrics
+        return self._update(m)
+
+    def _update(self, m):
+        """DDP gradient average, clip + Adam, metric reduction (trainMultiGPU.py:384-403)."""
         fp = self.eng.fp
         if self.world > 1:
             dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=self.pg)

@@ -31,6 +31,9 @@ enum { IMGCAP_OK = 0, IMGCAP_EINVAL = -1, IMGCAP_EUNSUPPORTED = -2 };
 enum { IMGCAP_ACT_NONE = 0, IMGCAP_ACT_GELU = 1, IMGCAP_ACT_RELU = 2, IMGCAP_ACT_DGELU = 3 };
 
 const char* imgcap_last_error_string(void);
+/* Split-reduction scratch slot (0 default, 1) of the calling thread: calls whose kernels may
+ * run concurrently with slot-0 work on another stream (the trainer's encoder pipeline) use 1. */
+int imgcap_workspace_slot(int slot);
 int imgcap_version(void);
 
 /* Device-resident step counter mixed into every dropout / stochastic-depth seed at kernel

@@ -85,3 +85,28 @@ def test_trainer_ddp2_hip_matches_reference_trainMultiGPU(hip_device, tmp_path):
     trainMultiGPU step (tests/golden/ddp2_lstm)."""
     import ddp_util
     ddp_util.check(ddp_util.run("hip", tmp_path))
+
+
+@pytest.mark.parametrize("decoder", ["lstm", "transformer"])
+@pytest.mark.parametrize("graph", [False, True])
+def test_pipelined_trainer_matches_sequential(hip_device, decoder, graph):
+    """pipeline=True runs the frozen encoder of batch i on a second stream beside the decoder
+    step of batch i-1: the metrics (one step late) and the parameter updates must be exactly
+    those of the sequential trainer."""
+    from imagecaptioningconvnext_amd import kernels as K
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    runs = []
+    for pipe in (False, True):
+        enc, dec = _models(hip_device, decoder, dropout=0.0, sd_off=True)
+        tr = TeacherForcedTrainer(enc, dec, lstm=decoder == "lstm", graph=graph, pipeline=pipe)
+        outs = [tr.step(*_batch(hip_device, i)) for i in range(4)]
+        if pipe:
+            assert outs[0] is None
+            tr.flush()
+        runs.append((tr.drain_metrics(), tr.eng.fp.flat.clone()))
+        K.set_seed_counter(None)
+    (m_s, p_s), (m_p, p_p) = runs
+    assert len(m_s) == len(m_p) == 4
+    for a, b in zip(m_s, m_p):
+        assert abs(a[0] - b[0]) < 1e-5 * abs(a[0]) and a[1] == b[1] and abs(a[2] - b[2]) < 1e-3
+    torch.testing.assert_close(p_p, p_s, rtol=1e-5, atol=5e-6)
