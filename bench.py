@@ -189,7 +189,7 @@ def main():
     fpi = flops_per_image(cfg, enc)
     if rank == 0:
         from imagecaptioningconvnext_amd import roofline
-        roof = roofline.measure(cfg, trainer, batches[0])
+        roof = roofline.measure(cfg, trainer, batches[0], cfgname=args.config)
         out = {
             "metric": "images/sec (train step, teacher-forced)",
             "value": round(imgs_per_s, 2),

@@ -72,17 +72,23 @@ def _gemm_groups(trainer, batch):
         name = _KIND_NAME.get(kind, f"gemm kind {kind}")
         if kind in (2, 3, 4, 5):
             name += f"<ak={c['ak']},bk={c['bk']}>" + (" (split-K)" if splits > 1 else "")
-        g = groups.setdefault(name, dict(name=name, calls=[], bound="mfma"))
+        tf = lambda v: "true" if v else "false"  # noqa: E731
+        sym = {4: f"gemm_glds_kernel<128, 128, {tf(c['ak'])}, {tf(c['bk'])}, 2>",
+               5: f"gemm256_kernel<64, 2, {tf(c['ak'])}, {tf(c['bk'])}>"}.get(kind, _KIND_NAME.get(kind, ""))
+        g = groups.setdefault(name, dict(name=name, calls=[], bound="mfma", symbol=sym))
         g["calls"].append(c)
     out = []
     for g in groups.values():
-        t_tot, f_tot = 0.0, 0.0
+        t_tot, f_tot, b_tot = 0.0, 0.0, 0.0
         for c in g["calls"]:
             t_tot += time_launch(c["call"], reps=20, warm=2)
             f_tot += 2.0 * c["M"] * c["N"] * c["K"]
+            cb = 4 if c["keep"][-1].c_dtype == 0 else 2
+            b_tot += 2.0 * (c["M"] + c["N"]) * c["K"] + cb * c["M"] * c["N"]  # A + B read, C written once
         n = len(g["calls"])
         shapes = sorted({(c["M"], c["N"], c["K"]) for c in g["calls"]})
-        out.append(dict(name=g["name"], bound="mfma", per_step=n, t=t_tot / n, flops=f_tot / n,
+        out.append(dict(name=g["name"], bound="mfma", per_step=n, t=t_tot / n, flops=f_tot / n, symbol=g["symbol"],
+                        bytes=b_tot / n,
                         note=f"{n} launches/step, shapes (M,N,K) {shapes[:6]}{' ...' if len(shapes) > 6 else ''}"))
     return out
 
@@ -108,19 +114,40 @@ def _encoder_groups(trainer, B, dev):
                 K.cnblock_mlp(z, blk["w1"], blk["b1"], blk["w2"], blk["b2"], blk["gamma"], x2, ln_w=blk["lnw"],
                               ln_b=blk["lnb"])
             out.append(dict(name=f"cnblock_mlp_kernel<{C}> (stage {st + 1} fused MLP)", bound="mfma",
+                            symbol=f"cnblock_mlp_kernel<{C},", bytes=3.0 * M * C * 2 + 2 * 4 * C * C * 2,
                             per_step=len(blocks), t=time_launch(mlp, reps=20), flops=2.0 * 2 * M * C * 4 * C,
                             note=f"M={M} C={C}: LN + Linear C->4C + GELU + Linear 4C->C + scale + residual"))
         if hw <= 64:
             def dw(blk=blk, x=x, y=y):
                 K.dwconv7(x, blk["w49"], blk["dwb"], y)
             out.append(dict(name=f"dwconv7_kernel (stage {st + 1}, C={C})", bound="hbm", per_step=len(blocks),
+                            symbol="dwconv7_kernel",
                             t=time_launch(dw, reps=20), bytes=2.0 * M * C * 2 + 49 * C * 4,
                             note=f"B*H*W={M} C={C}: read x + write y (bf16)"))
         hw //= 2
     return out
 
 
-def measure(cfg, trainer, batch):
+def pmc_traffic(symbol, cfgname):
+    """HBM bytes per launch of ``symbol`` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
+    summary of this config's bench run (profiles/*_<cfg>_pmc.json, tools/pmc_summary.py:
+    gfx950-corrected, averaged over the kernel's dispatches), or None."""
+    import glob
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(root, "profiles", f"*_{cfgname}_pmc.json")))
+    if not files or not symbol:
+        return None
+    data = json.load(open(files[-1]))
+    hits = [v for k, v in data.items() if symbol in k]
+    if not hits:
+        return None
+    n = sum(h["dispatches"] for h in hits)
+    return sum(h["traffic_bytes"] * h["dispatches"] for h in hits) / max(n, 1)
+
+
+def measure(cfg, trainer, batch, cfgname=None):
     dev = batch[0].device
     B = batch[0].shape[0]
     cands = _gemm_groups(trainer, batch) + _encoder_groups(trainer, B, dev)
@@ -135,7 +162,11 @@ def measure(cfg, trainer, batch):
         achieved = best["flops"] / t / 1e12
         peak, unit = PEAK_BF16_TFLOPS, "TFLOP/s"
     ranked = sorted(cands, key=lambda c: -c["share"])
+    traffic = pmc_traffic(best.get("symbol"), cfgname) if cfgname else None
     return {"bound": best["bound"], "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": None, "kernel": best["name"],
+            "frac": round(achieved / peak, 4), "traffic": None if traffic is None else round(traffic),
+            "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/)",
+            "algorithmic_bytes": round(best["bytes"]) if "bytes" in best else None,
+            "kernel": best["name"],
             "avg_launch_us": round(t * 1e6, 2), "launches_per_step": best["per_step"], "shape": best["note"],
             "others_us_per_step": {c["name"]: round(c["share"] * 1e6, 1) for c in ranked[1:8]}}
