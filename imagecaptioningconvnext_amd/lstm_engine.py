@@ -11,6 +11,7 @@ FlatParams buffer whose groups make the concatenated operands zero-copy views:
   init  = [init_h.weight; init_c.weight] [2D, E],  binit = [init_h.bias; init_c.bias]
 """
 import ctypes
+import os
 
 import torch
 
@@ -59,6 +60,59 @@ class LstmEngine:
     # to cover the CUs at batch 32 with D = 512 (x: 80 column tiles x 3, y: 32 x 8)
     X_SLICES = 3
     Y_SLICES = 8
+    # The batch rows are independent sequences, so the recurrence can run as CHAINS chains of
+    # B / CHAINS rows, each on its own HIP stream (forked from / joined to the caller's stream,
+    # graph-capturable).  Measured on MI355X (tools/microbench.py lstm): two chains take 1.85x
+    # the time of one -- the step kernels of concurrent streams do not overlap (also with 8 or
+    # 16 hardware queues) -- so the default is one chain; kept as a switch (IMGCAP_LSTM_CHAINS).
+    CHAINS = int(os.environ.get("IMGCAP_LSTM_CHAINS", "1"))
+
+    def _per_row_bytes(self, T, P):
+        """Byte stride per batch row of every row-indexed imgcap_lstm_desc pointer."""
+        E, A, D, W3 = self.E, self.A, self.D, self.W3
+        c = 2 if self.ct == torch.bfloat16 else 4
+        npc = (P + 6) // 7
+        return dict(enc=P * E * c, att1=P * A * c, xe=T * 4 * D * 4, c0=D * 4, dl=4, g1=T * W3 * 4,
+                    alphas=T * P * 4, awe=T * E * 4, zs=T * E * c, gates=T * 4 * D * 4, cs=T * D * 4, hs=T * D * c,
+                    hprev=T * D * c, dhs=T * D * c, dalpha=T * P * 4, dcat=T * W3 * c, dh=D * 4, dc=D * 4,
+                    de=T * P * 4, datt1=P * A * c, dwf=npc * A * 4, dbea=npc * A * 4, dawe=(T + 1) * E * 4)
+
+    def _chain_rows(self, B):
+        n = max(1, min(self.CHAINS, B))
+        return [(i * B // n, (i + 1) * B // n) for i in range(n)]
+
+    def _launch(self, fn, d, ws=None):
+        """Run imgcap_lstm_tf_fwd / _bwd over the row chains of ``d``; ws[i] = per-chain workspace
+        pointers (dz, ws_y, y_cnt) for the backward."""
+        rows = self._chain_rows(d.B)
+        if len(rows) == 1:
+            if ws:
+                for k, v in ws[0].items():
+                    setattr(d, k, v.data_ptr())
+            _abi.call(fn, ctypes.byref(d), K.stream())
+            return
+        main = torch.cuda.current_stream()
+        if getattr(self, "_streams", None) is None or len(self._streams) < len(rows) - 1:
+            prio = int(os.environ.get("IMGCAP_LSTM_STREAM_PRIO", "0"))
+            self._streams = [torch.cuda.Stream(device=main.device, priority=prio) for _ in range(len(rows) - 1)]
+        per = self._per_row_bytes(d.T, d.P)
+        for i, (b0, b1) in enumerate(rows):
+            sd = _abi.LstmDesc()
+            ctypes.memmove(ctypes.byref(sd), ctypes.byref(d), ctypes.sizeof(d))
+            sd.B = b1 - b0
+            for f, nb in per.items():
+                v = getattr(sd, f)
+                if v:
+                    setattr(sd, f, v + b0 * nb)
+            if ws:
+                for k, v in ws[i].items():
+                    setattr(sd, k, v.data_ptr())
+            st = main if i == 0 else self._streams[i - 1]
+            if i:
+                st.wait_stream(main)
+            _abi.call(fn, ctypes.byref(sd), st.cuda_stream)
+        for st in self._streams[:len(rows) - 1]:
+            main.wait_stream(st)
 
     # ---------------------------------------------------------------------------------------
     def weights(self):
@@ -130,7 +184,7 @@ class LstmEngine:
                          xe=xe, c0=c0, dl=dl, g1=g1, alphas=alphas, awe=awe, zs=zs, gates=gates, cs=cs, hs=hs,
                          hprev=hprev).items():
             setattr(d, k, v.data_ptr())
-        _abi.call("imgcap_lstm_tf_fwd", ctypes.byref(d), K.stream())
+        self._launch("imgcap_lstm_tf_fwd", d)
         # ---- fc(dropout(h)) over all B*T rows (decoder.py:144) ----------------------------------
         hd = hs.view(B * T, D)
         if p_drop > 0:
@@ -196,11 +250,17 @@ class LstmEngine:
         f32 = dict(device=dev, dtype=torch.float32)
         dcat = torch.empty(B, T, W3, device=dev, dtype=ct)
         xs, ys = self.X_SLICES, self.Y_SLICES
-        nrg = (B + 31) // 32
-        dz = torch.empty(xs, B, E + D, **f32)                    # K-slice slabs of the step GEMMs
-        ws_y = torch.empty(ys * nrg * (D // 16) * 512, **f32)
-        if self._y_cnt is None or self._y_cnt.numel() < nrg * (D // 16) or self._y_cnt.device != dev:
-            self._y_cnt = torch.zeros(nrg * (D // 16), device=dev, dtype=torch.int32)  # left at 0 by the kernel
+        # per chain: K-slice slabs of the step GEMMs and the last-arriver counters (left at 0)
+        chain_ws = []
+        rows = self._chain_rows(B)
+        if self._y_cnt is None or len(self._y_cnt) != len(rows) or self._y_cnt[0].device != dev:
+            self._y_cnt = [None] * len(rows)
+        for i, (b0, b1) in enumerate(rows):
+            nrg = (b1 - b0 + 31) // 32
+            if self._y_cnt[i] is None or self._y_cnt[i].numel() < nrg * (D // 16):
+                self._y_cnt[i] = torch.zeros(nrg * (D // 16), device=dev, dtype=torch.int32)
+            chain_ws.append(dict(dz=torch.empty(xs, b1 - b0, E + D, **f32),
+                                 ws_y=torch.empty(ys * nrg * (D // 16) * 512, **f32), y_cnt=self._y_cnt[i]))
         dh, dc = torch.empty(B, D, **f32), torch.empty(B, D, **f32)
         de = torch.empty(B, T, P, **f32)
         datt1 = torch.empty(B * P, A, device=dev, dtype=ct)
@@ -212,16 +272,17 @@ class LstmEngine:
         K.transpose(w["hcat"][A + E:], out=wzh_t[E:])
         watt_t = K.transpose(w["hcat"][:A + E])                    # [D, A + E] = [W_da; W_fb]^T
         d = s["desc"]
-        bufs = dict(w_zh_t=wzh_t, w_att_t=watt_t, dhs=dhs, dalpha=dalpha, dcat=dcat, dz=dz, ws_y=ws_y,
-                    y_cnt=self._y_cnt, dh=dh, dc=dc, de=de, datt1=datt1, dwf=dwf, dbea=dbea)
+        bufs = dict(w_zh_t=wzh_t, w_att_t=watt_t, dhs=dhs, dalpha=dalpha, dcat=dcat, dh=dh, dc=dc, de=de,
+                    datt1=datt1, dwf=dwf, dbea=dbea)
         for k, v in bufs.items():
             setattr(d, k, K.ptr(v))
         d.x_slices, d.y_slices = xs, ys
         dawe = torch.empty(B, T + 1, E, **f32) if want_denc else None
         d.dawe = K.ptr(dawe)
         bufs["dawe"] = dawe
+        bufs["chain_ws"] = chain_ws
         s["bwd_bufs"] = bufs  # the descriptor points into these: keep them alive as long as `s`
-        _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream())
+        self._launch("imgcap_lstm_tf_bwd", d, chain_ws)
         dc2 = dcat.view(BT, W3)
         dgates = dc2[:, A + E:]
         # W_hcat / b_hcat grads (batched over all B*T rows)

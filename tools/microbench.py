@@ -119,9 +119,12 @@ def lstm():
     eng.backward(s)
     d = s["desc"]
     T = s["T"]
-    t = time_launch(lambda: _abi.call("imgcap_lstm_tf_fwd", ctypes.byref(d), K.stream()), reps=5, warm=2)
-    print(f"lstm fwd recurrence: {t * 1e6:8.1f} us total, {t * 1e6 / T:6.2f} us/step")
-    t = time_launch(lambda: _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream()), reps=5, warm=2)
+    ws = s["bwd_bufs"]["chain_ws"]
+    t = time_launch(lambda: eng._launch("imgcap_lstm_tf_fwd", d), reps=5, warm=2)
+    print(f"lstm fwd recurrence ({eng.CHAINS} chains): {t * 1e6:8.1f} us total, {t * 1e6 / T:6.2f} us/step")
+    te = time_launch(lambda: eng._launch("imgcap_lstm_tf_fwd", d), reps=5, warm=2, graph=False)
+    print(f"lstm fwd recurrence ({eng.CHAINS} chains, eager streams): {te * 1e6:8.1f} us total")
+    t = time_launch(lambda: eng._launch("imgcap_lstm_tf_bwd", d, ws), reps=5, warm=2)
     print(f"lstm bwd recurrence: {t * 1e6:8.1f} us total, {t * 1e6 / T:6.2f} us/step")
 
 
@@ -198,10 +201,11 @@ def overlap():
     s = eng.forward(feats, caps, lens, fixed_T=True)
     eng.backward(s)
     d = s["desc"]
+    ws = s["bwd_bufs"]["chain_ws"]
 
     def rec():
-        _abi.call("imgcap_lstm_tf_fwd", ctypes.byref(d), K.stream())
-        _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream())
+        eng._launch("imgcap_lstm_tf_fwd", d)
+        eng._launch("imgcap_lstm_tf_bwd", d, ws)
 
     def encf():
         with torch.no_grad():
