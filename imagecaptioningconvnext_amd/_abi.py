@@ -46,6 +46,12 @@ class MhaDesc(ctypes.Structure):
         ("dv", c_void_p), ("lddq", c_int64), ("lddk", c_int64), ("lddv", c_int64)]
 
 
+class GemmProblem(ctypes.Structure):
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("C", c_void_p), ("lda", c_int64), ("ldb", c_int64),
+                ("ldc", c_int64), ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32),
+                ("alpha", c_float), ("beta", c_float)]
+
+
 class ColsumItem(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("out", c_void_p), ("ld", c_int64), ("rows", ctypes.c_int32),
                 ("cols", ctypes.c_int32), ("dtype", ctypes.c_int32), ("vec_ok", ctypes.c_int32),
@@ -104,6 +110,7 @@ _SIGS = {
     "imgcap_gemm_set_policy": [c_int],
     "imgcap_workspace_slot": [c_int],
     "imgcap_colsum_multi": [c_int, c_void_p, c_void_p],
+    "imgcap_gemm_grouped": [c_int, c_int, c_int, c_void_p, c_void_p],
     "imgcap_slice_reduce": [c_int64, c_int, c_void_p, c_int64, c_float, c_int64, c_void_p, c_void_p, c_void_p],
 }
 

@@ -846,3 +846,36 @@ extern "C" int imgcap_colsum_multi(int n, const imgcap_colsum_item* items, void*
   IMGCAP_CHECK_LAUNCH("imgcap_colsum_multi");
   return 0;
 }
+
+extern "C" int imgcap_gemm_grouped(int a_kmajor, int b_kmajor, int n, const imgcap_gemm_problem* probs,
+                                   void* stream) {
+  IMGCAP_REQUIRE(n >= 0 && n <= GEMM_GROUP_MAX, "imgcap_gemm_grouped: at most 48 problems per call");
+  if (n == 0) return 0;
+  GemmGroup g{};
+  int tiles = 0, m = 0;
+  for (int i = 0; i < n; ++i) {
+    const imgcap_gemm_problem& p = probs[i];
+    IMGCAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K > 0, "imgcap_gemm_grouped: bad sizes");
+    if (p.M == 0 || p.N == 0) continue;
+    IMGCAP_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.lda % 8 == 0 && p.ldb % 8 == 0,
+                   "imgcap_gemm_grouped: operands 16-byte aligned, leading dims multiples of 8");
+    IMGCAP_REQUIRE(a_kmajor ? p.lda >= p.K : p.lda >= p.M, "imgcap_gemm_grouped: lda too small");
+    IMGCAP_REQUIRE(b_kmajor ? p.ldb >= p.K : p.ldb >= p.N, "imgcap_gemm_grouped: ldb too small");
+    g.p[m] = p;
+    g.first[m] = tiles;
+    tiles += ((p.M + 127) / 128) * ((p.N + 127) / 128);
+    ++m;
+  }
+  g.n = m;
+  g.first[m] = tiles;
+  if (tiles == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+#define GG_(AKV, BKV) hipLaunchKernelGGL((gemm_glds_grouped_kernel<AKV, BKV>), dim3(tiles), dim3(256), 0, st, g)
+  if (a_kmajor && b_kmajor) GG_(true, true);
+  else if (a_kmajor) GG_(true, false);
+  else if (b_kmajor) GG_(false, true);
+  else GG_(false, false);
+#undef GG_
+  IMGCAP_CHECK_LAUNCH("imgcap_gemm_grouped");
+  return 0;
+}

@@ -91,21 +91,18 @@ DEV bf16x8 glds_frag_op(const char* img, int row0, int kk, int lane) {
   }
 }
 
+// One BM x BN output tile (rows m0.., columns n0..) over k-tiles of slice kz (split-K when
+// kslice > 0): the body shared by the single-problem and the grouped launch.
 template <int BM, int BN, bool AK, bool BKM, int S>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 : 1, S == 2 ? 2 : 1))) void
-gemm_glds_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, void* __restrict__ C,
-                 long ldc, int M, int N, int K, imgcap_epilogue ep, int vec_ok, const uint64_t* seed_ctr,
-                 int kslice) {
+DEV void glds_tile(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, void* __restrict__ C,
+                   long ldc, int M, int N, int K, const imgcap_epilogue& ep, int vec_ok, int kslice, int m0, int n0,
+                   int kz) {
   constexpr int TILE_A = BM * 64 * 2, TILE_B = BN * 64 * 2, STAGE = TILE_A + TILE_B;
   constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 fragments per wave (2 x 2 waves)
   constexpr int LDT = BN + 4, EPI_ROWS = BM / 2;
   constexpr int LPT = BM * 8 / 256 + BN * 8 / 256;  // LDS-DMA instructions per thread per k-tile
   static_assert(EPI_ROWS * LDT * 4 <= S * STAGE, "epilogue tile fits the stages");
   __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
-  if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
-  int bx, by;
-  xcd_remap(bx, by);
-  const int m0 = by * BM, n0 = bx * BN;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 1, wn = w & 1;
@@ -120,7 +117,7 @@ gemm_glds_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ 
 
   // k-tiles [kt0, nk): the whole K, or slice blockIdx.z of a split-K launch (kslice % 64 == 0).
   // S stages: tiles kt+1 .. kt+S-1 are in flight while tile kt is multiplied.
-  const int kt0 = kslice ? blockIdx.z * (kslice / 64) : 0;
+  const int kt0 = kslice ? kz * (kslice / 64) : 0;
   const int nk = kslice ? min((K + 63) / 64, kt0 + kslice / 64) : (K + 63) / 64;
 #pragma unroll
   for (int i = 0; i < S - 1; ++i) {
@@ -186,9 +183,55 @@ gemm_glds_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ 
     }
     __syncthreads();
     if (kslice)
-      partial_from_lds<BN>(tile, LDT, EPI_ROWS, m0 + pass * EPI_ROWS, n0, M, N, (float*)C + (long)blockIdx.z * M * N);
+      partial_from_lds<BN>(tile, LDT, EPI_ROWS, m0 + pass * EPI_ROWS, n0, M, N, (float*)C + (long)kz * M * N);
     else
       epilogue_tile<BN, EPI_ROWS, 256>(ep, tile, LDT, m0 + pass * EPI_ROWS, n0, M, N, C, ldc, vec_ok != 0);
     __syncthreads();
   }
+}
+
+template <int BM, int BN, bool AK, bool BKM, int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 : 1, S == 2 ? 2 : 1))) void
+gemm_glds_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, void* __restrict__ C,
+                 long ldc, int M, int N, int K, imgcap_epilogue ep, int vec_ok, const uint64_t* seed_ctr,
+                 int kslice) {
+  if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
+  int bx, by;
+  xcd_remap(bx, by);
+  glds_tile<BM, BN, AK, BKM, S>(A, lda, B, ldb, C, ldc, M, N, K, ep, vec_ok, kslice, by * BM, bx * BN, blockIdx.z);
+}
+
+// ---- grouped launch: many independent fp32-output products in one grid ------------------
+// (the weight gradients of a whole backward pass, deferred to its end: hundreds of 128x128
+// tiles at once instead of one small grid + split-K + reduce per product).  Block b walks the
+// problems' tile prefix; ids are dealt XCD-contiguously so a problem's tiles share an L2.
+constexpr int GEMM_GROUP_MAX = 48;
+struct GemmGroup {
+  int n;
+  int first[GEMM_GROUP_MAX + 1];
+  imgcap_gemm_problem p[GEMM_GROUP_MAX];
+};
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_glds_grouped_kernel(
+    GemmGroup g) {
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  int id = orig;
+  if (nwg >= 64) {
+    const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  int k = 0;
+  while (k + 1 < g.n && id >= g.first[k + 1]) ++k;
+  const imgcap_gemm_problem& p = g.p[k];
+  const int local = id - g.first[k];
+  const int nx = (p.N + 127) / 128;
+  imgcap_epilogue ep{};
+  ep.alpha = p.alpha;
+  ep.beta = p.beta;
+  ep.c_dtype = IMGCAP_F32;
+  ep.rows_per_scale = 1;
+  const int vec_ok = (((uintptr_t)p.C) & 15) == 0 && p.ldc % 8 == 0;
+  glds_tile<128, 128, AK, BKM, 2>((const bf16*)p.A, p.lda, (const bf16*)p.B, p.ldb, p.C, p.ldc, p.M, p.N, p.K, ep,
+                                  vec_ok, 0, (local / nx) * 128, (local % nx) * 128, 0);
 }

@@ -183,6 +183,39 @@ class ColsumBatch:
         self.items = []
 
 
+class GemmBatch:
+    """Deferred weight gradients: ``add(a, b, out, trans_a=, trans_b=)`` records the fp32 product
+    out = alpha * op(a) op(b) + beta * out (operands kept alive); ``run`` issues all of them as
+    grouped launches (imgcap_gemm_grouped, one per operand layout and 48 problems) -- hundreds of
+    128x128 tiles in one grid instead of a small split-K grid + reduce per product."""
+
+    def __init__(self):
+        self.items = {}
+
+    def add(self, a, b, out, *, trans_a=False, trans_b=False, M=None, N=None, K=None, alpha=1.0, beta=0.0):
+        _check_dev(a, b, out)
+        if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or out.dtype != torch.float32:
+            gemm(a, b, trans_a=trans_a, trans_b=trans_b, out=out, M=M, N=N, K=K, alpha=alpha, beta=beta, split_k=-1)
+            return
+        M = (a.shape[1] if trans_a else a.shape[0]) if M is None else M
+        K = (a.shape[0] if trans_a else a.shape[1]) if K is None else K
+        N = (b.shape[0] if trans_b else b.shape[1]) if N is None else N
+        key = (0 if trans_a else 1, 1 if trans_b else 0)
+        self.items.setdefault(key, []).append((a, b, out, M, N, K, _ld(a, trans_a), _ld(b, trans_b), alpha, beta))
+
+    def run(self):
+        for (ak, bk), lst in self.items.items():
+            for i0 in range(0, len(lst), 48):
+                chunk = lst[i0:i0 + 48]
+                arr = (_abi.GemmProblem * len(chunk))()
+                for p, (a, b, out, M, N, K, lda, ldb, alpha, beta) in zip(arr, chunk):
+                    p.A, p.B, p.C = a.data_ptr(), b.data_ptr(), out.data_ptr()
+                    p.lda, p.ldb, p.ldc = lda, ldb, out.stride(0)
+                    p.M, p.N, p.K, p.alpha, p.beta = M, N, K, alpha, beta
+                _abi.call("imgcap_gemm_grouped", ak, bk, len(chunk), ctypes.cast(arr, ctypes.c_void_p), stream())
+        self.items = {}
+
+
 def add_layernorm(x, r, gamma, beta, eps, *, drop_p=0.0, seed=0, drop_stream=0, s_out=None, y=None):
     rows, cols = x.shape
     y = torch.empty_like(x) if y is None else y

@@ -237,13 +237,14 @@ class LstmEngine:
         w = self.weights()
         gbuf.zero_()
         cb = K.ColsumBatch()  # every bias gradient, reduced in one launch at the end
+        wgb = K.GemmBatch()    # every weight gradient, grouped launches at the end
         if dlogits is None:
             dlogits = torch.empty(B * T, self.Vpad, device=dev, dtype=ct)
             K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
             dalpha = s["dalpha"]
         BT = B * T
         # fc: dW_fc = dlogits^T hd ; db_fc = colsum ; dh = (dlogits W_fc) * dropmask
-        K.gemm(dlogits, s["hd"], trans_a=True, out=_G.g("fc.weight"), M=V, **DW)
+        wgb.add(dlogits, s["hd"], out=_G.g("fc.weight"), M=V, trans_a=True)
         cb.add(dlogits, _G.g("fc.bias"), cols=V)
         dhs = K.gemm(dlogits, w["wfc"], K=V, drop_p=s["p_drop"], seed=s["seed"], drop_stream=_STREAM_DROPOUT_H,
                      drop_ld=D)
@@ -286,25 +287,26 @@ class LstmEngine:
         dc2 = dcat.view(BT, W3)
         dgates = dc2[:, A + E:]
         # W_hcat / b_hcat grads (batched over all B*T rows)
-        K.gemm(dc2, s["hprev"].view(BT, D), trans_a=True, out=_G.g("attention.decoder_att.weight", (W3, D), W3 * D), **DW)
+        wgb.add(dc2, s["hprev"].view(BT, D), out=_G.g("attention.decoder_att.weight", (W3, D), W3 * D), trans_a=True)
         cb.add(dc2, _G.g("attention.decoder_att.bias", (W3,), W3))
         # LSTMCell weight_ih (emb half | attention half), bias_ih
         gwih = _G.g("decode_step.weight_ih")
-        K.gemm(dgates, s["emb"], trans_a=True, out=gwih[:, :M], M=4 * D, **DW)
-        K.gemm(dgates, s["zs"].view(BT, E), trans_a=True, out=gwih[:, M:], M=4 * D, **DW)
+        wgb.add(dgates, s["emb"], out=gwih[:, :M], M=4 * D, trans_a=True)
+        wgb.add(dgates, s["zs"].view(BT, E), out=gwih[:, M:], M=4 * D, trans_a=True)
         cb.add(dgates, _G.g("decode_step.bias_ih"))
         # embedding: d_emb = dgates W_ih[:, :M]  -> scatter-add rows
         demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
         K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
         # init_h / init_c from dh0, dc0
         dinit = torch.cat([dh, dc], dim=1).to(ct)
-        K.gemm(dinit, s["mean"], trans_a=True, out=_G.g("init_h.weight", (2 * D, E), 2 * D * E), **DW)
+        wgb.add(dinit, s["mean"], out=_G.g("init_h.weight", (2 * D, E), 2 * D * E), trans_a=True)
         cb.add(dinit, _G.g("init_h.bias", (2 * D,), 2 * D))
         # encoder_att from the time-summed d att1
-        K.gemm(datt1, s["enc_s"].view(B * P, E), trans_a=True, out=_G.g("attention.encoder_att.weight"), **DW)
+        wgb.add(datt1, s["enc_s"].view(B * P, E), out=_G.g("attention.encoder_att.weight"), trans_a=True)
         cb.add(dbea, _G.g("attention.encoder_att.bias"))
         cb.add(dwf, _G.g("attention.full_att.weight", (A,)))
         # full_att.bias: exactly zero gradient (softmax is shift-invariant) -> left at 0
+        wgb.run()
         cb.run()
         s["denc"] = None
         if want_denc:

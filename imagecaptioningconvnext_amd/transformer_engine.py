@@ -180,10 +180,11 @@ class TransformerEngine:
         dev = s["xL"].device
         gbuf.zero_()
         cb = K.ColsumBatch()  # every bias gradient, reduced in one launch at the end
+        wgb = K.GemmBatch()    # every weight gradient, grouped launches at the end
         if dlogits is None:
             dlogits = torch.empty(BL, self.Vpad, device=dev, dtype=ct)
             K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
-        K.gemm(dlogits, s["xL"], trans_a=True, out=G("fc_out.weight"), M=V, **DW)
+        wgb.add(dlogits, s["xL"], out=G("fc_out.weight"), M=V, trans_a=True)
         cb.add(dlogits, G("fc_out.bias"), cols=V)
         dx = K.gemm(dlogits, fp.w("fc_out.weight"), K=V)                    # [BL, d]
         dmem = torch.zeros(BP, d, device=dev, dtype=torch.float32)
@@ -196,10 +197,10 @@ class TransformerEngine:
                                       G(lw("norm3.weight")), G(lw("norm3.bias")), drop_p=p, seed=seed,
                                       drop_stream=_s(i, 5), dr=dy3)
             # y3 = hdn W2^T + b2 ; hdn = drop(relu(x2 W1^T + b1))
-            K.gemm(dy3, st["hdn"], trans_a=True, out=G(lw("linear2.weight")), **DW)
+            wgb.add(dy3, st["hdn"], out=G(lw("linear2.weight")), trans_a=True)
             cb.add(dy3, G(lw("linear2.bias")))
             dpre = K.gemm(dy3, fp.w(lw("linear2.weight")), aux=st["hdn"], aux_scale=1.0 / (1.0 - p))
-            K.gemm(dpre, st["x2"], trans_a=True, out=G(lw("linear1.weight")), **DW)
+            wgb.add(dpre, st["x2"], out=G(lw("linear1.weight")), trans_a=True)
             cb.add(dpre, G(lw("linear1.bias")))
             K.gemm(dpre, fp.w(lw("linear1.weight")), out=ds3, beta=1.0)      # dx2 = ds3 + dpre W1
             # x2 = LN2(x1 + drop(y2))
@@ -207,7 +208,7 @@ class TransformerEngine:
             ds2 = K.add_layernorm_bwd(ds3, st["s2"], st["mu2"], st["rs2"], fp.f32(lw("norm2.weight")),
                                       G(lw("norm2.weight")), G(lw("norm2.bias")), drop_p=p, seed=seed,
                                       drop_stream=_s(i, 3), dr=dy2)
-            K.gemm(dy2, st["o2"], trans_a=True, out=G(lw("multihead_attn.out_proj.weight")), **DW)
+            wgb.add(dy2, st["o2"], out=G(lw("multihead_attn.out_proj.weight")), trans_a=True)
             cb.add(dy2, G(lw("multihead_attn.out_proj.bias")))
             do2 = K.gemm(dy2, fp.w(lw("multihead_attn.out_proj.weight")))
             dq2 = torch.empty(BL, d, device=dev, dtype=ct)
@@ -219,9 +220,9 @@ class TransformerEngine:
             gw = G(lw("multihead_attn.in_proj_weight"))
             gb = G(lw("multihead_attn.in_proj_bias"))
             wq = fp.w(lw("multihead_attn.in_proj_weight"))
-            K.gemm(dq2, st["x1"], trans_a=True, out=gw[:d], **DW)
+            wgb.add(dq2, st["x1"], out=gw[:d], trans_a=True)
             cb.add(dq2, gb[:d])
-            K.gemm(dkv2, s["mem"], trans_a=True, out=gw[d:], **DW)
+            wgb.add(dkv2, s["mem"], out=gw[d:], trans_a=True)
             cb.add(dkv2, gb[d:])
             K.gemm(dkv2, wq[d:], out=dmem, beta=1.0)                          # dmem += dkv2 W_kv
             K.gemm(dq2, wq[:d], out=ds2, beta=1.0)                            # dx1 = ds2 + dq2 W_q
@@ -230,7 +231,7 @@ class TransformerEngine:
             ds1 = K.add_layernorm_bwd(ds2, st["s1"], st["mu1"], st["rs1"], fp.f32(lw("norm1.weight")),
                                       G(lw("norm1.weight")), G(lw("norm1.bias")), drop_p=p, seed=seed,
                                       drop_stream=_s(i, 1), dr=dy)
-            K.gemm(dy, st["o"], trans_a=True, out=G(lw("self_attn.out_proj.weight")), **DW)
+            wgb.add(dy, st["o"], out=G(lw("self_attn.out_proj.weight")), trans_a=True)
             cb.add(dy, G(lw("self_attn.out_proj.bias")))
             do = K.gemm(dy, fp.w(lw("self_attn.out_proj.weight")))
             dqkv = torch.empty(BL, 3 * d, device=dev, dtype=ct)
@@ -239,7 +240,7 @@ class TransformerEngine:
                       o=None, ldo=d, lse=st["lse1"], causal=True, key_ids=s["key_ids"], pad_id=s["pad_id"], p=p,
                       seed=seed, sid=_s(i, 0), dout=do, lddo=d, dq=dqkv, lddq=3 * d, dk=dqkv[:, d:], lddk=3 * d,
                       dv=dqkv[:, 2 * d:], lddv=3 * d, bwd=True)
-            K.gemm(dqkv, st["x"], trans_a=True, out=G(lw("self_attn.in_proj_weight")), **DW)
+            wgb.add(dqkv, st["x"], out=G(lw("self_attn.in_proj_weight")), trans_a=True)
             cb.add(dqkv, G(lw("self_attn.in_proj_bias")))
             K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
             dx = ds1
@@ -248,12 +249,13 @@ class TransformerEngine:
         denc = None
         if self.has_proj:
             dmem_c = dmem.to(ct)
-            K.gemm(dmem_c, s["enc"].view(BP, self.E), trans_a=True, out=G("encoder_proj.weight"), **DW)
+            wgb.add(dmem_c, s["enc"].view(BP, self.E), out=G("encoder_proj.weight"), trans_a=True)
             cb.add(dmem, G("encoder_proj.bias"))
             if want_denc:
                 denc = K.gemm(dmem_c, fp.w("encoder_proj.weight")).view(B, P, self.E)
         elif want_denc:
             denc = dmem.to(ct).view(B, P, d)
+        wgb.run()
         cb.run()
         s["denc"] = denc
         return gbuf

@@ -86,6 +86,19 @@ int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
                 void* C, int64_t ldc, int64_t strideC, int batch,
                 const imgcap_epilogue* epi, void* stream);
 
+/* Grouped product launch: C_i = alpha_i * op(A_i) op(B_i) + beta_i * C_i, fp32 C, bf16 operands,
+ * one operand layout for all problems (a_kmajor / b_kmajor as imgcap_gemm), <= 48 problems.  The
+ * weight gradients of a backward pass (dW = dY^T X, K = rows) in one grid of 128x128 tiles. */
+typedef struct imgcap_gemm_problem {
+  const void* A;
+  const void* B;
+  float* C;
+  int64_t lda, ldb, ldc;
+  int32_t M, N, K;
+  float alpha, beta;
+} imgcap_gemm_problem;
+int imgcap_gemm_grouped(int a_kmajor, int b_kmajor, int n, const imgcap_gemm_problem* probs, void* stream);
+
 /* out[c, r] = in[r, c]  (weight transposes for the k-major skinny GEMMs) */
 /* Which kernel imgcap_gemm launches for these operands (diagnostics and the bench's roofline):
  * returns one of IMGCAP_GEMM_*; *splits (if not NULL) = K slices (1 = none). */

@@ -357,3 +357,25 @@ def test_cnblock_mlp_fused(hip_device, C, M, with_sd):
     K.cnblock_mlp(dev(z), dev(w1), dev(b1), dev(w2), dev(b2), dev(gamma), xd, sd=dev(sd), rows_per_sample=rps)
     got = xd.cpu().float() - x.float()
     assert _rel(got, delta) < 2e-2
+
+
+def test_gemm_grouped_weight_gradients(hip_device):
+    """GemmBatch / imgcap_gemm_grouped: many dW = dY^T X products (ragged M, N, K, strided
+    outputs, alpha/beta) in one grouped launch vs torch fp32 on the bf16-rounded operands."""
+    g = torch.Generator().manual_seed(3)
+    shapes = [(512, 512, 3328), (1536, 512, 3328), (9490, 512, 1632), (70, 200, 100), (256, 768, 3136), (8, 16, 64)]
+    batch = K.GemmBatch()
+    cases = []
+    for i, (M, N, Kd) in enumerate(shapes):
+        dy = torch.randn(Kd, M, generator=g)
+        x = torch.randn(Kd, N, generator=g)
+        dyd, xd = _padded(dy, hip_device, torch.bfloat16), _padded(x, hip_device, torch.bfloat16)
+        big = torch.randn(M, N + 24, generator=g)
+        out = big.to(hip_device)[:, 8:8 + N]                      # strided fp32 output view
+        alpha, beta = (1.0, 0.0) if i % 2 == 0 else (0.5, 1.0)
+        batch.add(dyd, xd, out, trans_a=True, M=M, N=N, K=Kd, alpha=alpha, beta=beta)
+        ref = alpha * dy.bfloat16().float().t() @ x.bfloat16().float() + beta * big[:, 8:8 + N]
+        cases.append((out, ref))
+    batch.run()
+    for out, ref in cases:
+        assert _rel(out.cpu(), ref) < 1e-5
