@@ -73,7 +73,7 @@ _SIGS = {
     "imgcap_add_layernorm_fwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_uint64, c_uint32, c_void_p,
                                  c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "imgcap_add_layernorm_bwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
-                                 c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+                                 c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "imgcap_convnext_stem": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p],
     "imgcap_dwconv7_ln": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -80,7 +80,8 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, con
                                                          const float* __restrict__ rstd_i, const float* __restrict__ g,
                                                          float p, uint64_t seed0, const uint64_t* seed_ctr,
                                                          uint32_t stream_id, T* __restrict__ dx, T* __restrict__ dr,
-                                                         float* __restrict__ ws, int rows_per_wave) {
+                                                         float* __restrict__ ws, float* __restrict__ dyx,
+                                                         int rows_per_wave) {
   constexpr int MAXJ = MAXC / (64 * G);
   __shared__ float part[2][4][MAXC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -114,6 +115,12 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, con
           lb[j][e] += dv[e];
           s1 += gdy[j][e];
           s2 += gdy[j][e] * xh[j][e];
+        }
+        if (dyx) {  // dy * xhat for a deferred dgamma column sum (imgcap_colsum_multi)
+          float q[G];
+#pragma unroll
+          for (int e = 0; e < G; ++e) q[e] = dv[e] * xh[j][e];
+          st_g<float, G>(dyx + idx, q);
         }
       }
     }
@@ -195,7 +202,8 @@ extern "C" int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const voi
 extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const void* dy, const void* s,
                                         const float* mean, const float* rstd, const float* gamma, float drop_p,
                                         uint64_t seed, uint32_t drop_stream, void* dx, void* dr, float* dgamma,
-                                        float* dbeta, void* stream) {
+                                        float* dbeta, float* dyx, void* stream) {
+  IMGCAP_REQUIRE(!dyx || (!dgamma && !dbeta), "imgcap_add_layernorm_bwd: dyx replaces dgamma/dbeta");
   IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_bwd: cols must be in (0, 2048]");
   if (rows == 0) return 0;
   const int rpw = std::max(1, (rows + 4 * 512 - 1) / (4 * 512));  // ~512 blocks of 4 waves
@@ -213,7 +221,7 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
   } while (0)
 #define LNB2_(T, G, MC)                                                                                         \
   hipLaunchKernelGGL((add_ln_bwd_kernel<T, G, MC>), grid, dim3(256), 0, st, rows, cols, (const T*)dy, (const T*)s,   \
-                     mean, rstd, gamma, drop_p, seed, g_seed_ctr, drop_stream, (T*)dx, (T*)dr, ws, rpw)
+                     mean, rstd, gamma, drop_p, seed, g_seed_ctr, drop_stream, (T*)dx, (T*)dr, ws, dyx, rpw)
   if (dtype == IMGCAP_BF16) {
     if (vec_rows<bf16>(cols, {dy, s, dx, dr})) LNB_(bf16, 8); else LNB_(bf16, 1);
   } else {

@@ -228,12 +228,20 @@ def add_layernorm(x, r, gamma, beta, eps, *, drop_p=0.0, seed=0, drop_stream=0, 
 
 
 def add_layernorm_bwd(dy, s, mean, rstd, gamma, dgamma, dbeta, *, drop_p=0.0, seed=0, drop_stream=0, dx=None,
-                      dr=None):
+                      dr=None, cb=None):
+    """LN backward; dgamma/dbeta accumulate (+=).  With a ColsumBatch ``cb`` their column sums
+    are deferred to cb.run() (dy * xhat materialised in fp32) instead of reduced here."""
     rows, cols = dy.shape
     dx = torch.empty_like(dy) if dx is None else dx
+    dyx = None
+    if cb is not None:
+        dyx = torch.empty(rows, cols, device=dy.device, dtype=torch.float32)
+        cb.add(dyx, dgamma, beta=1.0)
+        cb.add(dy, dbeta, beta=1.0)
+        dgamma = dbeta = None
     _abi.call("imgcap_add_layernorm_bwd", dt(dy), rows, cols, dy.data_ptr(), s.data_ptr(), mean.data_ptr(),
               rstd.data_ptr(), gamma.data_ptr(), drop_p, seed, drop_stream, dx.data_ptr(), ptr(dr), ptr(dgamma),
-              ptr(dbeta), stream())
+              ptr(dbeta), ptr(dyx), stream())
     return dx
 
 

@@ -195,7 +195,7 @@ class TransformerEngine:
             dy3 = torch.empty_like(dx)
             ds3 = K.add_layernorm_bwd(dx, st["s3"], st["mu3"], st["rs3"], fp.f32(lw("norm3.weight")),
                                       G(lw("norm3.weight")), G(lw("norm3.bias")), drop_p=p, seed=seed,
-                                      drop_stream=_s(i, 5), dr=dy3)
+                                      drop_stream=_s(i, 5), dr=dy3, cb=cb)
             # y3 = hdn W2^T + b2 ; hdn = drop(relu(x2 W1^T + b1))
             wgb.add(dy3, st["hdn"], out=G(lw("linear2.weight")), trans_a=True)
             cb.add(dy3, G(lw("linear2.bias")))
@@ -207,7 +207,7 @@ class TransformerEngine:
             dy2 = torch.empty_like(dx)
             ds2 = K.add_layernorm_bwd(ds3, st["s2"], st["mu2"], st["rs2"], fp.f32(lw("norm2.weight")),
                                       G(lw("norm2.weight")), G(lw("norm2.bias")), drop_p=p, seed=seed,
-                                      drop_stream=_s(i, 3), dr=dy2)
+                                      drop_stream=_s(i, 3), dr=dy2, cb=cb)
             wgb.add(dy2, st["o2"], out=G(lw("multihead_attn.out_proj.weight")), trans_a=True)
             cb.add(dy2, G(lw("multihead_attn.out_proj.bias")))
             do2 = K.gemm(dy2, fp.w(lw("multihead_attn.out_proj.weight")))
@@ -230,7 +230,7 @@ class TransformerEngine:
             dy = torch.empty_like(dx)
             ds1 = K.add_layernorm_bwd(ds2, st["s1"], st["mu1"], st["rs1"], fp.f32(lw("norm1.weight")),
                                       G(lw("norm1.weight")), G(lw("norm1.bias")), drop_p=p, seed=seed,
-                                      drop_stream=_s(i, 1), dr=dy)
+                                      drop_stream=_s(i, 1), dr=dy, cb=cb)
             wgb.add(dy, st["o"], out=G(lw("self_attn.out_proj.weight")), trans_a=True)
             cb.add(dy, G(lw("self_attn.out_proj.bias")))
             do = K.gemm(dy, fp.w(lw("self_attn.out_proj.weight")))

@@ -140,11 +140,13 @@ int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const void* x, const
                              const float* gamma, const float* beta, float eps,
                              void* s_out, void* y, float* mean, float* rstd, void* stream);
 /* dS = LN backward of dy;  dx = dS;  dr = dS * dropmask  (dr may be NULL);
- * dgamma/dbeta accumulated (+=) in fp32. */
+ * dgamma/dbeta accumulated (+=) in fp32 -- or, with dyx != NULL (and dgamma = dbeta = NULL),
+ * dyx[rows, cols] = dy * xhat (fp32) is written for the caller's deferred column sums
+ * (dgamma = colsum(dyx), dbeta = colsum(dy): imgcap_colsum_multi). */
 int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const void* dy, const void* s,
                              const float* mean, const float* rstd, const float* gamma,
                              float drop_p, uint64_t seed, uint32_t drop_stream,
-                             void* dx, void* dr, float* dgamma, float* dbeta, void* stream);
+                             void* dx, void* dr, float* dgamma, float* dbeta, float* dyx, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * ConvNeXt trunk (torchvision features reached via encoder.py:24), NHWC activations.

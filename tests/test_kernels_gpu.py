@@ -167,6 +167,14 @@ def test_add_layernorm_fwd_bwd(hip_device, dtype, tol):
     dx = K.add_layernorm_bwd(dy.to(hip_device, dtype), s, mean, rstd, g.to(hip_device), dg, db, dr=dr)
     assert _rel(dx.cpu(), xs.grad) < tol and _rel(dr.cpu(), xs.grad) < tol
     assert _rel(dg.cpu(), gg.grad) < tol and _rel(db.cpu(), bb.grad) < tol
+    # deferred parameter sums: dy*xhat materialised, reduced with the backward's other column sums
+    cb = K.ColsumBatch()
+    dg2 = torch.full((cols,), 0.5, device=hip_device)
+    db2 = torch.full((cols,), -0.5, device=hip_device)
+    dx2 = K.add_layernorm_bwd(dy.to(hip_device, dtype), s, mean, rstd, g.to(hip_device), dg2, db2, dr=dr, cb=cb)
+    cb.run()
+    assert torch.equal(dx2, dx)
+    assert _rel(dg2.cpu() - 0.5, gg.grad) < tol and _rel(db2.cpu() + 0.5, bb.grad) < tol
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
