@@ -138,6 +138,35 @@ template <> struct V8<float> {
   }
 };
 
+// NC (4 or 8) consecutive channels <-> fp32 (depthwise kernel lanes)
+template <typename T, int NC>
+DEV void ldc(const T* p, float (&v)[NC]) {
+  if constexpr (NC == 8) {
+    V8<T>::load(p, v);
+  } else if constexpr (sizeof(T) == 2) {
+    const bf16x4 x = *(const bf16x4*)p;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (float)x[j];
+  } else {
+    const f32x4 a = *(const f32x4*)p;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = a[j];
+  }
+}
+template <typename T, int NC>
+DEV void stc(T* p, const float (&v)[NC]) {
+  if constexpr (NC == 8) {
+    V8<T>::store(p, v);
+  } else if constexpr (sizeof(T) == 2) {
+    bf16x4 x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = (bf16)v[j];
+    *(bf16x4*)p = x;
+  } else {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  }
+}
+
 template <typename T, int PW>
 __global__ __launch_bounds__(256) void dwconv7_ln_kernel(int B, int H, int W, int C, const T* __restrict__ x,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
@@ -250,16 +279,33 @@ __global__ __launch_bounds__(256) void dwconv7_ln_kernel(int B, int H, int W, in
 // row land in distinct bank groups, and RS = 16/GW (mod 16) interleaves successive rows into
 // the remaining ones -- each 16-lane pass of a ds_read_b128 is conflict-free.
 constexpr int DW_CT = 32;  // channels per block
-template <typename T, int PW>
-__global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C, const T* __restrict__ x,
+// LDS row stride in 16-byte slots: >= the row's slots, = 16/GW (mod 16) (see above)
+__host__ __device__ constexpr int dw_row_slots(int W, int PW, int elem_bytes) {
+  const int GW = W / PW;
+  const int base = (4 * (W + 6) + (W + 5) / PW + 1) * (elem_bytes / 2);
+  const int target = (GW == 1 || GW == 2 || GW == 4 || GW == 8 || GW == 16) ? (16 / GW) % 16 : 1;
+  int rs = base;
+  while (rs % 16 != target) ++rs;
+  return rs;
+}
+// WC: the image width as a compile-time constant (0: runtime W) -- the staging index math
+// (patch row / column of each 16-byte load) then folds to multiplies by constants, which at
+// the encoder's widths removes about a third of the kernel's vector instructions.
+template <typename T, int PW, int WC, int NC>
+__global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_kernel(int B, int H, int W_, int C, const T* __restrict__ x,
                                                       const float* __restrict__ w, const float* __restrict__ bias,
-                                                      T* __restrict__ y, int TR, int RS,
+                                                      T* __restrict__ y, int TR_, int RS_,
                                                       const T* res, int flip) {
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   constexpr int VE = 16 / sizeof(T);   // elements per 16-byte vector
   constexpr int NV = DW_CT / VE;       // 16-byte vectors per pixel in the tile (4 bf16, 8 f32)
   constexpr int SPP = DW_CT * 2 / 16;  // 16-byte slots per pixel in the LDS image: bf16 layout
   static_assert(sizeof(T) == 2 || sizeof(T) == 4, "dtype");
+  constexpr int NT = 64 * DW_CT / NC;  // threads: one wave per NC channels of the tile
+  static_assert(NT % NV == 0, "vector index must be constant per thread");
+  const int W = WC ? WC : W_;
+  const int TR = WC ? 64 / (WC / PW) : TR_;
+  const int RS = WC ? dw_row_slots(WC, PW, (int)sizeof(T)) : RS_;
   const int WP = W + 6;                // padded row width (pixels)
   const long R = (long)B * H;
   const long r0 = (long)blockIdx.x * TR;
@@ -269,103 +315,101 @@ __global__ __launch_bounds__(256) void dwconv7_kernel(int B, int H, int W, int C
   auto slot = [&](int r, int px, int s) { return r * RS + (SPP * px + px / PW) * (NV / SPP) + s; };
   // ---- stage the input patch (rows r0-3 .. r0+TR+2 of the flattened sequence) ----
   // batches of 8 loads per thread in flight (clamped address + zero select, no branches around
-  // the loads), then their LDS stores: a couple of memory round trips per block
-  const int tot = (TR + 6) * WP * NV;
+  // the loads), then their LDS stores: a couple of memory round trips per block.  Load i of the
+  // block is (pixel i / NV, vector i % NV); the vector index is the same for all of a thread's
+  // loads (256 % NV == 0) and its pixel advances by 256 / NV per load.
+  const int npx = (TR + 6) * WP;
   constexpr int BATCH = 8;
-  for (int i0 = 0; i0 < tot; i0 += 256 * BATCH) {
+  constexpr int PSTEP = NT / NV;
+  const int v = threadIdx.x % NV;
+  // buffer loads: the zero halo (and the batch tail) comes from the descriptor's range check
+  // (an offset past the tensor reads 0), so the loads need no branches or selects
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(R * W * C * (long)sizeof(T)), 0x00020000);
+  for (int p0 = threadIdx.x / NV; p0 < npx; p0 += PSTEP * BATCH) {
     uint4 val[BATCH];
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
-      const int i = i0 + u * 256 + threadIdx.x;
-      const int v = i % NV, px = i / NV;
+      const int px = p0 + u * PSTEP;
       const int pc = px % WP, pr = px / WP;
       const long gr = r0 - 3 + pr;
       const int gw = pc - 3;
-      const bool ok = i < tot && gr >= 0 && gr < R && gw >= 0 && gw < W;
-      const long src = ok ? ((gr * W) + gw) * C + cb + v * VE : 0;
-      const uint4 ld = *(const uint4*)(x + src);
-      val[u] = ok ? ld : make_uint4(0u, 0u, 0u, 0u);
+      const bool ok = px < npx && gr >= 0 && gr < R && gw >= 0 && gw < W;
+      const uint32_t off = ok ? (uint32_t)((((gr * W) + gw) * C + cb + v * VE) * (long)sizeof(T)) : 0x80000000u;
+      val[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
-      const int i = i0 + u * 256 + threadIdx.x;
-      if (i < tot) {
-        const int v = i % NV, px = i / NV;
-        img[slot(px / WP, px % WP, v)] = val[u];
-      }
+      const int px = p0 + u * PSTEP;
+      if (px < npx) img[slot(px / WP, px % WP, v)] = val[u];
     }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c0 = cb + wv * 8;      // this wave's 8 channels
+  const int c0 = cb + wv * NC;     // this wave's NC channels
   const int GW = W / PW;           // pixel groups per row
   const int lr = lane / GW, g = lane % GW;
   const long orow = r0 + lr;
   if (lr >= TR || orow >= R) return;
   const int h = (int)(orow % H);
   const int w0 = g * PW;
-  f32x2 acc[PW][4];
+  constexpr int NP = NC / 2;       // channel pairs per lane (packed fp32 FMAs)
+  f32x2 acc[PW][NP];
   {
-    f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
-    if (bias) { b0 = *(const f32x4*)(bias + c0); b1 = *(const f32x4*)(bias + c0 + 4); }
+    float b[NC];
 #pragma unroll
-    for (int p = 0; p < PW; ++p) {
-      acc[p][0] = f32x2{b0[0], b0[1]}; acc[p][1] = f32x2{b0[2], b0[3]};
-      acc[p][2] = f32x2{b1[0], b1[1]}; acc[p][3] = f32x2{b1[2], b1[3]};
-    }
+    for (int j = 0; j < NC; ++j) b[j] = 0.f;
+    if (bias) ldc<float, NC>(bias + c0, b);
+#pragma unroll
+    for (int p = 0; p < PW; ++p)
+#pragma unroll
+      for (int j = 0; j < NP; ++j) acc[p][j] = f32x2{b[2 * j], b[2 * j + 1]};
   }
+  // byte offset of this wave's channels inside a pixel's LDS slots
+  const int cofs = wv * NC * (int)sizeof(T);
+  const char* imgb = (const char*)img;
   for (int kh = 0; kh < 7; ++kh) {
     const int ih = h + kh - 3;
-    // the 7 taps of this kernel row for the wave's 8 channels: wave-uniform, loaded in one batch
+    // the 7 taps of this kernel row for the wave's channels: wave-uniform, loaded in one batch
     // (scalar loads) ahead of the window, so the taps cost one load round trip per row
-    f32x2 wt[7][4];
+    f32x2 wt[7][NP];
 #pragma unroll
     for (int kw = 0; kw < 7; ++kw) {
       // flip: the transposed convolution of the backward pass (tap (kh,kw) -> (6-kh,6-kw))
-      const float* wp = w + (flip ? 48 - (kh * 7 + kw) : kh * 7 + kw) * C + c0;
-      const f32x4 wa = *(const f32x4*)wp, wb = *(const f32x4*)(wp + 4);
-      wt[kw][0] = f32x2{wa[0], wa[1]}; wt[kw][1] = f32x2{wa[2], wa[3]};
-      wt[kw][2] = f32x2{wb[0], wb[1]}; wt[kw][3] = f32x2{wb[2], wb[3]};
+      float t[NC];
+      ldc<float, NC>(w + (flip ? 48 - (kh * 7 + kw) : kh * 7 + kw) * C + c0, t);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) wt[kw][j] = f32x2{t[2 * j], t[2 * j + 1]};
     }
     if (ih < 0 || ih >= H) continue;  // outside this lane's image (zero padding)
-    f32x2 win[PW + 6][4];
+    f32x2 win[PW + 6][NP];
 #pragma unroll
     for (int q = 0; q < PW + 6; ++q) {
-      float v[8];
-      if constexpr (sizeof(T) == 2) {
-        const bf16x8 u = __builtin_bit_cast(bf16x8, img[slot(lr + kh, w0 + q, wv)]);
+      float v[NC];
+      ldc<T, NC>((const T*)(imgb + slot(lr + kh, w0 + q, 0) * 16 + cofs), v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (float)u[j];
-      } else {
-        const f32x4 a = __builtin_bit_cast(f32x4, img[slot(lr + kh, w0 + q, 2 * wv)]);
-        const f32x4 b = __builtin_bit_cast(f32x4, img[slot(lr + kh, w0 + q, 2 * wv + 1)]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[j + 4] = b[j]; }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) win[q][j] = f32x2{v[2 * j], v[2 * j + 1]};
+      for (int j = 0; j < NP; ++j) win[q][j] = f32x2{v[2 * j], v[2 * j + 1]};
     }
 #pragma unroll
     for (int kw = 0; kw < 7; ++kw)
 #pragma unroll
       for (int p = 0; p < PW; ++p)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[p][j] = win[p + kw][j] * wt[kw][j] + acc[p][j];
+        for (int j = 0; j < NP; ++j) acc[p][j] = win[p + kw][j] * wt[kw][j] + acc[p][j];
   }
   T* out = y + (orow * W + w0) * C + c0;
 #pragma unroll
   for (int p = 0; p < PW; ++p) {
-    float o[8];
+    float o[NC];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { o[2 * j] = acc[p][j][0]; o[2 * j + 1] = acc[p][j][1]; }
+    for (int j = 0; j < NP; ++j) { o[2 * j] = acc[p][j][0]; o[2 * j + 1] = acc[p][j][1]; }
     if (res) {
-      float r[8];
-      V8<T>::load(res + (orow * W + w0 + p) * C + c0, r);
+      float r[NC];
+      ldc<T, NC>(res + (orow * W + w0 + p) * C + c0, r);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] += r[j];
+      for (int j = 0; j < NC; ++j) o[j] += r[j];
     }
-    V8<T>::store(out + (long)p * C, o);
+    stc<T, NC>(out + (long)p * C, o);
   }
 }
 
@@ -458,6 +502,14 @@ __global__ void sd_scales_kernel(int n, int B, const float* __restrict__ probs, 
 using namespace imgcap;
 
 namespace {
+// IMGCAP_DW_NC=4|8 forces the channels per lane of the depthwise kernel (A/B timing)
+int dw_nc_override() {
+  static const int v = [] {
+    const char* e = getenv("IMGCAP_DW_NC");
+    return e ? atoi(e) : 0;
+  }();
+  return v == 4 || v == 8 ? v : 0;
+}
 template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
                    hipStream_t st, const void* res = nullptr, int flip = 0) {
@@ -465,23 +517,39 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
   const int PW = W % 7 == 0 ? 7 : W % 8 == 0 ? 8 : W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 1;
   const int GW = W / PW, TR = 64 / GW;
   const long R = (long)B * H;
-  // row stride in 16-byte slots (see dwconv7_kernel): >= the row's slots, = 16/GW (mod 16)
-  const int mult = sizeof(T) / 2;  // fp32 pixels take twice the slots
-  const int base = (4 * (W + 6) + (W + 5) / PW + 1) * mult;
-  const int target = (GW == 1 || GW == 2 || GW == 4 || GW == 8 || GW == 16) ? (16 / GW) % 16 : 1;
-  int RS = base;
-  while (RS % 16 != target) ++RS;
+  const int RS = dw_row_slots(W, PW, (int)sizeof(T));
   const size_t shm = (size_t)(TR + 6) * RS * 16;
   dim3 grid((unsigned)((R + TR - 1) / TR), C / DW_CT);
-#define DW_(P)                                                                                                  \
-  hipLaunchKernelGGL((dwconv7_kernel<T, P>), grid, dim3(256), shm, st, B, H, W, C, (const T*)x, w, bias, (T*)y, TR, \
-                     RS, (const T*)res, flip)
-  switch (PW) {
-    case 8: DW_(8); break;
-    case 7: DW_(7); break;
-    case 4: DW_(4); break;
-    case 2: DW_(2); break;
-    default: DW_(1); break;
+  // channels per lane: 8 (4 waves per block).  4 (8 waves, twice the waves of the small
+  // late-stage grids) measured slower at every encoder shape (tools/microbench.py dw): the
+  // b64 reads of the 16-byte slot layout conflict 2-way and the staging is the same per block
+  const int nc = dw_nc_override() ? dw_nc_override() : 8;
+#define DW_(P, WC)                                                                                              \
+  do {                                                                                                         \
+    if (nc == 4)                                                                                               \
+      hipLaunchKernelGGL((dwconv7_kernel<T, P, WC, 4>), grid, dim3(512), shm, st, B, H, W, C, (const T*)x, w,    \
+                         bias, (T*)y, TR, RS, (const T*)res, flip);                                            \
+    else                                                                                                       \
+      hipLaunchKernelGGL((dwconv7_kernel<T, P, WC, 8>), grid, dim3(256), shm, st, B, H, W, C, (const T*)x, w,    \
+                         bias, (T*)y, TR, RS, (const T*)res, flip);                                            \
+  } while (0)
+  switch (W) {  // the encoder's stage widths at 224 and 256 pixel inputs
+    case 56: DW_(7, 56); break;
+    case 28: DW_(7, 28); break;
+    case 14: DW_(7, 14); break;
+    case 7: DW_(7, 7); break;
+    case 64: DW_(8, 64); break;
+    case 32: DW_(8, 32); break;
+    case 16: DW_(8, 16); break;
+    case 8: DW_(8, 8); break;
+    default:
+      switch (PW) {
+        case 8: DW_(8, 0); break;
+        case 7: DW_(7, 0); break;
+        case 4: DW_(4, 0); break;
+        case 2: DW_(2, 0); break;
+        default: DW_(1, 0); break;
+      }
   }
 #undef DW_
   IMGCAP_CHECK_LAUNCH("imgcap_dwconv7");
@@ -492,6 +560,8 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
 extern "C" int imgcap_dwconv7(int dtype, int B, int H, int W, int C, const void* x, const float* w,
                               const float* bias, void* y, void* stream) {
   IMGCAP_REQUIRE(C % DW_CT == 0, "imgcap_dwconv7: C must be a multiple of 32");
+  IMGCAP_REQUIRE((long)B * H * W * C * (dtype == IMGCAP_BF16 ? 2 : 4) < (1L << 31),
+                 "imgcap_dwconv7: input must be < 2 GiB (32-bit buffer offsets)");
   IMGCAP_REQUIRE(W >= 1 && W <= 64, "imgcap_dwconv7: W must be in [1, 64]");
   IMGCAP_REQUIRE(aligned16(x) && aligned16(y) && aligned16(w) && aligned16(bias), "imgcap_dwconv7: alignment");
   if ((long)B * H == 0) return 0;
@@ -507,6 +577,8 @@ extern "C" int imgcap_dwconv7_bwd_data(int dtype, int B, int H, int W, int C, co
                  "imgcap_dwconv7_bwd_data: alignment");
   // res may alias dx (each output element reads its own residual first); dz may not (neighbours)
   IMGCAP_REQUIRE(dz != dx, "imgcap_dwconv7_bwd_data: dz and dx must differ");
+  IMGCAP_REQUIRE((long)B * H * W * C * (dtype == IMGCAP_BF16 ? 2 : 4) < (1L << 31),
+                 "imgcap_dwconv7_bwd_data: input must be < 2 GiB (32-bit buffer offsets)");
   if ((long)B * H == 0) return 0;
   if (dtype == IMGCAP_BF16)
     return dwconv7_launch<bf16>(B, H, W, C, dz, w, nullptr, dx, (hipStream_t)stream, res, 1);

@@ -157,8 +157,27 @@ def misc():
     print(f"add_ln bwd {rows}x{cols}: {t * 1e6:8.1f} us")
 
 
+def dw():
+    """depthwise 7x7 at the C5 (Large, B=64) and C3 (Tiny, B=64) stage shapes: HBM GB/s and
+    the fp32-VALU floor (49 FMA per output element at 256 CUs x 128 FMA/clk x 2.4 GHz)."""
+    B = 64
+    for C0 in (96, 192):
+        for s, H in enumerate((56, 28, 14, 7)):
+            C = C0 << s
+            x = torch.randn(B, H, H, C, device=dev).to(bf)
+            y = torch.empty_like(x)
+            w = torch.randn(49, C, device=dev)
+            b = torch.randn(C, device=dev)
+            t = time_launch(lambda: K.dwconv7(x, w, b, y))
+            floor = x.numel() * 49 / (256 * 128 * 2.4e9)
+            print(f"dwconv7 B={B} H={H:2d} C={C:4d}: {t * 1e6:7.1f} us {2 * x.numel() * 2 / t / 1e9:7.1f} GB/s"
+                  f"  hbm floor {2 * x.numel() * 2 / 8e12 * 1e6:5.1f} us  valu floor {floor * 1e6:5.1f} us")
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which == "dw":
+        dw()
     if which in ("all", "gemm"):
         gemms()
     if which == "probe":
@@ -229,6 +248,140 @@ def overlap():
         t_h = time_launch(both, reps=3, warm=1)
     print(f"overlap (recurrence on a high-priority stream): {t_h * 1e6:.0f} us")
 
+    def both_rev():  # recurrence captured first, encoder second (graph node order)
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        rec()
+        with torch.cuda.stream(side):
+            encf()
+        cur.wait_stream(side)
+    t = time_launch(both_rev, reps=3, warm=1)
+    print(f"overlap (recurrence captured first): {t * 1e6:.0f} us")
+    t = time_launch(both, reps=3, warm=1, graph=False)
+    print(f"overlap (eager, no graph): {t * 1e6:.0f} us")
+
+    def interleaved():  # encoder stages captured between the recurrence halves
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        eng._launch("imgcap_lstm_tf_fwd", d)
+        with torch.cuda.stream(side):
+            encf()
+        eng._launch("imgcap_lstm_tf_bwd", d, ws)
+        cur.wait_stream(side)
+    t = time_launch(interleaved, reps=3, warm=1)
+    print(f"overlap (encoder captured between fwd and bwd recurrence): {t * 1e6:.0f} us")
+    ge, gr = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(ge, stream=side):
+            encf()
+    with torch.cuda.graph(gr):
+        rec()
+    torch.cuda.synchronize()
+
+    def two_graphs(order):
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        for o in order:
+            if o == "e":
+                with torch.cuda.stream(side):
+                    ge.replay()
+            else:
+                gr.replay()
+        cur.wait_stream(side)
+    for order in ("er", "re"):
+        two_graphs(order)
+        torch.cuda.synchronize()
+        t = time_launch(lambda: two_graphs(order), reps=3, warm=1, graph=False)
+        print(f"overlap (two graphs, launch order {order}): {t * 1e6:.0f} us")
+
+
+def cu_stream(n_cus, first=0, total=256):
+    """A HIP stream whose kernels may only use CUs [first, first + n_cus) of the mask numbering
+    (hipExtStreamCreateWithCUMask), wrapped for torch."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    words = (ctypes.c_uint32 * (total // 32))()
+    for i in range(first, first + n_cus):
+        words[i // 32] |= 1 << (i % 32)
+    st = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(total // 32), words)
+    assert rc == 0, rc
+    return torch.cuda.ExternalStream(st.value)
+
+
+def cumask():
+    """Encoder on a CU-masked stream beside the LSTM recurrence: the recurrence's small grids
+    keep the CUs the encoder may not use."""
+    from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    B, L, V = 32, 52, 9490
+    dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=dev,
+                               encoder_dim=768, dropout=0.5, compute_dtype=bf).to(dev)
+    enc = Encoder(variant="tiny", compute_dtype=bf).to(dev)
+    enc.fine_tune(False)
+    enc.train()
+    img = torch.randn(B, 3, 224, 224, device=dev)
+    eng = dec.engine()
+    feats = torch.randn(B, 7, 7, 768, device=dev).to(bf)
+    caps = torch.randint(1, V - 3, (B, L), device=dev)
+    lens = torch.full((B, 1), L, device=dev, dtype=torch.long)
+    s = eng.forward(feats, caps, lens, fixed_T=True)
+    eng.backward(s)
+    d = s["desc"]
+    ws = s["bwd_bufs"]["chain_ws"]
+
+    def rec():
+        eng._launch("imgcap_lstm_tf_fwd", d)
+        eng._launch("imgcap_lstm_tf_bwd", d, ws)
+
+    def encf():
+        with torch.no_grad():
+            enc(img)
+    t_r = time_launch(rec, reps=3, warm=1)
+    print(f"recurrence alone {t_r * 1e6:.0f} us")
+    # graphs replay their nodes on the launch stream (single-branch graphs), so a CU mask on the
+    # replay stream applies: the encoder graph on a masked stream, the recurrence graph beside it
+    encf()
+    torch.cuda.synchronize()
+    plain = torch.cuda.Stream()
+    ge, gr = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    plain.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(plain):
+        with torch.cuda.graph(ge, stream=plain):
+            encf()
+        with torch.cuda.graph(gr, stream=plain):
+            rec()
+    torch.cuda.synchronize()
+    main = torch.cuda.current_stream()
+    for n in (256, 224, 192, 160, 128):
+        se = cu_stream(n)
+        for rmask in ((None, "all") if n == 256 else (None, "all", "rest")):
+            sr = main if rmask in (None, "all") else cu_stream(256 - n, first=n)
+
+            def both():
+                se.wait_stream(main)
+                sr.wait_stream(main)
+                with torch.cuda.stream(se):
+                    ge.replay()
+                with torch.cuda.stream(sr):
+                    gr.replay()
+                main.wait_stream(se)
+                main.wait_stream(sr)
+            if rmask is None:
+                def enc_only():
+                    se.wait_stream(main)
+                    with torch.cuda.stream(se):
+                        ge.replay()
+                    main.wait_stream(se)
+                t = time_launch(enc_only, reps=3, warm=1, graph=False)
+                print(f"encoder graph on {n} CUs alone: {t * 1e6:.0f} us")
+                continue
+            t = time_launch(both, reps=3, warm=1, graph=False)
+            print(f"encoder graph on {n} CUs + recurrence graph on {rmask}: {t * 1e6:.0f} us")
+
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "overlap":
     overlap()
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "cumask":
+    cumask()
