@@ -236,6 +236,29 @@ class TeacherForcedTrainer:
         self._metric_log.append(red)
         return red
 
+    # -- checkpoint I/O (checkpoint.py; utils.py:195-224, train.py:118-147) ------------------
+    def optimizers(self):
+        """(encoderOptimizer, decoderOptimizer) as torch.optim.Adam state dicts in the reference's
+        parameter order (None for a frozen encoder) -- the values save_checkpoint stores."""
+        from . import checkpoint as ck
+        dec = ck.optimizer_state_dict(self.eng.fp, ck.trainable_parameters(self.decoder), self.decoder_lr)
+        enc = None
+        if self.enc_eng is not None:
+            enc = ck.optimizer_state_dict(self.enc_eng.fp, ck.trainable_parameters(self.encoder), self.encoder_lr)
+        return enc, dec
+
+    def load_optimizers(self, decoderOptimizer, encoderOptimizer=None):
+        """Resume (train.py:135-143): Adam moments, step counts and learning rates from the
+        reference-layout state dicts (the model weights are loaded with load_state_dict)."""
+        from . import checkpoint as ck
+        self.decoder_lr = ck.load_optimizer_state_dict(self.eng.fp, ck.trainable_parameters(self.decoder),
+                                                       decoderOptimizer)
+        if encoderOptimizer is not None:
+            if self.enc_eng is None:
+                raise ValueError("encoder optimizer state given but the encoder is frozen")
+            self.encoder_lr = ck.load_optimizer_state_dict(self.enc_eng.fp, ck.trainable_parameters(self.encoder),
+                                                           encoderOptimizer)
+
     def drain_metrics(self):
         """(globalLoss, tokens, top5 %) per logged step, like reduceLossAndTokens + accuracy."""
         if not self._metric_log:

@@ -1,0 +1,92 @@
+"""Resume from a checkpoint written by the reference (train.py:118-147): weights + Adam state
+loaded into the HIP trainer, one more step on the same batch == the reference's second step
+(tests/golden/ckpt_*); and the checkpoint the trainer writes carries its live Adam moments."""
+import json
+import os
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+from golden_util import GOLDEN_DIR
+
+pytestmark = pytest.mark.gpu
+
+
+class PassThrough(torch.nn.Module):
+    def forward(self, x):
+        return x
+
+
+@pytest.mark.parametrize("lstm", [True, False])
+def test_resume_matches_reference_second_step(hip_device, lstm, tmp_path):
+    from imagecaptioningconvnext_amd import checkpoint as C
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    name = "ckpt_lstm_small" if lstm else "ckpt_transformer_small"
+    ck = C.load_checkpoint(os.path.join(GOLDEN_DIR, name + ".pth.tar"))
+    t = load_file(os.path.join(GOLDEN_DIR, name + ".safetensors"))
+    with open(os.path.join(GOLDEN_DIR, name + ".json")) as f:
+        cfg = json.load(f)["cfg"]
+    if lstm:
+        from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
+        dec = DecoderWithAttention(attention_dim=cfg["A"], embed_dim=cfg["Em"], decoder_dim=cfg["D"],
+                                   vocab_size=cfg["V"], device=hip_device, encoder_dim=cfg["E"], dropout=0.0,
+                                   compute_dtype=torch.float32)
+    else:
+        from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
+        dec = TransformerDecoder(embed_dim=cfg["d"], decoder_dim=cfg["ff"], vocab_size=cfg["V"], maxLen=cfg["L"],
+                                 device=hip_device, wordMap=None, pretrained_embeddings_path=None,
+                                 fine_tune_embeddings=True, dropout=0.0, encoder_dim=cfg["E"], num_heads=cfg["H"],
+                                 num_layers=cfg["layers"], compute_dtype=torch.float32)
+    dec.load_state_dict(ck["decoder"])
+    dec = dec.to(hip_device)
+    tr = TeacherForcedTrainer(PassThrough(), dec, lstm=lstm, decoder_lr=1e-3, grad_clip=5.0)
+    tr.load_optimizers(ck["decoderOptimizer"])
+    assert tr.decoder_lr == 1e-4 and tr.eng.fp.step_count == 1
+    tr.step(t["enc"].to(hip_device), t["caps"].to(hip_device), t["caplens"].to(hip_device))
+    (loss, tokens, top5), = tr.drain_metrics()
+    assert abs(loss - t["ref_step2_loss"].item()) < 1e-4 * abs(t["ref_step2_loss"].item())
+    st = ck["decoderOptimizer"]["state"]
+    names = [n for n, p in dec.named_parameters() if p.requires_grad]
+    for i, (n, p) in enumerate((n, p) for n, p in dec.named_parameters() if p.requires_grad):
+        ref = t["post2." + n]
+        # entries whose step-1 or step-2 gradient is round-off noise (|g| < 1e-6) take an Adam
+        # step of arbitrary sign; they agree within 2 lr (as in test_oracle_golden)
+        g1 = st[i]["exp_avg"] / 0.1
+        g2 = t["grad2." + n]
+        ok = (g1.abs() >= 1e-6) & (g2.abs() >= 1e-6)
+        got = p.detach().float().cpu()
+        torch.testing.assert_close(got[ok], ref[ok], rtol=1e-5, atol=2e-6, msg=n)
+        assert (got - ref).abs().max().item() <= 2.5e-4, n
+    assert len(names) == len(st)
+    # the trainer's checkpoint: reference schema, moments of step 2, loadable by torch Adam
+    enc_sd, dec_sd = tr.optimizers()
+    assert enc_sd is None and dec_sd["state"][0]["step"].item() == 2.0
+    path = C.save_checkpoint("coco", 1, 0, None, dec.state_dict(), enc_sd, dec_sd, 0.0, False, [], lstm, 5, 1e-4,
+                             None if lstm else "none", directory=str(tmp_path))
+    back = C.load_checkpoint(path)
+    params = [torch.nn.Parameter(p.detach().float().cpu().clone()) for p in C.trainable_parameters(dec)]
+    torch.optim.Adam(params, lr=1e-4).load_state_dict(back["decoderOptimizer"])
+    fp = tr.eng.fp
+    o, shp = fp.offsets[names[0]]
+    n0 = torch.Size(shp).numel()
+    assert torch.equal(back["decoderOptimizer"]["state"][0]["exp_avg"].reshape(-1), fp.m[o:o + n0].cpu())
+
+
+def test_train_py_saves_and_resumes(hip_device, tmp_path, capsys):
+    """train.py --saveDir writes the reference-named checkpoint each epoch; --checkpoint resumes
+    from it at the next epoch with the saved Adam step count."""
+    import train
+    from imagecaptioningconvnext_amd import checkpoint as C
+    common = ["--teacherForcing", "--lstmDecoder", "--encoder", "tiny", "--batchSize", "4", "--steps", "2",
+              "--saveDir", str(tmp_path)]
+    train.main(common)
+    name = C.checkpoint_filename("coco_5_cap_per_img_5_min_word_freq", True, 5, 1e-4, None)
+    ck = C.load_checkpoint(os.path.join(str(tmp_path), name))
+    assert ck["epoch"] == 0 and ck["decoderOptimizer"]["state"][0]["step"].item() == 2.0
+    assert ck["encoderOptimizer"] is None and len(ck["results"]) == 1
+    train.main(common + ["--checkpoint", os.path.join(str(tmp_path), name)])
+    ck2 = C.load_checkpoint(os.path.join(str(tmp_path), name))
+    assert ck2["epoch"] == 1 and ck2["decoderOptimizer"]["state"][0]["step"].item() == 4.0
+    assert len(ck2["results"]) == 2
+    assert "epoch 1:" in capsys.readouterr().out

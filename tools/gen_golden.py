@@ -279,5 +279,66 @@ def gen_transformer_h64():
     return "transformer_tf_h64", t, meta
 
 
+def _gen_ckpt(lstm):
+    """Resume fixture: one reference train step, the checkpoint the
+    reference's own utils.save_checkpoint writes after it, then a second step on the same
+    batch (its post-step parameters and clamped gradients).  encoderSaved is None: the
+    reference Encoder needs torchvision (§8c), and the encoder keys are checked separately."""
+    import shutil
+    import tempfile
+    cfg = LSTM_SMALL if lstm else TRF_H64  # head dim 64: the HIP attention kernel's tile
+    tr = _train_module(lstm)
+    if not lstm:
+        tr.wordMap = word_map(cfg["V"])
+    dec = _lstm_decoder(cfg) if lstm else _transformer_decoder(cfg)
+    enc, caps, caplens = _inputs(cfg)
+    opt = torch.optim.Adam(params=filter(lambda p: p.requires_grad, dec.parameters()), lr=tr.decoderLr)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def step():
+        return tr.trainWithTeacherForcing(trainDataLoader=[(enc, caps, caplens)], encoder=PassThroughEncoder(),
+                                          decoder=dec, criterion=crit, encoderOptimizer=None,
+                                          decoderOptimizer=opt, epoch=0, device="cpu")
+    step()
+    utils_mod = sys.modules["utils.utils"]
+    name = "ckpt_lstm_small" if lstm else "ckpt_transformer_small"
+    cwd = os.getcwd()
+    tmp = tempfile.mkdtemp()
+    try:
+        os.chdir(tmp)
+        utils_mod.save_checkpoint("coco_5_cap_per_img_5_min_word_freq", 0, 0, None, dec.state_dict(), None, opt,
+                                  0.0, False, [], lstm, 5, 1e-4, None if lstm else "none")
+        (written,) = os.listdir(tmp)
+        shutil.copy(written, os.path.join(GOLDEN_DIR, name + ".pth.tar"))
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(tmp)
+    loss2, top5_2, _, _ = step()
+    t = dict(enc=enc, caps=caps, caplens=caplens, ref_step2_loss=torch.tensor([loss2]))
+    t.update({"post2." + n: p.detach().clone() for n, p in dec.named_parameters()})
+    t.update({"grad2." + n: p.grad.detach().clone() for n, p in dec.named_parameters() if p.grad is not None})
+    meta = dict(cfg=cfg, filename=written, param_order=[n for n, p in dec.named_parameters() if p.requires_grad],
+                source="utils.py:195-224 (save_checkpoint), train.py:118-147 (resume), train.py:240-302")
+    return name, t, meta
+
+
+def gen_ckpt_lstm():
+    return _gen_ckpt(True)
+
+
+def gen_ckpt_transformer():
+    return _gen_ckpt(False)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "ckpt":
+        fns = (gen_ckpt_lstm, gen_ckpt_transformer)
+        for fn in (fns[int(sys.argv[2]):int(sys.argv[2]) + 1] if len(sys.argv) > 2 else fns):
+            name, tensors, meta = fn()
+            save_file({k: v.detach().contiguous() for k, v in tensors.items()},
+                      os.path.join(GOLDEN_DIR, name + ".safetensors"))
+            with open(os.path.join(GOLDEN_DIR, name + ".json"), "w") as f:
+                json.dump(meta, f, indent=1)
+            print("wrote", name)
+    else:
+        main()

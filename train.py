@@ -59,6 +59,9 @@ def parse(argv=None):
     p.add_argument('--epochs', type=int, default=1)
     p.add_argument('--fineTuneFromEpoch', type=int, default=20,
                    help='epoch at which the encoder starts fine-tuning from --startingLayer (reference: 20)')
+    p.add_argument('--saveDir', type=str, default=None,
+                   help='write the reference-schema checkpoint (utils.py:195-224) here after every epoch')
+    p.add_argument('--dataName', type=str, default='coco_5_cap_per_img_5_min_word_freq')
     return p.parse_args(argv)
 
 
@@ -91,11 +94,14 @@ def build_models(args, device):
         decoder = TransformerDecoder(embed_dim=embDim, decoder_dim=decoderDim, vocab_size=VOCAB, maxLen=maxLen,
                                      dropout=dropout, device=device, wordMap=None, pretrained_embeddings_path=None,
                                      fine_tune_embeddings=True, encoder_dim=E)
-    if args.checkpoint:
-        ck = torch.load(args.checkpoint, map_location=device, weights_only=True)
-        encoder.load_state_dict(ck['encoder'])
+    ck = None
+    if args.checkpoint:  # train.py:125-147 (weights here; optimizer state once the trainer exists)
+        from imagecaptioningconvnext_amd.checkpoint import load_checkpoint
+        ck = load_checkpoint(args.checkpoint, map_location=device)
+        if ck['encoder'] is not None:
+            encoder.load_state_dict(ck['encoder'])
         decoder.load_state_dict(ck['decoder'])
-    return encoder, decoder.to(device)
+    return encoder, decoder.to(device), ck
 
 
 def trainWithTeacherForcing(trainDataLoader, encoder, decoder, trainer, epoch, lstm, log=print):
@@ -122,6 +128,37 @@ def trainWithTeacherForcing(trainDataLoader, encoder, decoder, trainer, epoch, l
     return losses.avg, top5accs.avg, batchTime.avg, dataTime.avg
 
 
+def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, world=1):
+    """The epoch loop of train.py:159-229 / trainMultiGPU.py: resume (train.py:130-147) from
+    ``ck``, fine-tune from --fineTuneFromEpoch, checkpoint every epoch (rank 0) when --saveDir."""
+    startEpoch, epochsSinceImprovement, results = 0, 0, []
+    if ck is not None:  # train.py:130-147
+        startEpoch = ck['epoch'] + 1
+        if startEpoch > args.fineTuneFromEpoch:
+            trainer.enable_encoder_finetune(args.startingLayer)
+        trainer.load_optimizers(ck['decoderOptimizer'],
+                                ck['encoderOptimizer'] if trainer.enc_eng is not None else None)
+        epochsSinceImprovement, results = ck['epochsSinceImprovement'], ck['results']
+    for epoch in range(startEpoch, startEpoch + args.epochs):
+        if epoch == args.fineTuneFromEpoch:  # train.py:160-166
+            trainer.enable_encoder_finetune(args.startingLayer)
+            log(f"Fine-tuning encoder from epoch {epoch} onwards (starting from layer {args.startingLayer})",
+                flush=True)
+        loader = synthetic_loader(args.steps, args.batchSize, device, rank=rank)
+        out = trainWithTeacherForcing(loader, encoder, decoder, trainer, epoch, args.lstmDecoder, log=log)
+        log(f"epoch {epoch}: loss {out[0]:.4f} top5 {out[1]:.2f} batch {out[2] * 1e3:.2f} ms ({world} GPUs)",
+            flush=True)
+        results.append({'epoch': epoch, 'trainLoss': out[0], 'trainTop5Acc': out[1], 'trainBatchTime': out[2],
+                        'trainDataTime': out[3]})
+        if args.saveDir and rank == 0:  # train.py:224-229; no validation / BLEU here (SURVEY.md §8f row 3)
+            from imagecaptioningconvnext_amd.checkpoint import save_checkpoint
+            encOpt, decOpt = trainer.optimizers()
+            path = save_checkpoint(args.dataName, epoch, epochsSinceImprovement, encoder.state_dict(),
+                                   decoder.state_dict(), encOpt, decOpt, 0.0, False, results, args.lstmDecoder,
+                                   args.startingLayer, args.encoderLr, args.embeddingName, directory=args.saveDir)
+            log(f"saved {path}", flush=True)
+
+
 def main(argv=None):
     args = parse(argv)
     if not args.teacherForcing:
@@ -129,17 +166,10 @@ def main(argv=None):
     torch.manual_seed(42)
     device = torch.device("cuda")
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
-    encoder, decoder = build_models(args, device)
+    encoder, decoder, ck = build_models(args, device)
     trainer = TeacherForcedTrainer(encoder, decoder, lstm=args.lstmDecoder, decoder_lr=decoderLr,
                                    encoder_lr=args.encoderLr, grad_clip=gradClip, alphaC=alphaC, graph=True)
-    for epoch in range(args.epochs):
-        if epoch == args.fineTuneFromEpoch:  # train.py:160-166
-            trainer.enable_encoder_finetune(args.startingLayer)
-            print(f"Fine-tuning encoder from epoch {epoch} onwards (starting from layer {args.startingLayer})",
-                  flush=True)
-        loader = synthetic_loader(args.steps, args.batchSize, device)
-        out = trainWithTeacherForcing(loader, encoder, decoder, trainer, epoch, args.lstmDecoder)
-        print(f"epoch {epoch}: loss {out[0]:.4f} top5 {out[1]:.2f} batch {out[2] * 1e3:.2f} ms", flush=True)
+    run_epochs(args, encoder, decoder, trainer, ck, device)
 
 
 if __name__ == '__main__':

@@ -39,20 +39,13 @@ def main(argv=None):
     rank, local, world, device = setup_distributed()
     torch.manual_seed(42 + rank)
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
-    encoder, decoder = train.build_models(args, device)
+    encoder, decoder, ck = train.build_models(args, device)
     trainer = TeacherForcedTrainer(encoder, decoder, lstm=args.lstmDecoder, decoder_lr=train.decoderLr,
                                    encoder_lr=args.encoderLr, grad_clip=train.gradClip, alphaC=train.alphaC,
                                    graph=True)
     log = print if rank == 0 else (lambda *a, **k: None)
-    for epoch in range(args.epochs):
-        if epoch == args.fineTuneFromEpoch:  # trainMultiGPU.py: encoder fine-tuned (and DDP-averaged) from epoch 20
-            trainer.enable_encoder_finetune(args.startingLayer)
-            log(f"Fine-tuning encoder from epoch {epoch} onwards (starting from layer {args.startingLayer})",
-                flush=True)
-        loader = train.synthetic_loader(args.steps, args.batchSize, device, rank=rank)
-        out = train.trainWithTeacherForcing(loader, encoder, decoder, trainer, epoch, args.lstmDecoder, log=log)
-        log(f"epoch {epoch}: global loss {out[0]:.4f} top5 {out[1]:.2f} batch {out[2] * 1e3:.2f} ms "
-            f"({world} GPUs)", flush=True)
+    # trainMultiGPU.py: encoder fine-tuned (and DDP-averaged) from epoch 20; rank 0 checkpoints
+    train.run_epochs(args, encoder, decoder, trainer, ck, device, rank=rank, log=log, world=world)
     dist.barrier()
     dist.destroy_process_group()
 
