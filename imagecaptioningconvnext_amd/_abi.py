@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("IMGCAP_LIB") or os.path.join(_HERE, "libimgcap_hip.so")
 
 F32, BF16 = 0, 1
+FP8MX = 2
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU = 0, 1, 2, 3
 
 c_void_p, c_int, c_int64, c_float, c_uint64, c_uint32 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
@@ -26,6 +27,7 @@ class Epilogue(ctypes.Structure):
         ("act", ctypes.c_int32), ("c_dtype", ctypes.c_int32), ("rows_per_scale", ctypes.c_int32),
         ("drop_stream", c_uint32),
         ("split_k", ctypes.c_int32),
+        ("c_scale", c_void_p),
     ]
 
 
@@ -111,6 +113,10 @@ _SIGS = {
     "imgcap_workspace_slot": [c_int],
     "imgcap_colsum_multi": [c_int, c_void_p, c_void_p],
     "imgcap_gemm_grouped": [c_int, c_int, c_int, c_void_p, c_void_p],
+    "imgcap_gemm_mx": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                       c_int64, ctypes.POINTER(Epilogue), c_void_p],
+    "imgcap_mx_quant_rows": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                             c_void_p],
     "imgcap_slice_reduce": [c_int64, c_int, c_void_p, c_int64, c_float, c_int64, c_void_p, c_void_p, c_void_p],
 }
 

@@ -215,6 +215,30 @@ DEV void raw8_to_f(const Raw8v& r, int dtype, float (&v)[8]) {
 // issued before the first use, so the pass costs one memory round trip instead of one per row.
 // Semantics = epi_vec8 / epi_scalar (imgcap_epilogue).
 // GAP: staged row r maps to output row m_base + r + (r >= ROWS/2 ? GAP : 0) (two row bands)
+// ---- MX-FP8 (OCP e4m3fn + E8M0 block scales of 32) -----------------------------------
+// The 8 values a lane holds are 8 consecutive columns; the 4 lanes lane&~3 .. lane|3 hold a
+// 32-column block (callers keep all 4 active together).  e = floor(log2(amax)) - 8 so the
+// block's largest magnitude lands in [256, 512) and is clamped to e4m3's 448.
+DEV void mx_store8(const float (&x)[8], uint8_t* q, uint8_t* s, bool write_scale, bool store = true) {
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(x[j]));
+  amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+  const int ex = (int)((__float_as_uint(amax) >> 23) & 0xff);  // biased exponent (0: zero/denormal block)
+  const int sb = ex == 0 ? 127 : max(ex - 8, 1);               // scale byte = e + 127
+  const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);  // 2^-(sb-127)
+  float c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = fminf(fmaxf(x[j] * inv, -448.f), 448.f);
+  uint32_t w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w0, true);
+  uint32_t w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], w1, true);
+  if (store) *(uint2*)q = make_uint2(w0, w1);
+  if (store && write_scale) *s = (uint8_t)sb;
+}
+
 template <int BN, int ROWS, int NT, int CH = 2, int GAP = 0>
 DEV void epilogue_tile(const imgcap_epilogue& ep, const float* tile, int LDT, int m_base, int n_base, int M, int N,
                        void* C, long ldc, bool vec_ok) {
@@ -315,7 +339,9 @@ DEV void epilogue_tile(const imgcap_epilogue& ep, const float* tile, int LDT, in
         for (int j = 0; j < 8; ++j) x[j] += ep.beta * o[j];
       }
       const long ci = (long)m * ldc + n;
-      if (ep.c_dtype == IMGCAP_BF16) {
+      if (ep.c_dtype == IMGCAP_FP8MX) {  // 4 lanes = one 32-column block: shared E8M0 scale
+        mx_store8(x, (uint8_t*)C + ci, ep.c_scale + (long)m * (ldc / 32) + n / 32, (threadIdx.x & 3) == 0);
+      } else if (ep.c_dtype == IMGCAP_BF16) {
         bf16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (bf16)x[j];
@@ -377,6 +403,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 #include "gemm_tiled.h"
 #include "gemm_glds.h"
 #include "gemm256.h"
+#include "gemm_mx.h"
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
@@ -877,5 +904,53 @@ extern "C" int imgcap_gemm_grouped(int a_kmajor, int b_kmajor, int n, const imgc
   else GG_(false, false);
 #undef GG_
   IMGCAP_CHECK_LAUNCH("imgcap_gemm_grouped");
+  return 0;
+}
+
+extern "C" int imgcap_gemm_mx(int M, int N, int K, const void* A, int64_t lda, const uint8_t* As, const void* B,
+                              int64_t ldb, const uint8_t* Bs, void* C, int64_t ldc, const imgcap_epilogue* epi,
+                              void* stream) {
+  IMGCAP_REQUIRE(M >= 0 && N >= 0 && K > 0 && K % 128 == 0, "imgcap_gemm_mx: K must be a positive multiple of 128");
+  if (M == 0 || N == 0) return 0;
+  IMGCAP_REQUIRE(aligned16(A) && aligned16(B) && lda % 16 == 0 && ldb % 16 == 0 && lda >= K && ldb >= K,
+                 "imgcap_gemm_mx: operands 16-byte aligned, row pitches >= K and multiples of 16 bytes");
+  IMGCAP_REQUIRE(((uintptr_t)As & 3) == 0 && ((uintptr_t)Bs & 3) == 0, "imgcap_gemm_mx: scales 4-byte aligned");
+  imgcap_epilogue ep{};
+  if (epi) ep = *epi;
+  else { ep.alpha = 1.f; ep.c_dtype = IMGCAP_BF16; ep.rows_per_scale = 1; }
+  if (ep.rows_per_scale <= 0) ep.rows_per_scale = 1;
+  IMGCAP_REQUIRE(ep.drop_p == 0.f && ep.aux == nullptr && ep.beta == 0.f && ep.split_k <= 1,
+                 "imgcap_gemm_mx: no dropout, aux, beta or split-K in this epilogue");
+  const int esz = ep.c_dtype == IMGCAP_F32 ? 4 : ep.c_dtype == IMGCAP_BF16 ? 2 : 1;
+  const bool vec_ok = aligned16(C) && (ldc * esz) % 16 == 0 && (!ep.res || (aligned16(ep.res) && ep.ldr % 8 == 0)) &&
+                      (!ep.bias || aligned16(ep.bias)) && (!ep.colscale || aligned16(ep.colscale));
+  if (ep.c_dtype == IMGCAP_FP8MX)
+    IMGCAP_REQUIRE(vec_ok && N % 32 == 0 && ldc % 32 == 0 && ep.c_scale && ep.res == nullptr,
+                   "imgcap_gemm_mx: MX-FP8 output needs N, ldc % 32 == 0, 16-byte aligned C, c_scale, no res");
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((N + 127) / 128, (M + 127) / 128);
+  hipLaunchKernelGGL((gemm_mx_kernel<2>), grid, dim3(256), 0, st, (const uint8_t*)A, (long)lda, As,
+                     (const uint8_t*)B, (long)ldb, Bs, C, (long)ldc, M, N, K, ep, vec_ok ? 1 : 0);
+  IMGCAP_CHECK_LAUNCH("imgcap_gemm_mx");
+  return 0;
+}
+
+extern "C" int imgcap_mx_quant_rows(int dtype, int R, int K, const void* x, int64_t ldx, const float* ln_w,
+                                    const float* ln_b, float eps, uint8_t* q, uint8_t* s, void* stream) {
+  IMGCAP_REQUIRE(R >= 0 && K > 0 && K % 32 == 0, "imgcap_mx_quant_rows: K must be a positive multiple of 32");
+  IMGCAP_REQUIRE((ln_w == nullptr) == (ln_b == nullptr), "imgcap_mx_quant_rows: ln_w and ln_b together");
+  IMGCAP_REQUIRE(((uintptr_t)q & 7) == 0, "imgcap_mx_quant_rows: q 8-byte aligned");
+  if (dtype == IMGCAP_BF16)
+    IMGCAP_REQUIRE(aligned16(x) && ldx % 8 == 0, "imgcap_mx_quant_rows: bf16 rows 16-byte aligned");
+  if (R == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((R + 3) / 4);
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL((mx_quant_rows_kernel<bf16>), grid, dim3(256), 0, st, R, K, (const bf16*)x, (long)ldx, ln_w,
+                       ln_b, eps, q, s);
+  else
+    hipLaunchKernelGGL((mx_quant_rows_kernel<float>), grid, dim3(256), 0, st, R, K, (const float*)x, (long)ldx, ln_w,
+                       ln_b, eps, q, s);
+  IMGCAP_CHECK_LAUNCH("imgcap_mx_quant_rows");
   return 0;
 }

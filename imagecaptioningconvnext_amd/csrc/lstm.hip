@@ -574,20 +574,50 @@ __global__ __launch_bounds__(256) void lstm_denc_kernel(int T, int P, int E, con
 // ---- doubly stochastic attention regularisation (train.py:269) --------------------------
 //   reg = alphaC * mean_{b,p} (1 - sum_t alpha[b,t,p])^2
 //   dalpha[b,t,p] = d reg / d alpha[b,t,p] for t < dl[b] (the written alphas), else 0
-__global__ void attn_reg_kernel(int B, int Tn, int P, const float* __restrict__ alphas, const int32_t* __restrict__ dl,
-                                float alphaC, float* __restrict__ dalpha, float* __restrict__ reg_out) {
-  __shared__ float red[16];
-  float acc = 0.f;
-  for (int e = threadIdx.x; e < B * P; e += blockDim.x) {
-    const int b = e / P, p = e % P;
-    float s = 0.f;
-    for (int t = 0; t < Tn; ++t) s += alphas[((long)b * Tn + t) * P + p];
-    acc += (1.f - s) * (1.f - s);
-    const float g = alphaC * 2.f * (s - 1.f) / (float)(B * P);
-    for (int t = 0; t < Tn; ++t) dalpha[((long)b * Tn + t) * P + p] = t < dl[b] ? g : 0.f;
+// one block per sample b: thread (p, t-slice) sums alpha over its steps, the per-pixel sums are
+// combined in LDS in a fixed order; the block writes dalpha[b] and its share of the loss to
+// part[b], summed in a fixed order by attn_reg_sum_kernel (deterministic, no atomics)
+constexpr int REG_TS = 16;  // step slices per pixel
+__global__ __launch_bounds__(1024) void attn_reg_kernel(int B, int Tn, int P, const float* __restrict__ alphas,
+                                                        const int32_t* __restrict__ dl, float alphaC,
+                                                        float* __restrict__ dalpha, float* __restrict__ part) {
+  __shared__ float ps[REG_TS][MAXP];
+  __shared__ float gs[MAXP];
+  const int b = blockIdx.x;
+  const int p = threadIdx.x % MAXP, ts = threadIdx.x / MAXP;
+  const float* a = alphas + (long)b * Tn * P;
+  float s = 0.f;
+  if (p < P)
+    for (int t = ts; t < Tn; t += REG_TS) s += a[(long)t * P + p];
+  ps[ts][p] = s;
+  __syncthreads();
+  if (threadIdx.x < MAXP) {
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < REG_TS; ++k) tot += ps[k][threadIdx.x];
+    const bool on = threadIdx.x < P;
+    gs[threadIdx.x] = on ? alphaC * 2.f * (tot - 1.f) / (float)(B * P) : 0.f;
+    float sq = on ? (1.f - tot) * (1.f - tot) : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+    if (threadIdx.x == 0) part[b] = sq;
   }
-  const float tot = block_sum(acc, red);
-  if (threadIdx.x == 0) *reg_out = alphaC * tot / (float)(B * P);
+  __syncthreads();
+  const int db = dl[b];
+  float* da = dalpha + (long)b * Tn * P;
+  for (int e = threadIdx.x; e < Tn * P; e += blockDim.x) {
+    const int t = e / P, pp = e % P;
+    da[e] = t < db ? gs[pp] : 0.f;
+  }
+}
+
+__global__ void attn_reg_sum_kernel(int B, int P, float alphaC, const float* __restrict__ part,
+                                    float* __restrict__ reg_out) {
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int b = 0; b < B; ++b) tot += part[b];
+    *reg_out = alphaC * tot / (float)(B * P);
+  }
 }
 
 static dim3 pw_grid(long n) {
@@ -733,8 +763,13 @@ extern "C" int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream) {
 
 extern "C" int imgcap_attn_reg(int B, int T, int P, const float* alphas, const int32_t* dl, float alphaC,
                                float* dalpha, float* reg_out, void* stream) {
-  hipLaunchKernelGGL(attn_reg_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, T, P, alphas, dl, alphaC, dalpha,
-                     reg_out);
+  IMGCAP_REQUIRE(P <= MAXP, "imgcap_attn_reg: P must be <= 64");
+  if (B == 0) return 0;
+  float* part = (float*)workspace((size_t)B * sizeof(float), (hipStream_t)stream);
+  if (!part) return fail(IMGCAP_EINVAL, "imgcap_attn_reg: workspace allocation failed");
+  hipLaunchKernelGGL(attn_reg_kernel, dim3(B), dim3(REG_TS * MAXP), 0, (hipStream_t)stream, B, T, P, alphas, dl, alphaC,
+                     dalpha, part);
+  hipLaunchKernelGGL(attn_reg_sum_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, B, P, alphaC, part, reg_out);
   IMGCAP_CHECK_LAUNCH("imgcap_attn_reg");
   return 0;
 }

@@ -131,6 +131,70 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None, bias=N
     return out
 
 
+def mx_quant_rows(x, ln_w=None, ln_b=None, eps=1e-6, out=None):
+    """Rows of x [R, K] (bf16 / fp32), LayerNorm'd first when ln_w/ln_b are given, to MX-FP8:
+    (q [R, K] uint8 e4m3fn bytes, s [R, K/32] uint8 E8M0 scales)."""
+    _check_dev(x, ln_w, ln_b)
+    R, Kc = x.shape
+    if out is None:
+        out = (torch.empty(R, Kc, device=x.device, dtype=torch.uint8),
+               torch.empty(R, Kc // 32, device=x.device, dtype=torch.uint8))
+    q, sc = out
+    _abi.call("imgcap_mx_quant_rows", dt(x), R, Kc, x.data_ptr(), x.stride(0), ptr(ln_w), ptr(ln_b), eps,
+              q.data_ptr(), sc.data_ptr(), stream())
+    return q, sc
+
+
+def mx_dequant(q, sc):
+    """MX-FP8 (q, scales) -> fp32 (test / diagnostics helper, torch ops)."""
+    v = q.view(torch.float8_e4m3fn).float()
+    e = (sc.to(torch.int32) - 127).float()
+    return (v.view(q.shape[0], -1, 32) * torch.exp2(e).unsqueeze(-1)).view(q.shape)
+
+
+def gemm_mx(a, b, *, out=None, out_dtype=torch.bfloat16, bias=None, act=ACT_NONE, colscale=None, rowscale=None,
+            rows_per_scale=1, res=None):
+    """epilogue(A @ B^T) on block-scaled fp8 operands: ``a`` = (q [M, K], s [M, K/32]), ``b`` =
+    (q [N, K], s [N, K/32]) as mx_quant_rows returns them (b: an nn.Linear weight).  out_dtype
+    "mx" returns the product itself in MX-FP8 (q, s) -- the next GEMM's A operand."""
+    (aq, as_), (bq, bs) = a, b
+    _check_dev(aq, bq, bias, res, colscale, rowscale)
+    M, Kc = aq.shape
+    N = bq.shape[0]
+    if bq.shape[1] != Kc:
+        raise ValueError(f"gemm_mx: K mismatch {Kc} vs {bq.shape[1]}")
+    mx = out_dtype == "mx"
+    if out is None:
+        out = ((torch.empty(M, N, device=aq.device, dtype=torch.uint8),
+                torch.empty(M, N // 32, device=aq.device, dtype=torch.uint8)) if mx else
+               torch.empty(M, N, device=aq.device, dtype=out_dtype))
+    ep = Epilogue()
+    ep.bias = ptr(bias)
+    ep.colscale = ptr(colscale)
+    ep.rowscale = ptr(rowscale)
+    ep.rows_per_scale = rows_per_scale
+    ep.res = ptr(res)
+    ep.ldr = 0 if res is None else res.stride(0)
+    ep.alpha = 1.0
+    ep.act = act
+    if mx:
+        oq, osc = out
+        ep.c_dtype = _abi.FP8MX
+        ep.c_scale = osc.data_ptr()
+        cptr, ldc = oq.data_ptr(), oq.stride(0)
+    else:
+        ep.c_dtype = dt(out)
+        cptr, ldc = out.data_ptr(), out.stride(0)
+    args = (M, N, Kc, aq.data_ptr(), aq.stride(0), as_.data_ptr(), bq.data_ptr(), bq.stride(0), bs.data_ptr(), cptr,
+            ldc)
+    if _gemm_recorder is not None:
+        keep = (aq, as_, bq, bs, out, bias, res, colscale, rowscale, ep)
+        _gemm_recorder.append(dict(M=M, N=N, K=Kc, mx=True, keep=keep,
+                                   call=lambda: _abi.call("imgcap_gemm_mx", *args, ctypes.byref(ep), stream())))
+    _abi.call("imgcap_gemm_mx", *args, ctypes.byref(ep), stream())
+    return out
+
+
 def gemm_raw(dtype, a_kmajor, b_kmajor, M, N, K, A, lda, B, ldb, C, ldc, c_dtype, *, batch=1, sA=0, sB=0, sC=0,
              bias=None, act=ACT_NONE, alpha=1.0, beta=0.0, rowscale=None, rows_per_scale=1, drop_p=0.0, seed=0,
              drop_stream=0, drop_ld=0, split_k=0):

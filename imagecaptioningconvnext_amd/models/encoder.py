@@ -105,10 +105,14 @@ class _EncoderTrain(torch.autograd.Function):
 
 
 class Encoder(nn.Module):
-    def __init__(self, encoded_image_size=7, variant="base", compute_dtype=torch.bfloat16):
+    def __init__(self, encoded_image_size=7, variant="base", compute_dtype=torch.bfloat16, frozen_fp8=False):
         super().__init__()
         self.enc_image_size = encoded_image_size
         self.variant = variant
+        # frozen_fp8: the frozen CNBlocks that run as two GEMMs (C >= 384) use block-scaled fp8
+        # (MX-FP8: LayerNorm -> fp8 rows, W1/W2 packed once, GELU output re-quantized in the
+        # first GEMM's epilogue) -- config C5's "frozen stages in fp8" 
+        self.frozen_fp8 = frozen_fp8
         self.encoder_dim = VARIANTS[variant][0][3]
         self.compute_dtype = compute_dtype
         self.convnext = build_features(variant)
@@ -130,7 +134,8 @@ class Encoder(nn.Module):
     # -- weight packing into kernel layouts ----------------------------------------------------
     def _pack_key(self):
         ps = list(self.convnext.parameters())
-        return (self.compute_dtype, ps[0].device, tuple(p._version for p in ps), tuple(p.data_ptr() for p in ps))
+        return (self.compute_dtype, self.frozen_fp8, ps[0].device, tuple(p._version for p in ps),
+                tuple(p.data_ptr() for p in ps))
 
     def _pack(self):
         key = self._pack_key()
@@ -155,6 +160,9 @@ class Encoder(nn.Module):
                         w1=l1.weight.to(ct).contiguous(), b1=l1.bias.float().contiguous(),
                         w2=l2.weight.to(ct).contiguous(), b2=l2.bias.float().contiguous(),
                         gamma=blk.layer_scale.reshape(C).float().contiguous(), sd=blk.sd_prob))
+                    if self._mx_stage(C):  # fp8 copies of the frozen Linear weights (rows = outputs)
+                        blocks[-1].update(w1mx=K.mx_quant_rows(l1.weight.float().contiguous()),
+                                          w2mx=K.mx_quant_rows(l2.weight.float().contiguous()))
                 down = None
                 if st < 3:
                     ln, cv = f[2 + 2 * st][0], f[2 + 2 * st][1]
@@ -165,6 +173,10 @@ class Encoder(nn.Module):
             pk["stages"] = stages
         self._packed, self._packed_key = pk, key
         return pk
+
+    def _mx_stage(self, C):
+        return (self.frozen_fp8 and self.compute_dtype == torch.bfloat16 and C not in K.CNBLOCK_MLP_CHANNELS
+                and C % 128 == 0)
 
     def _sd_scales(self, B, device):
         """StochasticDepth(p, "row") per-sample scales keep/(1-p) for every block (train mode),
@@ -198,7 +210,12 @@ class Encoder(nn.Module):
             z = torch.empty_like(x)
             hid = zn = None
             fused = ct == torch.bfloat16 and C in K.CNBLOCK_MLP_CHANNELS
-            if not fused:
+            mx = self._mx_stage(C) and "w1mx" in blocks[0]
+            if mx:
+                u8 = dict(device=dev, dtype=torch.uint8)
+                znq = (torch.empty(M, C, **u8), torch.empty(M, C // 32, **u8))
+                hidq = (torch.empty(M, 4 * C, **u8), torch.empty(M, 4 * C // 32, **u8))
+            elif not fused:
                 hid = torch.empty(M, 4 * C, device=dev, dtype=ct)
                 zn = torch.empty(M, C, device=dev, dtype=ct)
             x2 = x.view(M, C)
@@ -210,7 +227,15 @@ class Encoder(nn.Module):
                 else:        # wide images: row kernel with the LayerNorm fused
                     K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], z)
                     ln = (None, None)
-                if fused:  # LN -> Linear -> GELU -> Linear -> layer_scale -> drop path -> residual, on chip
+                if mx:  # LN -> fp8 rows; fp8 Linear + GELU -> fp8 hidden; fp8 Linear + scale + residual
+                    if ln[0] is not None:
+                        K.mx_quant_rows(z.view(M, C), ln[0], ln[1], 1e-6, out=znq)
+                    else:
+                        K.mx_quant_rows(z.view(M, C), out=znq)
+                    K.gemm_mx(znq, blk["w1mx"], bias=blk["b1"], act=K.ACT_GELU, out_dtype="mx", out=hidq)
+                    K.gemm_mx(hidq, blk["w2mx"], bias=blk["b2"], colscale=blk["gamma"], rowscale=rs,
+                              rows_per_scale=h * w, res=x2, out=x2)
+                elif fused:  # LN -> Linear -> GELU -> Linear -> layer_scale -> drop path -> residual, on chip
                     K.cnblock_mlp(z.view(M, C), blk["w1"], blk["b1"], blk["w2"], blk["b2"], blk["gamma"], x2,
                                   sd=rs, rows_per_sample=h * w, ln_w=ln[0], ln_b=ln[1])
                 else:

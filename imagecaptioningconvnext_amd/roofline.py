@@ -23,6 +23,7 @@ from . import kernels as K
 
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0
+PEAK_FP8_TFLOPS = 5000.0  # dense block-scaled (MX) e4m3 MFMA
 
 _KIND_NAME = {1: "gemm_skinny_kernel", 2: "gemm_kernel<64,64,64>", 3: "gemm_kernel<128,128,64>",
               4: "gemm_glds_kernel<128,128>", 5: "gemm256_kernel<256,256>"}
@@ -67,6 +68,11 @@ def _gemm_groups(trainer, batch):
     torch.cuda.synchronize()
     groups = collections.OrderedDict()
     for c in rec:
+        if c.get("mx"):  # block-scaled fp8 (frozen encoder Linears of C5)
+            g = groups.setdefault("gemm_mx_kernel (MX-FP8)", dict(name="gemm_mx_kernel (MX-FP8)", calls=[],
+                                                                   bound="mfma", symbol="gemm_mx_kernel", mx=True))
+            g["calls"].append(c)
+            continue
         kind, splits = K.gemm_plan(c["dtype"], c["ak"], c["bk"], c["M"], c["N"], c["K"], c["lda"], c["ldb"], 1,
                                    c["split_k"])
         name = _KIND_NAME.get(kind, f"gemm kind {kind}")
@@ -83,12 +89,14 @@ def _gemm_groups(trainer, batch):
         for c in g["calls"]:
             t_tot += time_launch(c["call"], reps=20, warm=2)
             f_tot += 2.0 * c["M"] * c["N"] * c["K"]
-            cb = 4 if c["keep"][-1].c_dtype == 0 else 2
-            b_tot += 2.0 * (c["M"] + c["N"]) * c["K"] + cb * c["M"] * c["N"]  # A + B read, C written once
+            ct = c["keep"][-1].c_dtype
+            cb = 4 if ct == 0 else 2 if ct == 1 else 1 + 1 / 32
+            ab = (1 + 1 / 32) if c.get("mx") else 2.0  # operand bytes per element (MX: + its scale)
+            b_tot += ab * (c["M"] + c["N"]) * c["K"] + cb * c["M"] * c["N"]  # A + B read, C written once
         n = len(g["calls"])
         shapes = sorted({(c["M"], c["N"], c["K"]) for c in g["calls"]})
         out.append(dict(name=g["name"], bound="mfma", per_step=n, t=t_tot / n, flops=f_tot / n, symbol=g["symbol"],
-                        bytes=b_tot / n,
+                        bytes=b_tot / n, peak=PEAK_FP8_TFLOPS if g.get("mx") else PEAK_BF16_TFLOPS,
                         note=f"{n} launches/step, shapes (M,N,K) {shapes[:6]}{' ...' if len(shapes) > 6 else ''}"))
     return out
 
@@ -160,7 +168,7 @@ def measure(cfg, trainer, batch, cfgname=None):
         peak, unit = PEAK_HBM_GBS, "GB/s"
     else:
         achieved = best["flops"] / t / 1e12
-        peak, unit = PEAK_BF16_TFLOPS, "TFLOP/s"
+        peak, unit = best.get("peak", PEAK_BF16_TFLOPS), "TFLOP/s"
     ranked = sorted(cands, key=lambda c: -c["share"])
     traffic = pmc_traffic(best.get("symbol"), cfgname) if cfgname else None
     return {"bound": best["bound"], "achieved": round(achieved, 2), "peak": peak, "unit": unit,

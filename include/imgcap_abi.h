@@ -25,6 +25,10 @@ extern "C" {
 #endif
 
 enum { IMGCAP_F32 = 0, IMGCAP_BF16 = 1 };
+/* Block-scaled fp8 (OCP MX-FP8): e4m3fn bytes, one E8M0 scale byte (2^(s-127)) per 32
+ * consecutive elements of a row.  Only as an imgcap_epilogue.c_dtype (imgcap_gemm_mx output)
+ * and as the operands of imgcap_gemm_mx. */
+enum { IMGCAP_FP8MX = 2 };
 enum { IMGCAP_OK = 0, IMGCAP_EINVAL = -1, IMGCAP_EUNSUPPORTED = -2 };
 /* ACT_GELU with an aux operand also writes the pre-activation to aux (the saved input of the
  * backward pass); ACT_DGELU multiplies by GELU'(aux[m, n]) (aux = that saved pre-activation). */
@@ -78,6 +82,7 @@ typedef struct imgcap_epilogue {
                               fp32 C = alpha*A.B + beta*C (no other epilogue, batch 1): slices
                               write fp32 partials to library scratch, a second kernel adds them
                               in fixed order (deterministic) */
+  uint8_t* c_scale;        /* c_dtype IMGCAP_FP8MX: the E8M0 block scales of C, [M][ldc / 32] */
 } imgcap_epilogue;
 
 int imgcap_gemm(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K,
@@ -98,6 +103,22 @@ typedef struct imgcap_gemm_problem {
   float alpha, beta;
 } imgcap_gemm_problem;
 int imgcap_gemm_grouped(int a_kmajor, int b_kmajor, int n, const imgcap_gemm_problem* probs, void* stream);
+
+/* Block-scaled fp8 GEMM (v_mfma_scale_f32_16x16x128_f8f6f4): C = epilogue(A . B^T) with
+ * A [M][K] e4m3fn bytes (row pitch lda bytes) and its E8M0 scales As [M][K/32], B [N][K]
+ * (nn.Linear weight layout, pitch ldb) and Bs [N][K/32]; K % 128 == 0, pitches % 16 == 0.
+ * The epilogue is imgcap_gemm's (bias, act, colscale, rowscale, res; no dropout, aux, beta or
+ * split-K) with c_dtype IMGCAP_BF16 / IMGCAP_F32, or IMGCAP_FP8MX (N % 32 == 0): C then gets
+ * e4m3fn bytes and ep->c_scale the block scales -- the next product's A operand.  The frozen
+ * ConvNeXt pointwise Linears of config C5 ("frozen stages in fp8"). */
+int imgcap_gemm_mx(int M, int N, int K, const void* A, int64_t lda, const uint8_t* As, const void* B,
+                   int64_t ldb, const uint8_t* Bs, void* C, int64_t ldc, const imgcap_epilogue* epi,
+                   void* stream);
+/* Rows of x [R][K] (dtype, pitch ldx elements), optionally LayerNorm'd first (ln_w/ln_b not
+ * NULL: y = LN(x)*ln_w + ln_b, eps), to MX-FP8: q [R][K] bytes, s [R][K/32]; K % 32 == 0.
+ * Per block of 32: e = floor(log2(amax)) - 8, s = e + 127, q = e4m3(clamp(v * 2^-e, +-448)). */
+int imgcap_mx_quant_rows(int dtype, int R, int K, const void* x, int64_t ldx, const float* ln_w,
+                         const float* ln_b, float eps, uint8_t* q, uint8_t* s, void* stream);
 
 /* out[c, r] = in[r, c]  (weight transposes for the k-major skinny GEMMs) */
 /* Which kernel imgcap_gemm launches for these operands (diagnostics and the bench's roofline):

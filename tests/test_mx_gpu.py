@@ -1,0 +1,104 @@
+"""Block-scaled fp8 (MX-FP8) path of the frozen encoder (config C5): the
+quantizer against a torch restatement (exact bytes), the MX GEMM against fp32 products of the
+dequantized operands, and the fp8 encoder against its bf16 path."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _mx_ref(v):
+    """torch restatement of imgcap_mx_quant_rows' block encoding (fp32 rows [R, K])."""
+    R, Kc = v.shape
+    blk = v.view(R, Kc // 32, 32)
+    amax = blk.abs().amax(-1)
+    ex = ((amax.view(torch.int32) >> 23) & 0xFF)
+    sb = torch.where(ex == 0, torch.full_like(ex, 127), (ex - 8).clamp(min=1))
+    inv = torch.exp2((127 - sb).float()).unsqueeze(-1)
+    q = (blk * inv).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8).view(R, Kc)
+    return q, sb.to(torch.uint8)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mx_quant_rows_exact(hip_device, dtype):
+    from imagecaptioningconvnext_amd import kernels as K
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(37, 384, generator=g) * torch.logspace(-3, 2, 384)).to(dtype)
+    x[5, :32] = 0.0  # an all-zero block
+    q, s = K.mx_quant_rows(x.to(hip_device))
+    rq, rs = _mx_ref(x.float())
+    assert torch.equal(s.cpu(), rs)
+    assert torch.equal(q.cpu(), rq)
+    assert _rel(K.mx_dequant(q, s), x.float()) < 0.04
+
+
+def test_mx_quant_rows_layernorm(hip_device):
+    from imagecaptioningconvnext_amd import kernels as K
+    g = torch.Generator().manual_seed(4)
+    x = (torch.randn(50, 768, generator=g) * 3 + 1).bfloat16()
+    w, b = 1 + 0.1 * torch.randn(768, generator=g), 0.1 * torch.randn(768, generator=g)
+    q, s = K.mx_quant_rows(x.to(hip_device), w.to(hip_device), b.to(hip_device), 1e-6)
+    ref = F.layer_norm(x.float(), (768,), w, b, 1e-6)
+    assert _rel(K.mx_dequant(q, s), ref) < 0.04
+    rq, rs = _mx_ref(ref)
+    assert (s.cpu().int() - rs.int()).abs().max().item() <= 1  # block exponents agree (LN round-off)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(300, 192, 256), (128, 128, 128), (1000, 3072, 768), (517, 768, 3072)])
+def test_gemm_mx_matches_dequantized_product(hip_device, M, N, Kd):
+    from imagecaptioningconvnext_amd import kernels as K
+    g = torch.Generator().manual_seed(M + N)
+    a, b = torch.randn(M, Kd, generator=g), torch.randn(N, Kd, generator=g) / Kd ** 0.5
+    bias = torch.randn(N, generator=g)
+    aq, bq = K.mx_quant_rows(a.to(hip_device)), K.mx_quant_rows(b.to(hip_device))
+    ref = K.mx_dequant(*aq).cpu() @ K.mx_dequant(*bq).cpu().t() + bias
+    out = K.gemm_mx(aq, bq, bias=bias.to(hip_device), out_dtype=torch.float32)
+    assert _rel(out, ref) < 5e-5  # fp32 accumulation inside the MFMA (not bit-exact vs a sequential sum)
+    # fused GELU + MX-FP8 output (the hidden activation of the frozen CNBlock)
+    hq = K.gemm_mx(aq, bq, bias=bias.to(hip_device), act=K.ACT_GELU, out_dtype="mx")
+    rq, rs = _mx_ref(F.gelu(ref))
+    assert (hq[1].cpu().int() - rs.int()).abs().max().item() <= 1
+    assert _rel(K.mx_dequant(*hq), F.gelu(ref)) < 0.04
+
+
+def test_gemm_mx_residual_epilogue(hip_device):
+    """bf16 out = x + gamma * rowscale * (A B^T + b): the second Linear of the frozen CNBlock."""
+    from imagecaptioningconvnext_amd import kernels as K
+    g = torch.Generator().manual_seed(9)
+    M, N, Kd, hw = 2 * 196, 384, 1536, 196
+    a, b = torch.randn(M, Kd, generator=g), torch.randn(N, Kd, generator=g) / Kd ** 0.5
+    bias, gamma = torch.randn(N, generator=g), torch.rand(N, generator=g)
+    rs = torch.tensor([0.0, 2.0])
+    x = torch.randn(M, N, generator=g).bfloat16()
+    aq, bq = K.mx_quant_rows(a.to(hip_device)), K.mx_quant_rows(b.to(hip_device))
+    prod = K.mx_dequant(*aq).cpu() @ K.mx_dequant(*bq).cpu().t()
+    ref = x.float() + (prod + bias) * gamma * rs.repeat_interleave(hw).unsqueeze(1)
+    xd = x.to(hip_device)
+    K.gemm_mx(aq, bq, bias=bias.to(hip_device), colscale=gamma.to(hip_device), rowscale=rs.to(hip_device),
+              rows_per_scale=hw, res=xd, out=xd)
+    assert _rel(xd, ref) < 1e-2
+
+
+def test_fp8_encoder_close_to_bf16(hip_device):
+    """Frozen encoder with the MX-FP8 stages (C >= 384) vs its bf16 path: same weights, images."""
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    torch.manual_seed(0)
+    enc = Encoder(variant="tiny").to(hip_device).eval()
+    with torch.no_grad():
+        for m in enc.modules():  # layer scale 1e-6 would hide the blocks; make them count
+            if hasattr(m, "layer_scale"):
+                m.layer_scale.fill_(0.5)
+    img = torch.randn(2, 3, 224, 224, device=hip_device)
+    with torch.no_grad():
+        ref = enc(img).float()
+        enc.frozen_fp8 = True
+        got = enc(img).float()
+    assert enc._pack()["stages"][2][0][0].get("w1mx") is not None
+    err = _rel(got, ref)
+    assert 0 < err < 0.08, err
