@@ -31,9 +31,10 @@ CONFIGS = {
     "C3": dict(encoder="tiny", decoder="transformer", batch=64),
     "C4": dict(encoder="base", decoder="transformer", batch=32),
     # ConvNeXt-Large + Transformer, encoder fine-tuned from startingLayer=7 (stage 4 trains)
-    "C5": dict(encoder="large", decoder="transformer", batch=64, starting_layer=7),
+    "C5": dict(encoder="large", decoder="transformer", batch=64, starting_layer=7, frozen_fp8=True),
 }
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0    # dense block-scaled e4m3 MFMA
 PEAK_HBM_GBS = 8000.0       # HBM3E spec
 
 
@@ -48,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run encoder and decoder of a step back to back (no two-stream overlap)")
+    ap.add_argument("--no-fp8", action="store_true", help="C5: frozen encoder GEMMs in bf16 instead of MX-FP8")
     return ap.parse_args()
 
 
@@ -68,7 +70,8 @@ def synthetic_batch(B, rank, step, device):
 def build(cfg, device):
     from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
     from imagecaptioningconvnext_amd.models.encoder import Encoder
-    enc = Encoder(variant=cfg["encoder"], compute_dtype=torch.bfloat16).to(device)
+    enc = Encoder(variant=cfg["encoder"], compute_dtype=torch.bfloat16, frozen_fp8=cfg.get("frozen_fp8", False))
+    enc = enc.to(device)
     if "starting_layer" in cfg:
         enc.fine_tune(True, startingLayer=cfg["starting_layer"])
     else:
@@ -83,6 +86,22 @@ def build(cfg, device):
                                  wordMap=None, pretrained_embeddings_path=None, fine_tune_embeddings=True,
                                  dropout=0.5, encoder_dim=E, compute_dtype=torch.bfloat16).to(device)
     return enc, dec
+
+
+def fp8_flops_per_image(cfg, enc):
+    """FLOPs per image of the frozen CNBlock Linears that run in MX-FP8 (the rest is bf16)."""
+    if not enc.frozen_fp8:
+        return 0
+    from imagecaptioningconvnext_amd.models.encoder import VARIANTS
+    chans, depths, _ = VARIANTS[cfg["encoder"]]
+    start = cfg.get("starting_layer", 8)
+    f, h = 0, 56
+    for st in range(4):
+        C = chans[st]
+        if 1 + 2 * st < start and enc._mx_stage(C):
+            f += 2 * depths[st] * 2 * h * h * C * 4 * C
+        h //= 2
+    return f
 
 
 def flops_per_image(cfg, enc):
@@ -145,7 +164,9 @@ def cpu_baseline(seconds):
 
 def main():
     args = parse()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.no_fp8:
+        cfg["frozen_fp8"] = False
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -187,6 +208,7 @@ def main():
     ms = elapsed / args.steps * 1e3
     imgs_per_s = B * world * args.steps / elapsed
     fpi = flops_per_image(cfg, enc)
+    fp8_fpi = fp8_flops_per_image(cfg, enc)
     if rank == 0:
         from imagecaptioningconvnext_amd import roofline
         roof = roofline.measure(cfg, trainer, batches[0], cfgname=args.config)
@@ -201,7 +223,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" + (" + MX-FP8 (e4m3, 32-element E8M0 block scales) frozen encoder Linears"
+                               if fp8_fpi else ""),
             "pipeline": "encoder(batch i+1) || decoder fwd/bwd(batch i), two HIP streams in one graph"
                         if pipeline else "sequential",
             "data": "synthetic (224x224x3 U[0,1) ImageNet-normalised, random captions len 52), random-init weights",
@@ -212,7 +235,9 @@ def main():
                        "per_gpu_batch": B, "global_batch": B * world, "image": 224, "caption_len": CAPLEN,
                        "vocab": V, "parallelism": f"dp{world}"},
             "step_flops_per_image": fpi,
-            "step_mfma_frac": round(imgs_per_s * fpi / (world * PEAK_BF16_TFLOPS * 1e12), 5),
+            # mixed peak for fp8 configs: ideal = F_fp8 / 5 PF + F_bf16 / 2.5 PF
+            "step_mfma_frac": round(imgs_per_s * (fp8_fpi / PEAK_FP8_TFLOPS + (fpi - fp8_fpi) / PEAK_BF16_TFLOPS)
+                                    / (world * 1e12), 5),
             "last_loss": round(metrics[-1][0], 5) if metrics else None,
             "last_top5": round(metrics[-1][2], 4) if metrics else None,
             "roofline": roof,

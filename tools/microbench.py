@@ -157,6 +157,27 @@ def misc():
     print(f"add_ln bwd {rows}x{cols}: {t * 1e6:8.1f} us")
 
 
+def mx():
+    """MX-FP8 vs bf16 GEMMs at the frozen ConvNeXt-Large stage-3 shapes (C5, B=64)."""
+    M, C = 64 * 196, 768
+    for (N, Kd) in ((4 * C, C), (C, 4 * C)):
+        a = torch.randn(M, Kd, device=dev)
+        w = torch.randn(N, Kd, device=dev) / Kd ** 0.5
+        ab, wb = a.to(bf), w.to(bf)
+        aq, wq = K.mx_quant_rows(a), K.mx_quant_rows(w)
+        fl = 2.0 * M * N * Kd
+        t = time_launch(lambda: K.gemm(ab, wb, trans_b=True))
+        print(f"bf16 gemm M={M} N={N} K={Kd}: {t * 1e6:7.1f} us {fl / t / 1e12:7.1f} TF")
+        t = time_launch(lambda: K.gemm_mx(aq, wq))
+        print(f"mx   gemm M={M} N={N} K={Kd}: {t * 1e6:7.1f} us {fl / t / 1e12:7.1f} TF (bf16 out)")
+        t = time_launch(lambda: K.gemm_mx(aq, wq, act=K.ACT_GELU, out_dtype="mx"))
+        print(f"mx   gemm M={M} N={N} K={Kd}: {t * 1e6:7.1f} us {fl / t / 1e12:7.1f} TF (GELU + MX out)")
+    x = torch.randn(M, C, device=dev).to(bf)
+    g = torch.ones(C, device=dev)
+    t = time_launch(lambda: K.mx_quant_rows(x, g, g))
+    print(f"mx_quant_rows+LN {M}x{C}: {t * 1e6:7.1f} us {M * C * 3 / t / 1e9:7.1f} GB/s")
+
+
 def dw():
     """depthwise 7x7 at the C5 (Large, B=64) and C3 (Tiny, B=64) stage shapes: HBM GB/s and
     the fp32-VALU floor (49 FMA per output element at 256 CUs x 128 FMA/clk x 2.4 GHz)."""
@@ -178,6 +199,8 @@ if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which == "dw":
         dw()
+    if which == "mx":
+        mx()
     if which in ("all", "gemm"):
         gemms()
     if which == "probe":
