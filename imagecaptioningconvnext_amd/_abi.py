@@ -78,6 +78,7 @@ _SIGS = {
                                  c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "imgcap_convnext_stem": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p],
+    "imgcap_convnext_stem_u8": [c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 9,
     "imgcap_dwconv7_ln": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p],
     "imgcap_ln_patchify2": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,

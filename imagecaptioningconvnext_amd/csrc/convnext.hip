@@ -12,11 +12,28 @@ namespace imgcap {
 // stem: block = NPX output pixels; their 4x4x3 patches and the [48][C0] weights are staged in
 // LDS; thread = (pixel, 8 output channels): 48x8 MACs, then the per-pixel LayerNorm over C0
 // is a fixed-order LDS reduction across the pixel's C0/8 threads.
-template <typename T>
-__global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0, const float* __restrict__ img,
+// TI = uint8_t: raw 0..255 pixels (the reference's HDF5 images, dataLoader.py:43-46), turned into
+// the reference's normalised input in the patch load: x = float(u / 255.) (double division, as
+// numpy computes it), then (x - mean[c]) / std[c] in fp32 (torchvision Normalize).
+template <typename TI> struct StemIn;
+template <> struct StemIn<float> {
+  static DEV f32x4 load(const float* p, int, const float*, const float*) { return *(const f32x4*)p; }
+};
+template <> struct StemIn<uint8_t> {
+  static DEV f32x4 load(const uint8_t* p, int ci, const float* nmean, const float* nstd) {
+    const uchar4 u = *(const uchar4*)p;
+    const float m = nmean[ci], sd = nstd[ci];
+    auto f = [&](unsigned char c) { return __fdiv_rn((float)((double)c / 255.0) - m, sd); };
+    return f32x4{f(u.x), f(u.y), f(u.z), f(u.w)};
+  }
+};
+
+template <typename T, typename TI = float>
+__global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0, const TI* __restrict__ img,
                                                     const float* __restrict__ w, const float* __restrict__ bias,
                                                     const float* __restrict__ lw, const float* __restrict__ lb,
-                                                    T* __restrict__ out, int npx) {
+                                                    T* __restrict__ out, int npx, const float* __restrict__ nmean,
+                                                    const float* __restrict__ nstd) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int CV = C0 / 8;
   float* ws = sm;                     // [48][C0]
@@ -36,7 +53,7 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
     f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
     if (px < total) {
       const int b = (int)(px / (HO * WO)), rem = (int)(px % (HO * WO)), oh = rem / WO, ow = rem % WO;
-      v = *(const f32x4*)(img + (((long)b * 3 + ci) * H + oh * 4 + kh) * W + ow * 4);
+      v = StemIn<TI>::load(img + (((long)b * 3 + ci) * H + oh * 4 + kh) * W + ow * 4, ci, nmean, nstd);
     }
     *(f32x4*)(patch + q * 48 + ci * 16 + kh * 4) = v;
   }
@@ -610,12 +627,38 @@ extern "C" int imgcap_convnext_stem(int dtype, int B, int H, int W, int C0, cons
   const size_t shm = (48 * C0 + npx * 48 + npx * CV + npx * 2) * sizeof(float);
   IMGCAP_REQUIRE(shm <= 160 * 1024, "imgcap_convnext_stem: LDS");
   if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(stem_kernel<bf16>, grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, images, w, bias,
-                       ln_w, ln_b, (bf16*)out, npx);
+    hipLaunchKernelGGL((stem_kernel<bf16, float>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, images,
+                       w, bias, ln_w, ln_b, (bf16*)out, npx, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(stem_kernel<float>, grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, images, w, bias,
-                       ln_w, ln_b, (float*)out, npx);
+    hipLaunchKernelGGL((stem_kernel<float, float>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0,
+                       images, w, bias, ln_w, ln_b, (float*)out, npx, nullptr, nullptr);
   IMGCAP_CHECK_LAUNCH("imgcap_convnext_stem");
+  return 0;
+}
+
+extern "C" int imgcap_convnext_stem_u8(int dtype, int B, int H, int W, int C0, const uint8_t* images,
+                                       const float* mean3, const float* std3, const float* w, const float* bias,
+                                       const float* ln_w, const float* ln_b, void* out, void* stream) {
+  IMGCAP_REQUIRE(H % 4 == 0 && W % 4 == 0 && C0 % 8 == 0 && C0 <= 1024, "imgcap_convnext_stem_u8: bad shape");
+  IMGCAP_REQUIRE(((uintptr_t)images & 3) == 0 && aligned16(bias) && aligned16(ln_w) && aligned16(ln_b) &&
+                     aligned16(out) && mean3 && std3,
+                 "imgcap_convnext_stem_u8: alignment / normalisation constants");
+  const long total = (long)B * (H / 4) * (W / 4);
+  if (total == 0) return 0;
+  const int CV = C0 / 8;
+  int npx = 1024 / CV;
+  if (npx > 64) npx = 64;
+  const int threads = ((npx * CV + 63) / 64) * 64;
+  dim3 grid((unsigned)((total + npx - 1) / npx));
+  const size_t shm = (48 * C0 + npx * 48 + npx * CV + npx * 2) * sizeof(float);
+  IMGCAP_REQUIRE(shm <= 160 * 1024, "imgcap_convnext_stem_u8: LDS");
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL((stem_kernel<bf16, uint8_t>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0,
+                       images, w, bias, ln_w, ln_b, (bf16*)out, npx, mean3, std3);
+  else
+    hipLaunchKernelGGL((stem_kernel<float, uint8_t>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0,
+                       images, w, bias, ln_w, ln_b, (float*)out, npx, mean3, std3);
+  IMGCAP_CHECK_LAUNCH("imgcap_convnext_stem_u8");
   return 0;
 }
 

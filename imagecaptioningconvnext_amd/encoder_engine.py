@@ -67,7 +67,8 @@ class EncoderEngine:
     def forward(self, images):
         """Encoder.forward (encoder.py:23-27) in train mode; returns (features [B,s,s,E], saved)."""
         enc, ct = self.enc, self.ct
-        images = images.float().contiguous()
+        from .models.encoder import as_input
+        images = as_input(images)
         B, _, H, W = images.shape
         dev = images.device
         sd = enc._sd_scales(B, dev) if enc.training else None

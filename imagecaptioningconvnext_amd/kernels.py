@@ -354,8 +354,16 @@ def cast(x, out):
     return out
 
 
-def convnext_stem(images, w, bias, ln_w, ln_b, out):
+def convnext_stem(images, w, bias, ln_w, ln_b, out, norm=None):
+    """Stem conv 4x4/s4 + LayerNorm2d -> NHWC.  images: normalised fp32, or raw uint8 pixels with
+    ``norm`` = (mean[3], std[3]) fp32 device tensors (normalised in the kernel)."""
     B, _, H, W = images.shape
+    if images.dtype == torch.uint8:
+        mean, std = norm
+        _abi.call("imgcap_convnext_stem_u8", dt(out), B, H, W, w.shape[0], images.data_ptr(), mean.data_ptr(),
+                  std.data_ptr(), w.data_ptr(), bias.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(), out.data_ptr(),
+                  stream())
+        return out
     _abi.call("imgcap_convnext_stem", dt(out), B, H, W, w.shape[0], images.data_ptr(), w.data_ptr(),
               bias.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(), out.data_ptr(), stream())
     return out

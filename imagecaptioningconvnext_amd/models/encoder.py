@@ -42,6 +42,16 @@ class _Permute(nn.Module):
         self.dims = dims
 
 
+IMAGENET_MEAN = (0.485, 0.456, 0.406)  # train.py:152 transforms.Normalize
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def as_input(images):
+    """Encoder input: normalised fp32 images, or the dataset's raw uint8 pixels (kept as bytes:
+    the stem kernel normalises them, dataLoader.py:46 + train.py:152)."""
+    return images.contiguous() if images.dtype == torch.uint8 else images.float().contiguous()
+
+
 class CNBlock(nn.Module):
     """torchvision CNBlock parameter layout: block.{0: dwconv, 2: LayerNorm, 3: Linear C->4C,
     5: Linear 4C->C}, layer_scale [C,1,1]; stochastic-depth probability ``sd_prob``."""
@@ -200,7 +210,9 @@ class Encoder(nn.Module):
         dev = images.device
         C0 = pk["stem"][0].shape[0]
         x = torch.empty(B, H // 4, W // 4, C0, device=dev, dtype=ct)
-        K.convnext_stem(images, *pk["stem"], x)
+        if images.dtype == torch.uint8 and "norm" not in pk:  # train.py:152 ImageNet normalisation
+            pk["norm"] = (torch.tensor(IMAGENET_MEAN, device=dev), torch.tensor(IMAGENET_STD, device=dev))
+        K.convnext_stem(images, *pk["stem"], x, norm=pk.get("norm"))
         bid = 0
         for st, (blocks, down) in enumerate(pk["stages"]):
             if 1 + 2 * st >= upto:
@@ -268,7 +280,8 @@ class Encoder(nn.Module):
         return self._engine
 
     def forward(self, images):
-        """encoder.py:23-27.  images [B,3,H,W] (f32, on GPU) -> [B, s, s, E] NHWC, compute dtype.
+        """encoder.py:23-27.  images [B,3,H,W] on the GPU (normalised f32, or raw uint8 pixels that the
+        stem normalises) -> [B, s, s, E] NHWC, compute dtype.
         With trainable children (fine_tune) and grad enabled the output is differentiable:
         backward runs the HIP encoder backward into the parameters' .grad."""
         if not images.is_cuda:
@@ -276,7 +289,7 @@ class Encoder(nn.Module):
         if self.trainable() and torch.is_grad_enabled():
             eng = self.engine()
             return _EncoderTrain.apply(eng, images, *eng.fp.params.values())
-        images = images.float().contiguous()
+        images = as_input(images)
         B = images.shape[0]
         sd = self._sd_scales(B, images.device) if self.training else None
         x, _ = self._run_frozen(images, 8, sd)

@@ -209,10 +209,10 @@ class TeacherForcedTrainer:
         else:
             if self._graph is None:
                 self._capture(imgs, caps, caplens)
+            if any(d.shape != s_.shape or d.dtype != s_.dtype for d, s_ in zip(self._inputs, (imgs, caps, caplens))):
+                # a batch of another shape (the last, partial batch of an epoch): eager launches
+                return self._update(self._fwd_bwd(imgs, caps, caplens))
             for dst, src in zip(self._inputs, (imgs, caps, caplens)):
-                if dst.shape != src.shape:
-                    raise ValueError("graph mode needs a fixed batch shape; got %s, captured %s"
-                                     % (tuple(src.shape), tuple(dst.shape)))
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src, non_blocking=True)
             self._graph.replay()

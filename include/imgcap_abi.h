@@ -177,6 +177,12 @@ int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const void* dy, cons
 int imgcap_convnext_stem(int dtype, int B, int H, int W, int C0, const float* images,
                          const float* w, const float* bias, const float* ln_w, const float* ln_b,
                          void* out, void* stream);
+/* Same, from the reference's raw images: uint8 [B,3,H,W] (the HDF5 'images' dataset,
+ * dataLoader.py:43-46), normalised in the patch load exactly as the reference does on the host:
+ * x = float(u / 255.), (x - mean3[c]) / std3[c] (train.py:152, ImageNet mean/std). */
+int imgcap_convnext_stem_u8(int dtype, int B, int H, int W, int C0, const uint8_t* images, const float* mean3,
+                            const float* std3, const float* w, const float* bias, const float* ln_w,
+                            const float* ln_b, void* out, void* stream);
 /* CNBlock head: depthwise 7x7 (pad 3, bias) + LayerNorm(C, eps 1e-6).  w: f32 [49][C]. */
 /* Depthwise 7x7 conv + bias only, y [B,H,W,C] (the LayerNorm is applied by the consumer:
  * imgcap_cnblock_mlp's prologue or imgcap_add_layernorm_fwd).  C % 32 == 0, W <= 64.

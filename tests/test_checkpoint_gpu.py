@@ -90,3 +90,32 @@ def test_train_py_saves_and_resumes(hip_device, tmp_path, capsys):
     assert ck2["epoch"] == 1 and ck2["decoderOptimizer"]["state"][0]["step"].item() == 4.0
     assert len(ck2["results"]) == 2
     assert "epoch 1:" in capsys.readouterr().out
+
+
+def test_train_py_on_reference_files(hip_device, tmp_path, capsys):
+    """train.py --dataFolder: the reference's on-disk schema (TRAIN_IMAGES .npy form of the HDF5
+    uint8 [N,3,256,256], CAPTIONS / CAPLENS json), 256x256 images normalised in the stem kernel,
+    a ragged last batch (50 items / batch 4) taken eagerly beside the graph replays."""
+    import json
+    import numpy as np
+    import train
+    rng = np.random.default_rng(1)
+    n_img, cpi, L, V = 10, 5, 52, train.VOCAB
+    np.save(os.path.join(str(tmp_path), "TRAIN_IMAGES_d.npy"),
+            rng.integers(0, 256, size=(n_img, 3, 256, 256), dtype=np.uint8))
+    caps, lens = [], []
+    for _ in range(n_img * cpi):
+        n = int(rng.integers(8, L + 1))
+        c = [V - 2] + rng.integers(1, V - 3, size=n - 2).tolist() + [V - 1] + [0] * (L - n)
+        caps.append(c)
+        lens.append(n)
+    with open(os.path.join(str(tmp_path), "TRAIN_CAPTIONS_d.json"), "w") as f:
+        json.dump(caps, f)
+    with open(os.path.join(str(tmp_path), "TRAIN_CAPLENS_d.json"), "w") as f:
+        json.dump(lens, f)
+    train.main(["--teacherForcing", "--lstmDecoder", "--encoder", "tiny", "--batchSize", "4", "--steps", "0",
+                "--dataFolder", str(tmp_path), "--dataName", "d", "--workers", "0"])
+    out = capsys.readouterr().out
+    line = [ln for ln in out.splitlines() if ln.startswith("epoch 0:")][0]
+    loss = float(line.split("loss")[1].split()[0])
+    assert 5.0 < loss < 12.0  # ~ln(V) at random init

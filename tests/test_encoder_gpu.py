@@ -55,3 +55,41 @@ def test_encoder_stochastic_depth_train_mode(hip_device):
     with torch.no_grad():
         ref = convnext.encoder_forward(sd, "tiny", img.cpu(), sd_keep=list(scales))
     assert _rel(a, ref) < 1e-4
+
+
+def test_stem_uint8_normalises_like_the_reference(hip_device):
+    """Raw uint8 pixels (dataLoader.py:43-46) normalised in the stem kernel == the stem on the
+    reference's host-normalised float input (FloatTensor(img / 255.) -> Normalize), bit for bit."""
+    from imagecaptioningconvnext_amd import kernels as K
+    from imagecaptioningconvnext_amd.data import normalize
+    from imagecaptioningconvnext_amd.models.encoder import IMAGENET_MEAN, IMAGENET_STD
+    g = torch.Generator().manual_seed(11)
+    u8 = torch.randint(0, 256, (2, 3, 256, 256), generator=g, dtype=torch.uint8)
+    ref_in = normalize(torch.FloatTensor(u8.numpy() / 255.))
+    C0 = 96
+    w = torch.randn(C0, 48, generator=g).to(hip_device)
+    b, lw, lb = (torch.randn(C0, generator=g).to(hip_device) for _ in range(3))
+    out_f = torch.empty(2, 64, 64, C0, device=hip_device)
+    out_u = torch.empty_like(out_f)
+    K.convnext_stem(ref_in.to(hip_device), w, b, lw, lb, out_f)
+    norm = (torch.tensor(IMAGENET_MEAN, device=hip_device), torch.tensor(IMAGENET_STD, device=hip_device))
+    K.convnext_stem(u8.to(hip_device), w, b, lw, lb, out_u, norm=norm)
+    assert torch.equal(out_u, out_f)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 3e-2)])
+def test_encoder_uint8_256_vs_oracle(hip_device, dtype, tol):
+    """The dataset's 256x256 uint8 images end to end (stages 64/32/16/8, adaptive pool 8 -> 7)."""
+    from imagecaptioningconvnext_amd.data import normalize
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    sd = make_params(convnext.param_shapes("tiny"), 5)
+    enc = Encoder(variant="tiny", compute_dtype=dtype)
+    enc.load_state_dict(sd)
+    enc = enc.to(hip_device).eval()
+    g = torch.Generator().manual_seed(12)
+    u8 = torch.randint(0, 256, (2, 3, 256, 256), generator=g, dtype=torch.uint8)
+    with torch.no_grad():
+        out = enc(u8.to(hip_device))
+        ref = convnext.encoder_forward(sd, "tiny", normalize(torch.FloatTensor(u8.numpy() / 255.)))
+    assert out.shape == ref.shape == (2, 7, 7, 768)
+    assert _rel(out, ref) < tol

@@ -62,6 +62,9 @@ def parse(argv=None):
     p.add_argument('--saveDir', type=str, default=None,
                    help='write the reference-schema checkpoint (utils.py:195-224) here after every epoch')
     p.add_argument('--dataName', type=str, default='coco_5_cap_per_img_5_min_word_freq')
+    p.add_argument('--dataFolder', type=str, default=None,
+                   help="the reference's input files (train.py:35); synthetic batches when not given")
+    p.add_argument('--workers', type=int, default=6)
     return p.parse_args(argv)
 
 
@@ -75,6 +78,26 @@ def synthetic_loader(steps, B, device, rank=0, V=VOCAB, L=maxLen):
         caps = torch.randint(1, V - 3, (B, L), generator=g)
         caps[:, 0], caps[:, L - 1] = V - 2, V - 1
         yield img.to(device), caps.to(device), torch.full((B, 1), L, dtype=torch.long, device=device)
+
+
+def data_loader(args, device, epoch, rank=0, world=1):
+    """train.py:154-155 (trainMultiGPU.py:240: DistributedSampler) over the reference's files;
+    items stay uint8 (normalised in the stem kernel), batches go to the GPU as bytes.  --steps
+    caps the iterations per epoch (0: the whole split)."""
+    from torch.utils.data import DataLoader
+    from torch.utils.data.distributed import DistributedSampler
+    from imagecaptioningconvnext_amd.data import CaptionDataset
+    ds = CaptionDataset(args.dataFolder, args.dataName, 'TRAIN')
+    sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True) if world > 1 else None
+    if sampler is not None:
+        sampler.set_epoch(epoch)
+    dl = DataLoader(ds, batch_size=args.batchSize, shuffle=sampler is None, sampler=sampler,
+                    num_workers=args.workers, pin_memory=True, persistent_workers=args.workers > 0)
+    for i, (imgs, caps, caplens) in enumerate(dl):
+        if args.steps and i >= args.steps:
+            break
+        yield (imgs.to(device, non_blocking=True), caps.to(device, non_blocking=True),
+               caplens.to(device, non_blocking=True))
 
 
 def build_models(args, device):
@@ -144,7 +167,8 @@ def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, w
             trainer.enable_encoder_finetune(args.startingLayer)
             log(f"Fine-tuning encoder from epoch {epoch} onwards (starting from layer {args.startingLayer})",
                 flush=True)
-        loader = synthetic_loader(args.steps, args.batchSize, device, rank=rank)
+        loader = (data_loader(args, device, epoch, rank, world) if args.dataFolder else
+                  synthetic_loader(args.steps, args.batchSize, device, rank=rank))
         out = trainWithTeacherForcing(loader, encoder, decoder, trainer, epoch, args.lstmDecoder, log=log)
         log(f"epoch {epoch}: loss {out[0]:.4f} top5 {out[1]:.2f} batch {out[2] * 1e3:.2f} ms ({world} GPUs)",
             flush=True)
