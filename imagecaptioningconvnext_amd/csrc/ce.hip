@@ -67,7 +67,72 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(int V, const T* __restrict_
 
 }  // namespace imgcap
 
+namespace imgcap {
+// ---- greedy decoding step (decoder.py:150-161, transformerDecoder.py:137-155) -------------
+// one block per row; finished rows return at once (their outputs stay as the zeroed buffers)
+template <typename T>
+__global__ __launch_bounds__(256) void greedy_select_kernel(int V, const T* __restrict__ logits, long ldl, int t,
+                                                            int maxlen, int64_t end_id, uint8_t* __restrict__ finished,
+                                                            int64_t* __restrict__ next_ids, int64_t* __restrict__ seq,
+                                                            float* __restrict__ preds, const float* __restrict__ alpha,
+                                                            float* __restrict__ alphas, int P) {
+  __shared__ float bv_s[256];
+  __shared__ int bi_s[256];
+  const int b = blockIdx.x;
+  if (finished[b]) return;
+  const T* row = logits + (long)b * ldl;
+  float* pr = preds + ((long)b * maxlen + t) * V;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int v = threadIdx.x; v < V; v += 256) {
+    const float x = to_f(row[v]);
+    pr[v] = x;
+    if (x > bv) { bv = x; bi = v; }  // ascending v: the first maximum of this thread's slice
+  }
+  bv_s[threadIdx.x] = bv;
+  bi_s[threadIdx.x] = bi;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const float ov = bv_s[threadIdx.x + o];
+      const int oi = bi_s[threadIdx.x + o];
+      if (ov > bv_s[threadIdx.x] || (ov == bv_s[threadIdx.x] && oi < bi_s[threadIdx.x])) {
+        bv_s[threadIdx.x] = ov;
+        bi_s[threadIdx.x] = oi;
+      }
+    }
+    __syncthreads();
+  }
+  if (alpha)
+    for (int p = threadIdx.x; p < P; p += 256) alphas[((long)b * maxlen + t) * P + p] = alpha[(long)b * P + p];
+  if (threadIdx.x == 0) {
+    const int id = bi_s[0];
+    seq[(long)b * maxlen + t] = id;
+    next_ids[b] = id;
+    finished[b] = id == end_id ? 1 : 0;
+  }
+}
+
+}  // namespace imgcap
+
 using namespace imgcap;
+
+extern "C" int imgcap_greedy_select(int dtype, int B, int V, const void* logits, int64_t ldl, int t, int maxlen,
+                                    int64_t end_id, uint8_t* finished, int64_t* next_ids, int64_t* sequences,
+                                    float* predictions, const float* alpha, float* alphas, int P, void* stream) {
+  IMGCAP_REQUIRE(V > 0 && ldl >= V && t >= 0 && t < maxlen, "imgcap_greedy_select: bad V / ldl / t");
+  IMGCAP_REQUIRE(!alpha || (alphas && P > 0), "imgcap_greedy_select: alphas");
+  if (B == 0) return 0;
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(greedy_select_kernel<bf16>, dim3(B), dim3(256), 0, (hipStream_t)stream, V, (const bf16*)logits,
+                       (long)ldl, t, maxlen, end_id, finished, next_ids, sequences, predictions, alpha, alphas, P);
+  else
+    hipLaunchKernelGGL(greedy_select_kernel<float>, dim3(B), dim3(256), 0, (hipStream_t)stream, V,
+                       (const float*)logits, (long)ldl, t, maxlen, end_id, finished, next_ids, sequences, predictions,
+                       alpha, alphas, P);
+  IMGCAP_CHECK_LAUNCH("imgcap_greedy_select");
+  return 0;
+}
 
 extern "C" int imgcap_ce_fwd(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
                              float* lse, float* loss, float* hit5, void* stream) {

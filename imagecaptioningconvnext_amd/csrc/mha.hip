@@ -114,9 +114,10 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(imgcap_mha_desc d, const u
   T* Vt = Ks + Img<T>::ELEMS;
   const int bh = blockIdx.x, b = bh / d.H, h = bh % d.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long kvr = d.kv_rows ? d.kv_rows : d.Lk;  // batch stride of k / v in rows
   const T* q = (const T*)d.q + (long)b * d.Lq * d.ldq + h * HD;
-  const T* k = (const T*)d.k + (long)b * d.Lk * d.ldk + h * HD;
-  const T* v = (const T*)d.v + (long)b * d.Lk * d.ldv + h * HD;
+  const T* k = (const T*)d.k + (long)b * kvr * d.ldk + h * HD;
+  const T* v = (const T*)d.v + (long)b * kvr * d.ldv + h * HD;
   stage_rows<T>(Qs, q, d.ldq, d.Lq);
   stage_rows<T>(Ks, k, d.ldk, d.Lk);
   stage_rows_t<T>(Vt, v, d.ldv, d.Lk);
@@ -303,6 +304,7 @@ static int check(const imgcap_mha_desc* d) {
   IMGCAP_REQUIRE(d != nullptr, "mha desc NULL");
   IMGCAP_REQUIRE(d->dh == HD, "mha: head dim must be 64");
   IMGCAP_REQUIRE(d->Lq > 0 && d->Lq <= LP && d->Lk > 0 && d->Lk <= LP, "mha: sequence lengths must be in [1, 64]");
+  IMGCAP_REQUIRE(d->kv_rows == 0 || d->kv_rows >= d->Lk, "mha: kv_rows must be 0 or >= Lk");
   const int vec = d->dtype == IMGCAP_F32 ? 4 : 8;
   IMGCAP_REQUIRE(d->ldq % vec == 0 && d->ldk % vec == 0 && d->ldv % vec == 0 && aligned16(d->q) && aligned16(d->k) &&
                      aligned16(d->v),
@@ -329,6 +331,7 @@ extern "C" int imgcap_mha_fwd(const imgcap_mha_desc* d, void* stream) {
 
 extern "C" int imgcap_mha_bwd(const imgcap_mha_desc* d, void* stream) {
   if (int rc = check(d)) return rc;
+  IMGCAP_REQUIRE(d->kv_rows == 0 || d->kv_rows == d->Lk, "mha bwd: kv_rows (key/value cache stride) is fwd-only");
   const int vec = d->dtype == IMGCAP_F32 ? 4 : 8;
   IMGCAP_REQUIRE(d->lddo % vec == 0 && aligned16(d->dout), "mha bwd: dout alignment");
   const dim3 grid(d->B * d->H);

@@ -332,6 +332,15 @@ def clamp_adam(param, grad, m, v, shadow, lr, step, clip, grad_div=1.0, betas=(0
               stream())
 
 
+def greedy_select(logits, V, t, end_id, finished, next_ids, sequences, predictions, alpha=None, alphas=None):
+    """One greedy step over the unfinished rows (imgcap_greedy_select)."""
+    B = logits.shape[0]
+    maxlen = sequences.shape[1]
+    _abi.call("imgcap_greedy_select", dt(logits), B, V, logits.data_ptr(), logits.stride(0), t, maxlen, end_id,
+              finished.data_ptr(), next_ids.data_ptr(), sequences.data_ptr(), predictions.data_ptr(), ptr(alpha),
+              ptr(alphas), 0 if alpha is None else alpha.shape[1], stream())
+
+
 def embedding_fwd(ids, table, out, *, pe=None, L=1, drop_p=0.0, seed=0, drop_stream=0):
     _abi.call("imgcap_embedding_fwd", dt(out), ids.numel(), table.shape[1], ids.data_ptr(), table.data_ptr(),
               ptr(pe), L, drop_p, seed, drop_stream, out.data_ptr(), stream())

@@ -209,6 +209,61 @@ class LstmEngine:
             s.update(logits=logits, targets=targets, lse=lse, dalpha=dalpha, metrics=metrics)
         return s
 
+    def greedy(self, encoder_out, start_id, end_id, maxlen):
+        """decoder.py:119-163 (forwardWithoutTeacherForcing) on device: per step one embedding
+        lookup + the W_ih embedding half, the recurrence kernels of one step (imgcap_lstm_tf_fwd
+        with T = 1: attention, gate, LSTMCell), fc and imgcap_greedy_select.  Every row is
+        computed every step and finished rows' outputs stay zero (the reference compacts to the
+        active rows; same results, no host sync per step).  Returns (predictions [B, maxlen, V]
+        f32, alphas [B, maxlen, P] f32, sequences [B, maxlen] int64)."""
+        ct, dev = self.ct, encoder_out.device
+        A, E, D, M, V, W3 = self.A, self.E, self.D, self.M, self.V, self.W3
+        p_drop = self.dec.dropout_p if self.dec.training else 0.0
+        w = self.weights()
+        B = encoder_out.size(0)
+        enc = encoder_out.reshape(B, -1, E).to(ct).contiguous()
+        P = enc.size(1)
+        f32 = dict(device=dev, dtype=torch.float32)
+        ctd = dict(device=dev, dtype=ct)
+        mean = torch.empty(B, E, **ctd)
+        K.mean_mid(enc, mean)                                                       # decoder.py:99
+        h0c0 = K.gemm(mean, w["init"], trans_b=True, bias=w["binit"], out_dtype=torch.float32)  # :100-101
+        att1 = K.gemm(enc.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])    # :61, once
+        hprev = torch.empty(B, 1, D, **ctd)
+        hprev[:, 0].copy_(h0c0[:, :D])
+        c0 = h0c0[:, D:].contiguous()
+        preds = torch.zeros(B, maxlen, V, **f32)
+        alphas = torch.zeros(B, maxlen, P, **f32)
+        seqs = torch.zeros(B, maxlen, device=dev, dtype=torch.int64)
+        finished = torch.zeros(B, device=dev, dtype=torch.uint8)
+        ids = torch.full((B,), start_id, device=dev, dtype=torch.int64)
+        emb = torch.empty(B, M, **ctd)
+        xe = torch.empty(B, 1, 4 * D, **f32)
+        bufs = dict(g1=torch.empty(B, 1, W3, **f32), alphas=torch.empty(B, 1, P, **f32),
+                    awe=torch.empty(B, 1, E, **f32), zs=torch.empty(B, 1, E, **ctd),
+                    gates=torch.empty(B, 1, 4 * D, **f32), cs=torch.empty(B, 1, D, **f32),
+                    hs=torch.empty(B, 1, D, **ctd), dl=torch.ones(B, device=dev, dtype=torch.int32))
+        logits = torch.empty(B, self.Vpad, **ctd)
+        d = _abi.LstmDesc()
+        d.dtype, d.B, d.P, d.E, d.A, d.D, d.M, d.T = K.dt(emb), B, P, E, A, D, M, 1
+        for k, v in dict(w_hcat=w["hcat"], b_hcat=w["bhcat"], w_ih=w["wih"], w_f=w["wf"], enc=enc, att1=att1,
+                         xe=xe, c0=c0, hprev=hprev, **bufs).items():
+            setattr(d, k, v.data_ptr())
+        for t in range(maxlen):
+            K.embedding_fwd(ids, w["emb"], emb)                                     # :130 / :158
+            K.gemm(emb, w["wih"][:, :M], trans_b=True, bias=w["bih"], out=xe.view(B, 4 * D))
+            self._launch("imgcap_lstm_tf_fwd", d)                                   # :141-148, one step
+            hd = bufs["hs"].view(B, D)
+            if p_drop > 0:
+                hd = K.dropout(hd, p_drop, self.seed + self.step_id, _STREAM_DROPOUT_H)
+            K.gemm(hd, w["wfc"], trans_b=True, bias=w["bfc"], out=logits, N=V)     # :149
+            K.greedy_select(logits, V, t, end_id, finished, ids, seqs, preds, alpha=bufs["alphas"].view(B, P),
+                            alphas=alphas)                                          # :150-161
+            hprev.copy_(bufs["hs"])
+            c0.copy_(bufs["cs"].view(B, D))
+        self.step_id += 1
+        return preds, alphas, seqs
+
     def predictions(self, s):
         """decoder.py:129,145: zero-filled predictions [B, T, V] (fp32) from the saved state."""
         B, T, V = s["B"], s["T"], self.V

@@ -115,8 +115,11 @@ class DecoderWithAttention(nn.Module):
         return preds, caps_s, _decode_lengths(caption_lengths), alphas, sort_ind
 
     def forwardWithoutTeacherForcing(self, encoder_out, wordMap, maxDecodeLen):
-        raise NotImplementedError("greedy (non-teacher-forced) decoding is outside the accelerated path "
-                                  "(SURVEY.md §8f item 3)")
+        """decoder.py:119-163: greedy decoding -> (predictions [B, maxDecodeLen, V] f32, alphas
+        [B, maxDecodeLen, P] f32, sequences [B, maxDecodeLen] int64); LstmEngine.greedy.  Not
+        differentiable (the reference's trainWithoutTeacherForcing is outside this build)."""
+        with torch.no_grad():
+            return self.engine().greedy(encoder_out, wordMap['<start>'], wordMap['<end>'], maxDecodeLen)
 
     def forward(self, teacherForcing, encoder_out, encoded_captions=None, caption_lengths=None, wordMap=None,
                 maxDecodeLen=None):

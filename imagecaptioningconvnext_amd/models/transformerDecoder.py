@@ -104,8 +104,11 @@ class TransformerDecoder(nn.Module):
         return preds, encoded_captions, decode_lengths
 
     def forwardWithoutTeacherForcing(self, encoder_out, wordMap, maxDecodeLen):
-        raise NotImplementedError("greedy (non-teacher-forced) decoding is outside the accelerated path "
-                                  "(SURVEY.md §8f item 3)")
+        """transformerDecoder.py:110-160: greedy decoding -> (predictions [B, maxDecodeLen, V] f32,
+        sequences [B, maxDecodeLen] int64); TransformerEngine.greedy (key/value cache instead of
+        re-decoding the prefix).  Not differentiable."""
+        with torch.no_grad():
+            return self.engine().greedy(encoder_out, wordMap['<start>'], wordMap['<end>'], maxDecodeLen)
 
     def forward(self, teacherForcing, encoder_out, encoded_captions=None, caption_lengths=None,
                 tgt_key_padding_mask=None, wordMap=None, maxDecodeLen=None):

@@ -61,7 +61,7 @@ class TransformerEngine:
         return f"transformer_decoder.layers.{i}.{name}"
 
     def _mha(self, *, B, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, causal, key_ids, pad_id, p, seed, sid,
-             dout=None, lddo=0, dq=None, lddq=0, dk=None, lddk=0, dv=None, lddv=0, bwd=False):
+             dout=None, lddo=0, dq=None, lddq=0, dk=None, lddk=0, dv=None, lddv=0, bwd=False, kv_rows=0):
         m = _abi.MhaDesc()
         m.dtype, m.B, m.H, m.Lq, m.Lk, m.dh, m.causal = K.dt(q), B, self.H, Lq, Lk, 64, int(causal)
         m.pad_id = pad_id
@@ -69,6 +69,7 @@ class TransformerEngine:
         m.q, m.k, m.v, m.o, m.lse = q.data_ptr(), k.data_ptr(), v.data_ptr(), K.ptr(o), lse.data_ptr()
         m.key_ids = K.ptr(key_ids)
         m.scale = 1.0 / math.sqrt(64.0)
+        m.kv_rows = kv_rows
         m.drop_p, m.seed, m.drop_stream = p, seed, sid
         if bwd:
             m.dout, m.lddo = dout.data_ptr(), lddo
@@ -161,6 +162,84 @@ class TransformerEngine:
             K.loss_finalize(lrow, hit, targets, None, metrics)
             s.update(logits=logits, targets=targets, lse=lse, metrics=metrics)
         return s
+
+    def greedy(self, encoder_out, start_id, end_id, maxlen):
+        """transformerDecoder.py:110-160 (forwardWithoutTeacherForcing) with a key/value cache.
+
+        The reference re-decodes the whole prefix every step (O(T^2) per caption).  In a post-norm
+        decoder with a causal mask the layer outputs at positions < t do not change when token t
+        is appended, so each step here runs the 6 layers on the new position only: its self-
+        attention reads the cached K/V of positions 0..t (mha kv_rows = maxlen), the cross-
+        attention K/V of the memory are computed once.  Same results as the reference up to fp
+        reassociation.  Returns (predictions [B, maxlen, V] f32, sequences [B, maxlen] int64)."""
+        fp, ct, dev = self.fp, self.ct, encoder_out.device
+        d, V = self.d, self.V
+        if maxlen > 64:
+            raise ValueError("greedy decode: maxDecodeLen <= 64 (attention kernel tile)")
+        p = self.dec.dropout_p if self.dec.training else 0.0
+        B = encoder_out.size(0)
+        enc = encoder_out.reshape(B, -1, self.E).to(ct).contiguous()
+        P = enc.size(1)
+        BP = B * P
+        ctd = dict(device=dev, dtype=ct)
+        f32 = dict(device=dev, dtype=torch.float32)
+        seed = self.seed + 7919 * self.step_id
+        self.step_id += 1
+        if self.has_proj:                                                       # :112-114
+            mem = K.gemm(enc.view(BP, self.E), fp.w("encoder_proj.weight"), trans_b=True,
+                         bias=fp.f32("encoder_proj.bias"))
+        else:
+            mem = enc.view(BP, d)
+        kv_mem, cache = [], []
+        for i in range(self.layers):
+            wq = fp.w(self._lw(i, "multihead_attn.in_proj_weight"))
+            bq = fp.f32(self._lw(i, "multihead_attn.in_proj_bias"))
+            kv_mem.append(K.gemm(mem, wq[d:], trans_b=True, bias=bq[d:]))    # [B*P, 2d] once
+            cache.append(torch.empty(B, maxlen, 3 * d, **ctd))                # q | k | v per position
+        pe = self.dec.pos_encoding.pe.view(-1, d).float()
+        preds = torch.zeros(B, maxlen, V, **f32)
+        seqs = torch.zeros(B, maxlen, device=dev, dtype=torch.int64)
+        finished = torch.zeros(B, device=dev, dtype=torch.uint8)
+        ids = torch.full((B,), start_id, device=dev, dtype=torch.int64)
+        x = torch.empty(B, d, **ctd)
+        o = torch.empty(B, d, **ctd)
+        lse = torch.empty(B, self.H, 1, **f32)
+        logits = torch.empty(B, self.Vpad, **ctd)
+        for t in range(maxlen):
+            # the new position's input: embedding(last token) + pe[t]              :129-130
+            K.embedding_fwd(ids, fp.f32("embedding.weight"), x, pe=pe[t:t + 1].contiguous(), L=1, drop_p=p,
+                            seed=seed + t, drop_stream=_S_EMB)
+            for i in range(self.layers):
+                lw = lambda n: self._lw(i, n)  # noqa: E731
+                c = cache[i]
+                K.gemm(x, fp.w(lw("self_attn.in_proj_weight")), trans_b=True, bias=fp.f32(lw("self_attn.in_proj_bias")),
+                       out=c[:, t])                                             # q, k, v of position t
+                # Lq = 1: the query "row stride" ldq is the cache's batch stride
+                self._mha(B=B, Lq=1, Lk=t + 1, q=c[:, t], ldq=maxlen * 3 * d, k=c[:, :, d:], ldk=3 * d, v=c[:, :, 2 * d:],
+                          ldv=3 * d, o=o, ldo=d, lse=lse, causal=False, key_ids=None, pad_id=0, p=p, seed=seed + t,
+                          sid=_s(i, 0), kv_rows=maxlen)
+                y = K.gemm(o, fp.w(lw("self_attn.out_proj.weight")), trans_b=True,
+                           bias=fp.f32(lw("self_attn.out_proj.bias")))
+                x1, _, _ = K.add_layernorm(x, y, fp.f32(lw("norm1.weight")), fp.f32(lw("norm1.bias")), 1e-5,
+                                           drop_p=p, seed=seed + t, drop_stream=_s(i, 1))
+                wq = fp.w(lw("multihead_attn.in_proj_weight"))
+                bq = fp.f32(lw("multihead_attn.in_proj_bias"))
+                q2 = K.gemm(x1, wq[:d], trans_b=True, bias=bq[:d])
+                kv2 = kv_mem[i]
+                self._mha(B=B, Lq=1, Lk=P, q=q2, ldq=d, k=kv2, ldk=2 * d, v=kv2[:, d:], ldv=2 * d, o=o, ldo=d,
+                          lse=lse, causal=False, key_ids=None, pad_id=0, p=p, seed=seed + t, sid=_s(i, 2))
+                y2 = K.gemm(o, fp.w(lw("multihead_attn.out_proj.weight")), trans_b=True,
+                            bias=fp.f32(lw("multihead_attn.out_proj.bias")))
+                x2, _, _ = K.add_layernorm(x1, y2, fp.f32(lw("norm2.weight")), fp.f32(lw("norm2.bias")), 1e-5,
+                                           drop_p=p, seed=seed + t, drop_stream=_s(i, 3))
+                hdn = K.gemm(x2, fp.w(lw("linear1.weight")), trans_b=True, bias=fp.f32(lw("linear1.bias")),
+                             act=K.ACT_RELU, drop_p=p, seed=seed + t, drop_stream=_s(i, 4))
+                y3 = K.gemm(hdn, fp.w(lw("linear2.weight")), trans_b=True, bias=fp.f32(lw("linear2.bias")))
+                x, _, _ = K.add_layernorm(x2, y3, fp.f32(lw("norm3.weight")), fp.f32(lw("norm3.bias")), 1e-5,
+                                          drop_p=p, seed=seed + t, drop_stream=_s(i, 5))
+            K.gemm(x, fp.w("fc_out.weight"), trans_b=True, bias=fp.f32("fc_out.bias"), out=logits, N=V)  # :140
+            K.greedy_select(logits, V, t, end_id, finished, ids, seqs, preds)     # :141-155
+        return preds, seqs
 
     def predictions(self, s):
         """transformerDecoder.py:106: fc_out over all L positions -> [B, L, V] fp32."""

@@ -379,9 +379,19 @@ typedef struct imgcap_mha_desc {
   void* dk;
   void* dv;
   int64_t lddq, lddk, lddv;
+  int64_t kv_rows;     /* fwd only: rows between consecutive batch entries of k / v (0 = Lk): a
+                          [B][Lmax] key/value cache read at its first Lk rows (incremental decode) */
 } imgcap_mha_desc;
 
 int imgcap_mha_fwd(const imgcap_mha_desc* d, void* stream);
+/* One greedy decoding step (decoder.py:150-161, transformerDecoder.py:137-155) for rows not yet
+ * finished: predictions[b, t, :V] = logits[b, :V] (fp32), sequences[b, t] = argmax (first index
+ * of the maximum, as torch), alphas[b, t, :P] = alpha[b, :P] (if alpha), next_ids[b] = argmax,
+ * finished[b] |= (argmax == end_id).  Finished rows are left untouched (the outputs start zeroed,
+ * as the reference's torch.zeros).  logits: [B, ldl] of dtype. */
+int imgcap_greedy_select(int dtype, int B, int V, const void* logits, int64_t ldl, int t, int maxlen,
+                         int64_t end_id, uint8_t* finished, int64_t* next_ids, int64_t* sequences,
+                         float* predictions, const float* alpha, float* alphas, int P, void* stream);
 int imgcap_mha_bwd(const imgcap_mha_desc* d, void* stream);
 
 /* y = x * dropmask(seed, stream, i) (nn.Dropout, decoder.py:144 / transformer dropouts) */

@@ -330,8 +330,49 @@ def gen_ckpt_transformer():
     return _gen_ckpt(False)
 
 
+def gen_greedy():
+    """forwardWithoutTeacherForcing (decoder.py:119-163, transformerDecoder.py:110-160) of the
+    reference in eval mode: predictions, alphas (LSTM), sequences, for a maxDecodeLen run."""
+    t, meta = {}, {}
+    for name, cfg, lstm in (("lstm", LSTM_SMALL, True), ("trf", TRF_H64, False)):
+        for variant in ("", "_end"):
+            dec = _lstm_decoder(cfg) if lstm else _transformer_decoder(cfg)
+            dec.eval()
+            enc, _, _ = _inputs(cfg)
+            wm = word_map(cfg["V"])
+            fc = dec.fc if lstm else dec.fc_out
+            end_bias = 0.0
+            if variant:  # raise <end>'s bias until rows finish at different steps (the finished logic)
+                for end_bias in [0.05 * k for k in range(1, 200)]:
+                    with torch.no_grad():
+                        fc.bias[wm["<end>"]] += 0.05
+                        out = dec(teacherForcing=False, encoder_out=enc, wordMap=wm, maxDecodeLen=10)
+                    first = [(row == wm["<end>"]).nonzero()[:1].flatten().tolist() for row in out[-1]]
+                    stops = {f[0] if f else 99 for f in first}
+                    if len(stops) >= 2 and 99 not in stops or len(stops) >= 3:
+                        break
+            with torch.no_grad():
+                out = dec(teacherForcing=False, encoder_out=enc, wordMap=wm, maxDecodeLen=10)
+            key = name + variant
+            t[f"{key}.enc"] = enc
+            t[f"{key}.predictions"] = out[0]
+            t[f"{key}.sequences"] = out[-1]
+            if lstm:
+                t[f"{key}.alphas"] = out[1]
+            meta[key] = dict(cfg=cfg, maxDecodeLen=10, end_bias_added=round(end_bias, 6))
+    meta["source"] = "decoder.py:119-163; transformerDecoder.py:110-160 (eval, greedy)"
+    meta["note"] = "params: tests/golden_util.make_params(named_shapes, cfg.seed) (the same recipe as *_tf_*)"
+    return "greedy_small", t, meta
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "ckpt":
+    if len(sys.argv) > 1 and sys.argv[1] == "greedy":
+        name, tensors, meta = gen_greedy()
+        save_file({k: v.detach().contiguous() for k, v in tensors.items()}, os.path.join(GOLDEN_DIR, name + ".safetensors"))
+        with open(os.path.join(GOLDEN_DIR, name + ".json"), "w") as f:
+            json.dump(meta, f, indent=1)
+        print("wrote", name, {k: tuple(v.shape) for k, v in tensors.items()})
+    elif len(sys.argv) > 1 and sys.argv[1] == "ckpt":
         fns = (gen_ckpt_lstm, gen_ckpt_transformer)
         for fn in (fns[int(sys.argv[2]):int(sys.argv[2]) + 1] if len(sys.argv) > 2 else fns):
             name, tensors, meta = fn()
