@@ -101,21 +101,23 @@ def test_train_py_on_reference_files(hip_device, tmp_path, capsys):
     import train
     rng = np.random.default_rng(1)
     n_img, cpi, L, V = 10, 5, 52, train.VOCAB
-    np.save(os.path.join(str(tmp_path), "TRAIN_IMAGES_d.npy"),
-            rng.integers(0, 256, size=(n_img, 3, 256, 256), dtype=np.uint8))
-    caps, lens = [], []
-    for _ in range(n_img * cpi):
-        n = int(rng.integers(8, L + 1))
-        c = [V - 2] + rng.integers(1, V - 3, size=n - 2).tolist() + [V - 1] + [0] * (L - n)
-        caps.append(c)
-        lens.append(n)
-    with open(os.path.join(str(tmp_path), "TRAIN_CAPTIONS_d.json"), "w") as f:
-        json.dump(caps, f)
-    with open(os.path.join(str(tmp_path), "TRAIN_CAPLENS_d.json"), "w") as f:
-        json.dump(lens, f)
+    for split, ni in (("TRAIN", n_img), ("VAL", 3)):
+        np.save(os.path.join(str(tmp_path), f"{split}_IMAGES_d.npy"),
+                rng.integers(0, 256, size=(ni, 3, 256, 256), dtype=np.uint8))
+        caps, lens = [], []
+        for _ in range(ni * cpi):
+            n = int(rng.integers(8, L + 1))
+            c = [V - 2] + rng.integers(1, V - 3, size=n - 2).tolist() + [V - 1] + [0] * (L - n)
+            caps.append(c)
+            lens.append(n)
+        with open(os.path.join(str(tmp_path), f"{split}_CAPTIONS_d.json"), "w") as f:
+            json.dump(caps, f)
+        with open(os.path.join(str(tmp_path), f"{split}_CAPLENS_d.json"), "w") as f:
+            json.dump(lens, f)
     train.main(["--teacherForcing", "--lstmDecoder", "--encoder", "tiny", "--batchSize", "4", "--steps", "0",
                 "--dataFolder", str(tmp_path), "--dataName", "d", "--workers", "0"])
     out = capsys.readouterr().out
+    assert "No TF, Validation Loss" in out and "Bleu-4" in out  # greedy validation of the VAL split ran
     line = [ln for ln in out.splitlines() if ln.startswith("epoch 0:")][0]
     loss = float(line.split("loss")[1].split()[0])
     assert 5.0 < loss < 12.0  # ~ln(V) at random init

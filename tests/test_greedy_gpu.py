@@ -80,3 +80,32 @@ def test_greedy_bf16_runs_and_agrees_mostly(hip_device):
                       maxDecodeLen=m["maxDecodeLen"])
     assert preds.shape == t["trf.predictions"].shape and preds.dtype == torch.float32
     assert (seqs.cpu() == t["trf.sequences"]).float().mean().item() > 0.7
+
+
+@pytest.mark.parametrize("key", ["lstm_end", "trf_end"])
+def test_greedy_validation_loss_matches_reference_filtering(hip_device, key):
+    """metrics.greedy_loss (device) == train.py:398-407: preprocessDecoderOutputForMetrics +
+    CrossEntropyLoss (+ the LSTM's alpha regulariser) + top-5 over the kept rows."""
+    import torch.nn.functional as F
+    from imagecaptioningconvnext_amd.metrics import greedy_loss
+    from test_metrics_cpu import _ref_preprocess
+    t, meta = _fixture()
+    m = meta[key]
+    cfg = m["cfg"]
+    V, T = cfg["V"], m["maxDecodeLen"]
+    preds, seqs = t[key + ".predictions"], t[key + ".sequences"]
+    g = torch.Generator().manual_seed(3)
+    caps = torch.randint(1, V - 3, (preds.shape[0], 14), generator=g)
+    caps[1, 5:] = 0
+    alphas = t.get(key + ".alphas")
+    metrics, n = greedy_loss(preds.to(hip_device), seqs.to(hip_device), caps.to(hip_device), word_map(V), T,
+                             alphas=None if alphas is None else alphas.to(hip_device))
+    s, tg, lens = _ref_preprocess(preds, seqs, caps, V - 1, 0, T)
+    loss = F.cross_entropy(s, tg)
+    if alphas is not None:
+        loss = loss + ((1.0 - alphas.sum(dim=1)) ** 2).mean()
+    top5 = (s.topk(5, dim=1).indices == tg.view(-1, 1)).any(dim=1).float().sum()
+    mm = metrics.cpu()
+    assert n.cpu().tolist() == lens
+    assert abs(mm[0].item() - loss.item()) < 1e-5 * abs(loss.item()) + 1e-6
+    assert int(mm[1].item()) == tg.numel() and int(mm[2].item()) == int(top5.item())

@@ -80,6 +80,26 @@ def synthetic_loader(steps, B, device, rank=0, V=VOCAB, L=maxLen):
         yield img.to(device), caps.to(device), torch.full((B, 1), L, dtype=torch.long, device=device)
 
 
+def _val_loader(args):
+    """train.py:156-157: the VAL split (with its word map for <start>/<end>/<pad>), when present."""
+    import json
+    if not args.dataFolder:
+        return None
+    cap = os.path.join(args.dataFolder, 'VAL_CAPTIONS_' + args.dataName + '.json')
+    if not os.path.exists(cap):
+        return None
+    from torch.utils.data import DataLoader
+    from imagecaptioningconvnext_amd.data import CaptionDataset
+    ds = CaptionDataset(args.dataFolder, args.dataName, 'VAL')
+    wm_path = os.path.join(args.dataFolder, 'WORDMAP_' + args.dataName + '.json')
+    if os.path.exists(wm_path):
+        with open(wm_path) as f:
+            ds.wordMap = json.load(f)
+    else:  # SURVEY.md §8 ids: <pad>=0, <unk>=V-3, <start>=V-2, <end>=V-1
+        ds.wordMap = {'<pad>': 0, '<unk>': VOCAB - 3, '<start>': VOCAB - 2, '<end>': VOCAB - 1}
+    return DataLoader(ds, batch_size=args.batchSize, shuffle=True, num_workers=args.workers, pin_memory=True)
+
+
 def data_loader(args, device, epoch, rank=0, world=1):
     """train.py:154-155 (trainMultiGPU.py:240: DistributedSampler) over the reference's files;
     items stay uint8 (normalised in the stem kernel), batches go to the GPU as bytes.  --steps
@@ -162,7 +182,14 @@ def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, w
         trainer.load_optimizers(ck['decoderOptimizer'],
                                 ck['encoderOptimizer'] if trainer.enc_eng is not None else None)
         epochsSinceImprovement, results = ck['epochsSinceImprovement'], ck['results']
+    bestBleu4 = ck['bleu-4'] if ck is not None else 0.0
+    val = _val_loader(args) if rank == 0 else None
     for epoch in range(startEpoch, startEpoch + args.epochs):
+        if epochsSinceImprovement == 20:  # train.py:168-174
+            break
+        if epochsSinceImprovement > 0 and epochsSinceImprovement % 8 == 0:
+            trainer.decoder_lr *= 0.8
+            trainer.encoder_lr *= 0.8
         if epoch == args.fineTuneFromEpoch:  # train.py:160-166
             trainer.enable_encoder_finetune(args.startingLayer)
             log(f"Fine-tuning encoder from epoch {epoch} onwards (starting from layer {args.startingLayer})",
@@ -172,14 +199,27 @@ def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, w
         out = trainWithTeacherForcing(loader, encoder, decoder, trainer, epoch, args.lstmDecoder, log=log)
         log(f"epoch {epoch}: loss {out[0]:.4f} top5 {out[1]:.2f} batch {out[2] * 1e3:.2f} ms ({world} GPUs)",
             flush=True)
-        results.append({'epoch': epoch, 'trainLoss': out[0], 'trainTop5Acc': out[1], 'trainBatchTime': out[2],
-                        'trainDataTime': out[3]})
-        if args.saveDir and rank == 0:  # train.py:224-229; no validation / BLEU here
+        rec = {'epoch': epoch, 'trainLoss': out[0], 'trainTop5Acc': out[1], 'trainBatchTime': out[2],
+               'trainDataTime': out[3]}
+        recentBleu4, isBest = 0.0, False
+        if val is not None:  # train.py:190-222: greedy validation, BLEU, improvement bookkeeping
+            from imagecaptioningconvnext_amd.metrics import validate
+            vl, vt, b1, b2, b3, recentBleu4 = validate(val, encoder, decoder, val.dataset.wordMap, args.lstmDecoder,
+                                                       device, alphaC=alphaC, log=log)
+            rec.update(valLoss=vl, valTop5Acc=vt, bleu1=b1, bleu2=b2, bleu3=b3, bleu4=recentBleu4)
+            isBest = recentBleu4 > bestBleu4
+            bestBleu4 = max(recentBleu4, bestBleu4)
+            epochsSinceImprovement = 0 if isBest else epochsSinceImprovement + 1
+            encoder.train()
+            decoder.train()
+        results.append(rec)
+        if args.saveDir and rank == 0:  # train.py:224-229
             from imagecaptioningconvnext_amd.checkpoint import save_checkpoint
             encOpt, decOpt = trainer.optimizers()
             path = save_checkpoint(args.dataName, epoch, epochsSinceImprovement, encoder.state_dict(),
-                                   decoder.state_dict(), encOpt, decOpt, 0.0, False, results, args.lstmDecoder,
-                                   args.startingLayer, args.encoderLr, args.embeddingName, directory=args.saveDir)
+                                   decoder.state_dict(), encOpt, decOpt, recentBleu4, isBest, results,
+                                   args.lstmDecoder, args.startingLayer, args.encoderLr, args.embeddingName,
+                                   directory=args.saveDir)
             log(f"saved {path}", flush=True)
 
 
