@@ -421,14 +421,20 @@ def transpose(x, out=None):
     return out
 
 
+_seed_counter = None  # the registered counter tensor, kept alive while the library points at it
+
+
 def set_seed_counter(counter):
     """Mix the device int64 scalar ``counter`` into every mask seed (None = off); see
-    imgcap_set_seed_counter.  The tensor must outlive every launch that used it."""
+    imgcap_set_seed_counter.  The library keeps a raw pointer, so the tensor is held here until
+    it is replaced (a trainer going away must not leave a dangling counter behind)."""
+    global _seed_counter
     if counter is not None:
         _check_dev(counter)
         if counter.dtype != torch.int64 or counter.numel() != 1:
             raise ValueError("seed counter must be a one-element int64 tensor")
     _abi.call("imgcap_set_seed_counter", ptr(counter))
+    _seed_counter = counter
 
 
 # widths served by the fused CNBlock MLP kernel (the others run LN + two GEMMs); IMGCAP_FUSED_MLP_C
