@@ -216,53 +216,73 @@ class LstmEngine:
         computed every step and finished rows' outputs stay zero (the reference compacts to the
         active rows; same results, no host sync per step).  Returns (predictions [B, maxlen, V]
         f32, alphas [B, maxlen, P] f32, sequences [B, maxlen] int64)."""
-        ct, dev = self.ct, encoder_out.device
-        A, E, D, M, V, W3 = self.A, self.E, self.D, self.M, self.V, self.W3
-        p_drop = self.dec.dropout_p if self.dec.training else 0.0
-        w = self.weights()
-        B = encoder_out.size(0)
-        enc = encoder_out.reshape(B, -1, E).to(ct).contiguous()
-        P = enc.size(1)
+        st = self.decode_init(encoder_out)
+        B, P, V, dev = st["B"], st["P"], self.V, encoder_out.device
         f32 = dict(device=dev, dtype=torch.float32)
-        ctd = dict(device=dev, dtype=ct)
-        mean = torch.empty(B, E, **ctd)
-        K.mean_mid(enc, mean)                                                       # decoder.py:99
-        h0c0 = K.gemm(mean, w["init"], trans_b=True, bias=w["binit"], out_dtype=torch.float32)  # :100-101
-        att1 = K.gemm(enc.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])    # :61, once
-        hprev = torch.empty(B, 1, D, **ctd)
-        hprev[:, 0].copy_(h0c0[:, :D])
-        c0 = h0c0[:, D:].contiguous()
         preds = torch.zeros(B, maxlen, V, **f32)
         alphas = torch.zeros(B, maxlen, P, **f32)
         seqs = torch.zeros(B, maxlen, device=dev, dtype=torch.int64)
         finished = torch.zeros(B, device=dev, dtype=torch.uint8)
         ids = torch.full((B,), start_id, device=dev, dtype=torch.int64)
+        for t in range(maxlen):
+            logits, alpha = self.decode_step(st, ids)
+            K.greedy_select(logits, V, t, end_id, finished, ids, seqs, preds, alpha=alpha, alphas=alphas)  # :150-161
+        self.step_id += 1
+        return preds, alphas, seqs
+
+    # -- step-wise decoding primitives (greedy above, beam search in beam.py) ---------------
+    def decode_init(self, encoder_out):
+        """decoder.py:121-127 / caption.py:76-86: per-row decoding state -- the encoder rows, the
+        hoisted encoder_att projection and init_hidden_state's (h, c)."""
+        ct, dev = self.ct, encoder_out.device
+        E, D = self.E, self.D
+        w = self.weights()
+        B = encoder_out.size(0)
+        enc = encoder_out.reshape(B, -1, E).to(ct).contiguous()
+        P = enc.size(1)
+        mean = torch.empty(B, E, device=dev, dtype=ct)
+        K.mean_mid(enc, mean)                                                       # decoder.py:99
+        h0c0 = K.gemm(mean, w["init"], trans_b=True, bias=w["binit"], out_dtype=torch.float32)  # :100-101
+        att1 = K.gemm(enc.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])    # :61, once
+        h = h0c0[:, :D].to(ct).reshape(B, 1, D).contiguous()
+        c = h0c0[:, D:].contiguous()
+        return dict(B=B, P=P, enc=enc, att1=att1.view(B, P, self.A), h=h, c=c, w=w)
+
+    def decode_select(self, st, idx):
+        """Keep / reorder decoding rows (beam search: caption.py:140-142)."""
+        for k in ("enc", "att1", "h", "c"):
+            st[k] = st[k].index_select(0, idx).contiguous()
+        st["B"] = idx.numel()
+
+    def decode_step(self, st, ids):
+        """One decoding step for every row of ``st`` with input words ``ids`` [B]: embedding and the
+        W_ih embedding half, imgcap_lstm_tf_fwd with T = 1 (attention, gate, LSTMCell), fc.
+        Updates st's (h, c); returns (logits [B, Vpad] compute dtype, alpha [B, P] fp32)."""
+        ct, dev = self.ct, ids.device
+        A, E, D, M, V, W3 = self.A, self.E, self.D, self.M, self.V, self.W3
+        B, P, w = st["B"], st["P"], st["w"]
+        f32 = dict(device=dev, dtype=torch.float32)
+        ctd = dict(device=dev, dtype=ct)
         emb = torch.empty(B, M, **ctd)
-        xe = torch.empty(B, 1, 4 * D, **f32)
+        K.embedding_fwd(ids, w["emb"], emb)                                         # :130 / :158
+        xe = K.gemm(emb, w["wih"][:, :M], trans_b=True, bias=w["bih"], out_dtype=torch.float32)
         bufs = dict(g1=torch.empty(B, 1, W3, **f32), alphas=torch.empty(B, 1, P, **f32),
                     awe=torch.empty(B, 1, E, **f32), zs=torch.empty(B, 1, E, **ctd),
                     gates=torch.empty(B, 1, 4 * D, **f32), cs=torch.empty(B, 1, D, **f32),
                     hs=torch.empty(B, 1, D, **ctd), dl=torch.ones(B, device=dev, dtype=torch.int32))
-        logits = torch.empty(B, self.Vpad, **ctd)
         d = _abi.LstmDesc()
         d.dtype, d.B, d.P, d.E, d.A, d.D, d.M, d.T = K.dt(emb), B, P, E, A, D, M, 1
-        for k, v in dict(w_hcat=w["hcat"], b_hcat=w["bhcat"], w_ih=w["wih"], w_f=w["wf"], enc=enc, att1=att1,
-                         xe=xe, c0=c0, hprev=hprev, **bufs).items():
+        for k, v in dict(w_hcat=w["hcat"], b_hcat=w["bhcat"], w_ih=w["wih"], w_f=w["wf"], enc=st["enc"],
+                         att1=st["att1"], xe=xe, c0=st["c"], hprev=st["h"], **bufs).items():
             setattr(d, k, v.data_ptr())
-        for t in range(maxlen):
-            K.embedding_fwd(ids, w["emb"], emb)                                     # :130 / :158
-            K.gemm(emb, w["wih"][:, :M], trans_b=True, bias=w["bih"], out=xe.view(B, 4 * D))
-            self._launch("imgcap_lstm_tf_fwd", d)                                   # :141-148, one step
-            hd = bufs["hs"].view(B, D)
-            if p_drop > 0:
-                hd = K.dropout(hd, p_drop, self.seed + self.step_id, _STREAM_DROPOUT_H)
-            K.gemm(hd, w["wfc"], trans_b=True, bias=w["bfc"], out=logits, N=V)     # :149
-            K.greedy_select(logits, V, t, end_id, finished, ids, seqs, preds, alpha=bufs["alphas"].view(B, P),
-                            alphas=alphas)                                          # :150-161
-            hprev.copy_(bufs["hs"])
-            c0.copy_(bufs["cs"].view(B, D))
-        self.step_id += 1
-        return preds, alphas, seqs
+        self._launch("imgcap_lstm_tf_fwd", d)                                       # :141-148, one step
+        hd = bufs["hs"].view(B, D)
+        if self.dec.training and self.dec.dropout_p > 0:
+            hd = K.dropout(hd, self.dec.dropout_p, self.seed + self.step_id, _STREAM_DROPOUT_H)
+        logits = torch.empty(B, self.Vpad, **ctd)
+        K.gemm(hd, w["wfc"], trans_b=True, bias=w["bfc"], out=logits, N=V)         # :149
+        st["h"], st["c"] = bufs["hs"], bufs["cs"].view(B, D)
+        return logits, bufs["alphas"].view(B, P)
 
     def predictions(self, s):
         """decoder.py:129,145: zero-filled predictions [B, T, V] (fp32) from the saved state."""

@@ -172,74 +172,97 @@ class TransformerEngine:
         attention reads the cached K/V of positions 0..t (mha kv_rows = maxlen), the cross-
         attention K/V of the memory are computed once.  Same results as the reference up to fp
         reassociation.  Returns (predictions [B, maxlen, V] f32, sequences [B, maxlen] int64)."""
+        st = self.decode_init(encoder_out, maxlen)
+        B, V, dev = st["B"], self.V, encoder_out.device
+        preds = torch.zeros(B, maxlen, V, device=dev, dtype=torch.float32)
+        seqs = torch.zeros(B, maxlen, device=dev, dtype=torch.int64)
+        finished = torch.zeros(B, device=dev, dtype=torch.uint8)
+        ids = torch.full((B,), start_id, device=dev, dtype=torch.int64)
+        for t in range(maxlen):
+            logits = self.decode_step(st, ids)
+            K.greedy_select(logits, V, t, end_id, finished, ids, seqs, preds)     # :141-155
+        return preds, seqs
+
+    # -- step-wise decoding primitives (greedy above, beam search in beam.py) ---------------
+    def decode_init(self, encoder_out, maxlen):
+        """Decoding state: the per-layer cross-attention K/V of the projected memory (computed
+        once, :112-114) and an empty per-layer cache of (q | k | v) rows for ``maxlen`` positions."""
         fp, ct, dev = self.fp, self.ct, encoder_out.device
-        d, V = self.d, self.V
+        d = self.d
         if maxlen > 64:
-            raise ValueError("greedy decode: maxDecodeLen <= 64 (attention kernel tile)")
-        p = self.dec.dropout_p if self.dec.training else 0.0
+            raise ValueError("step-wise decode: at most 64 positions (attention kernel tile)")
         B = encoder_out.size(0)
         enc = encoder_out.reshape(B, -1, self.E).to(ct).contiguous()
         P = enc.size(1)
-        BP = B * P
-        ctd = dict(device=dev, dtype=ct)
-        f32 = dict(device=dev, dtype=torch.float32)
-        seed = self.seed + 7919 * self.step_id
-        self.step_id += 1
-        if self.has_proj:                                                       # :112-114
-            mem = K.gemm(enc.view(BP, self.E), fp.w("encoder_proj.weight"), trans_b=True,
+        if self.has_proj:
+            mem = K.gemm(enc.view(B * P, self.E), fp.w("encoder_proj.weight"), trans_b=True,
                          bias=fp.f32("encoder_proj.bias"))
         else:
-            mem = enc.view(BP, d)
+            mem = enc.view(B * P, d)
         kv_mem, cache = [], []
         for i in range(self.layers):
             wq = fp.w(self._lw(i, "multihead_attn.in_proj_weight"))
             bq = fp.f32(self._lw(i, "multihead_attn.in_proj_bias"))
-            kv_mem.append(K.gemm(mem, wq[d:], trans_b=True, bias=bq[d:]))    # [B*P, 2d] once
-            cache.append(torch.empty(B, maxlen, 3 * d, **ctd))                # q | k | v per position
-        pe = self.dec.pos_encoding.pe.view(-1, d).float()
-        preds = torch.zeros(B, maxlen, V, **f32)
-        seqs = torch.zeros(B, maxlen, device=dev, dtype=torch.int64)
-        finished = torch.zeros(B, device=dev, dtype=torch.uint8)
-        ids = torch.full((B,), start_id, device=dev, dtype=torch.int64)
+            kv_mem.append(K.gemm(mem, wq[d:], trans_b=True, bias=bq[d:]).view(B, P, 2 * d))
+            cache.append(torch.empty(B, maxlen, 3 * d, device=dev, dtype=ct))
+        seed = self.seed + 7919 * self.step_id
+        self.step_id += 1
+        return dict(B=B, P=P, t=0, maxlen=maxlen, kv_mem=kv_mem, cache=cache, seed=seed)
+
+    def decode_select(self, st, idx):
+        """Keep / reorder decoding rows with their caches (beam search: caption.py:229-248)."""
+        st["kv_mem"] = [m.index_select(0, idx).contiguous() for m in st["kv_mem"]]
+        st["cache"] = [c.index_select(0, idx).contiguous() for c in st["cache"]]
+        st["B"] = idx.numel()
+
+    def decode_step(self, st, ids):
+        """Position st["t"] for every row: embedding(ids) + pe[t], the layers on that position
+        only (self-attention over the cached K/V of positions 0..t), fc_out.  Returns logits
+        [B, Vpad] (compute dtype) and advances t."""
+        fp, ct, dev = self.fp, self.ct, ids.device
+        d, V, B, P, t, maxlen = self.d, self.V, st["B"], st["P"], st["t"], st["maxlen"]
+        if t >= maxlen:
+            raise ValueError("decode_step: cache full")
+        p = self.dec.dropout_p if self.dec.training else 0.0
+        seed = st["seed"] + t
+        ctd = dict(device=dev, dtype=ct)
+        pe = self.dec.pos_encoding.pe.view(-1, d)[t:t + 1].float().contiguous()
         x = torch.empty(B, d, **ctd)
         o = torch.empty(B, d, **ctd)
-        lse = torch.empty(B, self.H, 1, **f32)
+        lse = torch.empty(B, self.H, 1, device=dev, dtype=torch.float32)
+        # the new position's input: embedding(last token) + pe[t]                  :129-130
+        K.embedding_fwd(ids, fp.f32("embedding.weight"), x, pe=pe, L=1, drop_p=p, seed=seed, drop_stream=_S_EMB)
+        for i in range(self.layers):
+            lw = lambda n: self._lw(i, n)  # noqa: E731
+            c = st["cache"][i]
+            K.gemm(x, fp.w(lw("self_attn.in_proj_weight")), trans_b=True, bias=fp.f32(lw("self_attn.in_proj_bias")),
+                   out=c[:, t])                                                 # q, k, v of position t
+            # Lq = 1: the query "row stride" ldq is the cache's batch stride
+            self._mha(B=B, Lq=1, Lk=t + 1, q=c[:, t], ldq=maxlen * 3 * d, k=c[:, :, d:], ldk=3 * d, v=c[:, :, 2 * d:],
+                      ldv=3 * d, o=o, ldo=d, lse=lse, causal=False, key_ids=None, pad_id=0, p=p, seed=seed,
+                      sid=_s(i, 0), kv_rows=maxlen)
+            y = K.gemm(o, fp.w(lw("self_attn.out_proj.weight")), trans_b=True, bias=fp.f32(lw("self_attn.out_proj.bias")))
+            x1, _, _ = K.add_layernorm(x, y, fp.f32(lw("norm1.weight")), fp.f32(lw("norm1.bias")), 1e-5,
+                                       drop_p=p, seed=seed, drop_stream=_s(i, 1))
+            wq = fp.w(lw("multihead_attn.in_proj_weight"))
+            bq = fp.f32(lw("multihead_attn.in_proj_bias"))
+            q2 = K.gemm(x1, wq[:d], trans_b=True, bias=bq[:d])
+            kv2 = st["kv_mem"][i].view(B * P, 2 * d)
+            self._mha(B=B, Lq=1, Lk=P, q=q2, ldq=d, k=kv2, ldk=2 * d, v=kv2[:, d:], ldv=2 * d, o=o, ldo=d,
+                      lse=lse, causal=False, key_ids=None, pad_id=0, p=p, seed=seed, sid=_s(i, 2))
+            y2 = K.gemm(o, fp.w(lw("multihead_attn.out_proj.weight")), trans_b=True,
+                        bias=fp.f32(lw("multihead_attn.out_proj.bias")))
+            x2, _, _ = K.add_layernorm(x1, y2, fp.f32(lw("norm2.weight")), fp.f32(lw("norm2.bias")), 1e-5,
+                                       drop_p=p, seed=seed, drop_stream=_s(i, 3))
+            hdn = K.gemm(x2, fp.w(lw("linear1.weight")), trans_b=True, bias=fp.f32(lw("linear1.bias")),
+                         act=K.ACT_RELU, drop_p=p, seed=seed, drop_stream=_s(i, 4))
+            y3 = K.gemm(hdn, fp.w(lw("linear2.weight")), trans_b=True, bias=fp.f32(lw("linear2.bias")))
+            x, _, _ = K.add_layernorm(x2, y3, fp.f32(lw("norm3.weight")), fp.f32(lw("norm3.bias")), 1e-5,
+                                      drop_p=p, seed=seed, drop_stream=_s(i, 5))
         logits = torch.empty(B, self.Vpad, **ctd)
-        for t in range(maxlen):
-            # the new position's input: embedding(last token) + pe[t]              :129-130
-            K.embedding_fwd(ids, fp.f32("embedding.weight"), x, pe=pe[t:t + 1].contiguous(), L=1, drop_p=p,
-                            seed=seed + t, drop_stream=_S_EMB)
-            for i in range(self.layers):
-                lw = lambda n: self._lw(i, n)  # noqa: E731
-                c = cache[i]
-                K.gemm(x, fp.w(lw("self_attn.in_proj_weight")), trans_b=True, bias=fp.f32(lw("self_attn.in_proj_bias")),
-                       out=c[:, t])                                             # q, k, v of position t
-                # Lq = 1: the query "row stride" ldq is the cache's batch stride
-                self._mha(B=B, Lq=1, Lk=t + 1, q=c[:, t], ldq=maxlen * 3 * d, k=c[:, :, d:], ldk=3 * d, v=c[:, :, 2 * d:],
-                          ldv=3 * d, o=o, ldo=d, lse=lse, causal=False, key_ids=None, pad_id=0, p=p, seed=seed + t,
-                          sid=_s(i, 0), kv_rows=maxlen)
-                y = K.gemm(o, fp.w(lw("self_attn.out_proj.weight")), trans_b=True,
-                           bias=fp.f32(lw("self_attn.out_proj.bias")))
-                x1, _, _ = K.add_layernorm(x, y, fp.f32(lw("norm1.weight")), fp.f32(lw("norm1.bias")), 1e-5,
-                                           drop_p=p, seed=seed + t, drop_stream=_s(i, 1))
-                wq = fp.w(lw("multihead_attn.in_proj_weight"))
-                bq = fp.f32(lw("multihead_attn.in_proj_bias"))
-                q2 = K.gemm(x1, wq[:d], trans_b=True, bias=bq[:d])
-                kv2 = kv_mem[i]
-                self._mha(B=B, Lq=1, Lk=P, q=q2, ldq=d, k=kv2, ldk=2 * d, v=kv2[:, d:], ldv=2 * d, o=o, ldo=d,
-                          lse=lse, causal=False, key_ids=None, pad_id=0, p=p, seed=seed + t, sid=_s(i, 2))
-                y2 = K.gemm(o, fp.w(lw("multihead_attn.out_proj.weight")), trans_b=True,
-                            bias=fp.f32(lw("multihead_attn.out_proj.bias")))
-                x2, _, _ = K.add_layernorm(x1, y2, fp.f32(lw("norm2.weight")), fp.f32(lw("norm2.bias")), 1e-5,
-                                           drop_p=p, seed=seed + t, drop_stream=_s(i, 3))
-                hdn = K.gemm(x2, fp.w(lw("linear1.weight")), trans_b=True, bias=fp.f32(lw("linear1.bias")),
-                             act=K.ACT_RELU, drop_p=p, seed=seed + t, drop_stream=_s(i, 4))
-                y3 = K.gemm(hdn, fp.w(lw("linear2.weight")), trans_b=True, bias=fp.f32(lw("linear2.bias")))
-                x, _, _ = K.add_layernorm(x2, y3, fp.f32(lw("norm3.weight")), fp.f32(lw("norm3.bias")), 1e-5,
-                                          drop_p=p, seed=seed + t, drop_stream=_s(i, 5))
-            K.gemm(x, fp.w("fc_out.weight"), trans_b=True, bias=fp.f32("fc_out.bias"), out=logits, N=V)  # :140
-            K.greedy_select(logits, V, t, end_id, finished, ids, seqs, preds)     # :141-155
-        return preds, seqs
+        K.gemm(x, fp.w("fc_out.weight"), trans_b=True, bias=fp.f32("fc_out.bias"), out=logits, N=V)  # :140
+        st["t"] = t + 1
+        return logits
 
     def predictions(self, s):
         """transformerDecoder.py:106: fc_out over all L positions -> [B, L, V] fp32."""

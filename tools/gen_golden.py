@@ -365,9 +365,74 @@ def gen_greedy():
     return "greedy_small", t, meta
 
 
+def gen_beam():
+    """caption.py:39-155 / :160-255 (the reference's own beam-search functions) on a temp PNG with a
+    stand-in encoder that returns fixed features (the reference Encoder needs torchvision, §8c):
+    the returned word ids (and LSTM alphas) for beam sizes 3 and 5.  <end>'s fc bias is raised
+    (recorded) so that beams complete at different steps."""
+    import numpy as np
+    from PIL import Image
+    if "skimage" not in sys.modules:
+        ref_import._stub("skimage")
+        ref_import._stub("skimage.transform")
+    cap = ref_import.load("caption.py", "ref_caption", argv=["caption.py"])
+    cap.device = torch.device("cpu")
+    import types  # the image transform only feeds the stand-in encoder, which ignores it
+
+    def _normalize(mean, std):
+        m, s = torch.tensor(mean).view(-1, 1, 1), torch.tensor(std).view(-1, 1, 1)
+        return lambda x: (x - m) / s
+    cap.transforms = types.SimpleNamespace(Normalize=_normalize,
+                                           Compose=lambda fs: (lambda x: fs[0](x)))
+    tmp = tempfile.mkdtemp()
+    png = os.path.join(tmp, "img.png")
+    Image.fromarray(np.random.default_rng(0).integers(0, 256, size=(40, 30, 3), dtype=np.uint8)).save(png)
+
+    class FixedEncoder(torch.nn.Module):
+        def __init__(self, feats):
+            super().__init__()
+            self.feats = feats
+
+        def forward(self, image):
+            return self.feats
+
+    t, meta = {}, {}
+    # the Transformer beam search decodes up to 51 positions: positional table of maxLen 52
+    for name, cfg, lstm in (("lstm", LSTM_SMALL, True), ("trf", dict(TRF_H64, L=52), False)):
+        feats = make_features((1, cfg["S"], cfg["S"], cfg["E"]), cfg["seed"] + 5)
+        enc = FixedEncoder(feats)
+        wm = word_map(cfg["V"])
+        run = cap.caption_image_beam_search if lstm else cap.caption_image_beam_search_transformer
+        # smallest <end> bias (steps of 0.01) at which every beam size finishes with a caption of >= 3 ids
+        for bias in [0.01 * i for i in range(0, 1000)]:
+            dec = _lstm_decoder(cfg) if lstm else _transformer_decoder(cfg)
+            dec.eval()
+            fc = dec.fc if lstm else dec.fc_out
+            with torch.no_grad():
+                fc.bias[wm["<end>"]] += bias
+                try:
+                    lens = [len(run(enc, dec, png, wm, beamSize=k)[0]) for k in (3, 5)]
+                except ValueError:  # no beam completed (max() of an empty list)
+                    continue
+            if min(lens) >= 3:
+                break
+        t[f"{name}.feats"] = feats
+        for k in (3, 5):
+            with torch.no_grad():
+                if lstm:
+                    seq, alphas = cap.caption_image_beam_search(enc, dec, png, wm, beamSize=k)
+                    t[f"{name}.k{k}.alphas"] = torch.tensor(alphas, dtype=torch.float32)
+                else:
+                    seq, _ = cap.caption_image_beam_search_transformer(enc, dec, png, wm, beamSize=k)
+            t[f"{name}.k{k}.seq"] = torch.tensor(seq, dtype=torch.int64)
+        meta[name] = dict(cfg=cfg, end_bias_added=round(bias, 6))
+    meta["source"] = "caption.py:39-155 (LSTM), caption.py:160-255 (Transformer), run with a fixed-feature encoder"
+    return "beam_small", t, meta
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "greedy":
-        name, tensors, meta = gen_greedy()
+    if len(sys.argv) > 1 and sys.argv[1] in ("greedy", "beam"):
+        name, tensors, meta = gen_greedy() if sys.argv[1] == "greedy" else gen_beam()
         save_file({k: v.detach().contiguous() for k, v in tensors.items()}, os.path.join(GOLDEN_DIR, name + ".safetensors"))
         with open(os.path.join(GOLDEN_DIR, name + ".json"), "w") as f:
             json.dump(meta, f, indent=1)
