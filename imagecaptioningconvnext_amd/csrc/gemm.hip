@@ -928,9 +928,24 @@ extern "C" int imgcap_gemm_mx(int M, int N, int K, const void* A, int64_t lda, c
     IMGCAP_REQUIRE(vec_ok && N % 32 == 0 && ldc % 32 == 0 && ep.c_scale && ep.res == nullptr,
                    "imgcap_gemm_mx: MX-FP8 output needs N, ldc % 32 == 0, 16-byte aligned C, c_scale, no res");
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid((N + 127) / 128, (M + 127) / 128);
-  hipLaunchKernelGGL((gemm_mx_kernel<2>), grid, dim3(256), 0, st, (const uint8_t*)A, (long)lda, As,
-                     (const uint8_t*)B, (long)ldb, Bs, C, (long)ldc, M, N, K, ep, vec_ok ? 1 : 0);
+  // 256x256 tile when it fills at least one round of the 256 CUs and K is long enough for its
+  // main loop to matter (with K = 768 the 128-tile's second resident block hides the GELU + MX
+  // epilogue: 85 vs 98 us at C5's stage-3 shape, tools/microbench.py mx); IMGCAP_MX_TILE forces
+  static const int force = [] {
+    const char* e = getenv("IMGCAP_MX_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const bool big = force ? force == 256 : (tiles256 >= 256 && K >= 1024);
+  if (big) {
+    dim3 grid((N + 255) / 256, (M + 255) / 256);
+    hipLaunchKernelGGL((gemm_mx256_kernel<2>), grid, dim3(512), 0, st, (const uint8_t*)A, (long)lda, As,
+                       (const uint8_t*)B, (long)ldb, Bs, C, (long)ldc, M, N, K, ep, vec_ok ? 1 : 0);
+  } else {
+    dim3 grid((N + 127) / 128, (M + 127) / 128);
+    hipLaunchKernelGGL((gemm_mx_kernel<2>), grid, dim3(256), 0, st, (const uint8_t*)A, (long)lda, As,
+                       (const uint8_t*)B, (long)ldb, Bs, C, (long)ldc, M, N, K, ep, vec_ok ? 1 : 0);
+  }
   IMGCAP_CHECK_LAUNCH("imgcap_gemm_mx");
   return 0;
 }

@@ -50,7 +50,8 @@ def test_mx_quant_rows_layernorm(hip_device):
     assert (s.cpu().int() - rs.int()).abs().max().item() <= 1  # block exponents agree (LN round-off)
 
 
-@pytest.mark.parametrize("M,N,Kd", [(300, 192, 256), (128, 128, 128), (1000, 3072, 768), (517, 768, 3072)])
+@pytest.mark.parametrize("M,N,Kd", [(300, 192, 256), (128, 128, 128), (1000, 3072, 768), (517, 768, 3072),
+                                    (4100, 4096, 1024)])  # the last one takes the 256x256 tile
 def test_gemm_mx_matches_dequantized_product(hip_device, M, N, Kd):
     from imagecaptioningconvnext_amd import kernels as K
     g = torch.Generator().manual_seed(M + N)
