@@ -115,6 +115,13 @@ class LstmEngine:
             main.wait_stream(st)
 
     # ---------------------------------------------------------------------------------------
+    def _side_stream(self, dev):
+        """A second stream for work off the recurrence's critical path (forked / joined with
+        events, so it is captured into the step's graph like the main stream)."""
+        if getattr(self, "_side", None) is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(device=dev)
+        return self._side
+
     def weights(self):
         fp, A, E, D, M, V = self.fp, self.A, self.E, self.D, self.M, self.V
         return dict(
@@ -184,14 +191,28 @@ class LstmEngine:
                          xe=xe, c0=c0, dl=dl, g1=g1, alphas=alphas, awe=awe, zs=zs, gates=gates, cs=cs, hs=hs,
                          hprev=hprev).items():
             setattr(d, k, v.data_ptr())
+        # k-major copies of the weights the backward recurrence multiplies by, made on a side
+        # stream under the forward recurrence (they only depend on the weights)
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            wzh_t = torch.empty(E + D, 4 * D, **ctd)                  # [W_ih[:, M:] | W_hh]^T
+            K.transpose(w["wih"][:, M:], out=wzh_t[:E])
+            K.transpose(w["hcat"][A + E:], out=wzh_t[E:])
+            watt_t = K.transpose(w["hcat"][:A + E])                    # [D, A + E] = [W_da; W_fb]^T
         self._launch("imgcap_lstm_tf_fwd", d)
+        main.wait_stream(side)
+        wzh_t.record_stream(main)
+        watt_t.record_stream(main)
         # ---- fc(dropout(h)) over all B*T rows (decoder.py:144) ----------------------------------
         hd = hs.view(B * T, D)
         if p_drop > 0:
             hd = K.dropout(hd, p_drop, s["seed"], _STREAM_DROPOUT_H)
         tmask = torch.arange(T, device=dev).view(1, T) < dl.view(B, 1)
         s.update(enc_s=enc_s, ids=ids, emb=emb, mean=mean, att1=att1, xe=xe, c0=c0, g1=g1, alphas=alphas, awe=awe,
-                 zs=zs, gates=gates, cs=cs, hs=hs, hprev=hprev, hd=hd, tmask=tmask, desc=d)
+                 zs=zs, gates=gates, cs=cs, hs=hs, hprev=hprev, hd=hd, tmask=tmask, desc=d, wzh_t=wzh_t,
+                 watt_t=watt_t)
         if loss:
             logits = torch.empty(B * T, self.Vpad, **ctd)
             K.gemm(hd, w["wfc"], trans_b=True, bias=w["bfc"], out=logits, N=V)
@@ -318,11 +339,18 @@ class LstmEngine:
             K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
             dalpha = s["dalpha"]
         BT = B * T
-        # fc: dW_fc = dlogits^T hd ; db_fc = colsum ; dh = (dlogits W_fc) * dropmask
-        wgb.add(dlogits, s["hd"], out=_G.g("fc.weight"), M=V, trans_a=True)
-        cb.add(dlogits, _G.g("fc.bias"), cols=V)
+        # fc: dh = (dlogits W_fc) * dropmask on the critical path; dW_fc = dlogits^T hd and
+        # db_fc = colsum(dlogits) on a side stream beside the backward recurrence
         dhs = K.gemm(dlogits, w["wfc"], K=V, drop_p=s["p_drop"], seed=s["seed"], drop_stream=_STREAM_DROPOUT_H,
                      drop_ld=D)
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):  # no library scratch on this stream (no split-K, one-pass colsum)
+            K.gemm(dlogits, s["hd"], trans_a=True, M=V, out=_G.g("fc.weight"), out_dtype=torch.float32)
+            cbs = K.ColsumBatch()
+            cbs.add(dlogits, _G.g("fc.bias"), cols=V)
+            cbs.run()
         f32 = dict(device=dev, dtype=torch.float32)
         dcat = torch.empty(B, T, W3, device=dev, dtype=ct)
         xs, ys = self.X_SLICES, self.Y_SLICES
@@ -342,11 +370,7 @@ class LstmEngine:
         datt1 = torch.empty(B * P, A, device=dev, dtype=ct)
         npc = (P + 6) // 7  # pixel chunks of attn_param_grad_kernel
         dwf, dbea = torch.empty(B * npc, A, **f32), torch.empty(B * npc, A, **f32)
-        # k-major copies of the weights the backward recurrence multiplies by
-        wzh_t = torch.empty(E + D, 4 * D, device=dev, dtype=ct)   # [W_ih[:, M:] | W_hh]^T
-        K.transpose(w["wih"][:, M:], out=wzh_t[:E])
-        K.transpose(w["hcat"][A + E:], out=wzh_t[E:])
-        watt_t = K.transpose(w["hcat"][:A + E])                    # [D, A + E] = [W_da; W_fb]^T
+        wzh_t, watt_t = s["wzh_t"], s["watt_t"]  # made under the forward recurrence
         d = s["desc"]
         bufs = dict(w_zh_t=wzh_t, w_att_t=watt_t, dhs=dhs, dalpha=dalpha, dcat=dcat, dh=dh, dc=dc, de=de,
                     datt1=datt1, dwf=dwf, dbea=dbea)
@@ -381,6 +405,7 @@ class LstmEngine:
         cb.add(dbea, _G.g("attention.encoder_att.bias"))
         cb.add(dwf, _G.g("attention.full_att.weight", (A,)))
         # full_att.bias: exactly zero gradient (softmax is shift-invariant) -> left at 0
+        torch.cuda.current_stream(dev).wait_stream(side)  # fc dW / db (beside the recurrence) done
         wgb.run()
         cb.run()
         s["denc"] = None
