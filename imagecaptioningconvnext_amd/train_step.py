@@ -16,10 +16,19 @@ stochastic-depth masks stay fresh per replay through the device step counter
 (imgcap_set_seed_counter) bumped inside the graph.  The all-reduce and the Adam step (whose
 bias correction depends on the host step count) run eagerly after the replay.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 from . import kernels as K
+
+
+# pipeline mode: one two-branch graph (0, default) or separate encoder / decoder graphs replayed
+# on two streams (1).  Measured (bench, 1x MI355X): split C2 7,070 vs 8,017 img/s, C3 15,233 vs
+# 14,960, C4 6,221 vs 6,181 -- the two-branch graph wins where it matters (C2), the split is
+# within run-to-run spread elsewhere.
+PIPE_SPLIT = int(os.environ.get("IMGCAP_PIPE_SPLIT", "0"))
 
 
 def _trainable(encoder):
@@ -133,6 +142,29 @@ class TeacherForcedTrainer:
         main.wait_stream(side)
         P["feats"] = [torch.empty_like(f), torch.empty_like(f)]
         P["graphs"], P["metrics"] = [], []
+        if PIPE_SPLIT:
+            # one graph per branch and slot, replayed on their own streams (under rocprofv3 the
+            # second branch of a two-branch graph starts late; unprofiled the single graph is as
+            # fast or faster, see PIPE_SPLIT).  Separate memory pools: the two run concurrently.
+            P["genc"], P["gdec"] = [], []
+            pool_e = pool_d = None
+            for k in (0, 1):  # encode the new batch into slot k / train on slot 1-k
+                ge = torch.cuda.CUDAGraph()
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    with torch.cuda.graph(ge, pool=pool_e, stream=side):
+                        P["feats"][k].copy_(self._encode(P["img"]))
+                main.wait_stream(side)
+                pool_e = ge.pool()
+                gd = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gd, pool=pool_d):
+                    m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k])
+                pool_d = gd.pool()
+                P["genc"].append(ge)
+                P["gdec"].append(gd)
+                P["metrics"].append(m)
+            self._pipe = P
+            return
         pool = None
         for k in (0, 1):  # graph k: encode the new batch into slot k, train on slot 1-k
             g = torch.cuda.CUDAGraph()
@@ -176,6 +208,15 @@ class TeacherForcedTrainer:
         m = None
         if P["i"] == 0:
             P["feats"][k].copy_(self._encode(P["img"]))
+        elif "genc" in P:
+            main = torch.cuda.current_stream()
+            self._seed_ctr.add_(1)  # before both branches read it (masks drawn at kernel run time)
+            P["side"].wait_stream(main)
+            P["gdec"][k].replay()
+            with torch.cuda.stream(P["side"]):
+                P["genc"][k].replay()
+            main.wait_stream(P["side"])
+            m = P["metrics"][k]
         else:
             P["graphs"][k].replay()
             m = P["metrics"][k]
