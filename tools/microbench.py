@@ -157,6 +157,22 @@ def misc():
     print(f"add_ln bwd {rows}x{cols}: {t * 1e6:8.1f} us")
 
 
+def small():
+    """The Transformer decoder's GEMMs (M = B*L = 3328 at C3, d = ff = 512) under each kernel
+    policy: which tile serves latency-bound small grids best."""
+    M = 64 * 52
+    for (N, Kd, tb) in ((1536, 512, True), (512, 512, True), (512, 512, False), (512, 1536, True)):
+        a = torch.randn(M, Kd, device=dev).to(bf)
+        w = (torch.randn(N, Kd, device=dev) if tb else torch.randn(Kd, N, device=dev)).to(bf)
+        bias = torch.randn(N, device=dev)
+        fl = 2.0 * M * N * Kd
+        for pol, name in ((-1, "auto"), (4, "glds128"), (5, "tiled"), (0, "no256")):
+            K.gemm_set_policy(pol)
+            t = time_launch(lambda: K.gemm(a, w, trans_b=tb, bias=bias))
+            print(f"M={M} N={N} K={Kd} tb={int(tb)} {name:8s}: {t * 1e6:7.1f} us {fl / t / 1e12:6.1f} TF")
+        K.gemm_set_policy(-1)
+
+
 def mx():
     """MX-FP8 vs bf16 GEMMs at the frozen ConvNeXt-Large stage-3 shapes (C5, B=64)."""
     M, C = 64 * 196, 768
@@ -201,6 +217,8 @@ if __name__ == "__main__":
         dw()
     if which == "mx":
         mx()
+    if which == "small":
+        small()
     if which in ("all", "gemm"):
         gemms()
     if which == "probe":
