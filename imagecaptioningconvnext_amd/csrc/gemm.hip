@@ -463,7 +463,7 @@ static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, lon
     // the 256 tile wins only with >= ~1.5 rounds of tiles over the CUs and long K (measured:
     // tools/microbench.py probe); below that the 2-blocks-per-CU 128 tile overlaps better
     const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-    if ((mode >= 1 && mode <= 3) || (mode < 0 && tiles256 >= 384 && K >= 1024)) return {IMGCAP_GEMM_GLDS256, 1};
+    if ((mode >= 1 && mode <= 3) || ((mode < 0 || mode >= 7) && tiles256 >= 384 && K >= 1024)) return {IMGCAP_GEMM_GLDS256, 1};
   }
   const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
   const auto auto_split = [&] {
@@ -476,7 +476,14 @@ static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, lon
     int sk = 1;
     if (split < 0 || (split == 1 && tiles128 < 256 && K >= 2048)) sk = auto_split();
     else if (split > 1) sk = split;
+    // 64x64 LDS-DMA tile (4 blocks per CU): small grids (the Transformer decoder's d=512
+    // projections at B*L rows) and short-K mid-size grids, where the 128 tile's fixed per-tile
+    // latency dominates (tools/microbench.py small: 1.2-1.5x at 104-975 128-tiles with K <= 1536;
+    // the 128 tile wins back only on >= ~1000-tile grids)
+    if (sk == 1 && (mode == 6 || (mode < 0 && (tiles128 < 128 || (tiles128 < 1024 && K <= 1536)))))
+      return {IMGCAP_GEMM_GLDS64, 1};
     if (sk > 1 || tiles128 >= 128 || mode == 4) return {IMGCAP_GEMM_GLDS, sk};
+    if (mode == 7) return {IMGCAP_GEMM_GLDS128X64, 1};
   }
   if (split != 1) {
     const int sk = split < 0 ? auto_split() : split;
@@ -525,7 +532,7 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       dim3 grid((N + 255) / 256, (M + 255) / 256);
       const bf16* a = (const bf16*)A;
       const bf16* b = (const bf16*)B;
-      const int var = gemm256_mode() >= 1 ? gemm256_mode() : 1;  // 1: BK 64 x 2 stages, 2: BK 32 x 4, 3: BK 32 x 3
+      const int var = gemm256_mode() >= 1 && gemm256_mode() <= 3 ? gemm256_mode() : 1;  // 1: BK 64 x 2 stages, 2: BK 32 x 4, 3: BK 32 x 3
 #define G256_V(AKV, BKV, BKT, SV)                                                                               \
   hipLaunchKernelGGL((gemm256_kernel<BKT, SV, AKV, BKV>), grid, dim3(512), 0, st, a, lda, b, ldb, C, ldc, M, N, K, \
                      ep, vec_ok, g_seed_ctr, 0)
@@ -542,6 +549,28 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
 #undef G256_
 #undef G256_V
       IMGCAP_CHECK_LAUNCH("imgcap_gemm(glds256)");
+      return 0;
+    }
+    if (plan.kind == IMGCAP_GEMM_GLDS64 || plan.kind == IMGCAP_GEMM_GLDS128X64) {
+      const bool sq = plan.kind == IMGCAP_GEMM_GLDS64;
+      dim3 grid((N + 63) / 64, sq ? (M + 63) / 64 : (M + 127) / 128);
+      const bf16* a = (const bf16*)A;
+      const bf16* b = (const bf16*)B;
+#define GS_(AKV, BKV)                                                                                                 \
+  do {                                                                                                             \
+    if (sq)                                                                                                        \
+      hipLaunchKernelGGL((gemm_glds_kernel<64, 64, AKV, BKV, 2>), grid, dim3(256), 0, st, a, lda, b, ldb, C, ldc, M, N, \
+                         K, ep, vec_ok, g_seed_ctr, 0);                                                            \
+    else                                                                                                           \
+      hipLaunchKernelGGL((gemm_glds_kernel<128, 64, AKV, BKV, 2>), grid, dim3(256), 0, st, a, lda, b, ldb, C, ldc, M, \
+                         N, K, ep, vec_ok, g_seed_ctr, 0);                                                         \
+  } while (0)
+      if (ak && bk) GS_(true, true);
+      else if (ak) GS_(true, false);
+      else if (bk) GS_(false, true);
+      else GS_(false, false);
+#undef GS_
+      IMGCAP_CHECK_LAUNCH("imgcap_gemm(glds small)");
       return 0;
     }
     if (plan.kind == IMGCAP_GEMM_GLDS) {
@@ -842,7 +871,7 @@ extern "C" int imgcap_transpose(int dtype, int rows, int cols, const void* in, i
 }
 
 extern "C" int imgcap_gemm_set_policy(int glds256) {
-  IMGCAP_REQUIRE(glds256 >= -1 && glds256 <= 5, "imgcap_gemm_set_policy: -1..5");
+  IMGCAP_REQUIRE(glds256 >= -1 && glds256 <= 8, "imgcap_gemm_set_policy: -1..8");
   g_gemm256_mode = glds256;
   return 0;
 }

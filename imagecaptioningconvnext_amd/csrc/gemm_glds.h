@@ -36,7 +36,7 @@ DEV void glds_issue_op(const bf16* __restrict__ P, long ld, int r0, int R, int k
       src = P + (long)min(r0 + r, R - 1) * ld + min(k0 + c * 8, ((K - 1) >> 3) << 3);
     } else {
       constexpr int SL = ROWS / 8;
-      const int kr = p / SL, c = (p % SL) ^ tr_swz(kr);
+      const int kr = p / SL, c = (p % SL) ^ (tr_swz(kr) & (SL - 1));
       const int col = min(r0 + c * 8, ((R - 1) >> 3) << 3);  // past-the-end slots re-read a valid one
       src = P + (long)min(k0 + kr, K - 1) * ld + col;
     }
@@ -81,8 +81,9 @@ DEV bf16x8 glds_frag_op(const char* img, int row0, int kk, int lane) {
     const int q = fr >> 2, p = fr & 3, g = fq;
     const int kr = kk * 32 + 8 * g + q;
     const int col = row0 + 4 * p;
-    const int byte_lo = kr * (ROWS * 2) + (((col >> 3) ^ tr_swz(kr)) << 4) + ((col & 7) << 1);
-    const int byte_hi = (kr + 4) * (ROWS * 2) + (((col >> 3) ^ tr_swz(kr + 4)) << 4) + ((col & 7) << 1);
+    constexpr int SM = ROWS / 8 - 1;  // 64-row images have 8 slots per k-row: 3-bit swizzle
+    const int byte_lo = kr * (ROWS * 2) + (((col >> 3) ^ (tr_swz(kr) & SM)) << 4) + ((col & 7) << 1);
+    const int byte_hi = (kr + 4) * (ROWS * 2) + (((col >> 3) ^ (tr_swz(kr + 4) & SM)) << 4) + ((col & 7) << 1);
     typedef __attribute__((address_space(3))) glds_v4s16 lds_v4s16;
     const glds_v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(img + byte_lo));
     const glds_v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s16*)(img + byte_hi));
@@ -185,13 +186,17 @@ DEV void glds_tile(const bf16* __restrict__ A, long lda, const bf16* __restrict_
     if (kslice)
       partial_from_lds<BN>(tile, LDT, EPI_ROWS, m0 + pass * EPI_ROWS, n0, M, N, (float*)C + (long)kz * M * N);
     else
-      epilogue_tile<BN, EPI_ROWS, 256>(ep, tile, LDT, m0 + pass * EPI_ROWS, n0, M, N, C, ldc, vec_ok != 0);
+      epilogue_tile<BN, EPI_ROWS, 256, (EPI_ROWS * BN / 2048 >= 2 ? 2 : 1)>(ep, tile, LDT, m0 + pass * EPI_ROWS, n0, M,
+                                                                            N, C, ldc, vec_ok != 0);
     __syncthreads();
   }
 }
 
+// 128x128 tiles fit two blocks per CU; the small-grid 64-wide tiles (a quarter / half of the
+// LDS and accumulators) four
 template <int BM, int BN, bool AK, bool BKM, int S>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 2 ? 2 : 1, S == 2 ? 2 : 1))) void
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    S == 2 ? (BM * BN <= 128 * 64 ? 4 : 2) : 1, S == 2 ? (BM * BN <= 128 * 64 ? 4 : 2) : 1))) void
 gemm_glds_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, void* __restrict__ C,
                  long ldc, int M, int N, int K, imgcap_epilogue ep, int vec_ok, const uint64_t* seed_ctr,
                  int kslice) {

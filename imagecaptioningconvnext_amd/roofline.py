@@ -26,7 +26,8 @@ PEAK_BF16_TFLOPS = 2500.0
 PEAK_FP8_TFLOPS = 5000.0  # dense block-scaled (MX) e4m3 MFMA
 
 _KIND_NAME = {1: "gemm_skinny_kernel", 2: "gemm_kernel<64,64,64>", 3: "gemm_kernel<128,128,64>",
-              4: "gemm_glds_kernel<128,128>", 5: "gemm256_kernel<256,256>"}
+              4: "gemm_glds_kernel<128,128>", 5: "gemm256_kernel<256,256>", 6: "gemm_glds_kernel<64,64>",
+              7: "gemm_glds_kernel<128,64>"}
 
 
 def time_launch(fn, reps=50, warm=5, graph=True):
@@ -76,11 +77,13 @@ def _gemm_groups(trainer, batch):
         kind, splits = K.gemm_plan(c["dtype"], c["ak"], c["bk"], c["M"], c["N"], c["K"], c["lda"], c["ldb"], 1,
                                    c["split_k"])
         name = _KIND_NAME.get(kind, f"gemm kind {kind}")
-        if kind in (2, 3, 4, 5):
+        if kind in (2, 3, 4, 5, 6, 7):
             name += f"<ak={c['ak']},bk={c['bk']}>" + (" (split-K)" if splits > 1 else "")
         tf = lambda v: "true" if v else "false"  # noqa: E731
         sym = {4: f"gemm_glds_kernel<128, 128, {tf(c['ak'])}, {tf(c['bk'])}, 2>",
-               5: f"gemm256_kernel<64, 2, {tf(c['ak'])}, {tf(c['bk'])}>"}.get(kind, _KIND_NAME.get(kind, ""))
+               5: f"gemm256_kernel<64, 2, {tf(c['ak'])}, {tf(c['bk'])}>",
+               6: f"gemm_glds_kernel<64, 64, {tf(c['ak'])}, {tf(c['bk'])}, 2>",
+               7: f"gemm_glds_kernel<128, 64, {tf(c['ak'])}, {tf(c['bk'])}, 2>"}.get(kind, _KIND_NAME.get(kind, ""))
         g = groups.setdefault(name, dict(name=name, calls=[], bound="mfma", symbol=sym))
         g["calls"].append(c)
     out = []

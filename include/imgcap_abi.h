@@ -124,13 +124,15 @@ int imgcap_mx_quant_rows(int dtype, int R, int K, const void* x, int64_t ldx, co
 /* Which kernel imgcap_gemm launches for these operands (diagnostics and the bench's roofline):
  * returns one of IMGCAP_GEMM_*; *splits (if not NULL) = K slices (1 = none). */
 enum { IMGCAP_GEMM_SKINNY = 1, IMGCAP_GEMM_TILED64 = 2, IMGCAP_GEMM_TILED128 = 3, IMGCAP_GEMM_GLDS = 4,
-       IMGCAP_GEMM_GLDS256 = 5 };
+       IMGCAP_GEMM_GLDS256 = 5, IMGCAP_GEMM_GLDS64 = 6, IMGCAP_GEMM_GLDS128X64 = 7 };
 int imgcap_gemm_plan(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda, int64_t ldb,
                      int batch, int split_k, int* splits);
 /* Kernel-selection policy for A/B tests and benchmarks: glds256 >= 1 serves every eligible
  * GEMM (bf16, unsplit, 16-byte operand pitches) with the 256x256 tile (1: 64-deep k-steps x 2
  * stages, 2: 32-deep x 4 stages, 3: 32-deep x 3 stages), 0 never, 4 = the 128x128 LDS-DMA tile
- * wherever eligible, 5 = register-staged tiles only, -1 by shape (default).
+ * wherever eligible, 5 = register-staged tiles only, -1 by shape (default); 6 = the 64x64
+ * LDS-DMA tile wherever eligible and unsplit; 7 / 8 = by shape, but grids under 128 128x128
+ * tiles on the 128x64 LDS-DMA tile / the register-staged 64x64 tile.
  * Process-wide; set before capturing graphs. */
 int imgcap_gemm_set_policy(int glds256);
 int imgcap_transpose(int dtype, int rows, int cols, const void* in, int64_t ldi, void* out, int64_t ldo,

@@ -161,15 +161,28 @@ def small():
     """The Transformer decoder's GEMMs (M = B*L = 3328 at C3, d = ff = 512) under each kernel
     policy: which tile serves latency-bound small grids best."""
     M = 64 * 52
-    for (N, Kd, tb) in ((1536, 512, True), (512, 512, True), (512, 512, False), (512, 1536, True)):
+    for (N, Kd, tb) in ((1536, 512, True), (512, 512, True), (512, 512, False), (512, 1536, True), (512, 1536, False)):
         a = torch.randn(M, Kd, device=dev).to(bf)
         w = (torch.randn(N, Kd, device=dev) if tb else torch.randn(Kd, N, device=dev)).to(bf)
         bias = torch.randn(N, device=dev)
         fl = 2.0 * M * N * Kd
-        for pol, name in ((-1, "auto"), (4, "glds128"), (5, "tiled"), (0, "no256")):
+        for pol, name in ((-1, "auto"), (4, "glds128"), (5, "tiled"), (6, "glds64"), (7, "glds128x64"),
+                          (8, "tiled64")):
             K.gemm_set_policy(pol)
             t = time_launch(lambda: K.gemm(a, w, trans_b=tb, bias=bias))
             print(f"M={M} N={N} K={Kd} tb={int(tb)} {name:8s}: {t * 1e6:7.1f} us {fl / t / 1e12:6.1f} TF")
+        K.gemm_set_policy(-1)
+    # larger grids (encoder Linears, LSTM projections): 128x128 vs 64x64 LDS-DMA tiles
+    for (M2, N, Kd) in ((12544, 1536, 384), (12544, 384, 1536), (3136, 3072, 768), (3136, 768, 3072),
+                        (1632, 2048, 512), (1632, 9490, 512), (6272, 384, 768)):
+        a = torch.randn(M2, Kd, device=dev).to(bf)
+        w = torch.randn(N, Kd, device=dev).to(bf)
+        bias = torch.randn(N, device=dev)
+        fl = 2.0 * M2 * N * Kd
+        for pol, name in ((-1, "auto"), (4, "glds128"), (6, "glds64")):
+            K.gemm_set_policy(pol)
+            t = time_launch(lambda: K.gemm(a, w, trans_b=True, bias=bias))
+            print(f"M={M2} N={N} K={Kd} tb=1 {name:8s}: {t * 1e6:7.1f} us {fl / t / 1e12:6.1f} TF")
         K.gemm_set_policy(-1)
 
 
