@@ -56,10 +56,11 @@ class LstmEngine:
         self.step_id = 0
         self._y_cnt = None
 
-    # K-slices of the backward step GEMMs (imgcap_lstm_desc.x_slices / y_slices): enough blocks
-    # to cover the CUs at batch 32 with D = 512 (x: 80 column tiles x 3, y: 32 x 8)
-    X_SLICES = 3
-    Y_SLICES = 8
+    # K-slices of the backward step GEMMs (imgcap_lstm_desc.x_slices / y_slices).  Measured at
+    # the C2 shape (B=32, D=512, tools/gpu/lstm_sweep.sh): x 2 / y 3 (80 x 2 and 32 x 3 blocks)
+    # 24.4 us/step; the former x 3 / y 8 (more blocks, each a shorter K) 26.7; y 16 33
+    X_SLICES = int(os.environ.get("IMGCAP_LSTM_XS", "2"))
+    Y_SLICES = int(os.environ.get("IMGCAP_LSTM_YS", "3"))
     # The batch rows are independent sequences, so the recurrence can run as CHAINS chains of
     # B / CHAINS rows, each on its own HIP stream (forked from / joined to the caller's stream,
     # graph-capturable).  Measured on MI355X (tools/microbench.py lstm): two chains take 1.85x
