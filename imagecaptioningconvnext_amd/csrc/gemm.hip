@@ -474,13 +474,17 @@ static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, lon
     // with a long K, chosen here; partial tiles go to scratch and the reduce kernel applies the
     // epilogue.  Auto: ~2 blocks per CU, >= 4 k-tiles per slice.
     int sk = 1;
-    if (split < 0 || (split == 1 && tiles128 < 256 && K >= 2048)) sk = auto_split();
+    // (auto split-K only past K = 4096: below it the unsplit 64x64 tile wins, e.g. 1632x512x2048
+    // 14.7 vs 20.1 us, 3136x768x3072 30.6 vs 33.7; at K = 9490 split-K 128 tiles win 41 vs 53)
+    const bool long_k_small_grid = split == 1 && tiles128 < 256 && K >= 2048;
+    if (split < 0 || (long_k_small_grid && mode != 6 && !(mode < 0 && K <= 4096))) sk = auto_split();
     else if (split > 1) sk = split;
     // 64x64 LDS-DMA tile (4 blocks per CU): small grids (the Transformer decoder's d=512
     // projections at B*L rows) and short-K mid-size grids, where the 128 tile's fixed per-tile
     // latency dominates (tools/microbench.py small: 1.2-1.5x at 104-975 128-tiles with K <= 1536;
     // the 128 tile wins back only on >= ~1000-tile grids)
-    if (sk == 1 && (mode == 6 || (mode < 0 && (tiles128 < 128 || (tiles128 < 1024 && K <= 1536)))))
+    if (sk == 1 && (mode == 6 || (mode < 0 && (tiles128 < 128 || (tiles128 < 1024 && K <= 1536) ||
+                                                 (tiles128 < 256 && K <= 4096)))))
       return {IMGCAP_GEMM_GLDS64, 1};
     if (sk > 1 || tiles128 >= 128 || mode == 4) return {IMGCAP_GEMM_GLDS, sk};
     if (mode == 7) return {IMGCAP_GEMM_GLDS128X64, 1};

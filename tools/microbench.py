@@ -184,6 +184,18 @@ def small():
             t = time_launch(lambda: K.gemm(a, w, trans_b=True, bias=bias))
             print(f"M={M2} N={N} K={Kd} tb=1 {name:8s}: {t * 1e6:7.1f} us {fl / t / 1e12:6.1f} TF")
         K.gemm_set_policy(-1)
+    # long-K small grids (auto split-K on the 128 tile) vs the unsplit 64 tile; tb=0 = dX form
+    for (M2, N, Kd, tb) in ((1568, 768, 3072, True), (3136, 768, 3072, True), (1632, 512, 2048, False),
+                            (1632, 512, 9490, False), (3328, 512, 9490, False)):
+        kp = (Kd + 7) // 8 * 8  # 16-byte row pitch (the logits' padded vocab rows)
+        a = torch.randn(M2, kp, device=dev).to(bf)[:, :Kd]
+        w = (torch.randn(N, kp, device=dev).to(bf)[:, :Kd] if tb else torch.randn(Kd, N, device=dev).to(bf))
+        fl = 2.0 * M2 * N * Kd
+        for pol, name in ((-1, "auto"), (6, "glds64")):
+            K.gemm_set_policy(pol)
+            t = time_launch(lambda: K.gemm(a, w, trans_b=tb))
+            print(f"M={M2} N={N} K={Kd} tb={int(tb)} {name:8s}: {t * 1e6:7.1f} us {fl / t / 1e12:6.1f} TF")
+        K.gemm_set_policy(-1)
 
 
 def mx():
