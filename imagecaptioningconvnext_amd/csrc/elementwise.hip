@@ -125,6 +125,54 @@ __global__ void mean_mid_kernel(int B, int P, int E, const TI* __restrict__ x, T
   }
 }
 
+// decoder.py:99,114-116 in one launch: sort the batch by caption length (descending, stable --
+// the order the engine has always used), gather encoder_out and the captions into that order,
+// decode lengths (len - 1, int32) and the pixel mean of each gathered row (decoder.py:99, the
+// same p-order fp32 sum as mean_mid_kernel).  Block r = destination row r: every block ranks the
+// (<= 256) lengths itself, so no second launch is needed for the gather.
+template <typename T>
+__global__ __launch_bounds__(256) void sort_gather_kernel(int B, int P, int E, int L, const int64_t* __restrict__ lens,
+                                                          const T* __restrict__ enc, const int64_t* __restrict__ caps,
+                                                          T* __restrict__ enc_out, T* __restrict__ mean_out,
+                                                          int64_t* __restrict__ caps_out, int64_t* __restrict__ sort_ind,
+                                                          int32_t* __restrict__ dl) {
+  __shared__ int64_t ls[256];
+  __shared__ int src_s;
+  const int r = blockIdx.x, tid = threadIdx.x;
+  if (tid < B) ls[tid] = lens[tid];
+  __syncthreads();
+  if (tid < B) {
+    const int64_t li = ls[tid];
+    int rank = 0;
+    for (int j = 0; j < B; ++j) rank += (ls[j] > li) || (ls[j] == li && j < tid);
+    if (rank == r) src_s = tid;
+  }
+  __syncthreads();
+  const int src = src_s;
+  if (tid == 0) {
+    sort_ind[r] = src;
+    dl[r] = (int32_t)(ls[src] - 1);
+  }
+  for (int i = tid; i < L; i += 256) caps_out[(long)r * L + i] = caps[(long)src * L + i];
+  constexpr int VEC = 16 / sizeof(T);
+  const T* in = enc + (long)src * P * E;
+  T* out = enc_out + (long)r * P * E;
+  for (int v = tid; v < E / VEC; v += 256) {
+    float acc[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    for (int p = 0; p < P; ++p) {
+      const uint4 u = *(const uint4*)(in + (long)p * E + v * VEC);
+      *(uint4*)(out + (long)p * E + v * VEC) = u;
+      const T* x = (const T*)&u;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] += to_f(x[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) mean_out[(long)r * E + v * VEC + k] = from_f<T>(acc[k] / P);
+  }
+}
+
 static dim3 grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 4096) b = 4096;
@@ -213,6 +261,24 @@ extern "C" int imgcap_mean_mid(int dtype, int B, int P, int E, const void* x, vo
     hipLaunchKernelGGL((mean_mid_kernel<float, float>), grid_for(n), dim3(256), 0, (hipStream_t)stream, B, P, E,
                        (const float*)x, (float*)out);
   IMGCAP_CHECK_LAUNCH("imgcap_mean_mid");
+  return 0;
+}
+
+extern "C" int imgcap_sort_gather_rows(int dtype, int B, int P, int E, int L, const int64_t* lens, const void* enc,
+                                       const int64_t* caps, void* enc_out, void* mean_out, int64_t* caps_out,
+                                       int64_t* sort_ind, int32_t* dl, void* stream) {
+  if (B == 0) return 0;
+  IMGCAP_REQUIRE(B >= 1 && B <= 256, "imgcap_sort_gather_rows: 1 <= B <= 256");
+  const int vec = dtype == IMGCAP_BF16 ? 8 : 4;
+  IMGCAP_REQUIRE(E % vec == 0 && ((uintptr_t)enc & 15) == 0 && ((uintptr_t)enc_out & 15) == 0,
+                 "imgcap_sort_gather_rows: 16-byte aligned rows of E elements");
+  if (dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL((sort_gather_kernel<bf16>), dim3(B), dim3(256), 0, (hipStream_t)stream, B, P, E, L, lens,
+                       (const bf16*)enc, caps, (bf16*)enc_out, (bf16*)mean_out, caps_out, sort_ind, dl);
+  else
+    hipLaunchKernelGGL((sort_gather_kernel<float>), dim3(B), dim3(256), 0, (hipStream_t)stream, B, P, E, L, lens,
+                       (const float*)enc, caps, (float*)enc_out, (float*)mean_out, caps_out, sort_ind, dl);
+  IMGCAP_CHECK_LAUNCH("imgcap_sort_gather_rows");
   return 0;
 }
 

@@ -407,6 +407,25 @@ def adaptive_pool(x, OH, OW, out):
     return out
 
 
+def sort_gather_rows(lens, enc, caps):
+    """decoder.py:99,114-116 in one launch: (enc_sorted [B,P,E], mean [B,E], caps_sorted [B,L],
+    sort_ind int64 [B], decode lengths int32 [B]), rows by caption length descending (stable)."""
+    _check_dev(lens, enc, caps)
+    B, P, E = enc.shape
+    L = caps.shape[1]
+    if lens.dtype != torch.int64 or caps.dtype != torch.int64 or not (lens.is_contiguous() and enc.is_contiguous()
+                                                                     and caps.is_contiguous()):
+        raise ValueError("sort_gather_rows: contiguous int64 lengths / captions and a contiguous enc")
+    enc_s = torch.empty_like(enc)
+    mean = torch.empty(B, E, device=enc.device, dtype=enc.dtype)
+    caps_s = torch.empty_like(caps)
+    sort_ind = torch.empty(B, device=enc.device, dtype=torch.int64)
+    dl = torch.empty(B, device=enc.device, dtype=torch.int32)
+    _abi.call("imgcap_sort_gather_rows", dt(enc), B, P, E, L, lens.data_ptr(), enc.data_ptr(), caps.data_ptr(),
+              enc_s.data_ptr(), mean.data_ptr(), caps_s.data_ptr(), sort_ind.data_ptr(), dl.data_ptr(), stream())
+    return enc_s, mean, caps_s, sort_ind, dl
+
+
 def mean_mid(x, out):
     B, P, E = x.shape
     _abi.call("imgcap_mean_mid", dt(x), B, P, E, x.data_ptr(), out.data_ptr(), stream())

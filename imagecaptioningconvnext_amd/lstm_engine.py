@@ -152,15 +152,22 @@ class LstmEngine:
         enc = encoder_out.reshape(B, -1, E)
         P = enc.size(1)
         L = encoded_captions.size(1)
-        lens, sort_ind = caption_lengths.reshape(-1).sort(dim=0, descending=True, stable=True)
-        enc_s = enc.index_select(0, sort_ind).to(ct).contiguous()
-        caps_s = encoded_captions.index_select(0, sort_ind)
-        dl = (lens - 1).to(torch.int32)
+        lens = caption_lengths.reshape(-1)
+        mean = None
+        if (B <= 256 and enc.dtype == ct and enc.is_contiguous() and lens.dtype == torch.int64
+                and encoded_captions.dtype == torch.int64 and encoded_captions.is_contiguous()):
+            # decoder.py:99,114-116 (sort, gathers, decode lengths, pixel mean) in one launch
+            enc_s, mean, caps_s, sort_ind, dl = K.sort_gather_rows(lens.contiguous(), enc, encoded_captions)
+        else:
+            lens, sort_ind = lens.sort(dim=0, descending=True, stable=True)
+            enc_s = enc.index_select(0, sort_ind).to(ct).contiguous()
+            caps_s = encoded_captions.index_select(0, sort_ind)
+            dl = (lens - 1).to(torch.int32)
         if fixed_T:
             T = L - 1
             dls = None
         else:
-            dls = (lens - 1).tolist()  # decoder.py:126 (host list, part of the reference API)
+            dls = dl.tolist()  # decoder.py:126 (host list, part of the reference API)
             T = max(dls)
         s = dict(B=B, P=P, T=T, L=L, sort_ind=sort_ind, caps_s=caps_s, dl=dl, dls=dls, p_drop=p_drop,
                  seed=self.seed + self.step_id)
@@ -171,8 +178,9 @@ class LstmEngine:
         ids = caps_s[:, :T].contiguous()
         emb = torch.empty(B * T, M, **ctd)
         K.embedding_fwd(ids, w["emb"], emb)                                   # decoder.py:119
-        mean = torch.empty(B, E, **ctd)
-        K.mean_mid(enc_s, mean)                                               # decoder.py:99
+        if mean is None:
+            mean = torch.empty(B, E, **ctd)
+            K.mean_mid(enc_s, mean)                                           # decoder.py:99
         h0c0 = K.gemm(mean, w["init"], trans_b=True, bias=w["binit"], out_dtype=torch.float32)  # :100-101
         att1 = K.gemm(enc_s.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])             # :61 hoisted
         xe = K.gemm(emb, w["wih"][:, :M], trans_b=True, bias=w["bih"], out_dtype=torch.float32)  # W_ih emb half

@@ -407,6 +407,12 @@ int imgcap_loss_finalize(int n, const float* loss_rows, const float* hit5, const
 
 /* out[b, e] = mean_p x[b, p, e] (decoder.py:99, input of init_h/init_c) */
 int imgcap_mean_mid(int dtype, int B, int P, int E, const void* x, void* out, void* stream);
+/* decoder.py:99,114-116 fused: rows sorted by caption length (descending, stable), enc_out[r] =
+ * enc[sort_ind[r]] ([B,P,E]), caps_out[r] = caps[sort_ind[r]] ([B,L] int64), dl[r] = len - 1
+ * (int32), mean_out[r] = mean over P of enc_out[r]; B <= 256, E rows 16-byte aligned */
+int imgcap_sort_gather_rows(int dtype, int B, int P, int E, int L, const int64_t* lens, const void* enc,
+                            const int64_t* caps, void* enc_out, void* mean_out, int64_t* caps_out, int64_t* sort_ind,
+                            int32_t* dl, void* stream);
 
 /* elementwise helpers */
 int imgcap_cast(int in_dtype, int out_dtype, int64_t n, const void* x, void* y, void* stream);

@@ -387,3 +387,26 @@ def test_gemm_grouped_weight_gradients(hip_device):
     batch.run()
     for out, ref in cases:
         assert _rel(out.cpu(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B", [1, 5, 32, 256])
+def test_sort_gather_rows(hip_device, dtype, B):
+    """decoder.py:99,114-116 fused: stable descending length sort (ties keep batch order), the
+    gathered encoder rows / captions bit-exact, decode lengths, and the pixel mean."""
+    g = torch.Generator(device="cpu").manual_seed(B)
+    P, E, L = 49, 768, 52
+    lens = torch.randint(8, 14, (B, 1), generator=g)  # many ties
+    enc = torch.randn(B, P, E, generator=g).to(dtype)
+    caps = torch.randint(0, 9490, (B, L), generator=g)
+    enc_s, mean, caps_s, ind, dl = K.sort_gather_rows(lens.reshape(-1).to(hip_device), enc.to(hip_device),
+                                                      caps.to(hip_device))
+    ref_len, ref_ind = lens.reshape(-1).sort(dim=0, descending=True, stable=True)
+    assert torch.equal(ind.cpu(), ref_ind)
+    assert torch.equal(dl.cpu(), (ref_len - 1).to(torch.int32))
+    assert torch.equal(enc_s.cpu(), enc.index_select(0, ref_ind))
+    assert torch.equal(caps_s.cpu(), caps.index_select(0, ref_ind))
+    ref_mean = torch.empty(B, E, device=hip_device, dtype=dtype)
+    K.mean_mid(enc_s, ref_mean)  # the unfused kernel: identical summation order
+    assert torch.equal(mean, ref_mean)
+    assert _rel(mean.cpu(), enc.index_select(0, ref_ind).float().mean(1)) < (1e-2 if dtype == torch.bfloat16 else 1e-6)
