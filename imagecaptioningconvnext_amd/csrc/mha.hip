@@ -55,25 +55,51 @@ DEV void wave_mm(f32x4 (&acc)[4], const T* A, const T* Bm, int row0, int lane) {
   }
 }
 
-// stage rows [0, L) of a [L][HD] head slice (row stride ld) into an LDS image; rows >= L zero
+// Staging of a [L][HD] head slice (row stride ld) into an LDS image, rows >= L zero.  Split in
+// two so a kernel issues the global loads of ALL its slices (and its mask / lse reads) before
+// the first LDS store: one memory round trip instead of one per slice and loop trip.  256
+// threads, 16-byte vectors: 2 per thread per slice (bf16), 4 (fp32).
+template <typename T> struct RowVecs {
+  static constexpr int VEC = 16 / sizeof(T), NV = HD / VEC, PER = LP * NV / 256;
+  uint4 v[PER];
+};
 template <typename T>
-DEV void stage_rows(T* img, const T* src, long ld, int L) {
-  constexpr int LD = Img<T>::LD, VEC = 16 / sizeof(T);
-  for (int e = threadIdx.x; e < LP * (HD / VEC); e += blockDim.x) {
-    const int r = e / (HD / VEC), c = (e % (HD / VEC)) * VEC;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (r < L) v = *(const uint4*)(src + (long)r * ld + c);
-    *(uint4*)(img + r * LD + c) = v;
+DEV void load_rows(RowVecs<T>& rv, const T* src, long ld, int L) {
+  using R = RowVecs<T>;
+#pragma unroll
+  for (int i = 0; i < R::PER; ++i) {
+    const int e = threadIdx.x + i * 256;
+    const int r = e / R::NV, c = (e % R::NV) * R::VEC;
+    rv.v[i] = r < L ? *(const uint4*)(src + (long)r * ld + c) : make_uint4(0u, 0u, 0u, 0u);
   }
 }
-// transposed image: img[c][r] = src row r, column c
 template <typename T>
-DEV void stage_rows_t(T* img, const T* src, long ld, int L) {
+DEV void store_rows(T* img, const RowVecs<T>& rv) {
+  using R = RowVecs<T>;
   constexpr int LD = Img<T>::LD;
-  for (int e = threadIdx.x; e < LP * HD; e += blockDim.x) {
-    const int r = e / HD, c = e % HD;
-    img[c * LD + r] = r < L ? src[(long)r * ld + c] : from_f<T>(0.f);
+#pragma unroll
+  for (int i = 0; i < R::PER; ++i) {
+    const int e = threadIdx.x + i * 256;
+    *(uint4*)(img + (e / R::NV) * LD + (e % R::NV) * R::VEC) = rv.v[i];
   }
+}
+// transposed image: img[c][r] = row r, column c
+template <typename T>
+DEV void store_rows_t(T* img, const RowVecs<T>& rv) {
+  using R = RowVecs<T>;
+  constexpr int LD = Img<T>::LD;
+#pragma unroll
+  for (int i = 0; i < R::PER; ++i) {
+    const int e = threadIdx.x + i * 256;
+    const int r = e / R::NV, c = (e % R::NV) * R::VEC;
+    const T* x = (const T*)&rv.v[i];
+#pragma unroll
+    for (int k = 0; k < R::VEC; ++k) img[(c + k) * LD + r] = x[k];
+  }
+}
+// key-padding flags of batch row b (1 = masked) for the block's LDS copy
+DEV unsigned char key_pad_flag(const imgcap_mha_desc& d, int b, int j) {
+  return (j < d.Lk && d.key_ids && d.key_ids[(long)b * d.Lk + j] == d.pad_id) ? 1 : 0;
 }
 // transpose an LDS image
 template <typename T>
@@ -96,11 +122,10 @@ DEV float row_sum16(float v) {
   return v;
 }
 
-DEV bool key_masked(const imgcap_mha_desc& d, int b, int i, int j) {
+DEV bool key_masked(const imgcap_mha_desc& d, const unsigned char* kpad, int i, int j) {
   if (j >= d.Lk) return true;
   if (d.causal && j > i) return true;
-  if (d.key_ids && d.key_ids[(long)b * d.Lk + j] == d.pad_id) return true;
-  return false;
+  return kpad[j] != 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -118,9 +143,18 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(imgcap_mha_desc d, const u
   const T* q = (const T*)d.q + (long)b * d.Lq * d.ldq + h * HD;
   const T* k = (const T*)d.k + (long)b * kvr * d.ldk + h * HD;
   const T* v = (const T*)d.v + (long)b * kvr * d.ldv + h * HD;
-  stage_rows<T>(Qs, q, d.ldq, d.Lq);
-  stage_rows<T>(Ks, k, d.ldk, d.Lk);
-  stage_rows_t<T>(Vt, v, d.ldv, d.Lk);
+  __shared__ unsigned char kpad[LP];
+  {
+    RowVecs<T> qv, kv, vv;
+    load_rows<T>(qv, q, d.ldq, d.Lq);
+    load_rows<T>(kv, k, d.ldk, d.Lk);
+    load_rows<T>(vv, v, d.ldv, d.Lk);
+    const unsigned char kp = threadIdx.x < LP ? key_pad_flag(d, b, threadIdx.x) : 0;
+    store_rows<T>(Qs, qv);
+    store_rows<T>(Ks, kv);
+    store_rows_t<T>(Vt, vv);
+    if (threadIdx.x < LP) kpad[threadIdx.x] = kp;
+  }
   __syncthreads();
   f32x4 s[4];
   const int row0 = w * 16;
@@ -134,7 +168,7 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(imgcap_mha_desc d, const u
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = j * 16 + (lane & 15);
-      const float x = key_masked(d, b, i, col) ? -INFINITY : s[j][r] * d.scale;
+      const float x = key_masked(d, kpad, i, col) ? -INFINITY : s[j][r] * d.scale;
       s[j][r] = x;
       m = fmaxf(m, x);
     }
@@ -199,12 +233,28 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(imgcap_mha_desc d, const u
   const T* k = (const T*)d.k + (long)b * d.Lk * d.ldk + h * HD;
   const T* v = (const T*)d.v + (long)b * d.Lk * d.ldv + h * HD;
   const T* dO = (const T*)d.dout + (long)b * d.Lq * d.lddo + h * HD;
-  stage_rows<T>(Qs, q, d.ldq, d.Lq);
-  stage_rows<T>(Ks, k, d.ldk, d.Lk);
-  stage_rows<T>(Vs, v, d.ldv, d.Lk);
-  stage_rows<T>(dOs, dO, d.lddo, d.Lq);
-  __syncthreads();
+  __shared__ unsigned char kpad[LP];
   const int row0 = w * 16;
+  float lse_r[4];
+  {
+    RowVecs<T> qv, kv, vv, ov;
+    load_rows<T>(qv, q, d.ldq, d.Lq);
+    load_rows<T>(kv, k, d.ldk, d.Lk);
+    load_rows<T>(vv, v, d.ldv, d.Lk);
+    load_rows<T>(ov, dO, d.lddo, d.Lq);
+    const unsigned char kp = threadIdx.x < LP ? key_pad_flag(d, b, threadIdx.x) : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = row0 + 4 * (lane >> 4) + r;
+      lse_r[r] = i < d.Lq ? d.lse[(long)bh * d.Lq + i] : 0.f;
+    }
+    store_rows<T>(Qs, qv);
+    store_rows<T>(Ks, kv);
+    store_rows<T>(Vs, vv);
+    store_rows<T>(dOs, ov);
+    if (threadIdx.x < LP) kpad[threadIdx.x] = kp;
+  }
+  __syncthreads();
   f32x4 p[4], dp[4];
   wave_mm<T>(p, Qs, Ks, row0, lane);    // S
   wave_mm<T>(dp, dOs, Vs, row0, lane);  // dP~ = dO V^T
@@ -212,12 +262,12 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(imgcap_mha_desc d, const u
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = row0 + 4 * (lane >> 4) + r;
-    const float lse = i < d.Lq ? d.lse[(long)bh * d.Lq + i] : 0.f;
+    const float lse = lse_r[r];
     float dot = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = j * 16 + (lane & 15);
-      const bool masked = i >= d.Lq || key_masked(d, b, i, col);
+      const bool masked = i >= d.Lq || key_masked(d, kpad, i, col);
       const float pr = masked ? 0.f : __expf(p[j][r] * d.scale - lse);
       const float ms = (d.drop_p > 0.f && !masked)
                            ? dropout_scale(d.seed, d.drop_stream, (((uint64_t)bh * d.Lq + i) * d.Lk + col), d.drop_p)
@@ -233,7 +283,7 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(imgcap_mha_desc d, const u
       const int col = j * 16 + (lane & 15);
       const float pr = p[j][r];
       dp[j][r] = pr * (dp[j][r] - dot);  // dS
-      const bool masked = i >= d.Lq || key_masked(d, b, i, col);
+      const bool masked = i >= d.Lq || key_masked(d, kpad, i, col);
       const float ms = (d.drop_p > 0.f && !masked)
                            ? dropout_scale(d.seed, d.drop_stream, (((uint64_t)bh * d.Lq + i) * d.Lk + col), d.drop_p)
                            : 1.f;

@@ -198,6 +198,29 @@ def small():
         K.gemm_set_policy(-1)
 
 
+def mha():
+    """Fused attention at the C3 shape (B=64, 8 heads of 64, L=52; self causal + key padding,
+    cross over 49 pixels), forward and backward per launch."""
+    import ctypes
+    from imagecaptioningconvnext_amd import _abi
+    B, H, d = 64, 8, 512
+    for (Lq, Lk, causal) in ((52, 52, True), (52, 49, False)):
+        q, k, v, o, do = (torch.randn(B, L_, d, device=dev).to(bf) for L_ in (Lq, Lk, Lk, Lq, Lq))
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        lse = torch.empty(B, H, Lq, device=dev)
+        ids = torch.randint(1, 50, (B, Lk), device=dev)
+        m = _abi.MhaDesc()
+        m.dtype, m.B, m.H, m.Lq, m.Lk, m.dh, m.causal, m.pad_id, m.scale = K.dt(q), B, H, Lq, Lk, 64, int(causal), 0, 0.125
+        m.ldq = m.ldk = m.ldv = m.ldo = m.lddo = m.lddq = m.lddk = m.lddv = d
+        m.q, m.k, m.v, m.o, m.lse = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr()
+        m.dout, m.dq, m.dk, m.dv = do.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+        m.key_ids = ids.data_ptr() if causal else None
+        m.drop_p = 0.5
+        tf = time_launch(lambda: _abi.call("imgcap_mha_fwd", ctypes.byref(m), K.stream()))
+        tb = time_launch(lambda: _abi.call("imgcap_mha_bwd", ctypes.byref(m), K.stream()))
+        print(f"mha Lq={Lq} Lk={Lk} causal={int(causal)}: fwd {tf * 1e6:6.1f} us  bwd {tb * 1e6:6.1f} us")
+
+
 def mx():
     """MX-FP8 vs bf16 GEMMs at the frozen ConvNeXt-Large stage-3 shapes (C5, B=64)."""
     M, C = 64 * 196, 768
@@ -244,6 +267,8 @@ if __name__ == "__main__":
         mx()
     if which == "small":
         small()
+    if which == "mha":
+        mha()
     if which in ("all", "gemm"):
         gemms()
     if which == "probe":
