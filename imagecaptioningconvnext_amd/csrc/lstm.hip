@@ -98,6 +98,14 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
     const int p = pg + i * G;
     raw_load(ev[i], enc + (long)min(p, P - 1) * E + v * 8);
   }
+  // gate pre-activation of the output element(s) this thread writes at the end
+  constexpr int EPT = 2;  // E <= EPT * ATT_THREADS (checked on the host)
+  float gpre[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + k * ATT_THREADS;
+    gpre[k] = e < E ? g1[A + e] : 0.f;
+  }
   // ---- scores e_p = w_f . relu(att1_p + att2)   (full_att bias cancels in the softmax) ----
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -144,10 +152,13 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
   __syncthreads();
   T* zs = (T*)d.zs + bt * E;
   float* awe = d.awe + bt * E;
-  for (int e = threadIdx.x; e < E; e += ATT_THREADS) {
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = threadIdx.x + k * ATT_THREADS;
+    if (e >= E) break;
     float s = 0.f;
     for (int q = 0; q < G; ++q) s += part[q * E + e];
-    const float gate = sigmoidf_(g1[A + e]);
+    const float gate = sigmoidf_(gpre[k]);
     awe[e] = s;
     zs[e] = from_f<T>(gate * s);
   }
@@ -399,8 +410,13 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
       for (int j = 0; j < 8; ++j) dz[j] += q[j];
     }
   }
-  float alpha_in = 0.f;
-  if (tid < P) alpha_in = d.alphas[bt * P + tid];
+  float alpha_in = 0.f, dalpha_in = 0.f;
+  if (tid < P) {
+    alpha_in = d.alphas[bt * P + tid];
+    if (d.dalpha) dalpha_in = d.dalpha[bt * P + tid];
+  }
+  constexpr int APT = 1;  // A <= ATT_THREADS (checked on the host)
+  const float wf_a = tid < A ? d.w_f[tid] : 0.f;
   // ---- d awe = dz * sigmoid(gate), d gate_pre = dz * awe * s (1 - s) ----
   if (pg == 0) {
     float dg[8];
@@ -415,7 +431,10 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
     st_g<T, 8>(dcat + A + v * 8, dg);
     if (dawe_o) st_g<float, 8>(dawe_o + v * 8, da);
   }
-  if (tid < P) al[tid] = alpha_in;
+  if (tid < P) {
+    al[tid] = alpha_in;
+    dal[tid] = dalpha_in;  // upstream d alpha, read back by the softmax backward
+  }
   __syncthreads();
   // ---- d alpha_p = enc_p . d awe (+ upstream) ----
   if (pg < G) {
@@ -440,12 +459,12 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
     float s = 0.f;
     for (int q = lane; q < NVE; q += 64) s += red[p * NVE + q];
     s = wave_sum(s);
-    if (lane == 0) dal[p] = s;
+    if (lane == 0) dal[p] += s;
   }
   __syncthreads();
   if (w == 0) {  // softmax backward -> d score
     const float a = lane < P ? al[lane] : 0.f;
-    const float da = lane < P ? dal[lane] + (d.dalpha ? d.dalpha[bt * P + lane] : 0.f) : 0.f;
+    const float da = lane < P ? dal[lane] : 0.f;
     const float dot = wave_sum(a * da);
     if (lane < P) {
       const float de = a * (da - dot);
@@ -472,10 +491,11 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_bwd_kernel(imgcap_lstm_desc 
     for (int j = 0; j < 8; ++j) red[pga * A + va * 8 + j] = sacc[j];
   }
   __syncthreads();
-  for (int a = tid; a < A; a += ATT_THREADS) {
+  static_assert(APT == 1, "one attention unit per thread");
+  if (tid < A) {
     float s = 0.f;
-    for (int q = 0; q < GA; ++q) s += red[q * A + a];
-    dcat[a] = from_f<T>(s * d.w_f[a]);
+    for (int q = 0; q < GA; ++q) s += red[q * A + tid];
+    dcat[tid] = from_f<T>(s * wf_a);
   }
 }
 
@@ -733,7 +753,7 @@ static int check_desc(const imgcap_lstm_desc* d) {
   IMGCAP_REQUIRE(d->dtype == IMGCAP_F32 || d->dtype == IMGCAP_BF16, "lstm: dtype");
   IMGCAP_REQUIRE(d->B > 0 && d->T > 0 && d->P > 0 && d->P <= MAXP, "lstm: need 0 < P <= 64");
   IMGCAP_REQUIRE(d->E % 8 == 0 && d->A % 8 == 0 && d->M % 8 == 0 && d->D % 16 == 0, "lstm: E, A, M % 8, D % 16");
-  IMGCAP_REQUIRE(d->A <= 512 && d->E <= 8 * ATT_THREADS, "lstm: attention_dim <= 512, encoder_dim <= 8192");
+  IMGCAP_REQUIRE(d->A <= 512 && d->E <= 2 * ATT_THREADS, "lstm: attention_dim <= 512, encoder_dim <= 2048");
   IMGCAP_REQUIRE(attn_mpp(*d) <= 16, "lstm: too many pixels per attention thread");
   IMGCAP_REQUIRE((size_t)(ATT_THREADS / (d->E / 8)) * d->E * 4 <= 65536 && attn_bwd_shm(*d) <= 65536,
                  "lstm: attention LDS budget");
