@@ -45,7 +45,8 @@ class MhaDesc(ctypes.Structure):
         ("q", c_void_p), ("k", c_void_p), ("v", c_void_p), ("o", c_void_p), ("lse", c_void_p),
         ("key_ids", c_void_p), ("scale", c_float), ("drop_p", c_float), ("seed", c_uint64),
         ("drop_stream", c_uint32), ("dout", c_void_p), ("lddo", c_int64), ("dq", c_void_p), ("dk", c_void_p),
-        ("dv", c_void_p), ("lddq", c_int64), ("lddk", c_int64), ("lddv", c_int64), ("kv_rows", c_int64)]
+        ("dv", c_void_p), ("lddq", c_int64), ("lddk", c_int64), ("lddv", c_int64), ("kv_rows", c_int64),
+        ("probs", c_void_p)]
 
 
 class GemmProblem(ctypes.Structure):

@@ -10,9 +10,9 @@ with the surviving beams (the reference re-decodes every beam's whole prefix eac
 
 Image input: a path (PIL read, RGB, 256x256 bicubic, as caption.py:52-58) or a [3, H, W]
 tensor; the encoder normalises uint8 pixels on the GPU exactly as caption.py:59-63 does on the
-host.  Not here: the attention-weight export of ``caption_image_beam_search_transformer_attention``
-(its TransformerDecoderForAttentionViz layers return per-head attention probabilities, which
-the fused attention kernel does not materialise).
+host.  ``caption_image_beam_search_transformer_attention`` (caption.py:260-383, with a
+``TransformerDecoderForAttentionViz``) also returns the per-step cross-attention map averaged over
+layers and heads: the attention kernel writes its probabilities when asked (imgcap_mha_desc.probs).
 """
 import numpy as np
 import torch
@@ -96,6 +96,18 @@ def caption_image_beam_search(encoder, decoder, imagePath, wordMap, beamSize=3):
 
 def caption_image_beam_search_transformer(encoder, decoder, imagePath, wordMap, beamSize=3, max_decode_len=51):
     """caption.py:160-255 -> (seq: list of word ids incl. <start> / <end>, None)."""
+    return _transformer_beam(encoder, decoder, imagePath, wordMap, beamSize, max_decode_len, False)
+
+
+def caption_image_beam_search_transformer_attention(encoder, decoder, imagePath, wordMap, filename, beamSize=3,
+                                                    max_decode_len=51):
+    """caption.py:260-383 -> (seq, alphas: [max_decode_len][num_pixels] nested list, the cross-
+    attention of each emitted word averaged over layers and heads, zero past the caption).
+    ``filename`` is unused, as in the reference."""
+    return _transformer_beam(encoder, decoder, imagePath, wordMap, beamSize, max_decode_len, True)
+
+
+def _transformer_beam(encoder, decoder, imagePath, wordMap, beamSize, max_decode_len, with_alphas):
     k = beamSize
     vocab_size = len(wordMap)
     end_token_idx = wordMap['<end>']
@@ -103,40 +115,58 @@ def caption_image_beam_search_transformer(encoder, decoder, imagePath, wordMap, 
     encoderOut = _encode(encoder, imagePath, dev)
     encoderDim = encoderOut.size(3)
     eng = decoder.engine()
-    with torch.no_grad():
-        st = eng.decode_init(encoderOut.reshape(1, -1, encoderDim).expand(k, -1, encoderDim), max_decode_len)
-        kPrevWords = torch.full((k, 1), wordMap['<start>'], dtype=torch.long, device=dev)
-        topKScores = torch.zeros(k, 1, device=dev)
-        completeSeqs, completeSeqsScores = [], []
-        step = 0
-        while True:
-            logits = eng.decode_step(st, kPrevWords[:, -1].contiguous())    # caption.py:202-216
-            scoresActive = F.log_softmax(logits[:, :vocab_size].float(), dim=1)
-            scoresActive = topKScores.expand_as(scoresActive) + scoresActive
-            if step == 0:
-                topKScoresNew, topKUnrolledIndices = scoresActive[0].topk(k, 0, True, True)
-            else:
-                topKScoresNew, topKUnrolledIndices = scoresActive.view(-1).topk(k, 0, True, True)
-            prevWordActiveIndices = torch.div(topKUnrolledIndices, vocab_size, rounding_mode='floor')
-            nextWordsIds = topKUnrolledIndices % vocab_size
-            newKPrevWordsIds = torch.cat([kPrevWords[prevWordActiveIndices], nextWordsIds.unsqueeze(1)], dim=1)
-            newTopKScores = topKScoresNew.unsqueeze(1)
-            justCompletedMask = nextWordsIds == end_token_idx
-            justCompletedIndices = torch.nonzero(justCompletedMask, as_tuple=False).squeeze(1)
-            if len(justCompletedIndices) > 0:
-                completeSeqs.extend(newKPrevWordsIds[justCompletedIndices].tolist())
-                completeSeqsScores.extend(newTopKScores[justCompletedIndices].squeeze(1).tolist())
-            incompleteIndices = torch.nonzero(~justCompletedMask, as_tuple=False).squeeze(1)
-            k -= len(justCompletedIndices)
-            if k == 0:
-                break
-            kPrevWords = newKPrevWordsIds[incompleteIndices]
-            topKScores = newTopKScores[incompleteIndices]
-            eng.decode_select(st, prevWordActiveIndices[incompleteIndices])  # caches follow their beams
-            if step + 1 >= max_decode_len:
-                break
-            step += 1
+    try:
+        with torch.no_grad():
+            st = eng.decode_init(encoderOut.reshape(1, -1, encoderDim).expand(k, -1, encoderDim), max_decode_len)
+            num_pixels = st["P"]
+            kPrevWords = torch.full((k, 1), wordMap['<start>'], dtype=torch.long, device=dev)
+            topKScores = torch.zeros(k, 1, device=dev)
+            seqsAlphas = torch.zeros(k, max_decode_len, num_pixels, device=dev) if with_alphas else None
+            completeSeqs, completeSeqsScores, completeSeqsAlphas = [], [], []
+            step = 0
+            while True:
+                if with_alphas:
+                    eng.cross_probs = []
+                logits = eng.decode_step(st, kPrevWords[:, -1].contiguous())    # caption.py:202-216
+                scoresActive = F.log_softmax(logits[:, :vocab_size].float(), dim=1)
+                scoresActive = topKScores.expand_as(scoresActive) + scoresActive
+                if step == 0:
+                    topKScoresNew, topKUnrolledIndices = scoresActive[0].topk(k, 0, True, True)
+                else:
+                    topKScoresNew, topKUnrolledIndices = scoresActive.view(-1).topk(k, 0, True, True)
+                prevWordActiveIndices = torch.div(topKUnrolledIndices, vocab_size, rounding_mode='floor')
+                nextWordsIds = topKUnrolledIndices % vocab_size
+                newKPrevWordsIds = torch.cat([kPrevWords[prevWordActiveIndices], nextWordsIds.unsqueeze(1)], dim=1)
+                newTopKScores = topKScoresNew.unsqueeze(1)
+                justCompletedMask = nextWordsIds == end_token_idx
+                justCompletedIndices = torch.nonzero(justCompletedMask, as_tuple=False).squeeze(1)
+                if with_alphas:                                                   # caption.py:332-345
+                    # [layers, k, H, 1, P] -> this word's map averaged over layers and heads
+                    avg = torch.stack(eng.cross_probs, dim=0)[:, :, :, -1, :].mean(dim=(0, 2))
+                    newSeqsAlphas = torch.zeros(k, max_decode_len, num_pixels, device=dev)
+                    if step > 0:
+                        newSeqsAlphas[:, :step, :] = seqsAlphas[prevWordActiveIndices, :step, :]
+                    newSeqsAlphas[:, step, :] = avg[prevWordActiveIndices]
+                if len(justCompletedIndices) > 0:
+                    completeSeqs.extend(newKPrevWordsIds[justCompletedIndices].tolist())
+                    if with_alphas:
+                        completeSeqsAlphas.extend(newSeqsAlphas[justCompletedIndices].tolist())
+                    completeSeqsScores.extend(newTopKScores[justCompletedIndices].squeeze(1).tolist())
+                incompleteIndices = torch.nonzero(~justCompletedMask, as_tuple=False).squeeze(1)
+                k -= len(justCompletedIndices)
+                if k == 0:
+                    break
+                kPrevWords = newKPrevWordsIds[incompleteIndices]
+                topKScores = newTopKScores[incompleteIndices]
+                if with_alphas:
+                    seqsAlphas = newSeqsAlphas[incompleteIndices]
+                eng.decode_select(st, prevWordActiveIndices[incompleteIndices])  # caches follow their beams
+                if step + 1 >= max_decode_len:
+                    break
+                step += 1
+    finally:
+        eng.cross_probs = None
     if not completeSeqsScores:
         raise ValueError("beam search: no beam reached <end> within max_decode_len steps")
     i = completeSeqsScores.index(max(completeSeqsScores))
-    return completeSeqs[i], None
+    return completeSeqs[i], (completeSeqsAlphas[i] if with_alphas else None)

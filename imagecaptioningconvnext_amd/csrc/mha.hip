@@ -191,6 +191,7 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(imgcap_mha_desc d, const u
       if (d.drop_p > 0.f && i < d.Lq && col < d.Lk)
         p *= dropout_scale(d.seed, d.drop_stream, (((uint64_t)bh * d.Lq + i) * d.Lk + col), d.drop_p);
       s[j][r] = p;
+      if (d.probs && i < d.Lq && col < d.Lk) d.probs[((long)bh * d.Lq + i) * d.Lk + col] = p;
     }
   }
   __syncthreads();  // everyone is done reading Ks: reuse it for P~

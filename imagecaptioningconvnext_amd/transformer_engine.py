@@ -52,16 +52,23 @@ class TransformerEngine:
         self.layers = dec.num_layers
         self.Vpad = (self.V + 7) // 8 * 8
         self.has_proj = "encoder_proj.weight" in self.fp.params
+        self.layer_prefix = getattr(dec, "layer_prefix", "transformer_decoder.layers")
+        # per-layer cross-attention probabilities [B, H, Lq, P] of the last forward / decode
+        # step (set to a list to record them: the attention-visualisation decoder's alphas)
+        self.cross_probs = None
         if self.d // self.H != 64:
             raise NotImplementedError("the HIP attention kernel needs head dim 64 (embed_dim = 64 * num_heads)")
         self.seed = 4321
         self.step_id = 0
 
     def _lw(self, i, name):
-        return f"transformer_decoder.layers.{i}.{name}"
+        # nn.TransformerDecoder layers (transformerDecoder.py) or the attention-visualisation
+        # decoder's ModuleList (transformerDecoderAttVis.py:123: decoder_layers.{i}.*)
+        return f"{self.layer_prefix}.{i}.{name}"
 
     def _mha(self, *, B, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, causal, key_ids, pad_id, p, seed, sid,
-             dout=None, lddo=0, dq=None, lddq=0, dk=None, lddk=0, dv=None, lddv=0, bwd=False, kv_rows=0):
+             dout=None, lddo=0, dq=None, lddq=0, dk=None, lddk=0, dv=None, lddv=0, bwd=False, kv_rows=0,
+             probs=None):
         m = _abi.MhaDesc()
         m.dtype, m.B, m.H, m.Lq, m.Lk, m.dh, m.causal = K.dt(q), B, self.H, Lq, Lk, 64, int(causal)
         m.pad_id = pad_id
@@ -70,6 +77,7 @@ class TransformerEngine:
         m.key_ids = K.ptr(key_ids)
         m.scale = 1.0 / math.sqrt(64.0)
         m.kv_rows = kv_rows
+        m.probs = K.ptr(probs)
         m.drop_p, m.seed, m.drop_stream = p, seed, sid
         if bwd:
             m.dout, m.lddo = dout.data_ptr(), lddo
@@ -127,8 +135,12 @@ class TransformerEngine:
             kv2 = K.gemm(mem, wq[d:], trans_b=True, bias=bq[d:])
             o2 = torch.empty(BL, d, **ctd)
             lse2 = torch.empty(B, self.H, L, **f32)
+            pr = None
+            if self.cross_probs is not None:
+                pr = torch.empty(B, self.H, L, P, **f32)
+                self.cross_probs.append(pr)
             self._mha(B=B, Lq=L, Lk=P, q=q2, ldq=d, k=kv2, ldk=2 * d, v=kv2[:, d:], ldv=2 * d, o=o2, ldo=d, lse=lse2,
-                      causal=False, key_ids=None, pad_id=0, p=p, seed=seed, sid=_s(i, 2))
+                      causal=False, key_ids=None, pad_id=0, p=p, seed=seed, sid=_s(i, 2), probs=pr)
             y2 = K.gemm(o2, fp.w(lw("multihead_attn.out_proj.weight")), trans_b=True,
                         bias=fp.f32(lw("multihead_attn.out_proj.bias")))
             s2 = torch.empty(BL, d, **ctd)
@@ -248,8 +260,12 @@ class TransformerEngine:
             bq = fp.f32(lw("multihead_attn.in_proj_bias"))
             q2 = K.gemm(x1, wq[:d], trans_b=True, bias=bq[:d])
             kv2 = st["kv_mem"][i].view(B * P, 2 * d)
+            pr = None
+            if self.cross_probs is not None:
+                pr = torch.empty(B, self.H, 1, P, device=dev, dtype=torch.float32)
+                self.cross_probs.append(pr)
             self._mha(B=B, Lq=1, Lk=P, q=q2, ldq=d, k=kv2, ldk=2 * d, v=kv2[:, d:], ldv=2 * d, o=o, ldo=d,
-                      lse=lse, causal=False, key_ids=None, pad_id=0, p=p, seed=seed, sid=_s(i, 2))
+                      lse=lse, causal=False, key_ids=None, pad_id=0, p=p, seed=seed, sid=_s(i, 2), probs=pr)
             y2 = K.gemm(o, fp.w(lw("multihead_attn.out_proj.weight")), trans_b=True,
                         bias=fp.f32(lw("multihead_attn.out_proj.bias")))
             x2, _, _ = K.add_layernorm(x1, y2, fp.f32(lw("norm2.weight")), fp.f32(lw("norm2.bias")), 1e-5,

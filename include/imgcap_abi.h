@@ -383,6 +383,9 @@ typedef struct imgcap_mha_desc {
   int64_t lddq, lddk, lddv;
   int64_t kv_rows;     /* fwd only: rows between consecutive batch entries of k / v (0 = Lk): a
                           [B][Lmax] key/value cache read at its first Lk rows (incremental decode) */
+  float* probs;        /* fwd only, optional: the attention probabilities [B, H, Lq, Lk] fp32 as
+                          nn.MultiheadAttention returns them with need_weights=True,
+                          average_attn_weights=False (after dropout) -- transformerDecoderAttVis.py:72,83 */
 } imgcap_mha_desc;
 
 int imgcap_mha_fwd(const imgcap_mha_desc* d, void* stream);

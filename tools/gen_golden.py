@@ -430,9 +430,119 @@ def gen_beam():
     return "beam_small", t, meta
 
 
+ATT_CFG = dict(B=3, L=12, caplens=[12, 7, 9], V=50, E=48, d=128, ff=32, H=2, layers=2, S=2, seed=66)
+
+
+def _attvis_decoder(cfg):
+    import importlib
+    _train_module(False)  # stubs + the reference root on sys.path
+    mod = importlib.import_module("models.transformerDecoderAttVis")
+    dec = mod.TransformerDecoderForAttentionViz(embed_dim=cfg["d"], decoder_dim=cfg["ff"], vocab_size=cfg["V"],
+                                                maxLen=cfg["L"], device="cpu", dropout=0.0, encoder_dim=cfg["E"],
+                                                num_heads=cfg["H"], num_layers=cfg["layers"])
+    sd = dict(dec.state_dict())
+    sd.update(make_params(_named_shapes(dec), cfg["seed"]))
+    dec.load_state_dict(sd)
+    dec.eval()
+    return dec
+
+
+def gen_attvis():
+    """models/transformerDecoderAttVis.py (TransformerDecoderForAttentionViz) in eval mode:
+    teacher-forced predictions + alphas [H, B, P] (with a key-padding mask), greedy predictions /
+    sequences / alphas (rows ending at different steps), and caption.py:260-383
+    (caption_image_beam_search_transformer_attention) word ids + alphas, beam 3 and 5."""
+    import numpy as np
+    from PIL import Image
+    t, meta = {}, {}
+    cfg = ATT_CFG
+    dec = _attvis_decoder(cfg)
+    enc, caps, caplens = _inputs(cfg)
+    with torch.no_grad():
+        preds, _, dls, alphas = dec(teacherForcing=True, encoder_out=enc, encoded_captions=caps,
+                                    caption_lengths=caplens, tgt_key_padding_mask=caps == 0)
+    t.update({"tf.enc": enc, "tf.caps": caps, "tf.caplens": caplens, "tf.predictions": preds, "tf.alphas": alphas})
+    meta["tf"] = dict(cfg=cfg, decode_lengths=dls)
+    wm = word_map(cfg["V"])
+    end_bias = 0.0
+    for end_bias in [0.05 * k for k in range(1, 200)]:  # rows finish at different steps
+        with torch.no_grad():
+            dec.fc_out.bias[wm["<end>"]] += 0.05
+            out = dec(teacherForcing=False, encoder_out=enc, wordMap=wm, maxDecodeLen=10)
+        first = [(row == wm["<end>"]).nonzero()[:1].flatten().tolist() for row in out[1]]
+        stops = {f[0] if f else 99 for f in first}
+        if len(stops) >= 2 and 99 not in stops or len(stops) >= 3:
+            break
+    with torch.no_grad():
+        gp, gs, ga = dec(teacherForcing=False, encoder_out=enc, wordMap=wm, maxDecodeLen=10)
+    t.update({"greedy.predictions": gp, "greedy.sequences": gs, "greedy.alphas": ga})
+    meta["greedy"] = dict(maxDecodeLen=10, end_bias_added=round(end_bias, 6))
+    # beam search with attention maps (caption.py:260-383), maxLen 52 for up to 51 positions
+    if "skimage" not in sys.modules:
+        ref_import._stub("skimage")
+        ref_import._stub("skimage.transform")
+    cap = ref_import.load("caption.py", "ref_caption", argv=["caption.py"])
+    cap.device = torch.device("cpu")
+    import types
+
+    def _normalize(mean, std):
+        m, sd = torch.tensor(mean).view(-1, 1, 1), torch.tensor(std).view(-1, 1, 1)
+        return lambda x: (x - m) / sd
+    cap.transforms = types.SimpleNamespace(Normalize=_normalize, Compose=lambda fs: (lambda x: fs[0](x)))
+    png = os.path.join(tempfile.mkdtemp(), "img.png")
+    Image.fromarray(np.random.default_rng(0).integers(0, 256, size=(40, 30, 3), dtype=np.uint8)).save(png)
+
+    class FixedEncoder(torch.nn.Module):
+        def __init__(self, feats):
+            super().__init__()
+            self.feats = feats
+
+        def forward(self, image):
+            return self.feats
+
+    bcfg = dict(cfg, L=52)
+    # feature seed with the longest beam captions at the first <end> bias (steps of 0.01) at
+    # which both beam sizes finish
+    best = None
+    for fseed in range(bcfg["seed"] + 5, bcfg["seed"] + 17):
+        feats = make_features((1, bcfg["S"], bcfg["S"], bcfg["E"]), fseed)
+        fenc = FixedEncoder(feats)
+        for bias in [0.01 * i for i in range(0, 600)]:
+            bdec = _attvis_decoder(bcfg)
+            with torch.no_grad():
+                bdec.fc_out.bias[wm["<end>"]] += bias
+                try:
+                    lens = [len(cap.caption_image_beam_search_transformer_attention(fenc, bdec, png, wm, "x",
+                                                                                    beamSize=k)[0]) for k in (3, 5)]
+                except ValueError:
+                    continue
+            if best is None or min(lens) > best[0]:
+                best = (min(lens), fseed, bias)
+            break
+        if best is not None and best[0] >= 6:
+            break
+    _, fseed, bias = best
+    feats = make_features((1, bcfg["S"], bcfg["S"], bcfg["E"]), fseed)
+    fenc = FixedEncoder(feats)
+    bdec = _attvis_decoder(bcfg)
+    with torch.no_grad():
+        bdec.fc_out.bias[wm["<end>"]] += bias
+    bcfg["feature_seed"] = fseed
+    t["beam.feats"] = feats
+    for k in (3, 5):
+        with torch.no_grad():
+            seq, al = cap.caption_image_beam_search_transformer_attention(fenc, bdec, png, wm, "x", beamSize=k)
+        t[f"beam.k{k}.seq"] = torch.tensor(seq, dtype=torch.int64)
+        t[f"beam.k{k}.alphas"] = torch.tensor(al, dtype=torch.float32)
+    meta["beam"] = dict(cfg=bcfg, end_bias_added=round(bias, 6))
+    meta["source"] = ("models/transformerDecoderAttVis.py:108-239 (eval), caption.py:260-383 with a fixed-feature "
+                      "encoder; params: tests/golden_util.make_params(named_shapes, cfg.seed)")
+    return "attvis_small", t, meta
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] in ("greedy", "beam"):
-        name, tensors, meta = gen_greedy() if sys.argv[1] == "greedy" else gen_beam()
+    if len(sys.argv) > 1 and sys.argv[1] in ("greedy", "beam", "attvis"):
+        name, tensors, meta = {"greedy": gen_greedy, "beam": gen_beam, "attvis": gen_attvis}[sys.argv[1]]()
         save_file({k: v.detach().contiguous() for k, v in tensors.items()}, os.path.join(GOLDEN_DIR, name + ".safetensors"))
         with open(os.path.join(GOLDEN_DIR, name + ".json"), "w") as f:
             json.dump(meta, f, indent=1)
