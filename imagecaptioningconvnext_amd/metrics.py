@@ -115,8 +115,10 @@ def greedy_loss(predictions, sequences, captions, wordMap, maxlen, alphas=None, 
     return metrics, n
 
 
-def validate(valDataLoader, encoder, decoder, wordMap, lstm, device, maxDecodeLen=51, alphaC=1.0, log=print):
-    """train.py:367-441: greedy decoding over the VAL split -> (loss avg, top-5 avg, BLEU-1..4)."""
+def validate(valDataLoader, encoder, decoder, wordMap, lstm, device, maxDecodeLen=51, alphaC=1.0, log=print,
+             label="Validation"):
+    """train.py:367-441: greedy decoding over the VAL split -> (loss avg, top-5 avg, BLEU-1..4).
+    test.py:144-215 is the same loop over the TEST split (``label="Test"``)."""
     decoder.eval()
     if encoder is not None:
         encoder.eval()
@@ -126,7 +128,7 @@ def validate(valDataLoader, encoder, decoder, wordMap, lstm, device, maxDecodeLe
     with torch.no_grad():
         for i, (imgs, caps, caplens, allcaps) in enumerate(valDataLoader):
             if i % 100 == 0:
-                log(f"No TF, Validation Batch {i + 1}", flush=True)
+                log(f"No TF, {label} Batch {i + 1}", flush=True)
             imgs, caps = imgs.to(device), caps.to(device)
             feats = encoder(imgs) if encoder is not None else imgs
             out = decoder(teacherForcing=False, encoder_out=feats, wordMap=wordMap, maxDecodeLen=maxDecodeLen)
@@ -145,6 +147,6 @@ def validate(valDataLoader, encoder, decoder, wordMap, lstm, device, maxDecodeLe
     top5 = tot_hit / max(tot_tok, 1.0) * 100.0
     bleu = [corpus_bleu(references, hypotheses, weights=w) for w in
             ((1.0, 0.0, 0.0, 0.0), (0.5, 0.5, 0.0, 0.0), (0.33, 0.33, 0.33, 0.0), (0.25, 0.25, 0.25, 0.25))]
-    log(f"No TF, Validation Loss = {loss:.4f}, Top-5 Accuracy = {top5:.4f}, Bleu-1 = {bleu[0]:.4f}, "
+    log(f"No TF, {label} Loss = {loss:.4f}, Top-5 Accuracy = {top5:.4f}, Bleu-1 = {bleu[0]:.4f}, "
         f"Bleu-2 = {bleu[1]:.4f}, Bleu-3 = {bleu[2]:.4f}, Bleu-4 = {bleu[3]:.4f}", flush=True)
     return (loss, top5, *bleu)
