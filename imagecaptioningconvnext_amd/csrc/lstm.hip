@@ -34,6 +34,9 @@ namespace imgcap {
 constexpr int ATT_THREADS = 1024;
 constexpr int ATT_WAVES = ATT_THREADS / 64;
 constexpr int MAXP = 64;
+// default channel chunks per row in attn_fwd.  Swept at C2 (tools/gpu/att_ys.sh, ys = 1..6):
+// 8,138-8,226 img/s, all within run-to-run spread -- the step is latency-, not CU-bandwidth-bound.
+constexpr int LSTM_ATT_YS = 1;
 
 template <typename T> DEV void load8(const T* p, float (&v)[8]);
 template <> DEV void load8<bf16>(const bf16* p, float (&v)[8]) {
@@ -57,9 +60,12 @@ DEV void raw_load(Raw8<T>& r, const T* p) {
 template <typename T>
 DEV void raw_to_f(const Raw8<T>& r, float (&x)[8]) { load8<T>((const T*)r.u, x); }
 
-// ---- forward attention step: one block (16 waves) per batch row ------------------------
+// ---- forward attention step: gridDim.y blocks (16 waves each) per batch row --------------
 // Latency-bound (a few hundred KB per step spread over B blocks), so every global load the
-// block needs is issued up front, before any reduction:
+// block needs is issued up front, before any reduction.  Block (b, y) recomputes the 49 scores
+// and the softmax of row b (att1 is the smaller operand) and owns the context / gate outputs of
+// channel chunk y of E (E / gridDim.y channels), so a row's encoder features are read by
+// gridDim.y CUs at once instead of one:
 //   scores : wave w owns pixels p = w, w+16, ... (<= 4); lane l owns 8 attention units
 //            (att1 rows, att2 and w_f slices in registers)
 //   context: thread = (8-channel vector v of E, pixel group pg): pixels pg, pg + G, ...
@@ -71,13 +77,14 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
   const int b = blockIdx.x;
   const int P = d.P, E = d.E, A = d.A, Tn = d.T;
   const int W3 = A + E + 4 * d.D;
+  const int Ec = E / (int)gridDim.y, e0 = blockIdx.y * Ec;  // this block's channel chunk
   const long bt = (long)b * Tn + t;
   const bool active = t < d.dl[b];
   const float* g1 = d.g1 + bt * W3;  // [att2 | gate_pre | hh]
   const T* att1 = (const T*)d.att1 + (long)b * P * A;
-  const T* enc = (const T*)d.enc + (long)b * P * E;
+  const T* enc = (const T*)d.enc + (long)b * P * E + e0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int NVE = E / 8, G = ATT_THREADS / NVE;
+  const int NVE = Ec / 8, G = ATT_THREADS / NVE;
   const int v = threadIdx.x % NVE, pg = threadIdx.x / NVE;
   const bool ctx_thread = pg < G;
   // ---- all loads ----
@@ -104,7 +111,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
     const int e = threadIdx.x + k * ATT_THREADS;
-    gpre[k] = e < E ? g1[A + e] : 0.f;
+    gpre[k] = e < Ec ? g1[A + e0 + e] : 0.f;
   }
   // ---- scores e_p = w_f . relu(att1_p + att2)   (full_att bias cancels in the softmax) ----
 #pragma unroll
@@ -128,7 +135,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
     const float al = ex / wave_sum(ex);
     if (lane < P) {
       e_s[lane] = al;
-      d.alphas[bt * P + lane] = active ? al : 0.f;
+      if (blockIdx.y == 0) d.alphas[bt * P + lane] = active ? al : 0.f;
     }
   }
   __syncthreads();
@@ -147,17 +154,17 @@ __global__ __launch_bounds__(ATT_THREADS) void attn_fwd_kernel(imgcap_lstm_desc 
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) part[pg * E + v * 8 + j] = acc[j];
+    for (int j = 0; j < 8; ++j) part[pg * Ec + v * 8 + j] = acc[j];
   }
   __syncthreads();
-  T* zs = (T*)d.zs + bt * E;
-  float* awe = d.awe + bt * E;
+  T* zs = (T*)d.zs + bt * E + e0;
+  float* awe = d.awe + bt * E + e0;
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
     const int e = threadIdx.x + k * ATT_THREADS;
-    if (e >= E) break;
+    if (e >= Ec) break;
     float s = 0.f;
-    for (int q = 0; q < G; ++q) s += part[q * E + e];
+    for (int q = 0; q < G; ++q) s += part[q * Ec + e];
     const float gate = sigmoidf_(gpre[k]);
     awe[e] = s;
     zs[e] = from_f<T>(gate * s);
@@ -689,20 +696,31 @@ static int lstm_fwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
   const int nrg = (d.B + RG - 1) / RG;
   const imgcap_epilogue e1 = f32_epi(d.b_hcat);
   const int dpt_g = depth_for(d.E, 8, F32);
-  const int mpp = attn_mpp(d);
-  const size_t shm_f = (size_t)(ATT_THREADS / (d.E / 8)) * d.E * sizeof(float);
+  // channel chunks per row of the forward attention kernel (IMGCAP_LSTM_ATT_YS overrides)
+  static const int ys_env = [] {
+    const char* e = getenv("IMGCAP_LSTM_ATT_YS");
+    return e ? atoi(e) : 0;
+  }();
+  int ys = ys_env > 0 ? ys_env : LSTM_ATT_YS;
+  while (ys > 1 && d.E % (8 * ys) != 0) --ys;
+  const int Gf = ATT_THREADS / (d.E / ys / 8);
+  const int mpp = (d.P + Gf - 1) / Gf;  // <= attn_mpp(d) <= 16 (checked at entry)
+  const size_t shm_f = (size_t)Gf * (d.E / ys) * sizeof(float);
+  const dim3 gatt(d.B, ys);
   for (int t = 0; t < d.T; ++t) {
     int rc = imgcap_gemm(ct, 1, 1, d.B, W3, d.D, (const T*)d.hprev + (long)t * d.D, (long)d.T * d.D, 0, d.w_hcat,
                          d.D, 0, d.g1 + (long)t * W3, (long)d.T * W3, 0, 1, &e1, st);
     if (rc) return rc;
-    if (mpp <= 4)
-      hipLaunchKernelGGL((attn_fwd_kernel<T, 4>), dim3(d.B), dim3(ATT_THREADS), shm_f, st, d, t);
+    if (mpp <= 2)
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 2>), gatt, dim3(ATT_THREADS), shm_f, st, d, t);
+    else if (mpp <= 4)
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 4>), gatt, dim3(ATT_THREADS), shm_f, st, d, t);
     else if (mpp <= 5)
-      hipLaunchKernelGGL((attn_fwd_kernel<T, 5>), dim3(d.B), dim3(ATT_THREADS), shm_f, st, d, t);
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 5>), gatt, dim3(ATT_THREADS), shm_f, st, d, t);
     else if (mpp <= 8)
-      hipLaunchKernelGGL((attn_fwd_kernel<T, 8>), dim3(d.B), dim3(ATT_THREADS), shm_f, st, d, t);
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 8>), gatt, dim3(ATT_THREADS), shm_f, st, d, t);
     else
-      hipLaunchKernelGGL((attn_fwd_kernel<T, 16>), dim3(d.B), dim3(ATT_THREADS), shm_f, st, d, t);
+      hipLaunchKernelGGL((attn_fwd_kernel<T, 16>), gatt, dim3(ATT_THREADS), shm_f, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm attn_fwd");
     LSTM_DEPTH_SWITCH(dpt_g, gate_cell_fwd_kernel, 8, dim3(d.D / 4, nrg), dim3(512), 0, st, d, t);
     IMGCAP_CHECK_LAUNCH("lstm gate_cell_fwd");
