@@ -29,6 +29,11 @@ from . import kernels as K
 # 14,960, C4 6,221 vs 6,181 -- the two-branch graph wins where it matters (C2), the split is
 # within run-to-run spread elsewhere.
 PIPE_SPLIT = int(os.environ.get("IMGCAP_PIPE_SPLIT", "0"))
+# two-branch graph: where the encoder branch forks off the decoder stream -- at the start of the
+# step ("start") or after the decoder forward ("bwd": the encoder overlaps the backward only).
+# Measured (bench, 1x MI355X, two runs each): C2 8,254 vs 8,366 img/s (within spread), C3 16,605
+# vs 15,108, C4 7,007 vs 6,117 -- "start" stays the default.
+PIPE_FORK = os.environ.get("IMGCAP_PIPE_FORK", "start")
 
 
 def _trainable(encoder):
@@ -95,12 +100,14 @@ class TeacherForcedTrainer:
             feats = self._encode(imgs)
         return self._dec(feats, caps, caplens, es)
 
-    def _dec(self, feats, caps, caplens, es=None):
+    def _dec(self, feats, caps, caplens, es=None, mid=None):
         self.decoder.train()
         if self.lstm:
             s = self.eng.forward(feats, caps, caplens, fixed_T=True, alphaC=self.alphaC)
         else:
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
+        if mid is not None:
+            mid()
         if es is not None:
             self.eng.backward(s, want_denc=True)
             self.enc_eng.backward(es, s["denc"].reshape(feats.shape))
@@ -171,10 +178,15 @@ class TeacherForcedTrainer:
             with torch.cuda.graph(g, pool=pool):
                 self._seed_ctr.add_(1)
                 cur = torch.cuda.current_stream(dev)
-                side.wait_stream(cur)
-                with torch.cuda.stream(side):
-                    P["feats"][k].copy_(self._encode(P["img"]))
-                m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k])
+
+                def fork(k=k, cur=cur):
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        P["feats"][k].copy_(self._encode(P["img"]))
+                if PIPE_FORK != "bwd":
+                    fork()
+                m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k],
+                              mid=fork if PIPE_FORK == "bwd" else None)
                 cur.wait_stream(side)
             pool = g.pool()
             P["graphs"].append(g)
