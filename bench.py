@@ -1,7 +1,10 @@
 """Teacher-forced train-step throughput (images/sec) on MI355X — BASELINE.json's metric.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+``--gpus N`` without a launcher (no WORLD_SIZE in the environment) starts the N rank processes
+itself, before anything touches the GPU, and exits with their status.
 
 Default workload = BASELINE.json configs[1] (C2): ConvNeXt-Tiny encoder (frozen, train mode)
 + LSTM-attention decoder, teacher forced, 32 images per GPU, 224x224x3, captions of length
@@ -38,11 +41,11 @@ PEAK_FP8_TFLOPS = 5000.0    # dense block-scaled e4m3 MFMA
 PEAK_HBM_GBS = 8000.0       # HBM3E spec
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
@@ -50,7 +53,39 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run encoder and decoder of a step back to back (no two-stream overlap)")
     ap.add_argument("--no-fp8", action="store_true", help="C5: frozen encoder GEMMs in bf16 instead of MX-FP8")
-    return ap.parse_args()
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help="launcher check on CPU: gloo ranks time an empty step (tests/test_bench_cpu.py); "
+                         "prints the rank layout, not a measurement")
+    return ap.parse_args(argv)
+
+
+def spawn_ranks(n, argv):
+    """One process per GPU (rank r on GPU r), the torchrun environment set by hand; returns the
+    first non-zero exit status (the other ranks are terminated then) or 0."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # a dead rank would leave the others blocked in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def synthetic_batch(B, rank, step, device):
@@ -162,19 +197,44 @@ def cpu_baseline(seconds):
                        f"V={V}), {n} timed steps after 1 warm-up, {t_steps:.1f} s")
 
 
-def main():
-    args = parse()
+def launch_selftest(args, rank, world):
+    """The bench's rank/timing protocol around an empty step (gloo, CPU)."""
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"launch_selftest": True, "n_gpus": dist.get_world_size(), "steps": args.steps,
+                          "max_elapsed_s": t.item()}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main(argv=None):
+    raw = sys.argv[1:] if argv is None else list(argv)
+    args = parse(raw)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, raw))
     cfg = dict(CONFIGS[args.config])
     if args.no_fp8:
         cfg["frozen_fp8"] = False
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; running {world} ranks", file=sys.stderr)
+    if args.launch_selftest:
+        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+        return launch_selftest(args, rank, world)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
                                 device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
     device = torch.device("cuda", local)
     torch.manual_seed(42 + rank)
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer

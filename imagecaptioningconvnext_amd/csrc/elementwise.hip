@@ -113,7 +113,7 @@ __global__ void loss_finalize_kernel(int n, const float* __restrict__ loss_rows,
   }
 }
 
-// out[b, e] = mean_p x[b, p, e]  (decoder.py:99 encoder_out.mean(dim=1))
+// out[b, e] = mean_p x[b, p, e]  (decoder.py:64 encoder_out.mean(dim=1))
 template <typename TI, typename TO>
 __global__ void mean_mid_kernel(int B, int P, int E, const TI* __restrict__ x, TO* __restrict__ out) {
   const long n = (long)B * E;
@@ -125,9 +125,9 @@ __global__ void mean_mid_kernel(int B, int P, int E, const TI* __restrict__ x, T
   }
 }
 
-// decoder.py:99,114-116 in one launch: sort the batch by caption length (descending, stable --
+// decoder.py:64,79-81 in one launch: sort the batch by caption length (descending, stable --
 // the order the engine has always used), gather encoder_out and the captions into that order,
-// decode lengths (len - 1, int32) and the pixel mean of each gathered row (decoder.py:99, the
+// decode lengths (len - 1, int32) and the pixel mean of each gathered row (decoder.py:64, the
 // same p-order fp32 sum as mean_mid_kernel).  Block r = destination row r: every block ranks the
 // (<= 256) lengths itself, so no second launch is needed for the gather.
 template <typename T>

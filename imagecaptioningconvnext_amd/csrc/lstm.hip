@@ -1,15 +1,15 @@
-// Teacher-forced "Show, Attend and Tell" LSTM decoder recurrence (models/decoder.py:104-148)
+// Teacher-forced "Show, Attend and Tell" LSTM decoder recurrence (models/decoder.py:69-113)
 // and its backward-through-time, driven natively: one C-ABI call enqueues all T steps.
 //
 // Exact algebraic restructuring of the reference loop (results identical up to fp
 // reassociation):
-//   * att1 = enc W_ea^T + b_ea (decoder.py:61) is computed ONCE outside the loop (the
+//   * att1 = enc W_ea^T + b_ea (decoder.py:26) is computed ONCE outside the loop (the
 //     reference recomputes it every step)
 //   * the three GEMMs that read h_{t-1} (decoder_att, f_beta, LSTMCell weight_hh) are one
 //     GEMM against W_hcat = [W_da; W_fb; W_hh]
 //   * the embedding half of weight_ih (and bias_ih) is precomputed for all t (xe); only the
 //     attention half (z_t W_ih[:,M:]^T) stays in the loop
-//   * fc(dropout(h)) (decoder.py:144) runs once after the loop over all [B*T] rows
+//   * fc(dropout(h)) (decoder.py:109) runs once after the loop over all [B*T] rows
 //   * rows are never shrunk: rows with t >= decode_length[b] are computed and masked out
 //     (alphas = 0 there; the loss never reads their logits; their gradients are zero)
 //   * backward keeps only the recurrent chain in the loop: the encoder_att / full_att weight

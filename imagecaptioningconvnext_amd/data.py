@@ -22,17 +22,20 @@ from torch.utils.data import Dataset
 
 
 def _open_images(folder, split, name):
+    """(images array, captions_per_image or None, closer).  ``.npy`` is memory-mapped; HDF5 needs
+    h5py.  Called lazily in each DataLoader worker (dataLoader.py:39-41): an HDF5 handle must not
+    cross a fork."""
     base = os.path.join(folder, split + '_IMAGES_' + name)
     if os.path.exists(base + '.npy'):
         arr = np.load(base + '.npy', mmap_mode='r', allow_pickle=False)
-        return arr, None
+        return arr, None, None
     try:
         import h5py
     except ImportError as e:  # the image format needs h5py; say how to get the .npy form instead
         raise FileNotFoundError(f"{base}.npy not found and h5py is not installed to read {base}.hdf5 "
                                 "(convert once with tools/hdf5_to_npy.py where h5py exists)") from e
     h = h5py.File(base + '.hdf5', 'r')
-    return h['images'], int(h.attrs['captions_per_image'])
+    return h['images'], int(h.attrs['captions_per_image']), h.close
 
 
 class CaptionDataset(Dataset):
@@ -47,19 +50,28 @@ class CaptionDataset(Dataset):
             self.captions = json.load(j)
         with open(os.path.join(dataFolder, self.split + '_CAPLENS_' + dataName + '.json'), 'r') as j:
             self.caplens = json.load(j)
-        self.imgs, cpi = _open_images(dataFolder, split, dataName)
+        # open once for the image count / captions_per_image, then close: the handle is reopened
+        # lazily per process in __getitem__ (dataLoader.py:39-41), never shared across a fork
+        imgs, cpi, close = _open_images(dataFolder, split, dataName)
+        n_imgs = len(imgs)
+        if close is not None:
+            close()
+        del imgs
+        self.imgs = None
         if captions_per_image is not None:
             cpi = captions_per_image
         if cpi is None:  # .npy images: the Karpathy files hold exactly cpi captions per image
-            if len(self.captions) % len(self.imgs):
+            if len(self.captions) % n_imgs:
                 raise ValueError("captions do not divide evenly over the images; pass captions_per_image")
-            cpi = len(self.captions) // len(self.imgs)
+            cpi = len(self.captions) // n_imgs
         self.cpi = cpi
         self.transform = transform
         self.raw = raw and transform is None
         self.dataset_size = len(self.captions)
 
     def __getitem__(self, i):
+        if self.imgs is None:  # first item in this process (each DataLoader worker opens its own)
+            self.imgs = _open_images(self.dataFolder, self.split, self.dataName)[0]
         u8 = np.asarray(self.imgs[i // self.cpi])
         if self.raw:
             img = torch.from_numpy(np.array(u8, dtype=np.uint8, copy=True))

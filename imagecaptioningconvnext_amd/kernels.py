@@ -408,7 +408,7 @@ def adaptive_pool(x, OH, OW, out):
 
 
 def sort_gather_rows(lens, enc, caps):
-    """decoder.py:99,114-116 in one launch: (enc_sorted [B,P,E], mean [B,E], caps_sorted [B,L],
+    """decoder.py:64,79-81 in one launch: (enc_sorted [B,P,E], mean [B,E], caps_sorted [B,L],
     sort_ind int64 [B], decode lengths int32 [B]), rows by caption length descending (stable)."""
     _check_dev(lens, enc, caps)
     B, P, E = enc.shape

@@ -1,6 +1,6 @@
 """Explicit forward/backward engine of the teacher-forced LSTM-attention decoder on HIP.
 
-Mirrors DecoderWithAttention.forwardWithTeacherForcing (models/decoder.py:104-148) plus the
+Mirrors DecoderWithAttention.forwardWithTeacherForcing (models/decoder.py:69-113) plus the
 loss of train.py:263-269; the recurrence itself is one native call per direction
 (imgcap_lstm_tf_fwd / _bwd, csrc/lstm.hip).  Every GEMM is imgcap_gemm; the loss is the
 fused CE + top-5 kernel; parameters, grads, Adam state and the bf16 weight copy live in one
@@ -23,7 +23,7 @@ from .flat import FlatParams
 # grid (imgcap_epilogue.split_k)
 DW = dict(split_k=-1)
 
-_STREAM_DROPOUT_H = 11  # dropout stream id for fc(dropout(h)) (decoder.py:144)
+_STREAM_DROPOUT_H = 11  # dropout stream id for fc(dropout(h)) (decoder.py:109)
 
 
 def lstm_param_groups(dec):
@@ -139,7 +139,7 @@ class LstmEngine:
 
     def forward(self, encoder_out, encoded_captions, caption_lengths, *, fixed_T=False, dropout=None, loss=True,
                 alphaC=1.0):
-        """Runs decoder.py:104-148 (+ the train.py:265-269 loss when ``loss``).
+        """Runs decoder.py:69-113 (+ the train.py:265-269 loss when ``loss``).
 
         fixed_T: run T = L-1 steps without reading decode lengths on the host (no sync; rows are
         masked on device).  Otherwise T = max(decode_lengths) exactly as the reference.
@@ -156,7 +156,7 @@ class LstmEngine:
         mean = None
         if (B <= 256 and enc.dtype == ct and enc.is_contiguous() and lens.dtype == torch.int64
                 and encoded_captions.dtype == torch.int64 and encoded_captions.is_contiguous()):
-            # decoder.py:99,114-116 (sort, gathers, decode lengths, pixel mean) in one launch
+            # decoder.py:64,79-81 (sort, gathers, decode lengths, pixel mean) in one launch
             enc_s, mean, caps_s, sort_ind, dl = K.sort_gather_rows(lens.contiguous(), enc, encoded_captions)
         else:
             lens, sort_ind = lens.sort(dim=0, descending=True, stable=True)
@@ -167,7 +167,7 @@ class LstmEngine:
             T = L - 1
             dls = None
         else:
-            dls = dl.tolist()  # decoder.py:126 (host list, part of the reference API)
+            dls = dl.tolist()  # decoder.py:91 (host list, part of the reference API)
             T = max(dls)
         s = dict(B=B, P=P, T=T, L=L, sort_ind=sort_ind, caps_s=caps_s, dl=dl, dls=dls, p_drop=p_drop,
                  seed=self.seed + self.step_id)
@@ -177,10 +177,10 @@ class LstmEngine:
         # ---- loop-invariant precompute ------------------------------------------------------
         ids = caps_s[:, :T].contiguous()
         emb = torch.empty(B * T, M, **ctd)
-        K.embedding_fwd(ids, w["emb"], emb)                                   # decoder.py:119
+        K.embedding_fwd(ids, w["emb"], emb)                                   # decoder.py:84
         if mean is None:
             mean = torch.empty(B, E, **ctd)
-            K.mean_mid(enc_s, mean)                                           # decoder.py:99
+            K.mean_mid(enc_s, mean)                                           # decoder.py:64
         h0c0 = K.gemm(mean, w["init"], trans_b=True, bias=w["binit"], out_dtype=torch.float32)  # :100-101
         att1 = K.gemm(enc_s.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])             # :61 hoisted
         xe = K.gemm(emb, w["wih"][:, :M], trans_b=True, bias=w["bih"], out_dtype=torch.float32)  # W_ih emb half
@@ -214,7 +214,7 @@ class LstmEngine:
         main.wait_stream(side)
         wzh_t.record_stream(main)
         watt_t.record_stream(main)
-        # ---- fc(dropout(h)) over all B*T rows (decoder.py:144) ----------------------------------
+        # ---- fc(dropout(h)) over all B*T rows (decoder.py:109) ----------------------------------
         hd = hs.view(B * T, D)
         if p_drop > 0:
             hd = K.dropout(hd, p_drop, s["seed"], _STREAM_DROPOUT_H)
@@ -271,7 +271,7 @@ class LstmEngine:
         enc = encoder_out.reshape(B, -1, E).to(ct).contiguous()
         P = enc.size(1)
         mean = torch.empty(B, E, device=dev, dtype=ct)
-        K.mean_mid(enc, mean)                                                       # decoder.py:99
+        K.mean_mid(enc, mean)                                                       # decoder.py:64
         h0c0 = K.gemm(mean, w["init"], trans_b=True, bias=w["binit"], out_dtype=torch.float32)  # :100-101
         att1 = K.gemm(enc.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])    # :61, once
         h = h0c0[:, :D].to(ct).reshape(B, 1, D).contiguous()
@@ -315,7 +315,7 @@ class LstmEngine:
         return logits, bufs["alphas"].view(B, P)
 
     def predictions(self, s):
-        """decoder.py:129,145: zero-filled predictions [B, T, V] (fp32) from the saved state."""
+        """decoder.py:94,110: zero-filled predictions [B, T, V] (fp32) from the saved state."""
         B, T, V = s["B"], s["T"], self.V
         w = self.weights()
         out = torch.empty(B * T, V, device=s["hs"].device, dtype=torch.float32)
@@ -419,7 +419,7 @@ class LstmEngine:
         cb.run()
         s["denc"] = None
         if want_denc:
-            # decoder.py:61 (att1 = enc W_ea), :99-101 (mean -> init_h/c), :136 (context)
+            # decoder.py:26 (att1 = enc W_ea), :64-66 (mean -> init_h/c), :102-103 (context)
             K.gemm(dinit, w["init"], out=dawe[:, T, :])                      # dL/d mean(enc)
             base = K.gemm(datt1, w["wea"], out_dtype=torch.float32)         # [B*P, E]
             denc = torch.empty(B, P, E, **f32)

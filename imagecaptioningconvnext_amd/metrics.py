@@ -30,8 +30,8 @@ def _ngrams(seq, n):
 
 def _modified_precision(references, hypothesis, n):
     counts = Counter(_ngrams(hypothesis, n))
-    if not counts:
-        return 0, 0
+    if not counts:  # nltk: numerator 0 over max(1, 0) -- a too-short hypothesis still counts once
+        return 0, 1
     max_ref = {}
     for ref in references:
         rc = Counter(_ngrams(ref, n))

@@ -88,7 +88,7 @@ class DecoderWithAttention(nn.Module):
         self._engine = None
 
     def init_weights(self):
-        """decoder.py:93-96: U(-0.1, 0.1) embedding and fc weight, zero fc bias."""
+        """decoder.py:58-61: U(-0.1, 0.1) embedding and fc weight, zero fc bias."""
         with torch.no_grad():
             self.embedding.weight.uniform_(-0.1, 0.1)
             self.fc.bias.zero_()

@@ -57,7 +57,7 @@ int imgcap_set_seed_counter(const uint64_t* counter);
  *       -> (*= colscale[n]) -> (*= rowscale[m/rows_per_scale])
  *       -> (+= res[m,n]) -> (+= beta*C[m,n]) -> C[m,n] (c_dtype)
  * Replaces every nn.Linear / 1x1-conv / patchify-conv / projection matmul on the path:
- * decoder.py:61-63,100-101,139-144; transformerDecoder.py:95,104,106; torchvision CNBlock
+ * decoder.py:26-27,65-66,104-109; transformerDecoder.py:95,104,106; torchvision CNBlock
  * Linear pair + layer_scale + residual (reached via encoder.py:24); and their backward.
  * -------------------------------------------------------------------------------------- */
 typedef struct imgcap_epilogue {
@@ -255,7 +255,7 @@ int imgcap_stochastic_depth_scales(int nblocks, int B, const float* probs, uint6
                                    uint32_t drop_stream, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * Token embedding (+ dropout, + positional encoding) — decoder.py:119,
+ * Token embedding (+ dropout, + positional encoding) — decoder.py:84,
  * transformerDecoder.py:97-98.  out[n, :] = drop(table[ids[n], :]) + (pe ? pe[n % L, :] : 0)
  * -------------------------------------------------------------------------------------- */
 int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* ids, const float* table,
@@ -288,9 +288,9 @@ int imgcap_clamp_adam(int64_t n, float* param, const float* grad, float* m, floa
                       int step, float clip, float grad_div, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * LSTM + soft-attention decoder, teacher forced (decoder.py:104-148, Attention 60-66,
+ * LSTM + soft-attention decoder, teacher forced (decoder.py:69-113, Attention 25-31,
  * LSTMCell at :141).  One call enqueues all T steps (3 kernels per step each way).
- * Batch-major buffers [B, T, .]; rows sorted by decode length (decoder.py:114);
+ * Batch-major buffers [B, T, .]; rows sorted by decode length (decoder.py:79);
  * W3 = A + E + 4D.
  * fwd requires: hprev[:,0,:] = h0, c0, xe = emb_t W_ih[:, :M]^T + b_ih, att1
  *   (b_hh rides in b_hcat).
@@ -342,7 +342,7 @@ typedef struct imgcap_lstm_desc {
 
 int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream);
 int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream);
-/* dL/d encoder_out for encoder fine-tuning (the decoder.py:75-148 paths back into encoder_out):
+/* dL/d encoder_out for encoder fine-tuning (the decoder.py:75-113 paths back into encoder_out):
  *   denc[sort_ind[b], p, :] = base[b, p, :] + sum_{t<T} alphas[b,t,p] dawe[b,t,:] + dawe[b,T,:] / P
  * base [B, P, E] fp32 = datt1 . W_ea (sorted order, may be NULL); dawe [B, T+1, E] fp32 as
  * imgcap_lstm_desc.dawe with row T = dL/d mean(encoder_out); sort_ind NULL = identity; P <= 64. */
@@ -399,7 +399,7 @@ int imgcap_greedy_select(int dtype, int B, int V, const void* logits, int64_t ld
                          float* predictions, const float* alpha, float* alphas, int P, void* stream);
 int imgcap_mha_bwd(const imgcap_mha_desc* d, void* stream);
 
-/* y = x * dropmask(seed, stream, i) (nn.Dropout, decoder.py:144 / transformer dropouts) */
+/* y = x * dropmask(seed, stream, i) (nn.Dropout, decoder.py:109 / transformer dropouts) */
 int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint64_t seed, uint32_t drop_stream, void* y,
                    void* stream);
 /* Token-mean loss finalisation without host sync (train.py:268 + reduceLossAndTokens inputs):
@@ -408,9 +408,9 @@ int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint64_t seed, 
 int imgcap_loss_finalize(int n, const float* loss_rows, const float* hit5, const int64_t* targets,
                          const float* extra, float* out, void* stream);
 
-/* out[b, e] = mean_p x[b, p, e] (decoder.py:99, input of init_h/init_c) */
+/* out[b, e] = mean_p x[b, p, e] (decoder.py:64, input of init_h/init_c) */
 int imgcap_mean_mid(int dtype, int B, int P, int E, const void* x, void* out, void* stream);
-/* decoder.py:99,114-116 fused: rows sorted by caption length (descending, stable), enc_out[r] =
+/* decoder.py:64,79-81 fused: rows sorted by caption length (descending, stable), enc_out[r] =
  * enc[sort_ind[r]] ([B,P,E]), caps_out[r] = caps[sort_ind[r]] ([B,L] int64), dl[r] = len - 1
  * (int32), mean_out[r] = mean over P of enc_out[r]; B <= 256, E rows 16-byte aligned */
 int imgcap_sort_gather_rows(int dtype, int B, int P, int E, int L, const int64_t* lens, const void* enc,

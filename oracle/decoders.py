@@ -2,7 +2,7 @@
 
 ``p`` is a {state-dict key: tensor} dict with the reference's key names.
 
-lstm_tf_forward        models/decoder.py:104-148 (+ Attention 60-66, init_hidden_state 98-102)
+lstm_tf_forward        models/decoder.py:69-113 (+ Attention 25-31, init_hidden_state 63-67)
 transformer_tf_forward models/transformerDecoder.py:88-108 (+ PositionalEncoding 14-27) and
                        torch.nn.TransformerDecoderLayer's post-norm (norm_first=False) math
                        with ReLU FFN, as constructed at transformerDecoder.py:82-83.
@@ -22,38 +22,38 @@ def lstm_tf_forward(p, encoder_out, encoded_captions, caption_lengths):
     """Returns (predictions[B,Tmax,V], caps_sorted, decode_lengths(list), alphas[B,Tmax,P], sort_ind)."""
     B = encoder_out.size(0)
     E = encoder_out.size(-1)
-    enc = encoder_out.reshape(B, -1, E)                                      # decoder.py:110
+    enc = encoder_out.reshape(B, -1, E)                                      # decoder.py:75
     P = enc.size(1)
-    lens, sort_ind = caption_lengths.squeeze(1).sort(dim=0, descending=True)  # decoder.py:114
+    lens, sort_ind = caption_lengths.squeeze(1).sort(dim=0, descending=True)  # decoder.py:79
     enc = enc[sort_ind]
     caps = encoded_captions[sort_ind]
-    emb = p["embedding.weight"][caps]                                        # decoder.py:119
-    mean = enc.mean(dim=1)                                                   # decoder.py:99
+    emb = p["embedding.weight"][caps]                                        # decoder.py:84
+    mean = enc.mean(dim=1)                                                   # decoder.py:64
     h = _lin(mean, p, "init_h")
     c = _lin(mean, p, "init_c")
-    dls = (lens - 1).tolist()                                                # decoder.py:126
+    dls = (lens - 1).tolist()                                                # decoder.py:91
     T = max(dls)
     V = p["fc.weight"].shape[0]
     D = h.shape[1]
     preds = torch.zeros(B, T, V, dtype=enc.dtype)
     alphas = torch.zeros(B, T, P, dtype=enc.dtype)
-    att1_full = _lin(enc, p, "attention.encoder_att")                        # decoder.py:61
+    att1_full = _lin(enc, p, "attention.encoder_att")                        # decoder.py:26
     w_ih, w_hh = p["decode_step.weight_ih"], p["decode_step.weight_hh"]
     b_ih, b_hh = p["decode_step.bias_ih"], p["decode_step.bias_hh"]
-    for t in range(T):                                                       # decoder.py:135
+    for t in range(T):                                                       # decoder.py:100
         bt = sum(int(l > t) for l in dls)
         ht, ct = h[:bt], c[:bt]
-        att2 = _lin(ht, p, "attention.decoder_att")                          # decoder.py:62
+        att2 = _lin(ht, p, "attention.decoder_att")                          # decoder.py:27
         e = _lin(torch.relu(att1_full[:bt] + att2.unsqueeze(1)), p, "attention.full_att").squeeze(2)
-        alpha = torch.softmax(e, dim=1)                                      # decoder.py:64
-        awe = (enc[:bt] * alpha.unsqueeze(2)).sum(dim=1)                     # decoder.py:65
-        gate = torch.sigmoid(_lin(ht, p, "f_beta"))                          # decoder.py:139
-        x = torch.cat([emb[:bt, t, :], gate * awe], dim=1)                   # decoder.py:142
+        alpha = torch.softmax(e, dim=1)                                      # decoder.py:29
+        awe = (enc[:bt] * alpha.unsqueeze(2)).sum(dim=1)                     # decoder.py:30
+        gate = torch.sigmoid(_lin(ht, p, "f_beta"))                          # decoder.py:104
+        x = torch.cat([emb[:bt, t, :], gate * awe], dim=1)                   # decoder.py:107
         gates = x @ w_ih.t() + b_ih + ht @ w_hh.t() + b_hh                   # torch LSTMCell
         i, f, g, o = gates.split(D, dim=1)
         c = torch.sigmoid(f) * ct + torch.sigmoid(i) * torch.tanh(g)
         h = torch.sigmoid(o) * torch.tanh(c)
-        preds_t = _lin(h, p, "fc")                                           # decoder.py:144
+        preds_t = _lin(h, p, "fc")                                           # decoder.py:109
         preds = preds.index_put((torch.arange(bt), torch.full((bt,), t)), preds_t)
         alphas = alphas.index_put((torch.arange(bt), torch.full((bt,), t)), alpha)
     return preds, caps, dls, alphas, sort_ind

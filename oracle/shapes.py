@@ -4,7 +4,7 @@ utils/utils.py:209-216)."""
 
 def lstm_decoder_shapes(E, A, D, Em, V):
     """DecoderWithAttention(attention_dim=A, embed_dim=Em, decoder_dim=D, vocab_size=V, encoder_dim=E)
-    (models/decoder.py:70-90)."""
+    (models/decoder.py:35-57)."""
     return {
         "attention.encoder_att.weight": (A, E), "attention.encoder_att.bias": (A,),
         "attention.decoder_att.weight": (A, D), "attention.decoder_att.bias": (A,),

@@ -45,3 +45,19 @@ def test_caption_dataset_val_all_captions(tmp_path):
     loader = torch.utils.data.DataLoader(ds, batch_size=4, shuffle=False)
     b = next(iter(loader))
     assert b[0].shape == (4, 3, 16, 16) and b[0].dtype == torch.uint8 and b[3].shape == (4, 5, 12)
+
+
+def test_caption_dataset_opens_images_lazily_per_worker(tmp_path):
+    """dataLoader.py:39-41: no image handle is held after __init__, so forked DataLoader workers
+    each open their own (an HDF5 handle must not cross a fork)."""
+    import pickle
+    from imagecaptioningconvnext_amd.data import CaptionDataset
+    imgs, _, _ = _write(str(tmp_path), "TRAIN", "x")
+    ds = CaptionDataset(str(tmp_path), "x", "TRAIN")
+    assert ds.imgs is None
+    clone = pickle.loads(pickle.dumps(ds))  # what a spawned worker receives
+    assert torch.equal(clone[3][0], torch.from_numpy(imgs[0]))
+    loader = torch.utils.data.DataLoader(ds, batch_size=5, shuffle=False, num_workers=2)
+    got = torch.cat([b[0] for b in loader])
+    assert torch.equal(got, torch.from_numpy(np.repeat(imgs, 5, axis=0)))
+    assert ds.imgs is None  # the parent never opened it

@@ -392,7 +392,7 @@ def test_gemm_grouped_weight_gradients(hip_device):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B", [1, 5, 32, 256])
 def test_sort_gather_rows(hip_device, dtype, B):
-    """decoder.py:99,114-116 fused: stable descending length sort (ties keep batch order), the
+    """decoder.py:64,79-81 fused: stable descending length sort (ties keep batch order), the
     gathered encoder rows / captions bit-exact, decode lengths, and the pixel mean."""
     g = torch.Generator(device="cpu").manual_seed(B)
     P, E, L = 49, 768, 52

@@ -1,5 +1,5 @@
 """LSTM-attention decoder on the HIP path vs the golden vectors of the reference and the CPU
-oracle (decoder.py:104-148, train.py:263-291)."""
+oracle (decoder.py:69-113, train.py:263-291)."""
 import json
 import os
 

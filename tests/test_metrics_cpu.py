@@ -26,6 +26,19 @@ def test_corpus_bleu_known_answers():
     assert corpus_bleu([[['a', 'b']]], [['c', 'd']]) == 0.0  # no unigram match
 
 
+def test_corpus_bleu_short_hypothesis_counts_in_denominator():
+    """nltk's modified_precision divides by max(1, #hyp n-grams): a hypothesis shorter than n
+    adds 0/1.  Worked by hand: p1 = 6/6, p2 = (4+0)/(4+1), hyp_len 6 vs ref_len 11, so
+    BLEU-2 = exp(1 - 11/6) * sqrt(4/5)."""
+    import math
+    from imagecaptioningconvnext_amd.metrics import corpus_bleu
+    refs = [[[1, 2, 3, 4, 5]], [[1, 2, 3, 4, 5, 6]]]
+    hyps = [[1, 2, 3, 4, 5], [1]]
+    want = math.exp(1 - 11 / 6) * math.sqrt(0.8)
+    assert corpus_bleu(refs, hyps, weights=(0.5, 0.5)) == pytest.approx(want, abs=1e-12)
+    assert want == pytest.approx(0.3887, abs=1e-4)
+
+
 def _ref_preprocess(predictions, sequences, encodedCaptions, end, pad, maxlen):
     """utils.py:261-296 (the reference function, restated verbatim in behaviour)."""
     outs, tgts, lens = [], [], []

@@ -9,7 +9,7 @@ names, see tools/ref_import.py) on deterministic inputs from tests/golden_util.p
 inputs + outputs as data fixtures.  Reference source never leaves /root/reference.
 
 Fixtures:
-  lstm_tf_small       decoder.py:104-148 + train.py:240-302 (LSTM, 1 step, clip 5, Adam 1e-4)
+  lstm_tf_small       decoder.py:69-113 + train.py:240-302 (LSTM, 1 step, clip 5, Adam 1e-4)
   transformer_tf_small transformerDecoder.py:88-108 + train.py:270-302 (key-padding mask)
   ddp2_lstm            trainMultiGPU.py:339-420, 2-rank gloo DDP, different shard per rank
   lstm_full_spot / transformer_full_spot   full-size dims (E=768, V=9490, L=52), B=2:
@@ -144,7 +144,7 @@ def gen_lstm_small():
     t.update(params)
     t.update(grads)
     t.update(post)
-    meta = dict(cfg=cfg, decode_lengths=r["dls"], source="decoder.py:104-148; train.py:240-302")
+    meta = dict(cfg=cfg, decode_lengths=r["dls"], source="decoder.py:69-113; train.py:240-302")
     return "lstm_tf_small", t, meta
 
 

@@ -44,12 +44,17 @@ class AverageMeter:
         self.avg = self.sum / self.count
 
 
-def parse(argv=None):
+def make_parser(multi_gpu=False):
+    """train.py:59-65 (``multi_gpu``: trainMultiGPU.py:63-70, which adds --port and fine-tunes
+    from child 7 by default instead of 5)."""
     p = argparse.ArgumentParser()
     p.add_argument('--checkpoint', type=str, default=None, help='Path to checkpoint file')
     p.add_argument('--lstmDecoder', action='store_true', help='Use LSTM decoder instead of Transformer')
+    if multi_gpu:
+        p.add_argument('--port', type=str, default='29500', help='Master port for distributed training')
     p.add_argument('--teacherForcing', action='store_true', help='Use teacher forcing training strategy')
-    p.add_argument('--startingLayer', type=int, default=5, help='Starting layer index for encoder fine-tuning')
+    p.add_argument('--startingLayer', type=int, default=7 if multi_gpu else 5,
+                   help='Starting layer index for encoder fine-tuning')
     p.add_argument('--encoderLr', type=float, default=1e-4, help='Learning rate for encoder if fine-tuning')
     p.add_argument('--embeddingName', type=str, default=None, help='Pretrained embedding name from gensim')
     # additions of this build
@@ -65,7 +70,11 @@ def parse(argv=None):
     p.add_argument('--dataFolder', type=str, default=None,
                    help="the reference's input files (train.py:35); synthetic batches when not given")
     p.add_argument('--workers', type=int, default=6)
-    return p.parse_args(argv)
+    return p
+
+
+def parse(argv=None):
+    return make_parser().parse_args(argv)
 
 
 def synthetic_loader(steps, B, device, rank=0, V=VOCAB, L=maxLen):
@@ -101,14 +110,14 @@ def _val_loader(args):
 
 
 def data_loader(args, device, epoch, rank=0, world=1):
-    """train.py:154-155 (trainMultiGPU.py:240: DistributedSampler) over the reference's files;
+    """train.py:154-155 (trainMultiGPU.py:240: DistributedSampler, seed 42) over the reference's files;
     items stay uint8 (normalised in the stem kernel), batches go to the GPU as bytes.  --steps
     caps the iterations per epoch (0: the whole split)."""
     from torch.utils.data import DataLoader
     from torch.utils.data.distributed import DistributedSampler
     from imagecaptioningconvnext_amd.data import CaptionDataset
     ds = CaptionDataset(args.dataFolder, args.dataName, 'TRAIN')
-    sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True) if world > 1 else None
+    sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=42) if world > 1 else None
     if sampler is not None:
         sampler.set_epoch(epoch)
     dl = DataLoader(ds, batch_size=args.batchSize, shuffle=sampler is None, sampler=sampler,
@@ -163,7 +172,8 @@ def trainWithTeacherForcing(trainDataLoader, encoder, decoder, trainer, epoch, l
         n += 1
         batchTime.update(time.time() - start)
         start = time.time()
-    torch.cuda.synchronize()
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
     for loss, tokens, top5 in trainer.drain_metrics():
         losses.update(loss, tokens)
         top5accs.update(top5, tokens)
@@ -171,9 +181,23 @@ def trainWithTeacherForcing(trainDataLoader, encoder, decoder, trainer, epoch, l
     return losses.avg, top5accs.avg, batchTime.avg, dataTime.avg
 
 
-def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, world=1):
-    """The epoch loop of train.py:159-229 / trainMultiGPU.py: resume (train.py:130-147) from
-    ``ck``, fine-tune from --fineTuneFromEpoch, checkpoint every epoch (rank 0) when --saveDir."""
+def _bcast_from_rank0(values, device):
+    """trainMultiGPU.py:332-334: rank 0 owns the validation bookkeeping; every rank takes its
+    numbers so the lr decays and the early stop happen on all ranks together."""
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    dist.broadcast(t, src=0)
+    return t.tolist()
+
+
+def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, world=1, early_stop=20,
+               val=_val_loader, validate_fn=None):
+    """The epoch loop of train.py:159-229 / trainMultiGPU.py:247-334: resume (train.py:130-147)
+    from ``ck``, fine-tune from --fineTuneFromEpoch, lr decay x0.8 every 8 epochs without a BLEU-4
+    improvement, early stop after ``early_stop`` of them (20 in train.py:168, 40 in
+    trainMultiGPU.py:259), checkpoint every epoch (rank 0) when --saveDir.  With world > 1 rank 0
+    validates and broadcasts epochsSinceImprovement / bestBleu4 (trainMultiGPU.py:332-334).
+    ``val`` (a loader factory) and ``validate_fn`` exist for tests."""
     startEpoch, epochsSinceImprovement, results = 0, 0, []
     if ck is not None:  # train.py:130-147
         startEpoch = ck['epoch'] + 1
@@ -183,17 +207,21 @@ def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, w
                                 ck['encoderOptimizer'] if trainer.enc_eng is not None else None)
         epochsSinceImprovement, results = ck['epochsSinceImprovement'], ck['results']
     bestBleu4 = ck['bleu-4'] if ck is not None else 0.0
-    val = _val_loader(args) if rank == 0 else None
+    val = val(args) if (rank == 0 and val is not None) else None
+    if validate_fn is None:
+        from imagecaptioningconvnext_amd.metrics import validate as validate_fn
     for epoch in range(startEpoch, startEpoch + args.epochs):
-        if epochsSinceImprovement == 20:  # train.py:168-174
-            break
-        if epochsSinceImprovement > 0 and epochsSinceImprovement % 8 == 0:
-            trainer.decoder_lr *= 0.8
-            trainer.encoder_lr *= 0.8
-        if epoch == args.fineTuneFromEpoch:  # train.py:160-166
+        if epoch == args.fineTuneFromEpoch:  # train.py:160-166: a new encoder Adam at encoderLr
             trainer.enable_encoder_finetune(args.startingLayer)
+            trainer.encoder_lr = args.encoderLr
             log(f"Fine-tuning encoder from epoch {epoch} onwards (starting from layer {args.startingLayer})",
                 flush=True)
+        if epochsSinceImprovement == early_stop:  # train.py:168-169 / trainMultiGPU.py:259-260
+            break
+        if epochsSinceImprovement > 0 and epochsSinceImprovement % 8 == 0:  # train.py:170-173
+            trainer.decoder_lr *= 0.8
+            if trainer.enc_eng is not None:  # only an existing encoder optimizer decays
+                trainer.encoder_lr *= 0.8
         loader = (data_loader(args, device, epoch, rank, world) if args.dataFolder else
                   synthetic_loader(args.steps, args.batchSize, device, rank=rank))
         out = trainWithTeacherForcing(loader, encoder, decoder, trainer, epoch, args.lstmDecoder, log=log)
@@ -203,15 +231,17 @@ def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, w
                'trainDataTime': out[3]}
         recentBleu4, isBest = 0.0, False
         if val is not None:  # train.py:190-222: greedy validation, BLEU, improvement bookkeeping
-            from imagecaptioningconvnext_amd.metrics import validate
-            vl, vt, b1, b2, b3, recentBleu4 = validate(val, encoder, decoder, val.dataset.wordMap, args.lstmDecoder,
-                                                       device, alphaC=alphaC, log=log)
+            vl, vt, b1, b2, b3, recentBleu4 = validate_fn(val, encoder, decoder, val.dataset.wordMap,
+                                                          args.lstmDecoder, device, alphaC=alphaC, log=log)
             rec.update(valLoss=vl, valTop5Acc=vt, bleu1=b1, bleu2=b2, bleu3=b3, bleu4=recentBleu4)
             isBest = recentBleu4 > bestBleu4
             bestBleu4 = max(recentBleu4, bestBleu4)
             epochsSinceImprovement = 0 if isBest else epochsSinceImprovement + 1
             encoder.train()
             decoder.train()
+        if world > 1:
+            epochsSinceImprovement, bestBleu4 = _bcast_from_rank0((epochsSinceImprovement, bestBleu4), device)
+            epochsSinceImprovement = int(epochsSinceImprovement)
         results.append(rec)
         if args.saveDir and rank == 0:  # train.py:224-229
             from imagecaptioningconvnext_amd.checkpoint import save_checkpoint
@@ -221,6 +251,7 @@ def run_epochs(args, encoder, decoder, trainer, ck, device, rank=0, log=print, w
                                    args.lstmDecoder, args.startingLayer, args.encoderLr, args.embeddingName,
                                    directory=args.saveDir)
             log(f"saved {path}", flush=True)
+    return epochsSinceImprovement, results
 
 
 def main(argv=None):

@@ -4,8 +4,12 @@ LOCAL_RANK, backend "nccl" (= RCCL over xGMI), DDP-equivalent gradient averaging
 ``TeacherForcedTrainer`` (one all-reduce of the flat gradient buffer per step) and the
 ``reduceLossAndTokens`` metric reduction (:96-108).
 
+    srun python3 trainMultiGPU.py --port 29500 --teacherForcing        (the reference's launch line)
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 trainMultiGPU.py \
         --teacherForcing --encoder base --batchSize 32
+
+CLI: trainMultiGPU.py:63-70 (``--port``, ``--startingLayer`` default 7) plus this build's
+additions shared with train.py; early stop after 40 epochs without improvement (:259).
 """
 import os
 import sys
@@ -17,15 +21,31 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import train  # noqa: E402  (model construction, CLI and the epoch loop are shared)
 
 
-def setup_distributed():
-    """trainMultiGPU.py:144-160 (SLURM) or torchrun environment."""
-    if "SLURM_PROCID" in os.environ and "RANK" not in os.environ:
-        rank, world, local = (int(os.environ[k]) for k in ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID"))
+EARLY_STOP = 40  # trainMultiGPU.py:259 (train.py uses 20)
+
+
+def parse(argv=None):
+    return train.make_parser(multi_gpu=True).parse_args(argv)
+
+
+def dist_env(port, environ=None):
+    """(rank, world, local) from SLURM (trainMultiGPU.py:144-146) or torchrun's variables, and
+    the rendezvous address: under SLURM MASTER_PORT comes from --port (:148); under torchrun its
+    own MASTER_PORT stays (the workers join torchrun's store there)."""
+    env = os.environ if environ is None else environ
+    if "SLURM_PROCID" in env and "RANK" not in env:
+        rank, world, local = (int(env[k]) for k in ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID"))
+        env["MASTER_PORT"] = str(port)
     else:
-        rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1),
-                                                                       ("LOCAL_RANK", 0)))
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29500")
+        rank, world, local = (int(env.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
+        env.setdefault("MASTER_PORT", str(port))
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return rank, world, local
+
+
+def setup_distributed(port="29500"):
+    """trainMultiGPU.py:144-160 (SLURM) or torchrun environment."""
+    rank, world, local = dist_env(port)
     torch.cuda.set_device(local)
     device = torch.device(f"cuda:{local}")
     dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank, device_id=device)
@@ -33,10 +53,10 @@ def setup_distributed():
 
 
 def main(argv=None):
-    args = train.parse(argv)
+    args = parse(argv)
     if not args.teacherForcing:
         raise NotImplementedError("non-teacher-forced training is outside the accelerated path (SURVEY.md §8f)")
-    rank, local, world, device = setup_distributed()
+    rank, local, world, device = setup_distributed(args.port)
     torch.manual_seed(42 + rank)
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
     encoder, decoder, ck = train.build_models(args, device)
@@ -45,7 +65,8 @@ def main(argv=None):
                                    graph=True)
     log = print if rank == 0 else (lambda *a, **k: None)
     # trainMultiGPU.py: encoder fine-tuned (and DDP-averaged) from epoch 20; rank 0 checkpoints
-    train.run_epochs(args, encoder, decoder, trainer, ck, device, rank=rank, log=log, world=world)
+    train.run_epochs(args, encoder, decoder, trainer, ck, device, rank=rank, log=log, world=world,
+                     early_stop=EARLY_STOP)
     dist.barrier()
     dist.destroy_process_group()
 
