@@ -36,7 +36,8 @@ class LstmDesc(ctypes.Structure):
         (n, c_void_p) for n in ("w_hcat", "b_hcat", "w_ih", "w_f", "enc", "att1", "xe", "c0", "dl", "g1", "alphas",
                                 "awe", "zs", "gates", "cs", "hs", "hprev", "w_zh_t", "w_att_t", "dhs", "dalpha",
                                 "dcat", "dz", "ws_y", "y_cnt", "dh", "dc", "de", "datt1", "dwf", "dbea")] + [
-        ("x_slices", ctypes.c_int32), ("y_slices", ctypes.c_int32), ("dawe", c_void_p)]
+        ("x_slices", ctypes.c_int32), ("y_slices", ctypes.c_int32), ("dawe", c_void_p), ("sync", c_void_p),
+        ("sync_words", ctypes.c_int32)]
 
 
 class MhaDesc(ctypes.Structure):
@@ -96,6 +97,7 @@ _SIGS = {
                           c_float, c_int, c_float, c_float, c_void_p],
     "imgcap_lstm_tf_fwd": [ctypes.POINTER(LstmDesc), c_void_p],
     "imgcap_lstm_tf_bwd": [ctypes.POINTER(LstmDesc), c_void_p],
+    "imgcap_lstm_sync_words": [ctypes.POINTER(LstmDesc)],
     "imgcap_mha_fwd": [ctypes.POINTER(MhaDesc), c_void_p],
     "imgcap_mha_bwd": [ctypes.POINTER(MhaDesc), c_void_p],
     "imgcap_attn_reg": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],

@@ -688,9 +688,15 @@ static int depth_for(int klen, int sw, bool f32) {
     else hipLaunchKernelGGL((KERNEL<T, SW, (F32 ? 2 : 8)>), __VA_ARGS__);            \
   } while (0)
 
+int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used);  // lstm_persist.hip
+int lstm_persist_sync_words(const imgcap_lstm_desc& d);
+
 template <typename T>
 static int lstm_fwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
   constexpr bool F32 = sizeof(T) == 4;
+  bool used = false;
+  if (int rc = lstm_fwd_persistent(d, st, &used)) return rc;
+  if (used) return 0;
   const int W3 = d.A + d.E + 4 * d.D;
   const int ct = d.dtype;
   const int nrg = (d.B + RG - 1) / RG;
@@ -786,6 +792,11 @@ extern "C" int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream) {
   if (int rc = check_desc(d)) return rc;
   if (d->dtype == IMGCAP_BF16) return lstm_fwd_impl<bf16>(*d, (hipStream_t)stream);
   return lstm_fwd_impl<float>(*d, (hipStream_t)stream);
+}
+
+extern "C" int imgcap_lstm_sync_words(const imgcap_lstm_desc* d) {
+  if (check_desc(d)) return 0;
+  return lstm_persist_sync_words(*d);
 }
 
 extern "C" int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream) {

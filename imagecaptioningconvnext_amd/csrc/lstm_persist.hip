@@ -1,0 +1,698 @@
+// Persistent forward recurrence of the teacher-forced LSTM-attention decoder
+// (models/decoder.py:69-113): ONE launch runs every step t < min(T, max decode length).
+//
+// Why: the per-step kernels of lstm.hip (skinny GEMM -> attention -> gate/cell, three launches
+// per step) spend most of each launch refilling registers from L2 and draining; here every
+// workgroup keeps its operands resident in LDS for the whole sequence and the steps are chained
+// by in-launch hand-offs.
+//
+// Roles (one 256-thread workgroup per CU; the LDS request keeps it that way):
+//   UG blocks [0, NUG):   U role (blk < NU): UPB LSTM units = UC = 4*UPB gate columns (all four
+//                         gates of each unit), rows of [W_ih[:, M:] | W_hh] resident in LDS;
+//                         gates = xe + [z_t | h_{t-1}] . W^T + b_hh, then the LSTMCell -> h_t.
+//                         G role (blk < NG): 32 columns of [W_da; W_fb] resident in LDS;
+//                         [att2 | gate_pre]_t = h_{t-1} . W^T + b  (decoder.py:27,104).
+//   R blocks [NUG, +B*RS): batch row b, channel chunk s of E: att1[b] and enc[b][:, chunk]
+//                         resident in LDS; scores, softmax, context, sigmoid gate -> z_t[b]
+//                         (decoder.py:25-31, 102-105).
+// Per step three hand-offs: h_{t-1} (all U blocks) -> G and U;  [att2 | gate_pre] (all G
+// blocks) -> R;  z_t (all R blocks) -> U.  Each is the write-through form of the visibility
+// rules (MI355X_MICROARCH.md, inter-workgroup visibility, valid-forms table row 1): payload
+// stored sc1 (buffer stores, aux = sc1), every storing wave drains (s_waitcnt vmcnt(0)), a
+// workgroup barrier, ONE lane stores the block's flag (relaxed agent-scope atomic store =
+// sc1); the consumer's wave 0 polls the producers' flags with sc1 loads, then a workgroup
+// barrier, then every load of the payload is an sc1 buffer load.  No fences.  Flags are
+// per producer (no contended counter), epoch = step + 1, zeroed by a memset before the launch.
+// Every spin is bounded: on timeout (or when another block already gave up) the block writes
+// the error word and returns, so the grid always drains.
+//
+// Outputs are those of the per-step path (imgcap_lstm_tf_fwd), except g1's hh columns, which
+// only the per-step gate kernel reads.  Steps t >= max decode length are not computed; their
+// outputs are written as zeros (every row is past its decode length there, so the loss and
+// the backward never use them).
+#include <algorithm>
+
+#include "mfma.h"
+
+namespace imgcap {
+
+namespace {
+
+constexpr int PT = 512;            // threads per workgroup (8 waves: two per SIMD hide each other's latency)
+constexpr int PWV = PT / 64;       // waves
+constexpr int GCOLS = 32;          // G columns per workgroup
+constexpr int SPIN_LIMIT = 1 << 21;
+template <typename T> struct MaxKs { static constexpr int N = sizeof(T) == 2 ? 16 : 8; };  // U-phase k-steps per wave
+constexpr int SYNC_HDR = 16;       // words before the flags (word 0: error)
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+DEV rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// 16-byte write-through (sc1) load / store
+DEV uint4 ld_wt(rsrc_t r, uint32_t off) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+DEV void st_wt(rsrc_t r, uint32_t off, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, r, off, 0, 16);
+}
+
+struct Geo {
+  int NU, NG, NUG, RS, Ec, NR, UPB, KU, ldu, ldg, rc;
+  int ug_red, ug_hst, r_enc, r_red, r_red2, r_es;  // byte offsets into dynamic LDS
+  long long* stamps;  // diagnostics (IMGCAP_LSTM_STAMPS=1): per step, s_memrealtime at phase edges
+};
+
+// thread 0 of block 0 (U+G) and of the first R block records [role][t][k]
+DEV void stamp(const Geo& g, int role, int t, int k, bool drain = false) {
+  if (g.stamps && threadIdx.x == 0 && (blockIdx.x == 0 || (int)blockIdx.x == g.NUG)) {
+    if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    g.stamps[(role * 64 + t) * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (k == 0) g.stamps[(role * 64 + t) * 16 + 15] = (long long)__builtin_amdgcn_s_memtime();
+  }
+}
+
+// Wave 0 polls n per-producer flags (plus the error word) until all reach `epoch`; the result
+// is shared through LDS and a workgroup barrier follows (the other waves load after it).
+DEV bool poll_once(const int* flags, int n, int epoch, int* err, int lane, bool& bad) {
+  bool all = true;
+  bad = false;
+  for (int i = lane; i <= n; i += 64) {
+    const int v = __hip_atomic_load(i < n ? flags + i : err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (i < n) all = all && v >= epoch;
+    else bad = v != 0;
+  }
+  return all;
+}
+
+// Wave 0 polls n per-producer flags (plus the error word) until all reach `epoch`; the result
+// is shared through LDS and a workgroup barrier follows (the other waves load after it).
+DEV bool block_wait(const int* flags, int n, int epoch, int* err, int* s_ok) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    bool ok = false;
+    for (int spins = 0;; ++spins) {
+      bool bad;
+      const bool all = poll_once(flags, n, epoch, err, lane, bad);
+      if (__any(bad)) break;
+      if (__all(all)) { ok = true; break; }
+      if (spins >= SPIN_LIMIT) {
+        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    if (lane == 0) *s_ok = ok;
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+// every storing wave drains its write-through stores, then one lane publishes the flag
+DEV void block_publish(int* flag, int epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T> struct VecOf { static constexpr int N = 16 / sizeof(T); };
+
+// wave64 reductions on DPP (quad_perm, row mirrors, row_bcast15/31): the total lands in lane 63
+// and is broadcast with readlane -- no LDS round trip (ds_bpermute) per step
+#define IMGCAP_DPP(v, ctrl, rmask) \
+  __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, rmask, 0xF, false))
+DEV float wave_sum_dpp(float v) {
+  v += IMGCAP_DPP(v, 0xB1, 0xF);   // quad_perm [1,0,3,2]
+  v += IMGCAP_DPP(v, 0x4E, 0xF);   // quad_perm [2,3,0,1]
+  v += IMGCAP_DPP(v, 0x141, 0xF);  // row_half_mirror
+  v += IMGCAP_DPP(v, 0x140, 0xF);  // row_mirror
+  v += IMGCAP_DPP(v, 0x142, 0xA);  // row_bcast15
+  v += IMGCAP_DPP(v, 0x143, 0xC);  // row_bcast31
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+#define IMGCAP_DPP_MAX(v, ctrl, rmask)                                                              \
+  __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, -INFINITY),         \
+                                                        __builtin_bit_cast(int, v), ctrl, rmask, 0xF, false))
+DEV float wave_max_dpp(float v) {
+  v = fmaxf(v, IMGCAP_DPP_MAX(v, 0xB1, 0xF));
+  v = fmaxf(v, IMGCAP_DPP_MAX(v, 0x4E, 0xF));
+  v = fmaxf(v, IMGCAP_DPP_MAX(v, 0x141, 0xF));
+  v = fmaxf(v, IMGCAP_DPP_MAX(v, 0x140, 0xF));
+  v = fmaxf(v, IMGCAP_DPP_MAX(v, 0x142, 0xA));
+  v = fmaxf(v, IMGCAP_DPP_MAX(v, 0x143, 0xC));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+// sum over the 4 lanes of a quad, every lane of the quad gets it
+DEV float quad_sum_dpp(float v) {
+  v += IMGCAP_DPP(v, 0xB1, 0xF);
+  v += IMGCAP_DPP(v, 0x4E, 0xF);
+  return v;
+}
+
+DEV void unpack8(const uint4& a, const uint4& b, float (&v)[8]) {
+  v[0] = __uint_as_float(a.x); v[1] = __uint_as_float(a.y); v[2] = __uint_as_float(a.z); v[3] = __uint_as_float(a.w);
+  v[4] = __uint_as_float(b.x); v[5] = __uint_as_float(b.y); v[6] = __uint_as_float(b.z); v[7] = __uint_as_float(b.w);
+}
+
+// B fragment from LDS, zero for k0 >= K (a register select: the MFMA stays wave-uniform)
+template <typename T>
+DEV Frag<T> lds_frag_k(const T* row, int k0, int K) {
+  const bool ok = k0 < K;
+  Frag<T> f = lds_frag<T>(row + (ok ? k0 : 0));
+  if (!ok) f = frag_from<T>(make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u));
+  return f;
+}
+
+// A fragment (8 k of one row) from a write-through buffer; zero outside [0, rows) x [0, K)
+template <typename T>
+DEV Frag<T> frag_wt(rsrc_t r, uint32_t off, bool ok) {
+  uint4 lo = make_uint4(0u, 0u, 0u, 0u), hi = lo;
+  if (ok) {
+    lo = ld_wt(r, off);
+    if (sizeof(T) == 4) hi = ld_wt(r, off + 16);
+  }
+  return frag_from<T>(lo, hi);
+}
+
+template <typename T, int MT>
+__global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d, Geo g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_ok = (int*)smem;
+  const int B = d.B, P = d.P, E = d.E, A = d.A, D = d.D, M = d.M, Tn = d.T;
+  const int W3 = A + E + 4 * D;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int* err = d.sync;
+  int* fh = d.sync + SYNC_HDR;
+  int* fg = fh + g.NU;
+  int* fz = fg + g.NG;
+  // steps actually run: every row is past its decode length from max(dl) on
+  if (tid < 64) {
+    int m = 0;
+    for (int i = lane; i < B; i += 64) m = max(m, d.dl[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if (lane == 0) s_ok[1] = m;
+  }
+  __syncthreads();
+  const int Tmax = max(0, min(Tn, s_ok[1]));
+  const int blk = blockIdx.x;
+  constexpr int VEC = VecOf<T>::N;
+  const rsrc_t r_hs = make_rsrc(d.hs, (uint32_t)((long)B * Tn * D * sizeof(T)));
+  const rsrc_t r_h0 = make_rsrc(d.hprev, (uint32_t)((long)B * Tn * D * sizeof(T)));
+  const rsrc_t r_zs = make_rsrc(d.zs, (uint32_t)((long)B * Tn * E * sizeof(T)));
+  const rsrc_t r_g1 = make_rsrc(d.g1, (uint32_t)((long)B * Tn * W3 * sizeof(float)));
+
+  if (blk < g.NUG) {
+    // ======================= U / G workgroup =======================================
+    constexpr int KP = PWV / MT;         // K parts: wave w -> row tile w % MT, K part w / MT
+    constexpr int NTU = 2;  // UPB = 8 units = 32 gate columns
+    constexpr int UC = 16 * NTU;
+    constexpr int MAXKS = MaxKs<T>::N;
+    const int UPB = g.UPB;
+    const bool isU = blk < g.NU, isG = blk < g.NG;
+    const int u0 = blk * UPB;
+    const int KU = g.KU, ldu = g.ldu, ldg = g.ldg, RC = g.rc;
+    T* wu = (T*)(smem + 16);
+    T* wg = wu + UC * ldu;
+    float* red = (float*)(smem + g.ug_red);  // [KP][16*MT][RC]
+    T* hst = (T*)(smem + g.ug_hst);          // [16*MT][UPB]
+    // ---- resident weights ----
+    if (isU) {
+      const int cpr = KU / VEC;
+      for (int i = tid; i < UC * cpr; i += PT) {
+        const int c = i / cpr, k = (i % cpr) * VEC;
+        const int row = (c / UPB) * D + u0 + c % UPB;
+        const T* src = k < E ? (const T*)d.w_ih + (long)row * (M + E) + M + k
+                             : (const T*)d.w_hcat + (long)(A + E + row) * D + (k - E);
+        *(uint4*)(wu + c * ldu + k) = *(const uint4*)src;
+      }
+    }
+    if (isG) {
+      const int cpr = D / VEC;
+      for (int i = tid; i < GCOLS * cpr; i += PT) {
+        const int c = i / cpr, k = (i % cpr) * VEC;
+        const int col = blk * GCOLS + c;
+        *(uint4*)(wg + c * ldg + k) =
+            col < A + E ? *(const uint4*)((const T*)d.w_hcat + (long)col * D + k) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    // ---- cell state of this thread's (row, unit) items ----
+    constexpr int CPT = (16 * MT * 8 + PT - 1) / PT;  // (row, unit) items per thread
+    float creg[CPT], bh[CPT][4];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int i = tid + k * PT, b = i / UPB, j = u0 + i % UPB;
+      const bool ok = isU && b < B;
+      creg[k] = ok ? d.c0[(long)b * D + j] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bh[k][q] = ok ? d.b_hcat[A + E + q * D + j] : 0.f;
+    }
+    // G output bias: a thread always stores the same 4 columns (PT is a multiple of GCOLS / 4)
+    float gb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = blk * GCOLS + (tid % (GCOLS / 4)) * 4 + j;
+      gb[j] = isG && col < A + E ? d.b_hcat[col] : 0.f;
+    }
+    __syncthreads();
+    const int mi = w % MT, kp = w / MT;
+    const int fr = lane & 15, fk = 8 * (lane >> 4);
+    const int m = mi * 16 + fr;
+    const bool mok = m < B;
+    for (int t = 0; t < Tmax; ++t) {
+      stamp(g, 0, t, 0);
+      if (t > 0 && !block_wait(fh, g.NU, t, err, s_ok + 2)) return;
+      stamp(g, 0, t, 1);
+      // h_{t-1} rows: h0 (hprev slot 0) at t = 0, else hs slot t-1
+      const rsrc_t rh = t == 0 ? r_h0 : r_hs;
+      const long hrow = (long)m * Tn + (t == 0 ? 0 : t - 1);
+      // U prefetch (issued before the G phase so its round trip overlaps it): xe, h part of A
+      float xe[CPT][4];
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) {
+        const int i = tid + k * PT, b = i / UPB, j = u0 + i % UPB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xe[k][q] = isU && b < B ? d.xe[((long)b * Tn + t) * 4 * D + q * D + j] : 0.f;
+      }
+      // A = [z_t | h_{t-1}]: the h part is available now, the z part after the R blocks'
+      // hand-off; every fragment of this wave's K range is requested in one round trip each
+      const int nks = (KU + 31) / 32, per = (nks + KP - 1) / KP;
+      const int ks0 = kp * per, ks1 = min(nks, ks0 + per);
+      const long zrow = (long)m * Tn + t;
+      Frag<T> fa[MAXKS];
+#pragma unroll
+      for (int i = 0; i < MAXKS; ++i) {
+        const int k0 = (ks0 + i) * 32 + fk;
+        fa[i] = frag_wt<T>(rh, (uint32_t)((hrow * D + (k0 - E)) * sizeof(T)),
+                           isU && mok && ks0 + i < ks1 && k0 >= E && k0 < KU);
+      }
+      // ---------------- G: [att2 | gate_pre]_t ----------------
+      if (isG) {
+        f32x4 acc[2];
+        acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int nks = (D + 31) / 32, per = (nks + KP - 1) / KP;
+        const int ks0 = kp * per, ks1 = min(nks, ks0 + per);
+        for (int ks = ks0; ks < ks1; ks += 8) {
+          Frag<T> fa[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int k0 = (ks + i) * 32 + fk;
+            fa[i] = frag_wt<T>(rh, (uint32_t)((hrow * D + k0) * sizeof(T)), mok && ks + i < ks1 && k0 < D);
+          }
+          stamp(g, 0, t, 9, true);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {  // steps past ks1 have zero A fragments: no branch
+            const int k0 = (ks + i) * 32 + fk;
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) mma(acc[ni], fa[i], lds_frag_k<T>(wg + (ni * 16 + fr) * ldg, k0, D));
+          }
+        }
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[(kp * 16 * MT + mi * 16 + 4 * (lane >> 4) + r) * RC + ni * 16 + fr] = acc[ni][r];
+        __syncthreads();
+        // 16-byte write-through stores: row b, 4 consecutive columns per thread
+        const int col0 = blk * GCOLS;
+        for (int i = tid; i < 16 * MT * (GCOLS / 4); i += PT) {
+          const int b = i / (GCOLS / 4), c = (i % (GCOLS / 4)) * 4;
+          if (b >= B || col0 + c >= A + E) continue;
+          float v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float s = gb[j];
+#pragma unroll
+            for (int q = 0; q < KP; ++q) s += red[(q * 16 * MT + b) * RC + c + j];
+            v[j] = s;
+          }
+          st_wt(r_g1, (uint32_t)((((long)b * Tn + t) * W3 + col0 + c) * 4),
+                make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])));
+        }
+        stamp(g, 0, t, 2);
+        block_publish(fg + blk, t + 1);
+        stamp(g, 0, t, 3);
+      }
+      // ---------------- U: gates, LSTMCell -> h_t ----------------
+      if (isU) {
+        if (!block_wait(fz, g.NR, t + 1, err, s_ok + 3)) return;
+        stamp(g, 0, t, 4);
+#pragma unroll
+        for (int i = 0; i < MAXKS; ++i) {
+          const int k0 = (ks0 + i) * 32 + fk;
+          if (mok && ks0 + i < ks1 && k0 < E) fa[i] = frag_wt<T>(r_zs, (uint32_t)((zrow * E + k0) * sizeof(T)), true);
+        }
+        stamp(g, 0, t, 8, true);
+        f32x4 acc[NTU][2];  // two K-interleaved chains per column tile
+#pragma unroll
+        for (int ni = 0; ni < NTU; ++ni) acc[ni][0] = acc[ni][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i0 = 0; i0 < MAXKS; i0 += 4) {
+          if (ks0 + i0 < ks1) {  // uniform; steps past ks1 inside a group have zero A fragments
+#pragma unroll
+            for (int i = i0; i < i0 + 4; ++i) {
+              const int k0 = (ks0 + i) * 32 + fk;
+#pragma unroll
+              for (int ni = 0; ni < NTU; ++ni)
+                mma(acc[ni][i & 1], fa[i], lds_frag_k<T>(wu + (ni * 16 + fr) * ldu, k0, KU));
+            }
+          }
+        }
+#pragma unroll
+        for (int ni = 0; ni < NTU; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            red[(kp * 16 * MT + mi * 16 + 4 * (lane >> 4) + r) * RC + ni * 16 + fr] = acc[ni][0][r] + acc[ni][1][r];
+        __syncthreads();
+        stamp(g, 0, t, 5);
+        float cell[CPT][5];  // activated i, f, g, o and c_t, stored after the hand-off
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+          const int i = tid + k * PT, b = i / UPB, jj = i % UPB;
+          if (b >= B) continue;
+          float gq[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float s = xe[k][q] + bh[k][q];
+#pragma unroll
+            for (int p = 0; p < KP; ++p) s += red[(p * 16 * MT + b) * RC + q * UPB + jj];
+            gq[q] = s;
+          }
+          const float gi = sigmoidf_(gq[0]), gf = sigmoidf_(gq[1]), gg = tanhf(gq[2]), go = sigmoidf_(gq[3]);
+          const float cn = gf * creg[k] + gi * gg;
+          const float h = go * tanhf(cn);
+          creg[k] = cn;
+          cell[k][0] = gi; cell[k][1] = gf; cell[k][2] = gg; cell[k][3] = go; cell[k][4] = cn;
+          hst[b * UPB + jj] = from_f<T>(h);
+        }
+        __syncthreads();
+        // h_t of this block's units: one row per thread, write-through 16-byte pieces
+        const int pieces = UPB * (int)sizeof(T) / 16;  // UPB * sizeof(T) is 16 or 32
+        for (int i = tid; i < B * pieces; i += PT) {
+          const int b = i / pieces, pc = i % pieces;
+          const uint4 v = *(const uint4*)(hst + b * UPB + pc * VEC);
+          const long off = ((long)b * Tn + t) * D + u0 + pc * VEC;
+          st_wt(r_hs, (uint32_t)(off * sizeof(T)), v);
+        }
+        stamp(g, 0, t, 6);
+        block_publish(fh + blk, t + 1);
+        stamp(g, 0, t, 7);
+        // outputs nobody in this launch reads: after the hand-off
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+          const int i = tid + k * PT, b = i / UPB, jj = i % UPB, j = u0 + jj;
+          if (b >= B) continue;
+          const long bt = (long)b * Tn + t;
+          float* ga = d.gates + bt * 4 * D;
+          ga[j] = cell[k][0]; ga[D + j] = cell[k][1]; ga[2 * D + j] = cell[k][2]; ga[3 * D + j] = cell[k][3];
+          d.cs[bt * D + j] = cell[k][4];
+        }
+        if (t + 1 < Tn)
+          for (int i = tid; i < B * pieces; i += PT) {
+            const int b = i / pieces, pc = i % pieces;
+            const long off = ((long)b * Tn + t) * D + u0 + pc * VEC;
+            *(uint4*)((T*)d.hprev + off + D) = *(const uint4*)(hst + b * UPB + pc * VEC);
+          }
+      }
+    }
+    // ---- steps past every decode length: zero outputs ----
+    if (Tmax < Tn) {
+      if (isU) {
+        for (int i = tid; i < B * (Tn - Tmax) * UPB; i += PT) {
+          const int jj = i % UPB, rest = i / UPB, b = rest % B, t = Tmax + rest / B, j = u0 + jj;
+          const long bt = (long)b * Tn + t;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) d.gates[bt * 4 * D + q * D + j] = 0.f;
+          d.cs[bt * D + j] = 0.f;
+          ((T*)d.hs)[bt * D + j] = from_f<T>(0.f);
+          if (t + 1 < Tn) ((T*)d.hprev)[(bt + 1) * D + j] = from_f<T>(0.f);
+        }
+      }
+      if (isG) {
+        for (int i = tid; i < B * (Tn - Tmax) * GCOLS; i += PT) {
+          const int c = i % GCOLS, rest = i / GCOLS, b = rest % B, t = Tmax + rest / B;
+          const int col = blk * GCOLS + c;
+          if (col < A + E) d.g1[((long)b * Tn + t) * W3 + col] = 0.f;
+        }
+      }
+    }
+    return;
+  }
+  // ======================= R workgroup: attention of row b, channel chunk s ================
+  const int rr = blk - g.NUG, b = rr / g.RS, s = rr % g.RS;
+  const int Ec = g.Ec, e0 = s * Ec;
+  T* att1s = (T*)(smem + 16);                   // [P][A]
+  T* encs = (T*)(smem + g.r_enc);               // [P][Ec]
+  float* red2 = (float*)(smem + g.r_red2);      // [64] scores
+  float* es = (float*)(smem + g.r_es);          // [64] alpha
+  {
+    const T* a1 = (const T*)d.att1 + (long)b * P * A;
+    for (int i = tid; i < P * A / VEC; i += PT) *(uint4*)(att1s + i * VEC) = *(const uint4*)(a1 + i * VEC);
+    const T* en = (const T*)d.enc + (long)b * P * E + e0;
+    const int cpr = Ec / VEC;
+    for (int i = tid; i < P * cpr; i += PT) {
+      const int p = i / cpr, k = (i % cpr) * VEC;
+      *(uint4*)(encs + p * Ec + k) = *(const uint4*)(en + (long)p * E + k);
+    }
+  }
+  const int dlb = d.dl[b];
+  const int NVA = A / 8;                          // <= 64 (A <= 512)
+  const bool aok = lane < NVA;
+  float wf[8];
+  {
+    const float* wp = d.w_f + (aok ? lane * 8 : 0);
+    unpack8(*(const uint4*)wp, *(const uint4*)(wp + 4), wf);
+  }
+  // context mapping: thread = (8-channel vector v, pixel group pg = lane & 3); the four pixel
+  // groups of a vector are one lane quad, summed with two DPP steps (no LDS round trip)
+  const int NVE = Ec / 8;
+  const int pg = lane & 3;
+  __syncthreads();
+  for (int t = 0; t < Tmax; ++t) {
+    stamp(g, 1, t, 0);
+    if (!block_wait(fg, g.NG, t + 1, err, s_ok + 2)) return;
+    stamp(g, 1, t, 1);
+    const long bt = (long)b * Tn + t;
+    // att2 slice of this lane (the gate pre-activations are read by the context threads below)
+    float a2[8];
+    {
+      const uint32_t oa = (uint32_t)((bt * W3 + (aok ? lane * 8 : 0)) * 4);
+      unpack8(ld_wt(r_g1, oa), ld_wt(r_g1, oa + 16), a2);
+    }
+    stamp(g, 1, t, 5, true);
+    // scores e_p = w_f . relu(att1_p + att2): wave w takes pixels w, w+PWV, ..; lane = 8 units;
+    // each pixel's 64 lane partials summed by DPP, the total written by one lane
+    {
+      constexpr int H = sizeof(T) / 2;  // 16-byte words per 8 elements
+      constexpr int NPW = 64 / PWV;
+      uint4 xr[NPW][H];
+#pragma unroll
+      for (int i = 0; i < NPW; ++i) {
+        const int p = min(w + PWV * i, P - 1);
+#pragma unroll
+        for (int h = 0; h < H; ++h) xr[i][h] = *(const uint4*)(att1s + p * A + (aok ? lane * 8 : 0) + h * VEC);
+      }
+#pragma unroll
+      for (int i = 0; i < NPW; ++i) {
+        const int p = w + PWV * i;
+        if (p < P) {
+          const T* x8 = (const T*)&xr[i][0];
+          float sc = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sc += wf[j] * fmaxf(to_f(x8[j]) + a2[j], 0.f);
+          sc = wave_sum_dpp(aok ? sc : 0.f);
+          if (lane == 0) red2[p] = sc;
+        }
+      }
+    }
+    __syncthreads();
+    stamp(g, 1, t, 6);
+    if (tid < 64) {  // softmax over the P scores (full_att's bias cancels)
+      const float e = tid < P ? red2[tid] : -INFINITY;
+      const float mx = wave_max_dpp(e);
+      const float ex = tid < P ? __expf(e - mx) : 0.f;
+      const float al = ex / wave_sum_dpp(ex);
+      if (tid < P) es[tid] = al;
+    }
+    __syncthreads();
+    stamp(g, 1, t, 7);
+    for (int v = tid >> 2; v < NVE; v += PT / 4) {
+      // gate pre-activation of this vector (only the quad leader uses it)
+      float gp[8];
+      const uint32_t og = (uint32_t)((bt * W3 + A + e0 + v * 8) * 4);
+      unpack8(ld_wt(r_g1, og), ld_wt(r_g1, og + 16), gp);
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      constexpr int H = sizeof(T) / 2;
+      for (int p0 = pg; p0 < P; p0 += 32) {
+        uint4 xr[8][H];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int p = min(p0 + 4 * i, P - 1);
+#pragma unroll
+          for (int h = 0; h < H; ++h) xr[i][h] = *(const uint4*)(encs + p * Ec + v * 8 + h * VEC);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int p = p0 + 4 * i;
+          const float al = p < P ? es[min(p, P - 1)] : 0.f;
+          const T* x8 = (const T*)&xr[i][0];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += al * to_f(x8[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = quad_sum_dpp(acc[j]);
+      if (pg == 0) {
+        uint4 zz[2];
+        T* zt = (T*)zz;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) zt[j] = from_f<T>(sigmoidf_(gp[j]) * acc[j]);
+        const uint32_t off = (uint32_t)((bt * E + e0 + v * 8) * sizeof(T));
+        st_wt(r_zs, off, zz[0]);
+        if (sizeof(T) == 4) st_wt(r_zs, off + 16, zz[1]);
+        float* aw = d.awe + bt * E + e0 + v * 8;  // saved context (nobody in this launch reads it)
+        *(f32x4*)aw = f32x4{acc[0], acc[1], acc[2], acc[3]};
+        *(f32x4*)(aw + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+      }
+    }
+    stamp(g, 1, t, 3);
+    block_publish(fz + rr, t + 1);
+    stamp(g, 1, t, 4);
+    if (s == 0 && tid < P) d.alphas[bt * P + tid] = t < dlb ? es[tid] : 0.f;
+  }
+  if (Tmax < Tn) {
+    for (int i = tid; i < (Tn - Tmax) * Ec; i += PT) {
+      const long bt = (long)b * Tn + Tmax + i / Ec;
+      const int e = e0 + i % Ec;
+      d.awe[bt * E + e] = 0.f;
+      ((T*)d.zs)[bt * E + e] = from_f<T>(0.f);
+    }
+    if (s == 0)
+      for (int i = tid; i < (Tn - Tmax) * P; i += PT) d.alphas[((long)b * Tn + Tmax) * P + i] = 0.f;
+  }
+}
+
+size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+}  // namespace
+
+// Geometry + LDS plan; false when the shape is outside what the persistent kernel covers.
+static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds, int& mt, int& words) {
+  const size_t LDS_MAX = 160 * 1024;
+  if (d.B < 1 || d.B > 32 || d.P > 64 || d.A > 512 || d.A % 8 || d.E % 8 || d.D % 8 || d.M % 8) return false;
+  mt = d.B <= 16 ? 1 : 2;
+  g.UPB = 8;
+  const int UC = 4 * g.UPB;
+  g.NU = d.D / g.UPB;
+  g.NG = (d.A + d.E + GCOLS - 1) / GCOLS;
+  g.NUG = std::max(g.NU, g.NG);
+  g.KU = d.E + d.D;
+  const int pad = 16 / esz;
+  g.ldu = g.KU + pad;
+  g.ldg = d.D + pad;
+  g.rc = std::max(UC, GCOLS) + 4;
+  const int KP = PWV / mt;
+  if (((g.KU + 31) / 32 + KP - 1) / KP > (esz == 2 ? MaxKs<bf16>::N : MaxKs<float>::N)) return false;
+  size_t o = 16 + (size_t)UC * g.ldu * esz + (size_t)GCOLS * g.ldg * esz;
+  g.ug_red = (int)align16(o);
+  o = g.ug_red + (size_t)KP * 16 * mt * g.rc * 4;
+  g.ug_hst = (int)align16(o);
+  const size_t ug = align16(g.ug_hst + (size_t)16 * mt * g.UPB * esz);
+  // R blocks: smallest channel split that fits
+  size_t r = 0;
+  g.RS = 0;
+  for (int rs = 1; rs <= 8; ++rs) {
+    if (d.E % (8 * rs)) continue;
+    const int Ec = d.E / rs;
+    if (Ec > 2048) continue;
+    size_t q = align16(16 + (size_t)d.P * d.A * esz);
+    const size_t enc = q;
+    q = align16(q + (size_t)d.P * Ec * esz);
+    const size_t rd = q;
+    q = align16(q + 16);
+    const size_t rd2 = q;
+    q = align16(q + PWV * 64 * 4);
+    const size_t ees = q;
+    q = align16(q + 64 * 4);
+    if (q <= LDS_MAX) {
+      g.RS = rs;
+      g.Ec = Ec;
+      g.r_enc = (int)enc;
+      g.r_red = (int)rd;
+      g.r_red2 = (int)rd2;
+      g.r_es = (int)ees;
+      r = q;
+      break;
+    }
+  }
+  if (!g.RS) return false;
+  g.NR = d.B * g.RS;
+  if (g.NUG + g.NR > 256) return false;
+  // at least 81 KB: one workgroup per CU (the visibility form used here is the one measured so)
+  lds = std::max(std::max(ug, r), (size_t)81 * 1024);
+  if (lds > LDS_MAX) return false;
+  words = SYNC_HDR + g.NU + g.NG + g.NR;
+  return true;
+}
+
+template <typename T, int MT>
+static int launch_persist(const imgcap_lstm_desc& d, const Geo& g, size_t lds, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)lstm_fwd_persist_kernel<T, MT>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return fail(IMGCAP_EINVAL, "lstm persistent: cannot raise the dynamic LDS limit");
+    attr = true;
+  }
+  hipLaunchKernelGGL((lstm_fwd_persist_kernel<T, MT>), dim3(g.NUG + g.NR), dim3(PT), lds, st, d, g);
+  IMGCAP_CHECK_LAUNCH("lstm persistent forward");
+  return 0;
+}
+
+// Runs the whole forward recurrence in one launch when the shape fits; *used = false leaves
+// the call to the per-step path.
+int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
+  *used = false;
+  static const int env = [] {
+    const char* e = getenv("IMGCAP_LSTM_PERSIST");
+    return e ? atoi(e) : 1;
+  }();
+  if (!env || d.T < 2 || !d.sync) return 0;
+  const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
+  Geo g;
+  size_t lds;
+  int mt, words;
+  if (!persist_plan(d, esz, g, lds, mt, words)) return 0;
+  static const bool stamps = getenv("IMGCAP_LSTM_STAMPS") && atoi(getenv("IMGCAP_LSTM_STAMPS"));
+  g.stamps = nullptr;
+  if (stamps && d.T <= 64 && d.sync_words >= words + 64 + 2 * 64 * 16 * 2)
+    g.stamps = (long long*)(d.sync + ((words + 63) / 64 * 64 + 64));
+  IMGCAP_REQUIRE(d.sync_words >= words, "lstm persistent: sync workspace too small");
+  IMGCAP_REQUIRE(aligned16(d.sync), "lstm persistent: sync workspace must be 16-byte aligned");
+  // zero the error word and every flag (a memset node when captured)
+  if (hipMemsetAsync(d.sync, 0, align16((size_t)words * 4), st) != hipSuccess)
+    return fail(IMGCAP_EINVAL, "lstm persistent: memset of the sync words failed");
+  *used = true;
+  int rc;
+#define LP_CASE(TT, M_) \
+  if (mt == M_) return launch_persist<TT, M_>(d, g, lds, st);
+  if (esz == 2) {
+    LP_CASE(bf16, 1) LP_CASE(bf16, 2)
+  } else {
+    LP_CASE(float, 1) LP_CASE(float, 2)
+  }
+#undef LP_CASE
+  rc = fail(IMGCAP_EINVAL, "lstm persistent: no instantiation");
+  return rc;
+}
+
+int lstm_persist_sync_words(const imgcap_lstm_desc& d) {
+  Geo g;
+  size_t lds;
+  int mt, words;
+  const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
+  return persist_plan(d, esz, g, lds, mt, words) ? words : 0;
+}
+
+}  // namespace imgcap

@@ -55,6 +55,7 @@ class LstmEngine:
         self.seed = 1234
         self.step_id = 0
         self._y_cnt = None
+        self._sync = None
 
     # K-slices of the backward step GEMMs (imgcap_lstm_desc.x_slices / y_slices).  Measured at
     # the C2 shape (B=32, D=512, tools/gpu/lstm_sweep.sh): x 2 / y 3 (80 x 2 and 32 x 3 blocks)
@@ -77,6 +78,21 @@ class LstmEngine:
                     alphas=T * P * 4, awe=T * E * 4, zs=T * E * c, gates=T * 4 * D * 4, cs=T * D * 4, hs=T * D * c,
                     hprev=T * D * c, dhs=T * D * c, dalpha=T * P * 4, dcat=T * W3 * c, dh=D * 4, dc=D * 4,
                     de=T * P * 4, datt1=P * A * c, dwf=npc * A * 4, dbea=npc * A * 4, dawe=(T + 1) * E * 4)
+
+    def _sync_words(self, d, dev):
+        """Point ``d.sync`` at the engine's hand-off flag words when the persistent forward
+        recurrence covers this shape (imgcap_lstm_sync_words > 0).  Caller-owned, allocated once
+        (grown during warm-up, before any graph capture)."""
+        words = _abi.lib().imgcap_lstm_sync_words(ctypes.byref(d))
+        if words <= 0:
+            return
+        if self._sync is None or self._sync.numel() < words or self._sync.device != dev:
+            self._sync = torch.zeros(max(words, 8192), dtype=torch.int32, device=dev)
+        d.sync, d.sync_words = self._sync.data_ptr(), self._sync.numel()
+
+    def sync_error(self):
+        """Non-zero when the last persistent recurrence gave up on a hand-off (bounded spin)."""
+        return 0 if self._sync is None else int(self._sync[0].item())
 
     def _chain_rows(self, B):
         n = max(1, min(self.CHAINS, B))
@@ -101,6 +117,7 @@ class LstmEngine:
             sd = _abi.LstmDesc()
             ctypes.memmove(ctypes.byref(sd), ctypes.byref(d), ctypes.sizeof(d))
             sd.B = b1 - b0
+            sd.sync, sd.sync_words = None, 0  # concurrent chains: per-step launches
             for f, nb in per.items():
                 v = getattr(sd, f)
                 if v:
@@ -200,6 +217,7 @@ class LstmEngine:
                          xe=xe, c0=c0, dl=dl, g1=g1, alphas=alphas, awe=awe, zs=zs, gates=gates, cs=cs, hs=hs,
                          hprev=hprev).items():
             setattr(d, k, v.data_ptr())
+        self._sync_words(d, dev)
         # k-major copies of the weights the backward recurrence multiplies by, made on a side
         # stream under the forward recurrence (they only depend on the weights)
         main = torch.cuda.current_stream(dev)

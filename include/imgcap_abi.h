@@ -338,9 +338,21 @@ typedef struct imgcap_lstm_desc {
   int32_t y_slices;     /* 1..16 */
   float* dawe;          /* [B, T+1, E] out or NULL: dL/d(attention context) per step (rows t < T;
                            row T is left to the caller) -- the encoder-gradient path */
+  int32_t* sync;        /* caller-owned, 16-byte aligned, at least imgcap_lstm_sync_words() int32
+                           words (NULL: per-step launches only).  fwd: the persistent recurrence's
+                           hand-off flags, zeroed by the library (a memset on the stream) before
+                           each launch; word 0 is left non-zero if a hand-off timed out. */
+  int32_t sync_words;
 } imgcap_lstm_desc;
 
+/* fwd: with d->sync set and T >= 2, the whole recurrence is ONE persistent launch when the
+ * shape fits (B <= 64, P <= 64, A <= 512, E, D, M % 8 == 0; steps t >= max(dl) are skipped and
+ * their outputs zeroed); otherwise three launches per step.  Same outputs either way, except
+ * that g1's hh columns are written by the per-step path only. */
 int imgcap_lstm_tf_fwd(const imgcap_lstm_desc* d, void* stream);
+/* int32 words of imgcap_lstm_desc.sync the persistent forward needs for this shape (0: the
+ * shape runs on the per-step path) */
+int imgcap_lstm_sync_words(const imgcap_lstm_desc* d);
 int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream);
 /* dL/d encoder_out for encoder fine-tuning (the decoder.py:75-113 paths back into encoder_out):
  *   denc[sort_ind[b], p, :] = base[b, p, :] + sum_{t<T} alphas[b,t,p] dawe[b,t,:] + dawe[b,T,:] / P

@@ -134,3 +134,39 @@ def test_lstm_medium_vs_oracle_with_dropout_determinism(hip_device):
     s2 = eng.forward(enc.to(hip_device), caps.to(hip_device), caplens.to(hip_device), fixed_T=True)
     assert torch.equal(s1["metrics"], s2["metrics"])
     assert abs(s1["metrics"][0].item() - loss.item()) > 1e-4
+
+
+@pytest.mark.parametrize("dtype,B", [(torch.float32, 5), (torch.bfloat16, 32), (torch.float32, 24)])
+def test_lstm_persistent_recurrence_matches_per_step(hip_device, dtype, B):
+    """The one-launch forward recurrence (csrc/lstm_persist.hip) against the per-step launches
+    on the same descriptor: every saved buffer for t < max decode length, zeros past it."""
+    import ctypes
+    from imagecaptioningconvnext_amd import _abi
+    from imagecaptioningconvnext_amd import kernels as K
+    E, A, D, Em, V, L = (768, 512, 512, 512, 300, 24) if B == 32 else (64, 32, 48, 32, 100, 14)
+    p = make_params(shapes.lstm_decoder_shapes(E, A, D, Em, V), 5)
+    dec = _decoder(dict(E=E, A=A, D=D, Em=Em, V=V), p, dtype, hip_device)
+    eng = dec.engine()
+    enc = make_features((B, 7, 7, E), 6).to(hip_device).to(dtype)
+    lens = [L - 3 - (i * 7) % (L - 6) for i in range(B)]  # maximum L - 3 < L: skipped tail steps
+    caps, caplens = make_captions(B, L, lens, V, 7)
+    s = eng.forward(enc, caps.to(hip_device), caplens.to(hip_device), fixed_T=True, loss=False)
+    torch.cuda.synchronize()
+    d = s["desc"]
+    assert d.sync and eng.sync_error() == 0
+    names = ("alphas", "awe", "zs", "gates", "cs", "hs", "hprev")
+    got = {k: s[k].clone() for k in names}
+    g1 = s["g1"][..., :A + E].clone()
+    for k in names:
+        (s[k][:, 1:] if k == "hprev" else s[k]).fill_(float("nan"))  # hprev slot 0 = h0 (input)
+    d.sync, d.sync_words = None, 0
+    _abi.call("imgcap_lstm_tf_fwd", ctypes.byref(d), K.stream())
+    torch.cuda.synchronize()
+    T, tm = s["T"], max(lens) - 1
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    for k in names:
+        a, b = got[k].float(), s[k].float()
+        lo = 1 if k == "hprev" else 0  # hprev slot t holds h_{t-1}
+        assert _rel(a[:, :tm + lo], b[:, :tm + lo]) < tol, k
+        assert torch.all(a[:, tm + lo:] == 0), k
+    assert _rel(g1[:, :tm], s["g1"][:, :tm, :A + E]) < tol

@@ -126,6 +126,28 @@ def lstm():
     print(f"lstm fwd recurrence ({eng.CHAINS} chains, eager streams): {te * 1e6:8.1f} us total")
     t = time_launch(lambda: eng._launch("imgcap_lstm_tf_bwd", d, ws), reps=5, warm=2)
     print(f"lstm bwd recurrence: {t * 1e6:8.1f} us total, {t * 1e6 / T:6.2f} us/step")
+    if os.environ.get("IMGCAP_LSTM_STAMPS") == "1" and d.sync:
+        # phase stamps of the persistent forward (lstm_persist.hip, stamp()): 100 MHz ticks
+        eng._launch("imgcap_lstm_tf_fwd", d)
+        torch.cuda.synchronize()
+        words = _abi.lib().imgcap_lstm_sync_words(ctypes.byref(d))
+        off = (words + 63) // 64 * 64 + 64
+        st = eng._sync[off:off + 2 * 64 * 16 * 2].view(torch.int64).view(2, 64, 16).cpu().double() * 10.0  # ns
+        u, r = st[0, 1:T - 1], st[1, 1:T - 1]
+        nxt = st[0, 2:T, 0]
+        names = ["wait h", "G h loads", "G mma+store", "G publish", "wait z (U)", "U z loads", "U mma",
+                 "cell+h store", "h publish", "->next step"]
+        segs = [u[:, 1] - u[:, 0], u[:, 9] - u[:, 1], u[:, 2] - u[:, 9], u[:, 3] - u[:, 2], u[:, 4] - u[:, 3],
+                u[:, 8] - u[:, 4], u[:, 5] - u[:, 8], u[:, 6] - u[:, 5], u[:, 7] - u[:, 6], nxt - u[:, 7]]
+        print("U/G block 0, mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(names, segs)))
+        rn = ["wait g", "g loads", "scores", "softmax", "context+z", "z publish", "->next"]
+        rs = [r[:, 1] - r[:, 0], r[:, 5] - r[:, 1], r[:, 6] - r[:, 5], r[:, 7] - r[:, 6], r[:, 3] - r[:, 7],
+              r[:, 4] - r[:, 3], st[1, 2:T, 0] - r[:, 4]]
+        print("R block 0,     mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(rn, rs)))
+        clk = (st[0, T - 2, 15] - st[0, 1, 15]) / 10.0 / (st[0, T - 2, 0] - st[0, 1, 0]) * 1e3  # MHz
+        print(f"shader clock during the recurrence: {clk:.0f} MHz")
+        print("cross: G published -> R got g %.0f ns; R published -> U got z %.0f ns; U published -> U got h %.0f" % (
+            (r[:, 1] - u[:, 3]).mean(), (u[:, 4] - r[:, 4]).mean(), (st[0, 2:T, 1] - u[:, 7]).mean()))
 
 
 def misc():
