@@ -56,6 +56,7 @@ class LstmEngine:
         self.step_id = 0
         self._y_cnt = None
         self._sync = None
+        self._chain_sync = []
 
     # K-slices of the backward step GEMMs (imgcap_lstm_desc.x_slices / y_slices).  Measured at
     # the C2 shape (B=32, D=512, tools/gpu/lstm_sweep.sh): x 2 / y 3 (80 x 2 and 32 x 3 blocks)
@@ -67,6 +68,8 @@ class LstmEngine:
     # graph-capturable).  Measured on MI355X (tools/microbench.py lstm): two chains take 1.85x
     # the time of one -- the step kernels of concurrent streams do not overlap (also with 8 or
     # 16 hardware queues) -- so the default is one chain; kept as a switch (IMGCAP_LSTM_CHAINS).
+    # With the persistent forward (one launch per chain, own flag words) two chains are also
+    # serialised: 1.80 ms vs 0.96 ms for one (tools/gpu/lp2.sh).
     CHAINS = int(os.environ.get("IMGCAP_LSTM_CHAINS", "1"))
 
     def _per_row_bytes(self, T, P):
@@ -117,11 +120,18 @@ class LstmEngine:
             sd = _abi.LstmDesc()
             ctypes.memmove(ctypes.byref(sd), ctypes.byref(d), ctypes.sizeof(d))
             sd.B = b1 - b0
-            sd.sync, sd.sync_words = None, 0  # concurrent chains: per-step launches
             for f, nb in per.items():
                 v = getattr(sd, f)
                 if v:
                     setattr(sd, f, v + b0 * nb)
+            sd.sync, sd.sync_words = None, 0
+            if d.sync:  # persistent recurrence per chain: each chain its own flag words
+                words = _abi.lib().imgcap_lstm_sync_words(ctypes.byref(sd))
+                if words > 0:
+                    if len(self._chain_sync) <= i or self._chain_sync[i].device != main.device:
+                        self._chain_sync = self._chain_sync[:i] + [torch.zeros(8192, dtype=torch.int32,
+                                                                               device=main.device)]
+                    sd.sync, sd.sync_words = self._chain_sync[i].data_ptr(), 8192
             if ws:
                 for k, v in ws[i].items():
                     setattr(sd, k, v.data_ptr())

@@ -84,44 +84,70 @@ def _ln2d(x, w, b):  # LayerNorm2d on NCHW: normalise over C at each pixel, eps 
     return F.layer_norm(x.permute(0, 2, 3, 1), (x.shape[1],), w, b, 1e-6).permute(0, 3, 1, 2)
 
 
-def features_forward(sd, variant, images, sd_keep=None):
+def _rb(t):  # round to bf16 and back (the HIP path stores activations / MFMA operands in bf16)
+    return t.bfloat16().float()
+
+
+def _id(t):
+    return t
+
+
+def features_forward(sd, variant, images, sd_keep=None, numerics="fp32", mx_children=()):
     """Encoder.convnext(images) (encoder.py:24).  ``images`` NCHW float; returns NCHW.
 
     ``sd_keep``: optional list (one per CNBlock) of per-sample scale vectors [B] applied to
     the residual branch (StochasticDepth "row" mode: keep/(1-p)); None = eval (identity).
+
+    ``numerics`` (the build's arithmetic, for tighter parity gates than fp32-vs-bf16):
+      "fp32": torchvision's fp32 semantics (the reference).
+      "bf16": the HIP bf16 path's rounding points -- stem output, depthwise output, LayerNorm
+              output (a GEMM operand), GELU hidden, block output, downsample LayerNorm output and
+              result rounded to bf16; Linear / downsample weights bf16; stem and depthwise
+              weights, biases, LayerNorm parameters, layer scale fp32; fp32 accumulation.
+      "mx":   "bf16", and the CNBlocks of ``mx_children`` (feature indices 1/3/5/7) whose
+              width qualifies (C % 128 == 0 and not a fused-MLP width 96/128/192) run the
+              MX-FP8 path: LayerNorm output, both Linear weights and the GELU hidden are
+              quantised per 32 along K (oracle/mx.py) instead of rounded to bf16.
     """
+    from . import mx as mxq
+    r = _id if numerics == "fp32" else _rb
     chans, depths, _ = VARIANTS[variant]
     x = F.conv2d(images, sd["convnext.0.0.weight"], sd["convnext.0.0.bias"], stride=4)
-    x = _ln2d(x, sd["convnext.0.1.weight"], sd["convnext.0.1.bias"])
+    x = r(_ln2d(x, sd["convnext.0.1.weight"], sd["convnext.0.1.bias"]))
     blk = 0
     for st in range(4):
         C = chans[st]
         idx = 1 + 2 * st
+        use_mx = numerics == "mx" and idx in mx_children and C % 128 == 0 and C not in (96, 128, 192)
+        q = mxq.qdq if use_mx else r
         for j in range(depths[st]):
             p = f"convnext.{idx}.{j}."
-            y = F.conv2d(x, sd[p + "block.0.weight"], sd[p + "block.0.bias"], padding=3, groups=C)
+            y = r(F.conv2d(x, sd[p + "block.0.weight"], sd[p + "block.0.bias"], padding=3, groups=C))
             y = y.permute(0, 2, 3, 1)
-            y = F.layer_norm(y, (C,), sd[p + "block.2.weight"], sd[p + "block.2.bias"], 1e-6)
-            y = F.linear(y, sd[p + "block.3.weight"], sd[p + "block.3.bias"])
-            y = F.gelu(y)
-            y = F.linear(y, sd[p + "block.5.weight"], sd[p + "block.5.bias"])
+            y = q(F.layer_norm(y, (C,), sd[p + "block.2.weight"], sd[p + "block.2.bias"], 1e-6))
+            y = F.linear(y, q(sd[p + "block.3.weight"]), sd[p + "block.3.bias"])
+            y = q(F.gelu(y))
+            y = F.linear(y, q(sd[p + "block.5.weight"]), sd[p + "block.5.bias"])
             y = y.permute(0, 3, 1, 2)
             y = sd[p + "layer_scale"] * y
             if sd_keep is not None:
                 y = y * sd_keep[blk].view(-1, 1, 1, 1).to(y.dtype)
-            x = x + y
+            x = r(x + y)
             blk += 1
         if st < 3:
             d = 2 + 2 * st
-            x = _ln2d(x, sd[f"convnext.{d}.0.weight"], sd[f"convnext.{d}.0.bias"])
-            x = F.conv2d(x, sd[f"convnext.{d}.1.weight"], sd[f"convnext.{d}.1.bias"], stride=2)
+            x = r(_ln2d(x, sd[f"convnext.{d}.0.weight"], sd[f"convnext.{d}.0.bias"]))
+            x = r(F.conv2d(x, r(sd[f"convnext.{d}.1.weight"]), sd[f"convnext.{d}.1.bias"], stride=2))
     return x
 
 
-def encoder_forward(sd, variant, images, encoded_image_size=7, sd_keep=None):
+def encoder_forward(sd, variant, images, encoded_image_size=7, sd_keep=None, numerics="fp32", mx_children=()):
     """Encoder.forward (encoder.py:23-27): features -> AdaptiveAvgPool2d(7) -> NHWC."""
-    x = features_forward(sd, variant, images, sd_keep)
-    x = F.adaptive_avg_pool2d(x, (encoded_image_size, encoded_image_size))
+    x = features_forward(sd, variant, images, sd_keep, numerics, mx_children)
+    if x.shape[2] != encoded_image_size or x.shape[3] != encoded_image_size:
+        x = F.adaptive_avg_pool2d(x, (encoded_image_size, encoded_image_size))
+        if numerics != "fp32":
+            x = _rb(x)
     return x.permute(0, 2, 3, 1)
 
 

@@ -13,21 +13,39 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 3e-2)])
-@pytest.mark.parametrize("hw", [224, 256])
-def test_encoder_tiny_vs_oracle(hip_device, dtype, tol, hw):
+# bf16 path vs the bf16-emulating oracle (same rounding points, fp32 accumulation): what is
+# left are single-ulp rounding flips (accumulation order) carried through 18-36 blocks.
+# Measured on MI355X: 2.8e-3 (tiny 256) .. 4.9e-3 (large); vs plain fp32 3.1e-3 .. 5.4e-3
+BF16_EMU_TOL = 1e-2
+
+
+@pytest.mark.parametrize("variant,hw", [("tiny", 224), ("tiny", 256), ("base", 224), ("large", 224)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_encoder_vs_oracle(hip_device, variant, hw, dtype):
+    """Tiny (C2/C3), Base (C4, the reference's own variant, encoder.py:18) and Large (C5) trunks
+    + adaptive pool vs the oracle: fp32 path <= 1e-4 of torchvision fp32 semantics; bf16 path
+    <= 1e-2 of the bf16-emulating oracle and <= 1.5e-2 of fp32."""
     from imagecaptioningconvnext_amd.models.encoder import Encoder
-    sd = make_params(convnext.param_shapes("tiny"), 5)
-    enc = Encoder(variant="tiny", compute_dtype=dtype)
+    from oracle.convnext import VARIANTS
+    sd = make_params(convnext.param_shapes(variant), 5)
+    enc = Encoder(variant=variant, compute_dtype=dtype)
     enc.load_state_dict(sd)
     enc = enc.to(hip_device).eval()
     g = torch.Generator().manual_seed(6)
     img = torch.randn(2, 3, hw, hw, generator=g)
     with torch.no_grad():
         out = enc(img.to(hip_device))
-        ref = convnext.encoder_forward(sd, "tiny", img)
-    assert out.shape == ref.shape == (2, 7, 7, 768)
-    assert _rel(out, ref) < tol
+        ref = convnext.encoder_forward(sd, variant, img)
+    E = VARIANTS[variant][0][3]
+    assert out.shape == ref.shape == (2, 7, 7, E)
+    if dtype == torch.float32:
+        assert _rel(out, ref) < 1e-4
+    else:
+        emu = convnext.encoder_forward(sd, variant, img, numerics="bf16")
+        err = _rel(out, emu)
+        print(f"{variant} {hw} bf16 vs bf16-emulating oracle {err:.2e}, vs fp32 {_rel(out, ref):.2e}")
+        assert err < BF16_EMU_TOL
+        assert _rel(out, ref) < 1.5e-2
 
 
 def test_encoder_stochastic_depth_train_mode(hip_device):

@@ -125,10 +125,10 @@ def test_layer_scale_grad(hip_device):
 
 
 # ---- encoder with a trainable suffix ------------------------------------------------------
-def _oracle_grads(sd, img, R, start, sd_keep=None):
+def _oracle_grads(sd, img, R, start, sd_keep=None, variant="tiny"):
     children = {f"convnext.{i}." for i in range(start, 8)}
     p = {k: v.clone().requires_grad_(any(k.startswith(c) for c in children)) for k, v in sd.items()}
-    out = convnext.encoder_forward(p, "tiny", img, sd_keep=sd_keep)
+    out = convnext.encoder_forward(p, variant, img, sd_keep=sd_keep)
     (out * R).sum().backward()
     return out.detach(), {k: v.grad for k, v in p.items() if v.requires_grad}
 
@@ -153,6 +153,32 @@ def test_encoder_finetune_grads_vs_oracle(hip_device, start, dtype, tol):
     assert set(ref_g) == {n for n, p in got.items() if p.requires_grad}
     for n, g in ref_g.items():
         assert _rel(got[n].grad, g) < tol, n
+
+
+@pytest.mark.parametrize("variant,start", [("base", 7), ("base", 5), ("large", 7)])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-4), (torch.bfloat16, 4e-2)])
+def test_encoder_finetune_grads_base_large(hip_device, variant, start, dtype, tol):
+    """Base (C4 / the reference's encoder.py:18) and Large (C5) with trainable suffixes: output
+    and every trainable gradient vs the oracle's autograd."""
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    from oracle.convnext import VARIANTS
+    sd = make_params(convnext.param_shapes(variant), 17)
+    enc = Encoder(variant=variant, compute_dtype=dtype)
+    enc.load_state_dict(sd)
+    enc = enc.to(hip_device).eval()
+    enc.fine_tune(True, startingLayer=start)
+    img = torch.randn(2, 3, 224, 224, generator=_g(18))
+    R = torch.randn(2, 7, 7, VARIANTS[variant][0][3], generator=_g(19))
+    ref_out, ref_g = _oracle_grads(sd, img, R, start, variant=variant)
+    out = enc(img.to(hip_device))
+    assert _rel(out, ref_out) < tol
+    (out.float() * R.to(hip_device)).sum().backward()
+    got = dict(enc.named_parameters())
+    assert set(ref_g) == {n for n, p in got.items() if p.requires_grad}
+    errs = {n: _rel(got[n].grad, g) for n, g in ref_g.items()}
+    worst = max(errs, key=errs.get)
+    print(f"{variant} start {start} {dtype}: worst grad {worst} {errs[worst]:.2e}")
+    assert errs[worst] < tol
 
 
 def test_encoder_finetune_train_mode_stochastic_depth(hip_device):
@@ -243,3 +269,65 @@ def test_trainer_finetune_step_vs_oracle(hip_device, decoder):
             err = (named[k].detach().cpu() - v)[live].abs().max().item()
             # Adam's first step moves each entry by ~lr * sign(g): compare the update, not the value
             assert err <= 0.05 * max(moved, lr) + 1e-6, (k, err, moved)
+
+
+# ---- C5: ConvNeXt-Large, MX-FP8 frozen prefix, stage 4 fine-tuned ------------------------
+def test_c5_large_fp8_finetune_vs_emulating_oracle(hip_device):
+    """BASELINE configs[4] (C5) at B = 2: Large encoder with frozen_fp8 (children 1-6 of the
+    trunk with MX-FP8 Linears where C >= 384), fine_tune(True, 7) (stage 4 trains in bf16),
+    a Transformer decoder on top.  Features, loss and the stage-4 gradients vs the oracle that
+    emulates the same numerics (MX quantise-dequantise in the frozen stages, bf16 rounding
+    elsewhere), then one fused TeacherForcedTrainer step: its loss vs the same oracle."""
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    dev = hip_device
+    E, V, L, B, d = 1536, 150, 14, 2, 128  # head dim 64 (the HIP attention kernel's)
+    esd = make_params(convnext.param_shapes("large"), 61)
+    enc = Encoder(variant="large", frozen_fp8=True)
+    enc.load_state_dict(esd)
+    for m in enc.modules():  # eval-equivalent drop path so the oracle needs no masks
+        if hasattr(m, "sd_prob"):
+            m.sd_prob = 0.0
+    enc = enc.to(dev)
+    enc.fine_tune(True, startingLayer=7)
+    dp = make_params(shapes.transformer_decoder_shapes(E, d, d, V, 2), 62)
+    dec = TransformerDecoder(embed_dim=d, decoder_dim=d, vocab_size=V, maxLen=L, device=dev, wordMap=None,
+                             pretrained_embeddings_path=None, fine_tune_embeddings=True, dropout=0.0,
+                             encoder_dim=E, num_heads=2, num_layers=2, compute_dtype=torch.float32)
+    dp["pos_encoding.pe"] = dec.pos_encoding.pe.clone()
+    dec.load_state_dict(dp)
+    dec = dec.to(dev)
+    caps, caplens = make_captions(B, L, [L, 9], V, 63)
+    img = torch.randn(B, 3, 224, 224, generator=_g(64))
+    # oracle: MX prefix (children 1, 3, 5 hold the qualifying stages), bf16 stage 4, fp32 decoder
+    ep = {k: v.clone().requires_grad_(k.startswith("convnext.7.")) for k, v in esd.items()}
+    feats = convnext.encoder_forward(ep, "large", img, numerics="mx", mx_children=(1, 3, 5))
+    dq = {k: v.clone() for k, v in dp.items()}
+    pad = caps == 0
+    preds, cs, dls = decoders.transformer_tf_forward(dq, feats, caps, caplens, pad, 2, 2)
+    loss, _, _ = train_step.transformer_loss(preds, cs, dls)
+    loss.backward()
+    # HIP: differentiable encoder (EncoderEngine) + the decoder module
+    out = enc(img.to(dev))
+    f_err = _rel(out, feats)
+    p_out, _, _ = dec(True, out.float(), caps.to(dev), caplens.to(dev), pad.to(dev))
+    g_loss, _, _ = train_step.transformer_loss(p_out, caps.to(dev), dls)
+    g_loss.backward()
+    named = dict(enc.named_parameters())
+    g_errs = {k: _rel(named[k].grad, v.grad) for k, v in ep.items() if v.requires_grad}
+    worst = max(g_errs, key=g_errs.get)
+    print(f"C5: features rel {f_err:.2e}, loss rel {abs(g_loss.item() / loss.item() - 1):.2e}, "
+          f"worst stage-4 grad {worst} {g_errs[worst]:.2e}")
+    assert f_err < 2.5e-2
+    assert abs(g_loss.item() - loss.item()) < 1e-2 * abs(loss.item())
+    assert g_errs[worst] < 5e-2
+    # the fused step (MX prefix, bf16 stage-4 forward/backward, encoder Adam at encoderLr)
+    for p_ in list(enc.parameters()) + list(dec.parameters()):
+        p_.grad = None
+    tr = TeacherForcedTrainer(enc, dec, lstm=False, decoder_lr=1e-4, encoder_lr=1e-4)
+    assert tr.enc_eng is not None
+    tr.step(img.to(dev), caps.to(dev), caplens.to(dev))
+    (t_loss, t_tok, _), = tr.drain_metrics()
+    assert t_tok == sum(dls)
+    assert abs(t_loss - loss.item()) < 1e-2 * abs(loss.item())

@@ -70,7 +70,15 @@ def test_lstm_small_fused_step(hip_device, dtype, tol):
     m = s["metrics"].cpu()
     assert abs(m[0].item() - t["loss"].item()) < tol * abs(t["loss"].item())
     assert int(m[1].item()) == sum(meta["decode_lengths"])
-    assert abs(m[2].item() / m[1].item() * 100 - t["ref_step_top5"].item()) < (1e-4 if dtype == torch.float32 else 25)
+    if dtype == torch.float32:
+        assert abs(m[2].item() / m[1].item() * 100 - t["ref_step_top5"].item()) < 1e-4
+    # the fused top-5 count is exact for the logits the kernel saw: target's rank among strictly
+    # greater logits < 5 (utils.py:248-250 topk), recomputed here from the engine's own logits
+    lg = s["logits"][:, :cfg["V"]].float()
+    tg = s["targets"]
+    ok = tg >= 0
+    tl = lg[ok].gather(1, tg[ok].view(-1, 1))
+    assert int(m[2].item()) == int(((lg[ok] > tl).sum(1) < 5).sum().item())
     eng.backward(s)
     for n in eng.fp.params:
         if n == "attention.full_att.bias":
@@ -100,8 +108,10 @@ def test_lstm_full_size_spot(hip_device, dtype, tol):
     loss, scores, _ = train_step.lstm_loss(preds.cpu(), cs.cpu(), dls, al.cpu())
     assert abs(loss.item() - t["loss"].item()) < tol * abs(t["loss"].item())
     got = scores[t["rows"], t["cols"]]
-    assert _rel(got, t["values"]) < tol * 5
-    assert _rel(al, t["alphas"]) < tol * 5
+    print(f"lstm full size {dtype}: loss rel {abs(loss.item() / t['loss'].item() - 1):.2e}, "
+          f"logits rel {_rel(got, t['values']):.2e}, alphas rel {_rel(al, t['alphas']):.2e}")
+    assert _rel(got, t["values"]) < (1e-4 if dtype == torch.float32 else 1e-2)
+    assert _rel(al, t["alphas"]) < (1e-4 if dtype == torch.float32 else 1e-2)
 
 
 def test_lstm_medium_vs_oracle_with_dropout_determinism(hip_device):

@@ -1,0 +1,114 @@
+"""The fused train step (TeacherForcedTrainer, train.py:240-302) in fp32 at the real per-GPU
+batch sizes of C2 (LSTM, B = 32) and C3 (Transformer, B = 64) with full decoder dims and
+captions of TIED lengths (the length sort of decoder.py:79 must keep every row with its own
+caption; rows are compared per original sample), vs the CPU oracle: loss, top-5, logits (<= 1e-3 relative, the north-star bar) and post-Adam
+parameters.  The encoder is a pass-through (the batch is encoder features), as in the
+reference's own DDP golden (tests/ddp_util.py)."""
+import pytest
+import torch
+
+from golden_util import make_captions, make_features, make_params
+from oracle import decoders, shapes, train_step
+
+pytestmark = pytest.mark.gpu
+
+V, L, E = 1200, 52, 768
+
+
+class PassThrough(torch.nn.Module):
+    def forward(self, x):
+        return x
+
+
+def _rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _tied_lengths(B, seed):
+    g = torch.Generator().manual_seed(seed)
+    pool = torch.tensor([L, L, 40, 40, 40, 23, 23, 17, 17, 17, 9])
+    return pool[torch.randint(0, len(pool), (B,), generator=g)].tolist()
+
+
+def _check_post_adam(named, p0, grads, lr):
+    """Adam's first step moves an entry by lr * g / (|g| + eps): exactly sign(g) * lr unless g is
+    at round-off level, where only the 2 * lr bound means anything."""
+    new = train_step.adam_step({k: p0[k] for k in grads}, train_step.clip_gradient(grads, 5.0), {}, lr, 1)
+    for k, want in new.items():
+        got = named[k].detach().float().cpu()
+        sure = grads[k].abs() > 1e-5
+        if sure.any():
+            assert (got - want)[sure].abs().max().item() <= 1e-3 * lr + 1e-7, k
+        assert (got - want).abs().max().item() <= 2 * lr * 1.0001, k
+
+
+def test_lstm_trainer_b32_tied_lengths_vs_oracle(hip_device):
+    from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    B = 32
+    p = make_params(shapes.lstm_decoder_shapes(E, 512, 512, 512, V), 41)
+    feats = make_features((B, 7, 7, E), 42)
+    lens = _tied_lengths(B, 43)
+    caps, caplens = make_captions(B, L, lens, V, 44)
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    preds, cs, dls, al, sort_ind = decoders.lstm_tf_forward(pr, feats, caps, caplens)
+    loss, scores, targets = train_step.lstm_loss(preds, cs, dls, al)
+    loss.backward()
+    top5 = train_step.top5_correct(scores, targets) / len(targets) * 100
+    dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=hip_device,
+                               encoder_dim=E, dropout=0.0, compute_dtype=torch.float32)
+    dec.load_state_dict(p)
+    dec = dec.to(hip_device)
+    with torch.no_grad():  # module API: sort order and logits
+        gp, gcs, gdls, gal, gsi = dec(True, feats.to(hip_device), caps.to(hip_device), caplens.to(hip_device))
+    # decoder.py:79 sorts with torch's default (unstable) sort, whose order among tied lengths is
+    # implementation-defined (CPU and CUDA differ); the HIP sort is stable.  Both must order by
+    # length; rows are then compared per original sample.
+    gsi = gsi.cpu()
+    assert gdls == dls and torch.equal(caplens.view(-1)[gsi], caplens.view(-1)[sort_ind])
+    assert torch.equal(gsi, torch.sort(caplens.view(-1), descending=True, stable=True).indices)
+    pos_h, pos_o = torch.empty_like(gsi), torch.empty_like(sort_ind)
+    pos_h[gsi] = torch.arange(B)
+    pos_o[sort_ind] = torch.arange(B)
+    assert torch.equal(gcs.cpu()[pos_h], cs[pos_o])
+    assert _rel(gp.cpu()[pos_h], preds[pos_o]) < 1e-3 and _rel(gal.cpu()[pos_h], al[pos_o]) < 1e-3
+    tr = TeacherForcedTrainer(PassThrough(), dec, lstm=True, decoder_lr=1e-4, grad_clip=5.0)
+    tr.step(feats.to(hip_device), caps.to(hip_device), caplens.to(hip_device))
+    (g_loss, g_tok, g_top5), = tr.drain_metrics()
+    assert abs(g_loss - loss.item()) <= 1e-4 * loss.item()
+    assert g_tok == sum(dls) and abs(g_top5 - top5) < 1e-6
+    _check_post_adam(dict(dec.named_parameters()), p, {k: v.grad for k, v in pr.items()}, 1e-4)
+
+
+def test_transformer_trainer_b64_tied_lengths_vs_oracle(hip_device):
+    from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    B, d, ff, layers, H = 64, 512, 512, 6, 8
+    p = make_params(shapes.transformer_decoder_shapes(E, d, ff, V, layers), 51)
+    feats = make_features((B, 7, 7, E), 52)
+    lens = _tied_lengths(B, 53)
+    caps, caplens = make_captions(B, L, lens, V, 54)
+    dec = TransformerDecoder(embed_dim=d, decoder_dim=d, vocab_size=V, maxLen=L, device=hip_device, wordMap=None,
+                             pretrained_embeddings_path=None, fine_tune_embeddings=True, dropout=0.0, encoder_dim=E,
+                             num_heads=H, num_layers=layers, compute_dtype=torch.float32)
+    p["pos_encoding.pe"] = dec.pos_encoding.pe.clone()
+    dec.load_state_dict(p)
+    dec = dec.to(hip_device)
+    pr = {k: v.clone().requires_grad_(k != "pos_encoding.pe") for k, v in p.items()}
+    pad = caps == 0
+    preds, cs, dls = decoders.transformer_tf_forward(pr, feats, caps, caplens, pad, H, layers)
+    loss, scores, targets = train_step.transformer_loss(preds, cs, dls)
+    loss.backward()
+    top5 = train_step.top5_correct(scores, targets) / len(targets) * 100
+    with torch.no_grad():
+        gp, gcs, gdls = dec(True, feats.to(hip_device), caps.to(hip_device), caplens.to(hip_device),
+                            pad.to(hip_device))
+    assert gdls == dls and _rel(gp, preds) < 1e-3
+    tr = TeacherForcedTrainer(PassThrough(), dec, lstm=False, decoder_lr=1e-4, grad_clip=5.0)
+    tr.step(feats.to(hip_device), caps.to(hip_device), caplens.to(hip_device))
+    (g_loss, g_tok, g_top5), = tr.drain_metrics()
+    assert abs(g_loss - loss.item()) <= 1e-4 * loss.item()
+    assert g_tok == sum(dls) and abs(g_top5 - top5) < 1e-6
+    grads = {k: v.grad for k, v in pr.items() if v.requires_grad}
+    _check_post_adam(dict(dec.named_parameters()), p, grads, 1e-4)

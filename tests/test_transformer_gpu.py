@@ -152,7 +152,9 @@ def test_transformer_full_size_spot(hip_device, dtype, tol):
         preds, cs, dls = dec(True, enc, caps.to(hip_device), caplens.to(hip_device), caps.to(hip_device) == 0)
     loss, scores, _ = train_step.transformer_loss(preds.cpu(), cs.cpu(), dls)
     assert abs(loss.item() - t["loss"].item()) < tol * abs(t["loss"].item())
-    assert _rel(scores[t["rows"], t["cols"]], t["values"]) < tol * 5
+    print(f"transformer full size {dtype}: loss rel {abs(loss.item() / t['loss'].item() - 1):.2e}, "
+          f"logits rel {_rel(scores[t['rows'], t['cols']], t['values']):.2e}")
+    assert _rel(scores[t["rows"], t["cols"]], t["values"]) < (1e-4 if dtype == torch.float32 else 1e-2)
 
 
 def test_transformer_medium_vs_oracle_and_dropout(hip_device):
