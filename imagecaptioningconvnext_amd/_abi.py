@@ -116,6 +116,8 @@ _SIGS = {
     "imgcap_lstm_denc": [c_int] * 4 + [c_void_p] * 6,
     "imgcap_gemm_set_policy": [c_int],
     "imgcap_workspace_slot": [c_int],
+    "imgcap_workspace_attach": [c_int, c_void_p, c_uint64],
+    "imgcap_workspace_needed": [c_int, ctypes.POINTER(c_uint64)],
     "imgcap_colsum_multi": [c_int, c_void_p, c_void_p],
     "imgcap_gemm_grouped": [c_int, c_int, c_int, c_void_p, c_void_p],
     "imgcap_gemm_mx": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
@@ -152,8 +154,45 @@ def exported_symbols():
     return ["imgcap_last_error_string"] + list(_SIGS)
 
 
+IMGCAP_EWORKSPACE = -3
+# caller-owned split-reduction scratch (imgcap_workspace_attach): {(device, slot): uint8 tensor}
+# from the PyTorch caching allocator; superseded buffers stay referenced (a captured graph may
+# still point at them)
+_ws = {}
+_ws_old = []
+_WS_INITIAL = 32 << 20
+
+
+def _attach(dev, slot, nbytes):
+    import torch
+    nbytes = (int(nbytes) + (1 << 20) - 1) >> 20 << 20
+    t = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", dev))
+    if (dev, slot) in _ws:
+        _ws_old.append(_ws[(dev, slot)])
+    _ws[(dev, slot)] = t
+    rc = lib().imgcap_workspace_attach(slot, t.data_ptr(), nbytes)
+    if rc != 0:
+        raise RuntimeError("imgcap_workspace_attach: " + lib().imgcap_last_error_string().decode(errors="replace"))
+
+
+def _grow_workspaces(dev):
+    need = c_uint64(0)
+    for slot in (0, 1):
+        lib().imgcap_workspace_needed(slot, ctypes.byref(need))
+        if need.value > _ws[(dev, slot)].numel():
+            _attach(dev, slot, need.value * 5 // 4)
+
+
 def call(name, *args):
+    import torch
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+    if dev is not None and (dev, 0) not in _ws:
+        _attach(dev, 0, _WS_INITIAL)
+        _attach(dev, 1, _WS_INITIAL)
     rc = getattr(lib(), name)(*args)
+    if rc == IMGCAP_EWORKSPACE and dev is not None:  # nothing was enqueued: grow, then retry once
+        _grow_workspaces(dev)
+        rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().imgcap_last_error_string().decode(errors="replace")
         raise RuntimeError(f"{name} failed (rc={rc}): {msg}")

@@ -12,23 +12,31 @@
 namespace imgcap {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
+std::string last_error() { return g_last_error; }
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
 }
 const uint64_t* g_seed_ctr = nullptr;
 
-// Scratch for split reductions (GEMM split-K partials, colsum / LayerNorm-gradient slices).
-// Two slots: work that may run concurrently on another stream (the trainer's encoder beside
-// the decoder) selects slot 1 with imgcap_workspace_slot; kernels of one slot run one after
-// another.  Grow-only (a captured HIP graph may reference a buffer, and no allocation may
-// happen during capture: warm-up runs size them), a grown buffer never frees the old one.
+// Scratch for split reductions (GEMM split-K partials, colsum / LayerNorm-gradient slices),
+// per device and per slot.  Two slots: work that may run concurrently on another stream (the
+// trainer's encoder beside the decoder) selects slot 1 with imgcap_workspace_slot; kernels of
+// one slot run one after another.  The caller attaches its own buffer per (device, slot) with
+// imgcap_workspace_attach (the Python side does, from the PyTorch caching allocator); a request
+// larger than the attached buffer fails with IMGCAP_EWORKSPACE before anything is launched, and
+// imgcap_workspace_needed reports the size to attach.  Only a (device, slot) the caller never
+// attached falls back to a library-owned, grow-only allocation (a grown buffer is not freed: a
+// captured HIP graph may still reference it).
+constexpr int MAX_DEV = 64;
 struct Ws {
   void* p = nullptr;
   size_t bytes = 0;
+  size_t needed = 0;
+  bool caller = false;
 };
 static std::mutex g_ws_mu;
-static Ws g_ws[2];
+static Ws g_ws[MAX_DEV][2];
 static std::vector<void*> g_ws_retired;
 static thread_local int g_ws_slot = 0;
 int set_workspace_slot(int slot) {
@@ -36,17 +44,44 @@ int set_workspace_slot(int slot) {
   g_ws_slot = slot;
   return prev;
 }
+static Ws* ws_entry(int slot) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return nullptr;
+  return &g_ws[dev][slot];
+}
 void* workspace(size_t bytes, hipStream_t) {
   std::lock_guard<std::mutex> lk(g_ws_mu);
-  Ws& w = g_ws[g_ws_slot];
-  if (bytes <= w.bytes) return w.p;
+  Ws* w = ws_entry(g_ws_slot);
+  if (!w) return nullptr;
+  w->needed = std::max(w->needed, bytes);
+  if (bytes <= w->bytes) return w->p;
+  if (w->caller) {
+    set_error("library workspace: " + std::to_string(bytes) + " bytes needed in slot " + std::to_string(g_ws_slot) +
+              ", " + std::to_string(w->bytes) + " attached (imgcap_workspace_needed / imgcap_workspace_attach)");
+    return nullptr;
+  }
   size_t sz = std::max(bytes, (size_t)16 << 20);
   void* p = nullptr;
   if (hipMalloc(&p, sz) != hipSuccess) return nullptr;
-  if (w.p) g_ws_retired.push_back(w.p);
-  w.p = p;
-  w.bytes = sz;
+  if (w->p) g_ws_retired.push_back(w->p);
+  w->p = p;
+  w->bytes = sz;
   return p;
+}
+int attach_workspace(int slot, void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  Ws* w = ws_entry(slot);
+  if (!w) return fail(IMGCAP_EINVAL, "imgcap_workspace_attach: no current device");
+  if (w->p && !w->caller) g_ws_retired.push_back(w->p);  // a library buffer may be in a captured graph
+  w->p = p;
+  w->bytes = p ? bytes : 0;
+  w->caller = p != nullptr;
+  return IMGCAP_OK;
+}
+size_t workspace_needed(int slot) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  Ws* w = ws_entry(slot);
+  return w ? w->needed : 0;
 }
 }  // namespace imgcap
 
@@ -57,6 +92,18 @@ extern "C" int imgcap_set_seed_counter(const uint64_t* counter) {
 
 extern "C" const char* imgcap_last_error_string(void) { return imgcap::g_last_error.c_str(); }
 extern "C" int imgcap_version(void) { return 1; }
+
+extern "C" int imgcap_workspace_attach(int slot, void* ptr, uint64_t bytes) {
+  if (slot < 0 || slot > 1) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_attach: slot 0 or 1");
+  if (ptr && ((uintptr_t)ptr & 255)) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_attach: 256-byte alignment");
+  return imgcap::attach_workspace(slot, ptr, (size_t)bytes);
+}
+
+extern "C" int imgcap_workspace_needed(int slot, uint64_t* bytes) {
+  if (slot < 0 || slot > 1 || !bytes) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_needed: slot 0 or 1");
+  *bytes = imgcap::workspace_needed(slot);
+  return IMGCAP_OK;
+}
 
 extern "C" int imgcap_workspace_slot(int slot) {
   if (slot < 0 || slot > 1) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_slot: 0 or 1");

@@ -21,9 +21,12 @@ namespace imgcap {
 // ---- error plumbing (host) -------------------------------------------------------------
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
-// device scratch of at least `bytes` from the calling thread's current slot (NULL on
-// allocation failure); abi.cpp
+// device scratch of at least `bytes` from the calling thread's current slot on the current
+// device (NULL when the caller-attached buffer is too small or an allocation fails; callers
+// return IMGCAP_EWORKSPACE before launching anything, so the call can simply be retried after
+// imgcap_workspace_attach); abi.cpp
 void* workspace(size_t bytes, hipStream_t stream);
+std::string last_error();
 
 #define IMGCAP_CHECK_LAUNCH(what)                                                   \
   do {                                                                             \

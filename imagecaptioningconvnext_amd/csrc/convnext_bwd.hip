@@ -303,7 +303,7 @@ extern "C" int imgcap_dwconv7_wgrad(int dtype, int B, int H, int W, int C, const
   const int rpw = (int)((R + waves_wanted - 1) / waves_wanted);
   const int slices = (int)((R + 4L * rpw - 1) / (4L * rpw));
   float* ws = (float*)workspace((size_t)slices * C * 50 * sizeof(float), (hipStream_t)stream);
-  if (!ws) return fail(IMGCAP_EINVAL, "imgcap_dwconv7_wgrad: workspace allocation failed");
+  if (!ws) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_dwconv7_wgrad: ") + last_error());
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid(cblocks, slices);
   if (dtype == IMGCAP_BF16)
@@ -361,7 +361,7 @@ extern "C" int imgcap_ln_patchify2_bwd(int dtype, int B, int H, int W, int C, co
   const int ppw = (int)std::max<long>(1, (NPX + 4 * 512 - 1) / (4 * 512));
   const int blocks = (int)((NPX + 4L * ppw - 1) / (4L * ppw));
   float* ws = (float*)workspace((size_t)blocks * 2 * C * sizeof(float), (hipStream_t)stream);
-  if (!ws) return fail(IMGCAP_EINVAL, "imgcap_ln_patchify2_bwd: workspace allocation failed");
+  if (!ws) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_ln_patchify2_bwd: ") + last_error());
   hipStream_t st = (hipStream_t)stream;
   const size_t shm = (size_t)8 * C * sizeof(float);
   if (dtype == IMGCAP_BF16)

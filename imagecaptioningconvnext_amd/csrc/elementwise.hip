@@ -60,18 +60,54 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(int n, int dim, cons
   }
 }
 
+// Deterministic embedding backward (nn.Embedding, decoder.py:84 / transformerDecoder.py:94):
+// dtable[id] += sum over the positions r with ids[r] == id, IN POSITION ORDER, of dout[r]
+// (times the dropout mask of the Transformer path).  No float atomics, so the result is
+// bitwise the same on every run.  The ids are staged in LDS per workgroup; wave w owns
+// position r = w when r is the first occurrence of its id (a ballot scan over ids[0, r)), and
+// then walks the later occurrences in order (ballot scans over ids[r, n)), lane = 8 columns.
+constexpr int EMB_THREADS = 1024;
+constexpr int EMB_MAXN = 16384;
 template <typename T>
-__global__ __launch_bounds__(256) void embedding_bwd_kernel(int n, int dim, const int64_t* __restrict__ ids,
-                                                            const T* __restrict__ dout, float p, uint64_t seed0,
-                                                            const uint64_t* seed_ctr, uint32_t sid,
-                                                            float* __restrict__ dtable) {
+__global__ __launch_bounds__(EMB_THREADS) void embedding_bwd_kernel(int n, int dim, const int64_t* __restrict__ ids,
+                                                                    const T* __restrict__ dout, float p,
+                                                                    uint64_t seed0, const uint64_t* seed_ctr,
+                                                                    uint32_t sid, float* __restrict__ dtable) {
+  extern __shared__ int ids_s[];
+  for (int i = threadIdx.x; i < n; i += EMB_THREADS) ids_s[i] = (int)ids[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (EMB_THREADS / 64) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int id = ids_s[r];
+  bool dup = false;
+  for (int j0 = 0; j0 < r && !dup; j0 += 64) {
+    const int j = j0 + lane;
+    dup = __any(j < r && ids_s[j] == id);
+  }
+  if (dup) return;
   const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
-  const long total = (long)n * dim;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const long r = e / dim;
-    const int c = (int)(e % dim);
-    const float d = to_f(dout[e]) * dropout_scale(seed, sid, e, p);
-    if (d != 0.f) atomicAdd(&dtable[ids[r] * (long)dim + c], d);
+  for (int cb = 0; cb < dim; cb += 64 * 8) {  // wave-uniform bound: every lane joins the ballots
+    const int c0 = cb + lane * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j0 = r; j0 < n; j0 += 64) {
+      unsigned long long m = __ballot(j0 + lane < n && ids_s[j0 + lane] == id);
+      while (m) {
+        const long row = j0 + __ffsll((long long)m) - 1;
+        m &= m - 1;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int c = c0 + k;
+          if (c < dim) {
+            const long e = row * dim + c;
+            acc[k] += to_f(dout[e]) * dropout_scale(seed, sid, e, p);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (c0 + k < dim) dtable[(long)id * dim + c0 + k] += acc[k];
   }
 }
 
@@ -219,12 +255,14 @@ extern "C" int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* id
 extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* ids, const void* dout, float drop_p,
                                     uint64_t seed, uint32_t drop_stream, float* dtable, void* stream) {
   if (n == 0) return 0;
-  const long total = (long)n * dim;
+  IMGCAP_REQUIRE(n <= EMB_MAXN, "imgcap_embedding_bwd: n <= 16384 positions");
+  const dim3 grid((n + EMB_THREADS / 64 - 1) / (EMB_THREADS / 64));
+  const size_t shm = (size_t)n * sizeof(int);
   if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(embedding_bwd_kernel<bf16>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
+    hipLaunchKernelGGL(embedding_bwd_kernel<bf16>, grid, dim3(EMB_THREADS), shm, (hipStream_t)stream, n, dim, ids,
                        (const bf16*)dout, drop_p, seed, g_seed_ctr, drop_stream, dtable);
   else
-    hipLaunchKernelGGL(embedding_bwd_kernel<float>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
+    hipLaunchKernelGGL(embedding_bwd_kernel<float>, grid, dim3(EMB_THREADS), shm, (hipStream_t)stream, n, dim, ids,
                        (const float*)dout, drop_p, seed, g_seed_ctr, drop_stream, dtable);
   IMGCAP_CHECK_LAUNCH("imgcap_embedding_bwd");
   return 0;

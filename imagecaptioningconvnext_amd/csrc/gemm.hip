@@ -584,7 +584,7 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       void* Cdst = C;
       if (sk > 1) {
         Cdst = workspace((size_t)zdim * M * N * sizeof(float), st);
-        if (!Cdst) return fail(IMGCAP_EINVAL, "imgcap_gemm: split-K workspace allocation failed");
+        if (!Cdst) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_gemm: split-K ") + last_error());
       }
       dim3 grid((N + 127) / 128, (M + 127) / 128, zdim);
       const bf16* a = (const bf16*)A;
@@ -843,7 +843,7 @@ extern "C" int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64
   float* dst = out;
   if (slices > 1) {
     dst = (float*)workspace((size_t)slices * cols * sizeof(float), (hipStream_t)stream);
-    if (!dst) return fail(IMGCAP_EINVAL, "imgcap_colsum: workspace allocation failed");
+    if (!dst) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_colsum: ") + last_error());
   }
   const dim3 grid(cblocks, slices);
   const int vec_ok = aligned16(x) && ldx % 8 == 0;

@@ -220,7 +220,7 @@ static int launch_tiled(int ak, int bk, int M, int N, int K, const void* A, long
   void* Cout = C;
   if (split > 1) {
     C = workspace((size_t)zdim * M * N * sizeof(float), st);
-    if (!C) return fail(IMGCAP_EINVAL, "imgcap_gemm: split-K workspace allocation failed");
+    if (!C) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_gemm: split-K ") + last_error());
   }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, zdim);
   const T* a = (const T*)A;

@@ -213,7 +213,7 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
   float* ws = nullptr;
   if (dgamma || dbeta) {
     ws = (float*)workspace((size_t)nblk * 2 * cols * sizeof(float), st);
-    if (!ws) return fail(IMGCAP_EINVAL, "imgcap_add_layernorm_bwd: workspace allocation failed");
+    if (!ws) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_add_layernorm_bwd: ") + last_error());
   }
 #define LNB_(T, G)                                                                                              \
   do {                                                                                                          \

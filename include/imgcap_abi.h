@@ -15,7 +15,13 @@
  *     Accumulation is always fp32.  Optimizer state and master weights are fp32.
  *   - Return 0 on success, a hipError_t (>0) or IMGCAP_E* (<0) otherwise;
  *     imgcap_last_error_string() describes the last failure (thread-local).
- *   - The caller owns every buffer (including workspaces); the library never allocates.
+ *   - The caller owns every buffer.  Ops with split reductions draw scratch from a per-device,
+ *     per-slot workspace the caller attaches (imgcap_workspace_attach); a call whose scratch
+ *     would not fit returns IMGCAP_EWORKSPACE before enqueuing anything, and
+ *     imgcap_workspace_needed gives the size to attach before retrying it.  Only a (device,
+ *     slot) the caller never attached makes the library allocate (grow-only, never freed: a
+ *     captured graph may reference it).  Op-specific workspaces (the LSTM hand-off words) are
+ *     passed in the op's arguments.
  */
 #ifndef IMGCAP_ABI_H
 #define IMGCAP_ABI_H
@@ -29,7 +35,7 @@ enum { IMGCAP_F32 = 0, IMGCAP_BF16 = 1 };
  * consecutive elements of a row.  Only as an imgcap_epilogue.c_dtype (imgcap_gemm_mx output)
  * and as the operands of imgcap_gemm_mx. */
 enum { IMGCAP_FP8MX = 2 };
-enum { IMGCAP_OK = 0, IMGCAP_EINVAL = -1, IMGCAP_EUNSUPPORTED = -2 };
+enum { IMGCAP_OK = 0, IMGCAP_EINVAL = -1, IMGCAP_EUNSUPPORTED = -2, IMGCAP_EWORKSPACE = -3 };
 /* ACT_GELU with an aux operand also writes the pre-activation to aux (the saved input of the
  * backward pass); ACT_DGELU multiplies by GELU'(aux[m, n]) (aux = that saved pre-activation). */
 enum { IMGCAP_ACT_NONE = 0, IMGCAP_ACT_GELU = 1, IMGCAP_ACT_RELU = 2, IMGCAP_ACT_DGELU = 3 };
@@ -38,6 +44,11 @@ const char* imgcap_last_error_string(void);
 /* Split-reduction scratch slot (0 default, 1) of the calling thread: calls whose kernels may
  * run concurrently with slot-0 work on another stream (the trainer's encoder pipeline) use 1. */
 int imgcap_workspace_slot(int slot);
+/* Attach the caller's device buffer (256-byte aligned; NULL detaches) as the split-reduction
+ * scratch of `slot` on the current device. */
+int imgcap_workspace_attach(int slot, void* ptr, uint64_t bytes);
+/* Largest scratch request seen so far in `slot` on the current device (what to attach). */
+int imgcap_workspace_needed(int slot, uint64_t* bytes);
 int imgcap_version(void);
 
 /* Device-resident step counter mixed into every dropout / stochastic-depth seed at kernel
@@ -262,6 +273,9 @@ int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* ids, const fl
                          const float* pe, int L, float drop_p, uint64_t seed, uint32_t drop_stream,
                          void* out, void* stream);
 /* dtable[ids[n], :] += dout[n, :] * dropmask   (fp32 atomics) */
+/* Deterministic: the n row indices are sorted (stable, by (id, position)) inside one workgroup
+ * and every table row is the sum of its occurrences in position order -- bitwise the same on
+ * every run (n <= 16384, ids < 262144).  dtable rows are accumulated into (+=). */
 int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* ids, const void* dout,
                          float drop_p, uint64_t seed, uint32_t drop_stream, float* dtable,
                          void* stream);

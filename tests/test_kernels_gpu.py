@@ -410,3 +410,51 @@ def test_sort_gather_rows(hip_device, dtype, B):
     K.mean_mid(enc_s, ref_mean)  # the unfused kernel: identical summation order
     assert torch.equal(mean, ref_mean)
     assert _rel(mean.cpu(), enc.index_select(0, ref_ind).float().mean(1)) < (1e-2 if dtype == torch.bfloat16 else 1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,V,dim", [(1632, 9490, 512), (3328, 120, 512), (7, 5, 40), (200, 9490, 1000)])
+def test_embedding_bwd_deterministic(hip_device, dtype, n, V, dim):
+    """Rows of each id summed in position order (no float atomics): equal to a sequential fp64
+    sum to fp32 rounding, bitwise identical across runs, dropout mask as the forward's."""
+    from imagecaptioningconvnext_amd import kernels as K
+    g = torch.Generator().manual_seed(n)
+    ids = torch.randint(0, V, (n,), generator=g)
+    ids[: n // 3] = ids[0]  # a very frequent word
+    dout = torch.randn(n, dim, generator=g).to(dtype)
+    ref = torch.zeros(V, dim, dtype=torch.float64).index_add_(0, ids, dout.double())
+    outs = []
+    for _ in range(3):
+        dt_ = torch.zeros(V, dim, device=hip_device)
+        K.embedding_bwd(ids.to(hip_device), dout.to(hip_device), dt_)
+        outs.append(dt_.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert ((outs[0].double() - ref).norm() / ref.norm()).item() < 1e-6
+    # with dropout: bitwise repeatable too
+    a = torch.zeros(V, dim, device=hip_device)
+    b = torch.zeros(V, dim, device=hip_device)
+    K.embedding_bwd(ids.to(hip_device), dout.to(hip_device), a, drop_p=0.5, seed=9, drop_stream=3)
+    K.embedding_bwd(ids.to(hip_device), dout.to(hip_device), b, drop_p=0.5, seed=9, drop_stream=3)
+    assert torch.equal(a, b) and not torch.equal(a.cpu(), outs[0])
+
+
+def test_caller_workspace_grows_on_demand(hip_device):
+    """Split-K scratch comes from the caller's attached buffer (imgcap_workspace_attach); a call
+    that needs more returns IMGCAP_EWORKSPACE without enqueuing anything, the binding attaches a
+    bigger buffer and retries."""
+    import ctypes
+    from imagecaptioningconvnext_amd import _abi
+    from imagecaptioningconvnext_amd import kernels as K
+    dev = torch.cuda.current_device()
+    a = torch.randn(512, 9600, device=hip_device).bfloat16()
+    b = torch.randn(9600, 512, device=hip_device).bfloat16()
+    K.gemm(a[:8], b)  # first call attaches the initial buffers
+    _abi._attach(dev, 0, 1 << 20)  # shrink slot 0 to 1 MB
+    small = _abi._ws[(dev, 0)]
+    c = K.gemm(a, b, split_k=8, out_dtype=torch.float32)  # 8 x 512 x 512 fp32 partials = 8 MB
+    assert _abi._ws[(dev, 0)].numel() > small.numel()
+    need = ctypes.c_uint64(0)
+    _abi.lib().imgcap_workspace_needed(0, ctypes.byref(need))
+    assert need.value >= 8 * 512 * 512 * 4
+    ref = a.float() @ b.float()
+    assert ((c - ref).norm() / ref.norm()).item() < 1e-5

@@ -55,10 +55,32 @@ def test_graph_replay_matches_eager(hip_device, decoder):
     (m_e, p_e), (m_g, p_g) = runs
     for a, b in zip(m_e, m_g):
         assert abs(a[0] - b[0]) < 1e-5 * abs(a[0]) and a[1] == b[1] and abs(a[2] - b[2]) < 1e-3
-    # bias / LayerNorm-affine / embedding gradients are reduced with float atomics (order varies
-    # run to run), and Adam's early steps amplify ULP-level gradient differences on entries with
-    # near-zero gradient: agree to 5% of one lr=1e-4 step
-    torch.testing.assert_close(p_g, p_e, rtol=1e-5, atol=5e-6)
+    # no float atomics anywhere in the step (the embedding gradient sums its rows in position
+    # order): graph replay and eager launches run the same kernels in the same order
+    assert torch.equal(p_g, p_e)
+
+
+@pytest.mark.parametrize("decoder", ["lstm", "transformer"])
+def test_train_step_bitwise_repeatable(hip_device, decoder):
+    """Deterministic mode (the reference's test.py:12-24 seeds everything and its
+    results/checkingReproducibility shows ~1e-7 run-to-run drift): two trainers from the same
+    state over the same batches end with bitwise-identical parameters, Adam moments and metrics,
+    dropout and drop path active."""
+    from imagecaptioningconvnext_amd import kernels as K
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    runs = []
+    for _ in range(2):
+        enc, dec = _models(hip_device, decoder, dropout=0.5, sd_off=False)
+        tr = TeacherForcedTrainer(enc, dec, lstm=decoder == "lstm", graph=True)
+        for i in range(3):
+            tr.step(*_batch(hip_device, i))
+        fp = tr.eng.fp
+        runs.append((tr.drain_metrics(), fp.flat.clone(), fp.m.clone(), fp.v.clone()))
+        K.set_seed_counter(None)
+    (m1, *a), (m2, *b) = runs
+    assert m1 == m2
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
 
 
 def test_graph_replays_draw_fresh_masks(hip_device):
