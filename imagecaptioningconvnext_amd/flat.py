@@ -58,6 +58,17 @@ class FlatParams:
         o, shp = self.offsets[name]
         return o, math.prod(shp) if count is None else count
 
+    def span(self, names):
+        """[lo, hi) of the flat buffers covering ``names`` (must be contiguous up to alignment)."""
+        lo = min(self.offsets[n][0] for n in names)
+        hi = max(self.offsets[n][0] + math.prod(self.offsets[n][1]) for n in names)
+        hi = min(self.numel, (hi + ALIGN - 1) // ALIGN * ALIGN)
+        covered = sum(math.prod(self.offsets[n][1]) for n in names)
+        inside = [n for n in self.params if lo <= self.offsets[n][0] < hi]
+        if sorted(inside) != sorted(names) or covered > hi - lo:
+            raise ValueError(f"parameters {names} are not contiguous in the flat buffer")
+        return lo, hi
+
     def master(self, name):
         o, shp = self.offsets[name]
         return self.flat[o:o + math.prod(shp)].view(shp)

@@ -352,11 +352,18 @@ class LstmEngine:
         return out.view(B, T, V)
 
     # ---------------------------------------------------------------------------------------
-    def backward(self, s, dlogits=None, dalpha=None, gbuf=None, want_denc=False):
+    def early_bucket(self):
+        """Flat range whose gradients are final when backward() calls ``bucket_hook``: the
+        embedding and fc weights (64 % of the decoder at C2), reduced while the weight-gradient
+        GEMMs of the rest still run (DDP-style bucketed all-reduce)."""
+        return self.fp.span(["embedding.weight", "fc.weight", "fc.bias"])
+
+    def backward(self, s, dlogits=None, dalpha=None, gbuf=None, want_denc=False, bucket_hook=None):
         """Writes dL/dparams into ``gbuf`` (default: the flat grad buffer).  Default upstream:
         the fused loss of forward(loss=True); otherwise ``dlogits`` [B*T, V(pad)] (compute
         dtype) and ``dalpha`` [B, T, P] (f32).  want_denc: also dL/d encoder_out (fp32, the
-        caller's batch order) into s["denc"] -- encoder fine-tuning."""
+        caller's batch order) into s["denc"] -- encoder fine-tuning.  ``bucket_hook`` is called
+        (on the current stream's timeline) once the early_bucket() gradients are final."""
         fp, ct = self.fp, self.ct
         gbuf = fp.grad if gbuf is None else gbuf
 
@@ -443,6 +450,8 @@ class LstmEngine:
         cb.add(dwf, _G.g("attention.full_att.weight", (A,)))
         # full_att.bias: exactly zero gradient (softmax is shift-invariant) -> left at 0
         torch.cuda.current_stream(dev).wait_stream(side)  # fc dW / db (beside the recurrence) done
+        if bucket_hook is not None:
+            bucket_hook()
         wgb.run()
         cb.run()
         s["denc"] = None

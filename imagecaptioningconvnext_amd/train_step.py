@@ -11,7 +11,15 @@ Per step, exactly the reference's work:
 
 With ``graph=True`` the encoder + decoder forward/backward (several hundred kernel launches,
 most of them small on the LSTM recurrence) is captured once into a HIP graph and replayed
-per step; the batch is copied into the graph's static input buffers first.  Dropout and
+per step; the batch is copied into the graph's static input buffers first.
+
+Data parallel (world > 1): the gradient all-reduce is bucketed like DDP's.  The decoder engine
+names an early bucket (LSTM: embedding + fc, 64 % of its parameters; Transformer: the
+embedding) whose gradients are final before the weight-gradient GEMMs of the rest; its RCCL
+all-reduce runs on a communication stream while those GEMMs run (eager: issued from the
+backward's hook; graph mode: the step is captured as two graphs split at that point and the
+bucket is reduced between the two replays).  The rest is reduced after the backward, then
+clip + Adam (trainMultiGPU.py:384-394).  Dropout and
 stochastic-depth masks stay fresh per replay through the device step counter
 (imgcap_set_seed_counter) bumped inside the graph.  The all-reduce and the Adam step (whose
 bias correction depends on the host step count) run eagerly after the replay.
@@ -65,6 +73,17 @@ class TeacherForcedTrainer:
         # parameter updates are exactly the sequential ones (the encoder is frozen).
         self.pipeline = pipeline
         self._pipe = None
+        # bucketed gradient all-reduce (world > 1): early bucket [lo, hi) of the decoder's flat
+        # grads, reduced on self._comm while the rest of the backward runs
+        self._bucket = None
+        self._hook_mode = None   # None | "eager" (issue the bucket now) | "split" (capture split)
+        self._split = None
+        self._early_issued = False
+        self._comm = None
+        if self.world > 1 and hasattr(self.eng, "early_bucket"):
+            self._bucket = self.eng.early_bucket()
+            if torch.cuda.is_available() and self.eng.fp.grad.is_cuda:
+                self._comm = torch.cuda.Stream(device=self.eng.fp.grad.device)
         if self.world > 1:
             # DDP construction broadcasts rank 0's parameters (trainMultiGPU.py:233); the encoder is
             # broadcast too because its weights are randomly initialised here (SURVEY.md §7 v)
@@ -108,12 +127,64 @@ class TeacherForcedTrainer:
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
         if mid is not None:
             mid()
+        kw = {}
+        if self._bucket is not None and self._hook_mode is not None:
+            kw["bucket_hook"] = self._bucket_hook
         if es is not None:
-            self.eng.backward(s, want_denc=True)
+            self.eng.backward(s, want_denc=True, **kw)
             self.enc_eng.backward(es, s["denc"].reshape(feats.shape))
         else:
-            self.eng.backward(s)
+            self.eng.backward(s, **kw)
         return s["metrics"]
+
+    # ---- bucketed gradient all-reduce --------------------------------------------------------
+    def _reduce_early(self):
+        """All-reduce the early bucket on the communication stream (ordered after the current
+        stream's work so far)."""
+        lo, hi = self._bucket
+        g = self.eng.fp.grad
+        if self._comm is None:
+            dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.pg)
+        else:
+            self._comm.wait_stream(torch.cuda.current_stream(g.device))
+            with torch.cuda.stream(self._comm):
+                dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.pg)
+        self._early_issued = True
+
+    def _bucket_hook(self):
+        if self._hook_mode == "eager":
+            self._reduce_early()
+        elif self._hook_mode == "split":
+            self._split()
+
+    def _begin_split_capture(self, pool=None, join=None):
+        """Capture the step as two graphs split at the bucket hook (world > 1); returns
+        (g1, g2).  ``join``: streams to join before the split (forked branches of graph 1)."""
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+
+        def split():
+            cur = torch.cuda.current_stream()
+            for st in (join or ()):
+                cur.wait_stream(st)
+            g1.capture_end()
+            g2.capture_begin(pool=g1.pool())
+        self._split = split
+        self._hook_mode = "split"
+        g1.capture_begin(pool=pool)
+        return g1, g2
+
+    def _end_split_capture(self, g2):
+        self._hook_mode = None
+        self._split = None
+        g2.capture_end()
+
+    def _replay(self, g):
+        if isinstance(g, tuple):  # split step: early bucket reduced between the two halves
+            g[0].replay()
+            self._reduce_early()
+            g[1].replay()
+        else:
+            g.replay()
 
     def _capture(self, imgs, caps, caplens, warmup=2):
         dev = imgs.device
@@ -126,6 +197,18 @@ class TeacherForcedTrainer:
             for _ in range(warmup):
                 self._fwd_bwd(*self._inputs)
         torch.cuda.current_stream(dev).wait_stream(side)
+        if self._bucket is not None:
+            cap = torch.cuda.Stream(device=dev)
+            cap.wait_stream(torch.cuda.current_stream(dev))
+            torch.cuda.synchronize(dev)
+            with torch.cuda.stream(cap):
+                g1, g2 = self._begin_split_capture()
+                self._seed_ctr.add_(1)
+                self._metrics = self._fwd_bwd(*self._inputs)
+                self._end_split_capture(g2)
+            torch.cuda.current_stream(dev).wait_stream(cap)
+            self._graph = (g1, g2)
+            return
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._seed_ctr.add_(1)
@@ -174,8 +257,16 @@ class TeacherForcedTrainer:
             return
         pool = None
         for k in (0, 1):  # graph k: encode the new batch into slot k, train on slot 1-k
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            split = self._bucket is not None
+            cap = torch.cuda.Stream(device=dev)
+            cap.wait_stream(main)
+            torch.cuda.synchronize(dev)
+            with torch.cuda.stream(cap):
+                if split:  # two graphs; the encoder branch joins graph 1 at the split
+                    g1, g2 = self._begin_split_capture(pool, join=(side,))
+                else:
+                    g = torch.cuda.CUDAGraph()
+                    g.capture_begin(pool=pool)
                 self._seed_ctr.add_(1)
                 cur = torch.cuda.current_stream(dev)
 
@@ -188,7 +279,13 @@ class TeacherForcedTrainer:
                 m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k],
                               mid=fork if PIPE_FORK == "bwd" else None)
                 cur.wait_stream(side)
-            pool = g.pool()
+                if split:
+                    self._end_split_capture(g2)
+                    g = (g1, g2)
+                else:
+                    g.capture_end()
+            main.wait_stream(cap)
+            pool = g[0].pool() if split else g.pool()
             P["graphs"].append(g)
             P["metrics"].append(m)
         self._pipe = P
@@ -203,7 +300,9 @@ class TeacherForcedTrainer:
             P["side"].wait_stream(main)
             with torch.cuda.stream(P["side"]):
                 feats = self._encode(imgs)
+            self._hook_mode = "eager"
             m = self._dec(*P["pending"]) if P["pending"] is not None else None
+            self._hook_mode = None
             main.wait_stream(P["side"])
             feats.record_stream(main)
             P["pending"] = (feats, caps, caplens)
@@ -230,7 +329,7 @@ class TeacherForcedTrainer:
             main.wait_stream(P["side"])
             m = P["metrics"][k]
         else:
-            P["graphs"][k].replay()
+            self._replay(P["graphs"][k])
             m = P["metrics"][k]
         P["i"] += 1
         return m
@@ -240,17 +339,21 @@ class TeacherForcedTrainer:
         P = self._pipe
         if not self.pipeline or P is None:
             return None
+        self._hook_mode = "eager"
         if not self.graph:
             if P["pending"] is None:
+                self._hook_mode = None
                 return None
             m = self._dec(*P["pending"])
             P["pending"] = None
         else:
             if P["i"] == 0:
+                self._hook_mode = None
                 return None
             j = (P["i"] - 1) % 2
             m = self._dec(P["feats"][j], P["caps"][j], P["lens"][j])
             P["i"] = 0
+        self._hook_mode = None
         return self._update(m)
 
     def step(self, imgs, caps, caplens):
@@ -258,25 +361,41 @@ class TeacherForcedTrainer:
             m = self._pipe_step(imgs, caps, caplens)
             return None if m is None else self._update(m)
         if not self.graph:
-            m = self._fwd_bwd(imgs, caps, caplens)
+            m = self._eager(imgs, caps, caplens)
         else:
             if self._graph is None:
                 self._capture(imgs, caps, caplens)
             if any(d.shape != s_.shape or d.dtype != s_.dtype for d, s_ in zip(self._inputs, (imgs, caps, caplens))):
                 # a batch of another shape (the last, partial batch of an epoch): eager launches
-                return self._update(self._fwd_bwd(imgs, caps, caplens))
+                return self._update(self._eager(imgs, caps, caplens))
             for dst, src in zip(self._inputs, (imgs, caps, caplens)):
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src, non_blocking=True)
-            self._graph.replay()
+            self._replay(self._graph)
             m = self._metrics
         return self._update(m)
+
+    def _eager(self, imgs, caps, caplens):
+        self._hook_mode = "eager"
+        try:
+            return self._fwd_bwd(imgs, caps, caplens)
+        finally:
+            self._hook_mode = None
 
     def _update(self, m):
         """DDP gradient average, clip + Adam, metric reduction (trainMultiGPU.py:384-403)."""
         fp = self.eng.fp
         if self.world > 1:
-            dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
+            if self._early_issued:  # the early bucket is in flight on the comm stream: the rest
+                lo, hi = self._bucket
+                for a, b in ((0, lo), (hi, fp.grad.numel())):
+                    if b > a:
+                        dist.all_reduce(fp.grad[a:b], op=dist.ReduceOp.SUM, group=self.pg)
+                if self._comm is not None:
+                    torch.cuda.current_stream(fp.grad.device).wait_stream(self._comm)
+                self._early_issued = False
+            else:
+                dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
         fp.adam_step(self.decoder_lr, self.grad_clip, grad_div=float(self.world))
         if self.enc_eng is not None:
             efp = self.enc_eng.fp

@@ -288,7 +288,12 @@ class TransformerEngine:
         return out.view(B, L, self.V)
 
     # ---------------------------------------------------------------------------------------
-    def backward(self, s, dlogits=None, gbuf=None, want_denc=False):
+    def early_bucket(self):
+        """Flat range whose gradients are final when backward() calls ``bucket_hook``: the
+        token embedding, reduced while the grouped weight-gradient GEMMs run."""
+        return self.fp.span(["embedding.weight"])
+
+    def backward(self, s, dlogits=None, gbuf=None, want_denc=False, bucket_hook=None):
         fp, ct = self.fp, self.ct
         gbuf = fp.grad if gbuf is None else gbuf
         G = lambda name, shape=None, count=None: fp.g(name, shape, count, buf=gbuf)  # noqa: E731
@@ -373,6 +378,8 @@ class TransformerEngine:
                 denc = K.gemm(dmem_c, fp.w("encoder_proj.weight")).view(B, P, self.E)
         elif want_denc:
             denc = dmem.to(ct).view(B, P, d)
+        if bucket_hook is not None:
+            bucket_hook()
         wgb.run()
         cb.run()
         s["denc"] = denc

@@ -7,3 +7,8 @@ import ddp_util
 
 def test_trainer_ddp2_matches_reference_trainMultiGPU(tmp_path):
     ddp_util.check(ddp_util.run("oracle", tmp_path))
+
+
+def test_trainer_ddp2_unbucketed_matches_reference(tmp_path):
+    """The same run with the bucketed all-reduce switched off (one collective after backward)."""
+    ddp_util.check(ddp_util.run("oracle", tmp_path, bucketed=False))

@@ -102,11 +102,13 @@ def test_graph_replays_draw_fresh_masks(hip_device):
     K.set_seed_counter(None)
 
 
-def test_trainer_ddp2_hip_matches_reference_trainMultiGPU(hip_device, tmp_path):
+@pytest.mark.parametrize("graph,bucketed", [(False, True), (True, True), (True, False)])
+def test_trainer_ddp2_hip_matches_reference_trainMultiGPU(hip_device, tmp_path, graph, bucketed):
     """Two ranks (gloo, sharing the one GPU) through the HIP engine vs the reference's 2-rank
-    trainMultiGPU step (tests/golden/ddp2_lstm)."""
+    trainMultiGPU step (tests/golden/ddp2_lstm): eager (early bucket reduced from the backward's
+    hook on the comm stream) and graph replay (the step split into two graphs around it)."""
     import ddp_util
-    ddp_util.check(ddp_util.run("hip", tmp_path))
+    ddp_util.check(ddp_util.run("hip", tmp_path, graph=graph, bucketed=bucketed))
 
 
 @pytest.mark.parametrize("decoder", ["lstm", "transformer"])
@@ -132,3 +134,16 @@ def test_pipelined_trainer_matches_sequential(hip_device, decoder, graph):
     for a, b in zip(m_s, m_p):
         assert abs(a[0] - b[0]) < 1e-5 * abs(a[0]) and a[1] == b[1] and abs(a[2] - b[2]) < 1e-3
     torch.testing.assert_close(p_p, p_s, rtol=1e-5, atol=5e-6)
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_bucketed_allreduce_matches_single_collective_over_steps(hip_device, tmp_path, pipeline):
+    """Several DDP steps (gloo, 2 ranks on the one GPU) with graph replay, split into two graphs
+    around the early bucket (and, pipelined, with the encoder branch joined at the split):
+    bitwise the parameters and metrics of one all-reduce after the backward."""
+    import ddp_util
+    a = ddp_util.run_steps(tmp_path / "a", pipeline, True, True)
+    b = ddp_util.run_steps(tmp_path / "b", pipeline, True, False)
+    for ra, rb in zip(a, b):
+        assert torch.equal(ra["flat"], rb["flat"]) and torch.equal(ra["metrics"], rb["metrics"])
+    assert torch.equal(a[0]["flat"], a[1]["flat"])
