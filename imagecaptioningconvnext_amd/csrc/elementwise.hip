@@ -63,47 +63,79 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(int n, int dim, cons
 // Deterministic embedding backward (nn.Embedding, decoder.py:84 / transformerDecoder.py:94):
 // dtable[id] += sum over the positions r with ids[r] == id, IN POSITION ORDER, of dout[r]
 // (times the dropout mask of the Transformer path).  No float atomics, so the result is
-// bitwise the same on every run.  The ids are staged in LDS per workgroup; wave w owns
-// position r = w when r is the first occurrence of its id (a ballot scan over ids[0, r)), and
-// then walks the later occurrences in order (ballot scans over ids[r, n)), lane = 8 columns.
-constexpr int EMB_THREADS = 1024;
-constexpr int EMB_MAXN = 16384;
-template <typename T>
-__global__ __launch_bounds__(EMB_THREADS) void embedding_bwd_kernel(int n, int dim, const int64_t* __restrict__ ids,
-                                                                    const T* __restrict__ dout, float p,
-                                                                    uint64_t seed0, const uint64_t* seed_ctr,
-                                                                    uint32_t sid, float* __restrict__ dtable) {
-  extern __shared__ int ids_s[];
-  for (int i = threadIdx.x; i < n; i += EMB_THREADS) ids_s[i] = (int)ids[i];
+// bitwise the same on every run.  Three launches:
+//   emb_rank:    rank of position i in the (id, position) order, counted against one chunk of
+//                EMB_CHUNK ids per workgroup (chunk staged in LDS, broadcast reads) -> partial
+//                counts [chunk][i]
+//   emb_scatter: rank = sum of the partial counts; sorted position / id at that rank
+//   emb_segsum:  one wave per sorted index; a run's first index sums the run's rows in order
+constexpr int EMB_CHUNK = 1024;
+constexpr int EMB_MAXN = 1 << 20;
+__global__ __launch_bounds__(256) void emb_rank_kernel(int n, const int64_t* __restrict__ ids,
+                                                       int* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) int chunk[EMB_CHUNK];
+  const int c0 = blockIdx.y * EMB_CHUNK, cn = min(EMB_CHUNK, n - c0);
+  // pad the chunk with INT_MAX (never < id, never == id: ids < 2^31 - 1)
+  for (int k = threadIdx.x; k < EMB_CHUNK; k += 256) chunk[k] = k < cn ? (int)ids[c0 + k] : 0x7fffffff;
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * (EMB_THREADS / 64) + (threadIdx.x >> 6);
-  if (r >= n) return;
-  const int id = ids_s[r];
-  bool dup = false;
-  for (int j0 = 0; j0 < r && !dup; j0 += 64) {
-    const int j = j0 + lane;
-    dup = __any(j < r && ids_s[j] == id);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int id = (int)ids[i];
+  const int before = i - c0;  // chunk entries k < before precede position i
+  int cnt = 0;
+  const int4* c4 = (const int4*)chunk;
+  const int nq = (cn + 3) / 4;
+#pragma unroll 8
+  for (int q = 0; q < nq; ++q) {  // broadcast 16-byte LDS reads, 4 ids each
+    const int4 v = c4[q];
+    const int k = 4 * q;
+    cnt += (v.x < id) | ((v.x == id) & (k < before));
+    cnt += (v.y < id) | ((v.y == id) & (k + 1 < before));
+    cnt += (v.z < id) | ((v.z == id) & (k + 2 < before));
+    cnt += (v.w < id) | ((v.w == id) & (k + 3 < before));
   }
-  if (dup) return;
+  part[(long)blockIdx.y * n + i] = cnt;
+}
+
+__global__ __launch_bounds__(256) void emb_scatter_kernel(int n, int nchunks, const int64_t* __restrict__ ids,
+                                                          const int* __restrict__ part, int* __restrict__ spos,
+                                                          int* __restrict__ sid) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int r = 0;
+  for (int c = 0; c < nchunks; ++c) r += part[(long)c * n + i];
+  spos[r] = i;
+  sid[r] = (int)ids[i];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void emb_segsum_kernel(int n, int dim, const int* __restrict__ spos,
+                                                         const int* __restrict__ sid, const T* __restrict__ dout,
+                                                         float p, uint64_t seed0, const uint64_t* seed_ctr,
+                                                         uint32_t stream_id, float* __restrict__ dtable) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const int id = sid[i];
+  if (i > 0 && sid[i - 1] == id) return;  // not the first index of its run
+  int end = i + 1;
+  while (end < n && sid[end] == id) ++end;
   const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
-  for (int cb = 0; cb < dim; cb += 64 * 8) {  // wave-uniform bound: every lane joins the ballots
+  const bool vec = (dim % 8) == 0;
+  for (int cb = 0; cb < dim; cb += 64 * 8) {
     const int c0 = cb + lane * 8;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int j0 = r; j0 < n; j0 += 64) {
-      unsigned long long m = __ballot(j0 + lane < n && ids_s[j0 + lane] == id);
-      while (m) {
-        const long row = j0 + __ffsll((long long)m) - 1;
-        m &= m - 1;
+    for (int j = i; j < end; ++j) {
+      const long row = spos[j];
+      if (c0 >= dim) continue;
+      float x[8];
+      if (vec) {
+        ld_g<T, 8>(dout + row * dim + c0, x);
+      } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int c = c0 + k;
-          if (c < dim) {
-            const long e = row * dim + c;
-            acc[k] += to_f(dout[e]) * dropout_scale(seed, sid, e, p);
-          }
-        }
+        for (int k = 0; k < 8; ++k) x[k] = c0 + k < dim ? to_f(dout[row * dim + c0 + k]) : 0.f;
       }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += x[k] * dropout_scale(seed, stream_id, row * dim + c0 + k, p);
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -255,15 +287,23 @@ extern "C" int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* id
 extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* ids, const void* dout, float drop_p,
                                     uint64_t seed, uint32_t drop_stream, float* dtable, void* stream) {
   if (n == 0) return 0;
-  IMGCAP_REQUIRE(n <= EMB_MAXN, "imgcap_embedding_bwd: n <= 16384 positions");
-  const dim3 grid((n + EMB_THREADS / 64 - 1) / (EMB_THREADS / 64));
-  const size_t shm = (size_t)n * sizeof(int);
+  IMGCAP_REQUIRE(n <= EMB_MAXN, "imgcap_embedding_bwd: n <= 2^20 positions");
+  hipStream_t st = (hipStream_t)stream;
+  const int nchunks = (n + EMB_CHUNK - 1) / EMB_CHUNK;
+  int* part = (int*)workspace(((size_t)nchunks + 2) * n * sizeof(int), st);
+  if (!part) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_embedding_bwd: ") + last_error());
+  int* spos = part + (size_t)nchunks * n;
+  int* sid = spos + n;
+  const int nb = (n + 255) / 256;
+  hipLaunchKernelGGL(emb_rank_kernel, dim3(nb, nchunks), dim3(256), 0, st, n, ids, part);
+  hipLaunchKernelGGL(emb_scatter_kernel, dim3(nb), dim3(256), 0, st, n, nchunks, ids, part, spos, sid);
+  const dim3 g((n + 3) / 4);
   if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(embedding_bwd_kernel<bf16>, grid, dim3(EMB_THREADS), shm, (hipStream_t)stream, n, dim, ids,
-                       (const bf16*)dout, drop_p, seed, g_seed_ctr, drop_stream, dtable);
+    hipLaunchKernelGGL(emb_segsum_kernel<bf16>, g, dim3(256), 0, st, n, dim, spos, sid, (const bf16*)dout, drop_p,
+                       seed, g_seed_ctr, drop_stream, dtable);
   else
-    hipLaunchKernelGGL(embedding_bwd_kernel<float>, grid, dim3(EMB_THREADS), shm, (hipStream_t)stream, n, dim, ids,
-                       (const float*)dout, drop_p, seed, g_seed_ctr, drop_stream, dtable);
+    hipLaunchKernelGGL(emb_segsum_kernel<float>, g, dim3(256), 0, st, n, dim, spos, sid, (const float*)dout,
+                       drop_p, seed, g_seed_ctr, drop_stream, dtable);
   IMGCAP_CHECK_LAUNCH("imgcap_embedding_bwd");
   return 0;
 }

@@ -273,9 +273,9 @@ int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* ids, const fl
                          const float* pe, int L, float drop_p, uint64_t seed, uint32_t drop_stream,
                          void* out, void* stream);
 /* dtable[ids[n], :] += dout[n, :] * dropmask   (fp32 atomics) */
-/* Deterministic: the n row indices are sorted (stable, by (id, position)) inside one workgroup
- * and every table row is the sum of its occurrences in position order -- bitwise the same on
- * every run (n <= 16384, ids < 262144).  dtable rows are accumulated into (+=). */
+/* Deterministic: positions are ranked in (id, position) order and every table row is the sum
+ * of its occurrences in position order -- bitwise the same on every run (no float atomics).
+ * Scratch: the split-reduction workspace.  dtable rows are accumulated into (+=). */
 int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* ids, const void* dout,
                          float drop_p, uint64_t seed, uint32_t drop_stream, float* dtable,
                          void* stream);
