@@ -32,12 +32,31 @@ namespace imgcap {
 #ifndef MLP96_WPE
 #define MLP96_WPE 2
 #endif
+#ifndef MLP96_HC
+#define MLP96_HC 64
+#endif
+#ifndef MLP192_HC
+#define MLP192_HC 32
+#endif
 #ifndef MLP192_BM
 #define MLP192_BM 64
 #endif
 #ifndef MLP192_WPE
 #define MLP192_WPE 2
 #endif
+#ifdef MLP_STAMPS  // kernel-bench diagnostics only (tools/kbench): s_memtime at phase edges
+__device__ long long* g_mlp_stamps;
+#define MLP_STAMP(k)                                                                       \
+  do {                                                                                     \
+    if (g_mlp_stamps && threadIdx.x == 0 && blockIdx.x < 64) {                             \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                          \
+      g_mlp_stamps[blockIdx.x * 64 + (k)] = (long long)__builtin_amdgcn_s_memtime();       \
+    }                                                                                      \
+  } while (0)
+#else
+#define MLP_STAMP(k) do { } while (0)
+#endif
+
 // GELU of the hidden activation.  MLP_GELU (kernel-variant experiments, tools/kbench): 0 =
 // erf form (torch nn.GELU default), 1 = identity (timing only), 2 = fast erf.
 DEV float mlp_gelu(float v) {
@@ -125,6 +144,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   bf16* zimg = wbuf + G::BUFE + 4 * G::HE;  // ZL only
   const int m0 = blockIdx.x * BM;
   const int wr0 = m0 + w * G::WR;
+  MLP_STAMP(0);
 
   // this wave's Z rows as A fragments (row fr of each 16-row slab, k = 8*fq..): kept in
   // registers for the whole chunk loop, or (ZL, wide C) staged once into an LDS image
@@ -188,11 +208,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
     for (int tn = 0; tn < G::TN2; ++tn) acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  MLP_STAMP(1);
 
   uint4 r1[G::V1], r2[G::V2];
   mlp_load<C, HC>(r1, r2, w1, w2, 0);
   mlp_store<C, HC, G::LD1, G::LD2>(wbuf, r1, r2);
   __syncthreads();  // (also publishes the Z image)
+  MLP_STAMP(2);
 
   constexpr int NCH = 4 * C / HC;
   for (int ch = 0; ch < NCH; ++ch) {
@@ -218,31 +240,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
             za = *(const bf16x8*)(zimg + (w * G::WR + tm * 16 + fr) * G::LDZ + ks * 32 + 8 * fq);
           else
             za = zf[tm < ZR ? tm : 0][ks < ZK ? ks : 0];
-          acc1[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(za, bfr, acc1[tm][tn], 0, 0, 0);
+          // operands swapped: the tile is H^T (rows = hidden units, columns = rows of Z), so each
+          // lane ends with 4 CONSECUTIVE hidden units of one row -- one 8-byte LDS write below
+          acc1[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr, za, acc1[tm][tn], 0, 0, 0);
         }
       }
     }
-    // bias + GELU -> bf16 hidden chunk in this wave's LDS image
+    if (ch < 8) MLP_STAMP(3 + 4 * ch);
+    // bias + GELU -> bf16 hidden chunk in this wave's LDS image: lane (row fr, units 4fq..4fq+3)
     const int h0 = ch * HC;
 #pragma unroll
     for (int tn = 0; tn < G::TN1; ++tn) {
-      const float bb = b1[h0 + tn * 16 + fr];
+      const f32x4 bb = *(const f32x4*)(b1 + h0 + tn * 16 + 4 * fq);
 #pragma unroll
       for (int tm = 0; tm < G::TM; ++tm) {
-        bf16* hp = hbuf + (tm * 16 + 4 * fq) * G::LDH + tn * 16 + fr;
+        bf16x4 hv;
 #if MLP_GELU == 2
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const f32x2 gv = gelu_fast2(f32x2{acc1[tm][tn][r] + bb, acc1[tm][tn][r + 1] + bb});
-          hp[r * G::LDH] = (bf16)gv[0];
-          hp[(r + 1) * G::LDH] = (bf16)gv[1];
-        }
+        const f32x2 g01 = gelu_fast2(f32x2{acc1[tm][tn][0] + bb[0], acc1[tm][tn][1] + bb[1]});
+        const f32x2 g23 = gelu_fast2(f32x2{acc1[tm][tn][2] + bb[2], acc1[tm][tn][3] + bb[3]});
+        hv[0] = (bf16)g01[0]; hv[1] = (bf16)g01[1]; hv[2] = (bf16)g23[0]; hv[3] = (bf16)g23[1];
 #else
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hp[r * G::LDH] = (bf16)mlp_gelu(acc1[tm][tn][r] + bb);
+        for (int r = 0; r < 4; ++r) hv[r] = (bf16)mlp_gelu(acc1[tm][tn][r] + bb[r]);
 #endif
+        *(bf16x4*)(hbuf + (tm * 16 + fr) * G::LDH + tn * 16 + 4 * fq) = hv;
       }
     }
+    if (ch < 8) MLP_STAMP(4 + 4 * ch);
     // GEMM2: O[WR, C] += H W2c^T   (the hidden image is written and read by this wave only)
     const bf16* w2c = cur + HC * G::LD1;
 #pragma unroll
@@ -258,9 +282,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
           acc2[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hf[tm], bfr, acc2[tm][tn], 0, 0, 0);
       }
     }
+    if (ch < 8) MLP_STAMP(5 + 4 * ch);
     __syncthreads();  // every wave is done with the staged chunk
     mlp_store<C, HC, G::LD1, G::LD2>(wbuf, r1, r2);
     __syncthreads();
+    if (ch < 8) MLP_STAMP(6 + 4 * ch);
   }
 
   // epilogue: fp32 tile through LDS, then x += gamma * sd * (o + b2) on 8-column vectors
@@ -276,6 +302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       for (int r = 0; r < 4; ++r)
         tile[(w * G::WR + tm * 16 + 4 * fq + r) * G::LDO + tn * 16 + fr] = acc2[tm][tn][r];
   __syncthreads();
+  MLP_STAMP(40);
 #if MLP_EPI_BATCH
   // residual rows of all NIT iterations loaded at once (one memory round trip)
   bf16x8 xres[NIT];
@@ -307,6 +334,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
     }
     *(bf16x8*)(x + (long)m * C + c) = o;
   }
+  MLP_STAMP(41);
 }
 
 }  // namespace imgcap
@@ -329,9 +357,9 @@ extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const float* ln_w
                      (const bf16*)z, (const bf16*)w1, b1, (const bf16*)w2, b2, gamma, sd, rows_per_sample, ln_w, \
                      ln_b, (bf16*)x)
   switch (C) {
-    case 96: MLP_(96, MLP96_BM, 64, false, MLP96_WPE); break;
+    case 96: MLP_(96, MLP96_BM, MLP96_HC, false, MLP96_WPE); break;
     case 128: MLP_(128, 128, 64, false, 1); break;
-    case 192: MLP_(192, MLP192_BM, 32, false, MLP192_WPE); break;
+    case 192: MLP_(192, MLP192_BM, MLP192_HC, false, MLP192_WPE); break;
     default: return fail(IMGCAP_EUNSUPPORTED, "imgcap_cnblock_mlp: C must be 96, 128 or 192");
   }
 #undef MLP_

@@ -63,16 +63,17 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(int n, int dim, cons
 // Deterministic embedding backward (nn.Embedding, decoder.py:84 / transformerDecoder.py:94):
 // dtable[id] += sum over the positions r with ids[r] == id, IN POSITION ORDER, of dout[r]
 // (times the dropout mask of the Transformer path).  No float atomics, so the result is
-// bitwise the same on every run.  Three launches:
+// bitwise the same on every run.  Three launches after a memset of the rank words:
 //   emb_rank:    rank of position i in the (id, position) order, counted against one chunk of
-//                EMB_CHUNK ids per workgroup (chunk staged in LDS, broadcast reads) -> partial
-//                counts [chunk][i]
-//   emb_scatter: rank = sum of the partial counts; sorted position / id at that rank
-//   emb_segsum:  one wave per sorted index; a run's first index sums the run's rows in order
-constexpr int EMB_CHUNK = 1024;
+//                EMB_CHUNK ids per workgroup (chunk in LDS, broadcast reads); the chunk counts
+//                are summed with integer atomics (exact, order-free)
+//   emb_scatter: sorted position / id at that rank
+//   emb_segsum:  one wave per sorted index; a run's first index reads the run's positions a
+//                window of 64 at a time and sums their rows in order
+constexpr int EMB_CHUNK = 128;  // ids per rank workgroup: many small workgroups fill the chip
 constexpr int EMB_MAXN = 1 << 20;
 __global__ __launch_bounds__(256) void emb_rank_kernel(int n, const int64_t* __restrict__ ids,
-                                                       int* __restrict__ part) {
+                                                       int* __restrict__ rank) {
   __shared__ __attribute__((aligned(16))) int chunk[EMB_CHUNK];
   const int c0 = blockIdx.y * EMB_CHUNK, cn = min(EMB_CHUNK, n - c0);
   // pad the chunk with INT_MAX (never < id, never == id: ids < 2^31 - 1)
@@ -84,9 +85,8 @@ __global__ __launch_bounds__(256) void emb_rank_kernel(int n, const int64_t* __r
   const int before = i - c0;  // chunk entries k < before precede position i
   int cnt = 0;
   const int4* c4 = (const int4*)chunk;
-  const int nq = (cn + 3) / 4;
-#pragma unroll 8
-  for (int q = 0; q < nq; ++q) {  // broadcast 16-byte LDS reads, 4 ids each
+#pragma unroll
+  for (int q = 0; q < EMB_CHUNK / 4; ++q) {  // broadcast 16-byte LDS reads, 4 ids each
     const int4 v = c4[q];
     const int k = 4 * q;
     cnt += (v.x < id) | ((v.x == id) & (k < before));
@@ -94,20 +94,20 @@ __global__ __launch_bounds__(256) void emb_rank_kernel(int n, const int64_t* __r
     cnt += (v.z < id) | ((v.z == id) & (k + 2 < before));
     cnt += (v.w < id) | ((v.w == id) & (k + 3 < before));
   }
-  part[(long)blockIdx.y * n + i] = cnt;
+  if (cnt) atomicAdd(rank + i, cnt);
 }
 
-__global__ __launch_bounds__(256) void emb_scatter_kernel(int n, int nchunks, const int64_t* __restrict__ ids,
-                                                          const int* __restrict__ part, int* __restrict__ spos,
+__global__ __launch_bounds__(256) void emb_scatter_kernel(int n, const int64_t* __restrict__ ids,
+                                                          const int* __restrict__ rank, int* __restrict__ spos,
                                                           int* __restrict__ sid) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  int r = 0;
-  for (int c = 0; c < nchunks; ++c) r += part[(long)c * n + i];
+  const int r = rank[i];
   spos[r] = i;
   sid[r] = (int)ids[i];
 }
 
+constexpr int EMB_MAXDIM = 2048;  // columns: 8 per lane, at most 4 passes of 512
 template <typename T>
 __global__ __launch_bounds__(256) void emb_segsum_kernel(int n, int dim, const int* __restrict__ spos,
                                                          const int* __restrict__ sid, const T* __restrict__ dout,
@@ -117,30 +117,49 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(int n, int dim, const i
   if (i >= n) return;
   const int id = sid[i];
   if (i > 0 && sid[i - 1] == id) return;  // not the first index of its run
-  int end = i + 1;
-  while (end < n && sid[end] == id) ++end;
   const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
   const bool vec = (dim % 8) == 0;
-  for (int cb = 0; cb < dim; cb += 64 * 8) {
-    const int c0 = cb + lane * 8;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int j = i; j < end; ++j) {
-      const long row = spos[j];
-      if (c0 >= dim) continue;
-      float x[8];
-      if (vec) {
-        ld_g<T, 8>(dout + row * dim + c0, x);
-      } else {
+  constexpr int NC = EMB_MAXDIM / 512;
+  float acc[NC][8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = c0 + k < dim ? to_f(dout[row * dim + c0 + k]) : 0.f;
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[c][k] = 0.f;
+  // the run is sorted indices [i, end): windows of 64; its members are a prefix of each window
+  for (int base = i;; base += 64) {
+    const int j = base + lane;
+    const int jid = j < n ? sid[j] : -1;
+    const int jpos = j < n ? spos[j] : 0;
+    unsigned long long m = __ballot(jid == id);
+    const bool more = (m >> 63) & 1ull;
+    while (m) {  // rows in position order
+      const int l = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const long row = __shfl(jpos, l, 64);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int c0 = c * 512 + lane * 8;
+        if (c0 >= dim) continue;
+        float x[8];
+        if (vec) {
+          ld_g<T, 8>(dout + row * dim + c0, x);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) x[k] = c0 + k < dim ? to_f(dout[row * dim + c0 + k]) : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[c][k] += x[k] * dropout_scale(seed, stream_id, row * dim + c0 + k, p);
       }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += x[k] * dropout_scale(seed, stream_id, row * dim + c0 + k, p);
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (c0 + k < dim) dtable[(long)id * dim + c0 + k] += acc[k];
+    if (!more || base + 64 >= n) break;
   }
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int col = c * 512 + lane * 8 + k;
+      if (col < dim) dtable[(long)id * dim + col] += acc[c][k];
+    }
 }
 
 template <typename TI, typename TO>
@@ -287,16 +306,18 @@ extern "C" int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* id
 extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* ids, const void* dout, float drop_p,
                                     uint64_t seed, uint32_t drop_stream, float* dtable, void* stream) {
   if (n == 0) return 0;
-  IMGCAP_REQUIRE(n <= EMB_MAXN, "imgcap_embedding_bwd: n <= 2^20 positions");
+  IMGCAP_REQUIRE(n <= EMB_MAXN && dim <= EMB_MAXDIM, "imgcap_embedding_bwd: n <= 2^20 positions, dim <= 2048");
   hipStream_t st = (hipStream_t)stream;
-  const int nchunks = (n + EMB_CHUNK - 1) / EMB_CHUNK;
-  int* part = (int*)workspace(((size_t)nchunks + 2) * n * sizeof(int), st);
-  if (!part) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_embedding_bwd: ") + last_error());
-  int* spos = part + (size_t)nchunks * n;
+  const size_t rank_bytes = ((size_t)n * sizeof(int) + 15) / 16 * 16;
+  int* rank = (int*)workspace(rank_bytes + 2 * (size_t)n * sizeof(int), st);
+  if (!rank) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_embedding_bwd: ") + last_error());
+  int* spos = rank + rank_bytes / sizeof(int);
   int* sid = spos + n;
+  if (hipMemsetAsync(rank, 0, rank_bytes, st) != hipSuccess)
+    return fail(IMGCAP_EINVAL, "imgcap_embedding_bwd: memset failed");
   const int nb = (n + 255) / 256;
-  hipLaunchKernelGGL(emb_rank_kernel, dim3(nb, nchunks), dim3(256), 0, st, n, ids, part);
-  hipLaunchKernelGGL(emb_scatter_kernel, dim3(nb), dim3(256), 0, st, n, nchunks, ids, part, spos, sid);
+  hipLaunchKernelGGL(emb_rank_kernel, dim3(nb, (n + EMB_CHUNK - 1) / EMB_CHUNK), dim3(256), 0, st, n, ids, rank);
+  hipLaunchKernelGGL(emb_scatter_kernel, dim3(nb), dim3(256), 0, st, n, ids, rank, spos, sid);
   const dim3 g((n + 3) / 4);
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(emb_segsum_kernel<bf16>, g, dim3(256), 0, st, n, dim, spos, sid, (const bf16*)dout, drop_p,

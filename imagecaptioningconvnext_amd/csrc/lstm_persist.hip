@@ -64,6 +64,8 @@ struct Geo {
   int NU, NG, NUG, RS, Ec, NR, UPB, KU, ldu, ldg, rc;
   int ug_red, ug_hst, r_enc, r_red, r_red2, r_es;  // byte offsets into dynamic LDS
   long long* stamps;  // diagnostics (IMGCAP_LSTM_STAMPS=1): per step, s_memrealtime at phase edges
+  int gran_off;       // sync word offset of the [B][A + E] {epoch, value} granules (G -> R hand-off)
+  int r_gv;           // R: LDS offset of the row's [att2 | gate_pre chunk] values
 };
 
 // thread 0 of block 0 (U+G) and of the first R block records [role][t][k]
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d
   const rsrc_t r_hs = make_rsrc(d.hs, (uint32_t)((long)B * Tn * D * sizeof(T)));
   const rsrc_t r_h0 = make_rsrc(d.hprev, (uint32_t)((long)B * Tn * D * sizeof(T)));
   const rsrc_t r_zs = make_rsrc(d.zs, (uint32_t)((long)B * Tn * E * sizeof(T)));
-  const rsrc_t r_g1 = make_rsrc(d.g1, (uint32_t)((long)B * Tn * W3 * sizeof(float)));
+  const rsrc_t r_gr = make_rsrc(d.sync + g.gran_off, (uint32_t)((long)B * (A + E) * 8));
 
   if (blk < g.NUG) {
     // ======================= U / G workgroup =======================================
@@ -327,11 +329,16 @@ __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d
             for (int q = 0; q < KP; ++q) s += red[(q * 16 * MT + b) * RC + c + j];
             v[j] = s;
           }
-          st_wt(r_g1, (uint32_t)((((long)b * Tn + t) * W3 + col0 + c) * 4),
-                make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])));
+          // hand-off to the R blocks as 8-byte {epoch, value} granules: the data is its own flag
+          // (no drain, no separate flag; R2 of cdna_hip_programming.md Guideline 16); two
+          // granules per 16-byte write-through store, each 8-byte half written whole
+          const unsigned ep = (unsigned)(t + 1);
+          const uint32_t go = (uint32_t)(((long)b * (A + E) + col0 + c) * 8);
+          st_wt(r_gr, go, make_uint4(__float_as_uint(v[0]), ep, __float_as_uint(v[1]), ep));
+          st_wt(r_gr, go + 16, make_uint4(__float_as_uint(v[2]), ep, __float_as_uint(v[3]), ep));
+          *(f32x4*)(d.g1 + ((long)b * Tn + t) * W3 + col0 + c) = f32x4{v[0], v[1], v[2], v[3]};  // saved for bwd
         }
         stamp(g, 0, t, 2);
-        block_publish(fg + blk, t + 1);
         stamp(g, 0, t, 3);
       }
       // ---------------- U: gates, LSTMCell -> h_t ----------------
@@ -446,6 +453,8 @@ __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d
   T* encs = (T*)(smem + g.r_enc);               // [P][Ec]
   float* red2 = (float*)(smem + g.r_red2);      // [64] scores
   float* es = (float*)(smem + g.r_es);          // [64] alpha
+  float* gv = (float*)(smem + g.r_gv);          // [A + Ec] att2 | gate_pre chunk of this step
+  if (tid == 0) s_ok[2] = 1;
   {
     const T* a1 = (const T*)d.att1 + (long)b * P * A;
     for (int i = tid; i < P * A / VEC; i += PT) *(uint4*)(att1s + i * VEC) = *(const uint4*)(a1 + i * VEC);
@@ -471,15 +480,43 @@ __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d
   __syncthreads();
   for (int t = 0; t < Tmax; ++t) {
     stamp(g, 1, t, 0);
-    if (!block_wait(fg, g.NG, t + 1, err, s_ok + 2)) return;
+    // [att2 | gate_pre of this chunk] of row b: poll the G blocks' granules until every tag is
+    // this step's epoch, values into LDS (pairs of granules per 16-byte write-through load)
+    {
+      const unsigned ep = (unsigned)(t + 1);
+      const int npair = (A + Ec) / 2;
+      bool bad = false;
+      for (int j = tid; j < npair; j += PT) {
+        const int col = 2 * j < A ? 2 * j : A + e0 + (2 * j - A);
+        const uint32_t off = (uint32_t)(((long)b * (A + E) + col) * 8);
+        for (int spins = 0;; ++spins) {
+          const uint4 q = ld_wt(r_gr, off);
+          if (q.y == ep && q.w == ep) {
+            gv[2 * j] = __uint_as_float(q.x);
+            gv[2 * j + 1] = __uint_as_float(q.z);
+            break;
+          }
+          if ((spins & 255) == 255 &&
+              (spins >= SPIN_LIMIT || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            bad = true;
+            break;
+          }
+        }
+        if (bad) break;
+      }
+      if (bad) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ok[2] = 0;
+      }
+      __syncthreads();
+      if (s_ok[2] == 0) return;
+    }
     stamp(g, 1, t, 1);
     const long bt = (long)b * Tn + t;
     // att2 slice of this lane (the gate pre-activations are read by the context threads below)
     float a2[8];
-    {
-      const uint32_t oa = (uint32_t)((bt * W3 + (aok ? lane * 8 : 0)) * 4);
-      unpack8(ld_wt(r_g1, oa), ld_wt(r_g1, oa + 16), a2);
-    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a2[j] = aok ? gv[lane * 8 + j] : 0.f;
     stamp(g, 1, t, 5, true);
     // scores e_p = w_f . relu(att1_p + att2): wave w takes pixels w, w+PWV, ..; lane = 8 units;
     // each pixel's 64 lane partials summed by DPP, the total written by one lane
@@ -520,8 +557,8 @@ __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d
     for (int v = tid >> 2; v < NVE; v += PT / 4) {
       // gate pre-activation of this vector (only the quad leader uses it)
       float gp[8];
-      const uint32_t og = (uint32_t)((bt * W3 + A + e0 + v * 8) * 4);
-      unpack8(ld_wt(r_g1, og), ld_wt(r_g1, og + 16), gp);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gp[j] = gv[A + v * 8 + j];
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       constexpr int H = sizeof(T) / 2;
       for (int p0 = pg; p0 < P; p0 += 32) {
@@ -615,7 +652,10 @@ static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds
     q = align16(q + PWV * 64 * 4);
     const size_t ees = q;
     q = align16(q + 64 * 4);
+    const size_t gvo = q;
+    q = align16(q + (size_t)(d.A + Ec) * 4);
     if (q <= LDS_MAX) {
+      g.r_gv = (int)gvo;
       g.RS = rs;
       g.Ec = Ec;
       g.r_enc = (int)enc;
@@ -632,7 +672,8 @@ static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds
   // at least 81 KB: one workgroup per CU (the visibility form used here is the one measured so)
   lds = std::max(std::max(ug, r), (size_t)81 * 1024);
   if (lds > LDS_MAX) return false;
-  words = SYNC_HDR + g.NU + g.NG + g.NR;
+  g.gran_off = (SYNC_HDR + g.NU + g.NG + g.NR + 63) / 64 * 64;  // 256-byte aligned granule block
+  words = g.gran_off + d.B * (d.A + d.E) * 2;
   return true;
 }
 

@@ -1,3 +1,5 @@
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from imagecaptioningconvnext_amd import kernels as K
 for n, V in ((1632, 9490), (3328, 9490)):
