@@ -93,6 +93,8 @@ _SIGS = {
     "imgcap_ce_fwd": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "imgcap_ce_bwd": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                       c_void_p],
+    "imgcap_ce_fused": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                        c_void_p, c_int64, c_void_p],
     "imgcap_clamp_adam": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
                           c_float, c_int, c_float, c_float, c_void_p],
     "imgcap_lstm_tf_fwd": [ctypes.POINTER(LstmDesc), c_void_p],

@@ -65,6 +65,97 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(int V, const T* __restrict_
   }
 }
 
+// ---- fused forward + backward (the training step: loss, top-5 and dlogits in one pass) ----
+// The row is read ONCE into registers (16-byte vectors, NV per thread), reduced (max, then
+// sum-exp and the count of logits above the target's), and dlogits = (softmax - onehot) *
+// scale written from the same registers: one read and one write of [n, V] instead of the
+// fwd + bwd kernels' two reads and one write (element-wise 2-byte loads there).  Padding
+// columns [V, ceil(V / VEC) * VEC) of dlogits are written as 0.
+template <typename T, int NV>
+__global__ __launch_bounds__(256) void ce_fused_kernel(int V, const T* __restrict__ logits, long ld,
+                                                       const int64_t* __restrict__ tgt,
+                                                       const float* __restrict__ scale_p, float* __restrict__ lse_o,
+                                                       float* __restrict__ loss_o, float* __restrict__ hit_o,
+                                                       T* __restrict__ d, long ldd) {
+  constexpr int VEC = 16 / sizeof(T);
+  __shared__ float red[2][4];
+  const int row = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+  const T* x = logits + (long)row * ld;
+  const long t = tgt[row];
+  const bool valid = t >= 0 && t < V;
+  const int nvec = (V + VEC - 1) / VEC;
+  float v[NV][VEC];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int q = j * 256 + tid;
+    if (q < nvec) {
+      ld_g<T, VEC>(x + (long)q * VEC, v[j]);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        if (q * VEC + e >= V) v[j][e] = -INFINITY;
+    } else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[j][e] = -INFINITY;
+    }
+  }
+  const float xt = valid ? to_f(x[t]) : 0.f;
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) m = fmaxf(m, v[j][e]);
+  m = wave_max(m);
+  if ((tid & 63) == 0) red[0][w] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  float s = 0.f, cnt = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      s += __expf(v[j][e] - m);  // exp(-inf) = 0 for masked slots
+      cnt += (v[j][e] > xt) ? 1.f : 0.f;
+    }
+  s = wave_sum(s);
+  cnt = wave_sum(cnt);
+  __syncthreads();  // red[0] read by every thread above
+  if ((tid & 63) == 0) { red[0][w] = s; red[1][w] = cnt; }
+  __syncthreads();
+  const float S = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  const float C = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  const float lse = m + logf(S);
+  if (tid == 0) {
+    lse_o[row] = lse;
+    if (loss_o) loss_o[row] = valid ? lse - xt : 0.f;
+    if (hit_o) hit_o[row] = (valid && C < 5.f) ? 1.f : 0.f;
+  }
+  const float sc = valid ? *scale_p : 0.f;
+  T* o = d + (long)row * ldd;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int q = j * 256 + tid;
+    if (q < nvec) {
+      float g[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const int c = q * VEC + e;
+        g[e] = c < V ? sc * (__expf(v[j][e] - lse) - (c == t ? 1.f : 0.f)) : 0.f;
+      }
+      st_g<T, VEC>(o + (long)q * VEC, g);
+    }
+  }
+}
+
+// 1 / (number of rows with a target): the scale of the fused kernel's dlogits (the same value
+// loss_finalize_kernel writes to its out[3] afterwards)
+__global__ __launch_bounds__(1024) void ce_scale_kernel(int n, const int64_t* __restrict__ tgt, float* __restrict__ out) {
+  __shared__ float red[16];
+  float c = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) c += tgt[i] >= 0 ? 1.f : 0.f;
+  c = block_sum(c, red);
+  if (threadIdx.x == 0) *out = 1.f / (c > 0.f ? c : 1.f);
+}
+
 }  // namespace imgcap
 
 namespace imgcap {
@@ -159,5 +250,38 @@ extern "C" int imgcap_ce_bwd(int dtype, int n, int V, const void* logits, int64_
     hipLaunchKernelGGL(ce_bwd_kernel<float>, dim3(n), dim3(256), 0, (hipStream_t)stream, V, (const float*)logits, ld,
                        targets, lse, scale, (float*)dlogits, ldd);
   IMGCAP_CHECK_LAUNCH("imgcap_ce_bwd");
+  return 0;
+}
+
+extern "C" int imgcap_ce_fused(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
+                               float* scale, float* lse, float* loss, float* hit5, void* dlogits, int64_t ldd,
+                               void* stream) {
+  if (n == 0) return 0;
+  IMGCAP_REQUIRE(V > 0 && ld >= V && ldd >= V, "imgcap_ce_fused: bad V / ld / ldd");
+  IMGCAP_REQUIRE(scale && lse && dlogits, "imgcap_ce_fused: scale, lse and dlogits required");
+  const int vec = dtype == IMGCAP_BF16 ? 8 : 4;
+  const int nvec = (V + vec - 1) / vec;
+  IMGCAP_REQUIRE(ld % vec == 0 && ldd % vec == 0 && ldd >= (int64_t)nvec * vec && aligned16(logits) &&
+                     aligned16(dlogits),
+                 "imgcap_ce_fused: 16-byte aligned rows whose pitch covers ceil(V / vec) * vec elements");
+  const int per = (nvec + 255) / 256;
+  IMGCAP_REQUIRE(per <= 8, "imgcap_ce_fused: V <= 16384 (bf16) / 8192 (fp32)");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ce_scale_kernel, dim3(1), dim3(1024), 0, st, n, targets, scale);
+#define CEF_(T, NV)                                                                                       \
+  hipLaunchKernelGGL((ce_fused_kernel<T, NV>), dim3(n), dim3(256), 0, st, V, (const T*)logits, (long)ld, targets, \
+                     scale, lse, loss, hit5, (T*)dlogits, (long)ldd)
+#define CEF_T(T)                               \
+  do {                                         \
+    if (per <= 2) CEF_(T, 2);                  \
+    else if (per <= 4) CEF_(T, 4);             \
+    else if (per <= 6) CEF_(T, 6);             \
+    else CEF_(T, 8);                           \
+  } while (0)
+  if (dtype == IMGCAP_BF16) CEF_T(bf16);
+  else CEF_T(float);
+#undef CEF_T
+#undef CEF_
+  IMGCAP_CHECK_LAUNCH("imgcap_ce_fused");
   return 0;
 }

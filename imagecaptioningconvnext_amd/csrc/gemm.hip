@@ -18,6 +18,7 @@
 //   block owns 16 output columns; its 8 waves split K and stream A/B fragments straight from
 //   global into registers (no LDS round trip, no barriers in the loop), then reduce in LDS.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "common.h"
@@ -447,6 +448,32 @@ static int glds_stages() {
   return s;
 }
 
+// 64x64 tile stages (IMGCAP_GLDS64_STAGES, 2-4) and the XCD tile order of the LDS-DMA tiles
+// (IMGCAP_GEMM_ORDER: 0 row-major bands, 1 grouped rectangles; glds_tile_order)
+static int glds64_stages() {
+  static const int s = [] {
+    const char* e = getenv("IMGCAP_GLDS64_STAGES");
+    const int v = e ? atoi(e) : 2;
+    return v >= 2 && v <= 4 ? v : 2;
+  }();
+  return s;
+}
+static int gemm_order() {
+  static const int o = [] {
+    const char* e = getenv("IMGCAP_GEMM_ORDER");
+    return e ? atoi(e) : 0;
+  }();
+  return o;
+}
+// band height in tile rows for a grid of nx x ny tiles (glds_tile_order): each XCD's run of
+// ~nx*ny/8 tiles as a square-ish rectangle; 0 = row-major
+static int glds_group(int nx, int ny) {
+  if (gemm_order() == 0 || nx * ny < 64) return 0;
+  const double run = (double)nx * ny / 8.0;
+  int g = (int)(std::sqrt(run) + 0.5);
+  return std::max(1, std::min(g, ny));
+}
+
 // 256x256 tile (gemm256.h): 0 never, 1 wherever it applies, -1 by shape (default; the
 // IMGCAP_GEMM256 environment variable or imgcap_gemm_set_policy override it)
 static int g_gemm256_mode = [] {
@@ -560,20 +587,27 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       dim3 grid((N + 63) / 64, sq ? (M + 63) / 64 : (M + 127) / 128);
       const bf16* a = (const bf16*)A;
       const bf16* b = (const bf16*)B;
+      const int grp = glds_group(grid.x, grid.y), S64 = glds64_stages();
+#define GS_S(AKV, BKV, SV)                                                                                            \
+  hipLaunchKernelGGL((gemm_glds_kernel<64, 64, AKV, BKV, SV>), grid, dim3(256), 0, st, a, lda, b, ldb, C, ldc, M, N, K, \
+                     ep, vec_ok, g_seed_ctr, 0, grp)
 #define GS_(AKV, BKV)                                                                                                 \
   do {                                                                                                             \
-    if (sq)                                                                                                        \
-      hipLaunchKernelGGL((gemm_glds_kernel<64, 64, AKV, BKV, 2>), grid, dim3(256), 0, st, a, lda, b, ldb, C, ldc, M, N, \
-                         K, ep, vec_ok, g_seed_ctr, 0);                                                            \
-    else                                                                                                           \
+    if (sq) {                                                                                                      \
+      if (S64 == 4) GS_S(AKV, BKV, 4);                                                                             \
+      else if (S64 == 3) GS_S(AKV, BKV, 3);                                                                        \
+      else GS_S(AKV, BKV, 2);                                                                                      \
+    } else {                                                                                                       \
       hipLaunchKernelGGL((gemm_glds_kernel<128, 64, AKV, BKV, 2>), grid, dim3(256), 0, st, a, lda, b, ldb, C, ldc, M, \
-                         N, K, ep, vec_ok, g_seed_ctr, 0);                                                         \
+                         N, K, ep, vec_ok, g_seed_ctr, 0, grp);                                                    \
+    }                                                                                                              \
   } while (0)
       if (ak && bk) GS_(true, true);
       else if (ak) GS_(true, false);
       else if (bk) GS_(false, true);
       else GS_(false, false);
 #undef GS_
+#undef GS_S
       IMGCAP_CHECK_LAUNCH("imgcap_gemm(glds small)");
       return 0;
     }
@@ -590,9 +624,10 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       const bf16* a = (const bf16*)A;
       const bf16* b = (const bf16*)B;
       const int S = glds_stages();
+      const int grp = glds_group(grid.x, grid.y);
 #define GL_S(AKV, BKV, SV)                                                                                           \
   hipLaunchKernelGGL((gemm_glds_kernel<128, 128, AKV, BKV, SV>), grid, dim3(256), 0, st, a, lda, b, ldb, Cdst, ldc, M, \
-                     N, K, ep, vec_ok, g_seed_ctr, kslice)
+                     N, K, ep, vec_ok, g_seed_ctr, kslice, grp)
 #define GL_(AKV, BKV)              \
   do {                             \
     if (S == 4) GL_S(AKV, BKV, 4);  \

@@ -192,17 +192,40 @@ DEV void glds_tile(const bf16* __restrict__ A, long lda, const bf16* __restrict_
   }
 }
 
-// 128x128 tiles fit two blocks per CU; the small-grid 64-wide tiles (a quarter / half of the
-// LDS and accumulators) four
+// Blocks per CU the stages' LDS allows (160 KiB), at most 4: 128x128 x 2 stages two, the
+// small-grid 64x64 tile four (2 stages), three (3) or two (4)
+template <int BM, int BN, int S>
+constexpr int glds_blocks_per_cu() {
+  constexpr int lds = S * (BM + BN) * 64 * 2;
+  return 160 * 1024 / lds < 4 ? 160 * 1024 / lds : 4;
+}
+
+// Block -> output tile.  The hardware deals blocks round-robin over the 8 XCDs (block b on XCD
+// b % 8, MI355X_MICROARCH.md "Workgroup dispatch"); each XCD gets a contiguous run of tile ids
+// (xcd_remap).  With grp == 0 ids walk the tile grid row-major, so an XCD's run is a band of
+// whole tile rows: it reads all of B through its own L2 (the vocab projection: every XCD reads
+// the whole 9.7 MB weight).  With grp > 0 ids walk bands of grp tile rows column by column, so
+// an XCD's run is a grp x (run / grp) rectangle; grp ~ sqrt(run) balances its A and B bytes.
+DEV void glds_tile_order(int grp, int& bx, int& by) {
+  xcd_remap(bx, by);
+  if (grp <= 0) return;
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int id = by * nx + bx;
+  const int band = id / (grp * nx), within = id - band * grp * nx;
+  const int rows = min(grp, ny - band * grp);
+  by = band * grp + within % rows;
+  bx = within / rows;
+}
+
 template <int BM, int BN, bool AK, bool BKM, int S>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    S == 2 ? (BM * BN <= 128 * 64 ? 4 : 2) : 1, S == 2 ? (BM * BN <= 128 * 64 ? 4 : 2) : 1))) void
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(glds_blocks_per_cu<BM, BN, S>(),
+                                                                     glds_blocks_per_cu<BM, BN, S>()))) void
 gemm_glds_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ B, long ldb, void* __restrict__ C,
                  long ldc, int M, int N, int K, imgcap_epilogue ep, int vec_ok, const uint64_t* seed_ctr,
-                 int kslice) {
+                 int kslice, int grp) {
   if (ep.drop_p > 0.f) ep.seed = eff_seed(ep.seed, seed_ctr);
   int bx, by;
-  xcd_remap(bx, by);
+  glds_tile_order(grp, bx, by);
   glds_tile<BM, BN, AK, BKM, S>(A, lda, B, ldb, C, ldc, M, N, K, ep, vec_ok, kslice, by * BM, bx * BN, blockIdx.z);
 }
 

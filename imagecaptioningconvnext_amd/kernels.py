@@ -321,6 +321,13 @@ def ce_bwd(logits, targets, V, lse, scale, dlogits):
               lse.data_ptr(), scale.data_ptr(), dlogits.data_ptr(), dlogits.stride(0), stream())
 
 
+def ce_fused(logits, targets, V, scale, lse, loss, hit5, dlogits):
+    """Training-step CE in one pass: scale[0] = 1/tokens, lse/loss/hit5, dlogits (imgcap_ce_fused)."""
+    n = targets.numel()
+    _abi.call("imgcap_ce_fused", dt(logits), n, V, logits.data_ptr(), logits.stride(0), targets.data_ptr(),
+              scale.data_ptr(), lse.data_ptr(), ptr(loss), ptr(hit5), dlogits.data_ptr(), dlogits.stride(0), stream())
+
+
 def loss_finalize(loss_rows, hit5, targets, extra, out):
     _abi.call("imgcap_loss_finalize", targets.numel(), loss_rows.data_ptr(), hit5.data_ptr(), targets.data_ptr(),
               ptr(extra), out.data_ptr(), stream())

@@ -90,7 +90,7 @@ class LstmEngine:
         if words <= 0:
             return
         if self._sync is None or self._sync.numel() < words or self._sync.device != dev:
-            self._sync = torch.zeros(max(words, 8192), dtype=torch.int32, device=dev)
+            self._sync = torch.zeros(max(words + 4608, 8192), dtype=torch.int32, device=dev)  # + diagnostics stamps
         d.sync, d.sync_words = self._sync.data_ptr(), self._sync.numel()
 
     def sync_error(self):
@@ -257,14 +257,17 @@ class LstmEngine:
             lse = torch.empty(B * T, **f32)
             lrow = torch.empty(B * T, **f32)
             hit = torch.empty(B * T, **f32)
-            K.ce_fwd(logits, targets, V, lse, lrow, hit)
+            metrics = torch.empty(4, **f32)  # loss, tokens, top5 hits, 1/tokens
+            # loss, top-5 and the loss gradient in one pass over the logits (train.py:266-276);
+            # backward() starts from these dlogits
+            dlogits = torch.empty(B * T, self.Vpad, **ctd)
+            K.ce_fused(logits, targets, V, metrics[3:4], lse, lrow, hit, dlogits)
             dalpha = torch.empty(B, T, P, **f32)
             reg = torch.empty(1, **f32)
             _abi.call("imgcap_attn_reg", B, T, P, alphas.data_ptr(), dl.data_ptr(), alphaC, dalpha.data_ptr(),
                       reg.data_ptr(), K.stream())
-            metrics = torch.empty(4, **f32)  # loss, tokens, top5 hits, 1/tokens
             K.loss_finalize(lrow, hit, targets, reg, metrics)
-            s.update(logits=logits, targets=targets, lse=lse, dalpha=dalpha, metrics=metrics)
+            s.update(logits=logits, targets=targets, lse=lse, dalpha=dalpha, metrics=metrics, dlogits=dlogits)
         return s
 
     def greedy(self, encoder_out, start_id, end_id, maxlen):
@@ -379,8 +382,7 @@ class LstmEngine:
         cb = K.ColsumBatch()  # every bias gradient, reduced in one launch at the end
         wgb = K.GemmBatch()    # every weight gradient, grouped launches at the end
         if dlogits is None:
-            dlogits = torch.empty(B * T, self.Vpad, device=dev, dtype=ct)
-            K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
+            dlogits = s["dlogits"]  # imgcap_ce_fused in forward(loss=True)
             dalpha = s["dalpha"]
         BT = B * T
         # fc: dh = (dlogits W_fc) * dropmask on the critical path; dW_fc = dlogits^T hd and

@@ -80,10 +80,10 @@ def _gemm_groups(trainer, batch):
         if kind in (2, 3, 4, 5, 6, 7):
             name += f"<ak={c['ak']},bk={c['bk']}>" + (" (split-K)" if splits > 1 else "")
         tf = lambda v: "true" if v else "false"  # noqa: E731
-        sym = {4: f"gemm_glds_kernel<128, 128, {tf(c['ak'])}, {tf(c['bk'])}, 2>",
+        sym = {4: f"gemm_glds_kernel<128, 128, {tf(c['ak'])}, {tf(c['bk'])}, ",  # any stage count
                5: f"gemm256_kernel<64, 2, {tf(c['ak'])}, {tf(c['bk'])}>",
-               6: f"gemm_glds_kernel<64, 64, {tf(c['ak'])}, {tf(c['bk'])}, 2>",
-               7: f"gemm_glds_kernel<128, 64, {tf(c['ak'])}, {tf(c['bk'])}, 2>"}.get(kind, _KIND_NAME.get(kind, ""))
+               6: f"gemm_glds_kernel<64, 64, {tf(c['ak'])}, {tf(c['bk'])}, ",
+               7: f"gemm_glds_kernel<128, 64, {tf(c['ak'])}, {tf(c['bk'])}, "}.get(kind, _KIND_NAME.get(kind, ""))
         g = groups.setdefault(name, dict(name=name, calls=[], bound="mfma", symbol=sym))
         g["calls"].append(c)
     out = []
@@ -158,6 +158,28 @@ def pmc_traffic(symbol, cfgname):
     return sum(h["traffic_bytes"] * h["dispatches"] for h in hits) / max(n, 1)
 
 
+def pmc_sq(symbol, cfgname):
+    """SQ counters of ``symbol`` from the committed rocprofv3 summary of this config's bench run
+    (profiles/*_<cfg>_sq.json, tools/sq_summary.py): {mfma_busy, wait_frac, ...} or None."""
+    import glob
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(root, "profiles", f"*_{cfgname}_sq.json")))
+    if not files or not symbol:
+        return None
+    data = json.load(open(files[-1]))
+    hits = [v for k, v in data.items() if symbol in k and "mfma_busy" in v]
+    if not hits:
+        return None
+    n = sum(h["dispatches"] for h in hits)
+    out = {"source": os.path.relpath(files[-1], root)}
+    for key in ("mfma_busy", "wait_frac", "lds_conflict_per_inst"):
+        if all(key in h for h in hits):
+            out[key] = round(sum(h[key] * h["dispatches"] for h in hits) / max(n, 1), 4)
+    return out
+
+
 def measure(cfg, trainer, batch, cfgname=None):
     dev = batch[0].device
     B = batch[0].shape[0]
@@ -179,5 +201,7 @@ def measure(cfg, trainer, batch, cfgname=None):
             "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/)",
             "algorithmic_bytes": round(best["bytes"]) if "bytes" in best else None,
             "kernel": best["name"],
+            # SIMD-cycle share of the matrix pipe while the kernel ran (rocprofv3 SQ counters)
+            "sq": pmc_sq(best.get("symbol"), cfgname) if cfgname else None,
             "avg_launch_us": round(t * 1e6, 2), "launches_per_step": best["per_step"], "shape": best["note"],
             "others_us_per_step": {c["name"]: round(c["share"] * 1e6, 1) for c in ranked[1:8]}}

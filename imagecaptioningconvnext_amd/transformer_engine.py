@@ -169,10 +169,12 @@ class TransformerEngine:
             lse = torch.empty(BL, **f32)
             lrow = torch.empty(BL, **f32)
             hit = torch.empty(BL, **f32)
-            K.ce_fwd(logits, targets, V, lse, lrow, hit)
-            metrics = torch.empty(4, **f32)
+            metrics = torch.empty(4, **f32)  # loss, tokens, top5 hits, 1/tokens
+            # loss, top-5 and the loss gradient in one pass over the logits (train.py:266-276)
+            dlogits = torch.empty(BL, self.Vpad, **ctd)
+            K.ce_fused(logits, targets, V, metrics[3:4], lse, lrow, hit, dlogits)
             K.loss_finalize(lrow, hit, targets, None, metrics)
-            s.update(logits=logits, targets=targets, lse=lse, metrics=metrics)
+            s.update(logits=logits, targets=targets, lse=lse, metrics=metrics, dlogits=dlogits)
         return s
 
     def greedy(self, encoder_out, start_id, end_id, maxlen):
@@ -305,8 +307,7 @@ class TransformerEngine:
         cb = K.ColsumBatch()  # every bias gradient, reduced in one launch at the end
         wgb = K.GemmBatch()    # every weight gradient, grouped launches at the end
         if dlogits is None:
-            dlogits = torch.empty(BL, self.Vpad, device=dev, dtype=ct)
-            K.ce_bwd(s["logits"], s["targets"], V, s["lse"], s["metrics"][3:4], dlogits)
+            dlogits = s["dlogits"]  # imgcap_ce_fused in forward(loss=True)
         wgb.add(dlogits, s["xL"], out=G("fc_out.weight"), M=V, trans_a=True)
         cb.add(dlogits, G("fc_out.bias"), cols=V)
         dx = K.gemm(dlogits, fp.w("fc_out.weight"), K=V)                    # [BL, d]

@@ -290,6 +290,15 @@ int imgcap_ce_fwd(int dtype, int n, int V, const void* logits, int64_t ld, const
                   float* lse, float* loss, float* hit5, void* stream);
 int imgcap_ce_bwd(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
                   const float* lse, const float* scale, void* dlogits, int64_t ldd, void* stream);
+/* fwd + bwd in one pass over the logits (the training step): scale[0] = 1 / (rows with a
+ * target) is computed first and written, then lse / loss / hit5 as imgcap_ce_fwd and
+ * dlogits = (softmax - onehot) * scale[0] as imgcap_ce_bwd; one read + one write of [n, V]
+ * (train.py:266-276 -- the loss, its gradient and utils.py:248-250's top-5 of one step).
+ * Rows: 16-byte aligned, pitches multiples of 8 (bf16) / 4 (fp32) elements, V <= 16384 / 8192;
+ * dlogits' padding columns up to the next multiple of 8 / 4 are written as 0. */
+int imgcap_ce_fused(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
+                    float* scale, float* lse, float* loss, float* hit5, void* dlogits, int64_t ldd,
+                    void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * clip_gradient (utils.py:183-192, clamp to +-clip) + torch.optim.Adam step

@@ -210,6 +210,48 @@ def test_cross_entropy_top5(hip_device, dtype, tol):
     assert _rel(dl[:, :V].cpu(), x.grad) < tol
 
 
+@pytest.mark.parametrize("dtype,tol,V,ld", [(torch.float32, 1e-5, 9490, 9496), (torch.bfloat16, 1e-2, 9490, 9496),
+                                            (torch.bfloat16, 1e-2, 9491, 9496), (torch.float32, 1e-5, 37, 40),
+                                            (torch.bfloat16, 1e-2, 16384, 16384)])
+def test_cross_entropy_fused(hip_device, dtype, tol, V, ld):
+    """imgcap_ce_fused (train step) == torch's cross_entropy / topk / autograd, and == the
+    separate fwd + bwd kernels (same lse up to summation order, same hits, same gradient)."""
+    torch.manual_seed(5)
+    n = 203
+    logits = torch.randn(n, V) * 3
+    tgt = torch.randint(0, V, (n,))
+    tgt[::7] = -1
+    tgt[3] = V - 1  # target in the last (ragged) vector
+    lg = torch.full((n, ld), 7.0, dtype=dtype)  # padding columns must be ignored
+    lg[:, :V] = logits.to(dtype)
+    lgd, td = lg.to(hip_device), tgt.to(hip_device)
+    f32 = dict(device=hip_device, dtype=torch.float32)
+    scale, lse, loss, hit = (torch.empty(1, **f32), torch.empty(n, **f32), torch.empty(n, **f32),
+                             torch.empty(n, **f32))
+    dl = torch.full((n, ld), 5.0, dtype=dtype, device=hip_device)
+    K.ce_fused(lgd, td, V, scale, lse, loss, hit, dl)
+    lf = lg[:, :V].float()
+    valid = tgt >= 0
+    assert scale.item() == 1.0 / valid.sum().item()
+    ref_rows = F.cross_entropy(lf[valid], tgt[valid], reduction="none")
+    assert _rel(loss.cpu()[valid], ref_rows) < 1e-5
+    ref_hit = (lf.topk(5, 1).indices == tgt.clamp(min=0).view(-1, 1)).any(1) & valid
+    assert torch.equal(hit.cpu().bool(), ref_hit)
+    x = lf.clone().requires_grad_(True)
+    F.cross_entropy(x[valid], tgt[valid]).backward()
+    assert _rel(dl[:, :V].cpu().float(), x.grad) < tol
+    pad_end = (V + (8 if dtype == torch.bfloat16 else 4) - 1) // (8 if dtype == torch.bfloat16 else 4) * (
+        8 if dtype == torch.bfloat16 else 4)
+    assert torch.all(dl[:, V:pad_end] == 0)
+    # the two-kernel path on the same rows
+    lse2, loss2, hit2 = torch.empty(n, **f32), torch.empty(n, **f32), torch.empty(n, **f32)
+    K.ce_fwd(lgd, td, V, lse2, loss2, hit2)
+    assert torch.allclose(lse, lse2, rtol=1e-6, atol=1e-5) and torch.equal(hit, hit2)
+    dl2 = torch.zeros(n, ld, dtype=dtype, device=hip_device)
+    K.ce_bwd(lgd, td, V, lse2, scale, dl2)
+    assert _rel(dl[:, :V].float(), dl2[:, :V].float()) < (1e-5 if dtype == torch.float32 else 5e-3)
+
+
 def test_clamp_adam_matches_oracle(hip_device):
     from oracle import train_step
     torch.manual_seed(3)
