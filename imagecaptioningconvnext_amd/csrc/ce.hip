@@ -265,7 +265,7 @@ extern "C" int imgcap_ce_fused(int dtype, int n, int V, const void* logits, int6
                      aligned16(dlogits),
                  "imgcap_ce_fused: 16-byte aligned rows whose pitch covers ceil(V / vec) * vec elements");
   const int per = (nvec + 255) / 256;
-  IMGCAP_REQUIRE(per <= 8, "imgcap_ce_fused: V <= 16384 (bf16) / 8192 (fp32)");
+  IMGCAP_REQUIRE(per <= 12, "imgcap_ce_fused: V <= 24576 (bf16) / 12288 (fp32)");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(ce_scale_kernel, dim3(1), dim3(1024), 0, st, n, targets, scale);
 #define CEF_(T, NV)                                                                                       \
@@ -276,7 +276,8 @@ extern "C" int imgcap_ce_fused(int dtype, int n, int V, const void* logits, int6
     if (per <= 2) CEF_(T, 2);                  \
     else if (per <= 4) CEF_(T, 4);             \
     else if (per <= 6) CEF_(T, 6);             \
-    else CEF_(T, 8);                           \
+    else if (per <= 8) CEF_(T, 8);             \
+    else CEF_(T, 12);                          \
   } while (0)
   if (dtype == IMGCAP_BF16) CEF_T(bf16);
   else CEF_T(float);

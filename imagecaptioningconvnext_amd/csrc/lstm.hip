@@ -690,6 +690,7 @@ static int depth_for(int klen, int sw, bool f32) {
 
 int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used);  // lstm_persist.hip
 int lstm_persist_sync_words(const imgcap_lstm_desc& d);
+int lstm_bwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used);  // lstm_persist.hip
 
 template <typename T>
 static int lstm_fwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
@@ -748,6 +749,9 @@ static int lstm_bwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
   imgcap_lstm_desc dd = d;
   dd.x_slices = sx;
   dd.y_slices = sy;
+  bool used = false;
+  if (int rc = lstm_bwd_persistent(dd, st, &used)) return rc;
+  if (!used) {
   hipLaunchKernelGGL(cell_bwd_last_kernel<T>, pw_grid((long)d.B * d.D), dim3(256), 0, st, dd);
   IMGCAP_CHECK_LAUNCH("lstm cell_bwd_last");
   for (int t = d.T - 1; t >= 0; --t) {
@@ -764,6 +768,7 @@ static int lstm_bwd_impl(const imgcap_lstm_desc& d, hipStream_t st) {
     IMGCAP_CHECK_LAUNCH("lstm attn_bwd");
     LSTM_DEPTH_SWITCH(dpt_y, dh_cell_kernel, 4, dim3(d.D / 16, sy, nrg), dim3(256), 0, st, dd, t, ky);
     IMGCAP_CHECK_LAUNCH("lstm dh_cell");
+  }
   }
   const size_t shm2 = (size_t)d.T * PCH * sizeof(float);
   const int thr = d.A >= 512 ? 512 : ((d.A + 63) / 64) * 64;

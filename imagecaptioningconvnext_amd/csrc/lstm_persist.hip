@@ -612,6 +612,424 @@ __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d
 
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+DEV void ldf8(const float* p, float (&v)[8]) {
+  unpack8(*(const uint4*)p, *(const uint4*)(p + 4), v);
+}
+// 8 floats as T in 16-byte words (hi unused for bf16), in registers
+template <typename T> DEV void pack8(const float (&v)[8], uint4& lo, uint4& hi);
+template <> DEV void pack8<bf16>(const float (&v)[8], uint4& lo, uint4& hi) {
+  bf16x8 x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (bf16)v[j];
+  lo = __builtin_bit_cast(uint4, x);
+  hi = lo;
+}
+template <> DEV void pack8<float>(const float (&v)[8], uint4& lo, uint4& hi) {
+  lo = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+  hi = make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7]));
+}
+
+// =========================================================================================
+// Persistent BACKWARD recurrence (backpropagation through time of decoder.py:69-113): ONE
+// launch runs every step t = max(decode length) - 1 .. 0 of what imgcap_lstm_tf_bwd's per-step
+// path does with three launches per step (x_partial -> attn_bwd -> dh_cell).
+//
+// Roles (one 512-thread workgroup per CU):
+//   U blocks [0, NU):       UPB LSTM units; rows of [W_hh | W_da; W_fb] for those units resident
+//                           in LDS.  Per step: the LSTMCell backward of (row, unit) items ->
+//                           dgates_t (published), then dh_{t-1}[:, units] = dgates_t . W_hh[:,
+//                           units] + [d att2 | d gate_pre]_t . [W_da; W_fb][:, units] -- the
+//                           recurrent dh the next (earlier) step's cell backward adds to dhs.
+//   X blocks [NU, +NX):     16 columns of W_ih[:, M:] resident; dz_t[:, cols] = dgates_t . W_ih
+//                           [:, M + cols], handed to the R blocks as {value, epoch} granules.
+//   R blocks [NU+NX, +B):   batch row b; att1[b] (and enc[b] when it fits) resident; the
+//                           attention backward (decoder.py:25-31,102-105 reversed): d awe, d
+//                           gate_pre, d alpha, softmax backward -> de, d att2 (published).
+// Per step three hand-offs: dgates_t (U -> X, U), dz_t (X -> R, granules), [d att2 | d
+// gate_pre]_t (R -> U).  dgates and d att are stored write-through into dcat itself (the
+// weight-gradient GEMMs after the launch read the same rows), published with per-producer flags
+// (block_publish / block_wait, epoch = steps done + 1), and loaded with sc1 loads.  The U blocks
+// request the dgates part of their product right after its flags, so only the d att part sits
+// on the R -> U edge.  Outputs equal the per-step path's up to summation order (dcat, de, dawe,
+// dh = dL/dh0, dc = dL/dc0); steps t >= max decode length are zeros, as there.
+struct BGeo {
+  int NU, UPB, NX, NR;
+  int ldu, ldx;                 // LDS row pitches (elements) of the resident weights
+  int u_red, u_dg, x_red;       // byte offsets (U / X)
+  int r_enc, r_dz, r_dawe, r_red, r_al, r_dal, r_dtt;  // byte offsets (R); r_enc < 0: enc from global
+  int gran_off;                 // sync word offset of the [B][E] dz granules
+};
+
+struct CellIn {
+  float gi, gf, gg, go, c, cp, dhs;
+};
+
+template <typename T>
+DEV CellIn cell_in_load(const imgcap_lstm_desc& d, int t, int b, int j) {
+  const int D = d.D, Tn = d.T;
+  const long bt = (long)b * Tn + t;
+  const float* ga = d.gates + bt * 4 * D;
+  CellIn in;
+  in.gi = ga[j]; in.gf = ga[D + j]; in.gg = ga[2 * D + j]; in.go = ga[3 * D + j];
+  in.c = d.cs[bt * D + j];
+  in.cp = t == 0 ? d.c0[(long)b * D + j] : d.cs[(bt - 1) * D + j];
+  in.dhs = to_f(((const T*)d.dhs)[bt * D + j]);
+  return in;
+}
+
+template <typename T, int MT>
+__global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d, BGeo g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* s_ok = (int*)smem;
+  const int B = d.B, P = d.P, E = d.E, A = d.A, D = d.D, Tn = d.T;
+  const int KY = A + E, K4 = 4 * D, W3 = KY + K4;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int* err = d.sync;
+  int* fdg = d.sync + SYNC_HDR;  // U blocks: dgates_t published
+  int* fdt = fdg + g.NU;         // R blocks: [d att2 | d gate_pre]_t published
+  if (tid < 64) {
+    int m = 0;
+    for (int i = lane; i < B; i += 64) m = max(m, d.dl[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if (lane == 0) s_ok[1] = m;
+  }
+  __syncthreads();
+  const int Tmax = max(0, min(Tn, s_ok[1]));
+  const int blk = blockIdx.x;
+  constexpr int VEC = VecOf<T>::N;
+  constexpr int KP = PWV / MT;                      // K parts: wave w -> row tile w % MT, K part w / MT
+  constexpr int KCH = sizeof(T) == 2 ? 16 : 8;      // A fragments requested per round trip
+  const rsrc_t r_dcat = make_rsrc(d.dcat, (uint32_t)((long)B * Tn * W3 * sizeof(T)));
+  const rsrc_t r_gr = make_rsrc(d.sync + g.gran_off, (uint32_t)((long)B * E * 8));
+  const int mi = w % MT, kp = w / MT;
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  const int m = mi * 16 + fr;
+  const bool mok = m < B;
+  const int nk1 = K4 / 32, nk2 = (KY + 31) / 32;   // k-steps of the dgates / d att parts
+  const int per1 = (nk1 + KP - 1) / KP, per2 = (nk2 + KP - 1) / KP;
+  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
+
+  if (blk < g.NU + g.NX) {
+    // ======================= U and X workgroups ==========================================
+    const bool isU = blk < g.NU;
+    const int UPB = g.UPB, u0 = blk * UPB;
+    const int x0 = (blk - g.NU) * 16;
+    const int ld = isU ? g.ldu : g.ldx;
+    const int KW = isU ? K4 + KY : K4;  // resident k per weight row
+    const int nrows = isU ? UPB : 16;
+    T* wr = (T*)(smem + 16);
+    float* red = (float*)(smem + (isU ? g.u_red : g.x_red));  // [KP][16 * MT][20]
+    T* dgs = (T*)(smem + g.u_dg);                              // U: [B][4][UPB] staged dgates
+    {
+      const int cpr = KW / VEC;
+      for (int i = tid; i < nrows * cpr; i += PT) {
+        const int c = i / cpr, k = (i % cpr) * VEC;
+        uint4 v = zero4;
+        if (isU) {
+          const int j = u0 + c;
+          v = k < K4 ? *(const uint4*)((const T*)d.w_zh_t + (long)(E + j) * K4 + k)
+                     : *(const uint4*)((const T*)d.w_att_t + (long)j * KY + (k - K4));
+        } else if (x0 + c < E) {
+          v = *(const uint4*)((const T*)d.w_zh_t + (long)(x0 + c) * K4 + k);
+        }
+        *(uint4*)(wr + c * ld + k) = v;
+      }
+    }
+    // this thread's (row, unit) item of the cell backward (U)
+    const int ib = tid / UPB, ijj = tid % UPB, ij = u0 + ijj;
+    const bool iok = isU && tid < B * UPB;
+    const int dlb = iok ? d.dl[ib] : 0;
+    float dc = 0.f, dh_rec = 0.f;
+    CellIn cin{};
+    if (iok && Tmax > 0 && Tmax - 1 < dlb) cin = cell_in_load<T>(d, Tmax - 1, ib, ij);
+    const bool bok = fr < nrows;  // B fragment rows past UPB are zero
+    __syncthreads();
+    for (int t = Tmax - 1; t >= 0; --t) {
+      const int ep = Tmax - t;
+      const long mbt = (long)m * Tn + t;
+      if (isU) {
+        // ---- LSTMCell backward of step t (cell_bwd_apply of lstm.hip) ----
+        if (iok) {
+          float dg[4] = {0.f, 0.f, 0.f, 0.f};
+          if (t < dlb) {
+            const float dh = cin.dhs + dh_rec;
+            const float tc = tanhf(cin.c);
+            const float dct = dc + dh * cin.go * (1.f - tc * tc);
+            dg[0] = dct * cin.gg * cin.gi * (1.f - cin.gi);
+            dg[1] = dct * cin.cp * cin.gf * (1.f - cin.gf);
+            dg[2] = dct * cin.gi * (1.f - cin.gg * cin.gg);
+            dg[3] = dh * tc * cin.go * (1.f - cin.go);
+            dc = dct * cin.gf;
+          } else {
+            dc = 0.f;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dgs[(ib * 4 + q) * UPB + ijj] = from_f<T>(dg[q]);
+        }
+        __syncthreads();
+        // dgates_t rows of this block's units -> dcat (write-through): row b, gate q, UPB elements
+        const int pieces = UPB * (int)sizeof(T) / 16;
+        for (int i = tid; i < B * 4 * pieces; i += PT) {
+          const int pc = i % pieces, bq = i / pieces, b = bq / 4, q = bq % 4;
+          const uint4 v = *(const uint4*)(dgs + bq * UPB + pc * VEC);
+          const long off = ((long)b * Tn + t) * W3 + KY + (long)q * D + u0 + pc * VEC;
+          st_wt(r_dcat, (uint32_t)(off * sizeof(T)), v);
+        }
+        block_publish(fdg + blk, ep);
+        // cell inputs of the next (earlier) step: independent of every hand-off
+        if (iok && t > 0 && t - 1 < dlb) cin = cell_in_load<T>(d, t - 1, ib, ij);
+      }
+      // ---- dgates_t . W[:, cols]  (U: W_hh part of dh_{t-1}; X: dz_t) ----
+      if (!block_wait(fdg, g.NU, ep, err, s_ok + 2)) return;
+      f32x4 acc[2];
+      acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      {
+        const int ks0 = kp * per1, ks1 = min(nk1, ks0 + per1);
+        for (int ks = ks0; ks < ks1; ks += KCH) {
+          Frag<T> fa[KCH];
+#pragma unroll
+          for (int i = 0; i < KCH; ++i) {
+            const int k0 = (ks + i) * 32 + fk;
+            fa[i] = frag_wt<T>(r_dcat, (uint32_t)((mbt * W3 + KY + k0) * sizeof(T)), mok && ks + i < ks1);
+          }
+#pragma unroll
+          for (int i = 0; i < KCH; ++i) {  // steps past ks1 have zero A fragments
+            const int k0 = (ks + i) * 32 + fk;
+            Frag<T> fb = lds_frag_k<T>(wr + (bok ? fr : 0) * ld, k0, K4);
+            if (!bok) fb = frag_from<T>(zero4, zero4);
+            mma(acc[i & 1], fa[i], fb);
+          }
+        }
+      }
+      if (isU) {
+        // ---- + [d att2 | d gate_pre]_t . [W_da; W_fb][:, units]: after the R blocks ----
+        if (!block_wait(fdt, g.NR, ep, err, s_ok + 3)) return;
+        const int ks0 = kp * per2, ks1 = min(nk2, ks0 + per2);
+        for (int ks = ks0; ks < ks1; ks += KCH) {
+          Frag<T> fa[KCH];
+#pragma unroll
+          for (int i = 0; i < KCH; ++i) {
+            const int k0 = (ks + i) * 32 + fk;
+            fa[i] = frag_wt<T>(r_dcat, (uint32_t)((mbt * W3 + k0) * sizeof(T)), mok && ks + i < ks1 && k0 < KY);
+          }
+#pragma unroll
+          for (int i = 0; i < KCH; ++i) {
+            const int k0 = (ks + i) * 32 + fk;
+            Frag<T> fb = lds_frag_k<T>(wr + (bok ? fr : 0) * ld + K4, k0, KY);
+            if (!bok) fb = frag_from<T>(zero4, zero4);
+            mma(acc[i & 1], fa[i], fb);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(kp * 16 * MT + mi * 16 + 4 * (lane >> 4) + r) * 20 + fr] = acc[0][r] + acc[1][r];
+      __syncthreads();
+      if (isU) {
+        if (iok) {
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < KP; ++q) s += red[(q * 16 * MT + ib) * 20 + ijj];
+          dh_rec = s;
+          if (t == 0) d.dh[(long)ib * D + ij] = s;  // dL/dh0
+        }
+      } else {
+        // dz_t granules {value, epoch} of this block's 16 columns, two per 16-byte store
+        for (int i = tid; i < B * 8; i += PT) {
+          const int b = i / 8, c = (i % 8) * 2;
+          float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+          for (int q = 0; q < KP; ++q) {
+            v0 += red[(q * 16 * MT + b) * 20 + c];
+            v1 += red[(q * 16 * MT + b) * 20 + c + 1];
+          }
+          if (x0 + c < E)
+            st_wt(r_gr, (uint32_t)(((long)b * E + x0 + c) * 8),
+                  make_uint4(__float_as_uint(v0), (unsigned)ep, __float_as_uint(v1), (unsigned)ep));
+        }
+      }
+      __syncthreads();  // red is rewritten next step
+    }
+    if (isU) {
+      if (iok) d.dc[(long)ib * D + ij] = dc;  // dL/dc0
+      // steps past every decode length: zero dgates rows (as the per-step path leaves them)
+      for (int i = tid; i < B * (Tn - Tmax) * 4 * UPB; i += PT) {
+        const int jj = i % UPB, rest = i / UPB, q = rest % 4, rest2 = rest / 4, b = rest2 % B, t = Tmax + rest2 / B;
+        ((T*)d.dcat)[((long)b * Tn + t) * W3 + KY + (long)q * D + u0 + jj] = from_f<T>(0.f);
+      }
+      if (Tmax == 0 && iok) {
+        d.dh[(long)ib * D + ij] = 0.f;
+        d.dc[(long)ib * D + ij] = 0.f;
+      }
+    }
+    return;
+  }
+
+  // ======================= R workgroup: attention backward of row b ======================
+  const int b = blk - g.NU - g.NX;
+  T* att1s = (T*)(smem + 16);                       // [P][A]
+  const bool enc_lds = g.r_enc >= 0;
+  const T* encs = enc_lds ? (const T*)(smem + g.r_enc) : (const T*)d.enc + (long)b * P * E;  // [P][E]
+  float* dzs = (float*)(smem + g.r_dz);             // [E]
+  float* dawes = (float*)(smem + g.r_dawe);         // [E]
+  float* red = (float*)(smem + g.r_red);            // [GA][A]
+  float* als = (float*)(smem + g.r_al);             // [64]
+  float* dal = (float*)(smem + g.r_dal);            // [64]
+  T* dtt = (T*)(smem + g.r_dtt);                    // [A] d att2 staged for 16-byte stores
+  {
+    const T* a1 = (const T*)d.att1 + (long)b * P * A;
+    for (int i = tid; i < P * A / VEC; i += PT) *(uint4*)(att1s + i * VEC) = *(const uint4*)(a1 + i * VEC);
+    if (enc_lds) {
+      const T* en = (const T*)d.enc + (long)b * P * E;
+      for (int i = tid; i < P * E / VEC; i += PT) *(uint4*)((T*)encs + i * VEC) = *(const uint4*)(en + i * VEC);
+    }
+  }
+  if (tid == 0) s_ok[2] = 1;
+  const int dlb = d.dl[b];
+  const int NVE = E / 8, NVA = A / 8, GA = PT / NVA;
+  const int va = tid % NVA, pga = tid / NVA;
+  const float wf_a = tid < A ? d.w_f[tid] : 0.f;
+  __syncthreads();
+  for (int t = Tmax - 1; t >= 0; --t) {
+    const int ep = Tmax - t;
+    const long bt = (long)b * Tn + t;
+    float* dawe_o = d.dawe ? d.dawe + ((long)b * (Tn + 1) + t) * E : nullptr;
+    if (t >= dlb) {  // past this row's decode length: zero outputs, publish at once
+      for (int i = tid; i < KY / VEC; i += PT) st_wt(r_dcat, (uint32_t)((bt * W3 + i * VEC) * sizeof(T)), zero4);
+      if (tid < P) d.de[bt * P + tid] = 0.f;
+      if (dawe_o)
+        for (int i = tid; i < E; i += PT) dawe_o[i] = 0.f;
+      block_publish(fdt + b, ep);
+      continue;
+    }
+    // ---- operands independent of the hand-off, requested first ----
+    const float* g1 = d.g1 + bt * W3;
+    float gp[8], aw[8], a2[8];
+    const bool vth = tid < NVE;
+    if (vth) {
+      ldf8(g1 + A + tid * 8, gp);
+      ldf8(d.awe + bt * E + tid * 8, aw);
+    }
+    ldf8(g1 + va * 8, a2);  // att2 slice of this thread's 8 units
+    float alpha_in = 0.f, dalpha_in = 0.f;
+    if (tid < P) {
+      alpha_in = d.alphas[bt * P + tid];
+      if (d.dalpha) dalpha_in = d.dalpha[bt * P + tid];
+    }
+    // ---- dz_t[b] from the X blocks' granules ----
+    {
+      bool bad = false;
+      for (int j = tid; j < E / 2; j += PT) {
+        const uint32_t off = (uint32_t)(((long)b * E + 2 * j) * 8);
+        for (int spins = 0;; ++spins) {
+          const uint4 q = ld_wt(r_gr, off);
+          if (q.y == (unsigned)ep && q.w == (unsigned)ep) {
+            dzs[2 * j] = __uint_as_float(q.x);
+            dzs[2 * j + 1] = __uint_as_float(q.z);
+            break;
+          }
+          if ((spins & 255) == 255 &&
+              (spins >= SPIN_LIMIT || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            bad = true;
+            break;
+          }
+        }
+        if (bad) break;
+      }
+      if (bad) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_ok[2] = 0;
+      }
+      __syncthreads();
+      if (s_ok[2] == 0) return;
+    }
+    // ---- d awe = dz * sigmoid(gate), d gate_pre = dz * awe * s (1 - s) ----
+    if (vth) {
+      float da[8], dg[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dz = dzs[tid * 8 + j];
+        const float s = sigmoidf_(gp[j]);
+        da[j] = dz * s;
+        dg[j] = dz * aw[j] * s * (1.f - s);
+        dawes[tid * 8 + j] = da[j];
+      }
+      uint4 lo, hi;
+      pack8<T>(dg, lo, hi);
+      const uint32_t off = (uint32_t)((bt * W3 + A + tid * 8) * sizeof(T));
+      st_wt(r_dcat, off, lo);
+      if (sizeof(T) == 4) st_wt(r_dcat, off + 16, hi);
+      if (dawe_o) {
+        *(f32x4*)(dawe_o + tid * 8) = f32x4{da[0], da[1], da[2], da[3]};
+        *(f32x4*)(dawe_o + tid * 8 + 4) = f32x4{da[4], da[5], da[6], da[7]};
+      }
+    }
+    if (tid < P) {
+      als[tid] = alpha_in;
+      dal[tid] = dalpha_in;  // upstream d alpha
+    }
+    __syncthreads();
+    // ---- d alpha_p += enc_p . d awe: wave w takes pixels w, w + 8, ..; lane = 8-channel vectors ----
+    {
+      for (int p = w; p < P; p += PWV) {
+        float s = 0.f;
+        for (int v = lane; v < NVE; v += 64) {
+          float x[8];
+          ld_g<T, 8>(encs + (long)p * E + v * 8, x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s += x[j] * dawes[v * 8 + j];
+        }
+        s = wave_sum_dpp(s);
+        if (lane == 0) dal[p] += s;
+      }
+    }
+    __syncthreads();
+    if (w == 0) {  // softmax backward -> d score
+      const float a = lane < P ? als[lane] : 0.f;
+      const float da = lane < P ? dal[lane] : 0.f;
+      const float dot = wave_sum_dpp(a * da);
+      if (lane < P) {
+        const float de = a * (da - dot);
+        dal[lane] = de;
+        d.de[bt * P + lane] = de;
+      }
+    }
+    __syncthreads();
+    // ---- d att2[a] = w_f[a] * sum_p de_p [att1[p, a] + att2[a] > 0] ----
+    if (pga < GA) {
+      float sacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int p = pga; p < P; p += GA) {
+        float x[8];
+        ld_g<T, 8>(att1s + p * A + va * 8, x);
+        const float de = dal[p];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sacc[j] += (x[j] + a2[j] > 0.f) ? de : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[pga * A + va * 8 + j] = sacc[j];
+    }
+    __syncthreads();
+    if (tid < A) {
+      float s = 0.f;
+      for (int q = 0; q < GA; ++q) s += red[q * A + tid];
+      dtt[tid] = from_f<T>(s * wf_a);
+    }
+    __syncthreads();
+    for (int i = tid; i < A / VEC; i += PT)
+      st_wt(r_dcat, (uint32_t)((bt * W3 + i * VEC) * sizeof(T)), *(const uint4*)(dtt + i * VEC));
+    block_publish(fdt + b, ep);
+  }
+  // steps past every decode length: zero outputs
+  for (int t = Tmax; t < Tn; ++t) {
+    const long bt = (long)b * Tn + t;
+    for (int i = tid; i < KY; i += PT) ((T*)d.dcat)[bt * W3 + i] = from_f<T>(0.f);
+    if (tid < P) d.de[bt * P + tid] = 0.f;
+    if (d.dawe)
+      for (int i = tid; i < E; i += PT) d.dawe[((long)b * (Tn + 1) + t) * E + i] = 0.f;
+  }
+}
+
 }  // namespace
 
 // Geometry + LDS plan; false when the shape is outside what the persistent kernel covers.
@@ -728,12 +1146,109 @@ int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   return rc;
 }
 
-int lstm_persist_sync_words(const imgcap_lstm_desc& d) {
-  Geo g;
+// ---- backward ------------------------------------------------------------------------------
+static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, int& mt, int& words) {
+  const size_t LDS_MAX = 160 * 1024;
+  if (d.B < 1 || d.B > 32 || d.P > 64 || d.A > 512 || d.A % 8 || d.E % 16 || d.D % 16 || !d.w_zh_t || !d.w_att_t)
+    return false;
+  mt = d.B <= 16 ? 1 : 2;
+  const int KY = d.A + d.E, K4 = 4 * d.D;
+  if (KY % 8) return false;
+  const int pad = 16 / esz;
+  // U: 16 units per block in bf16, 8 in fp32 (rows of 4D + A + E elements in LDS)
+  g.UPB = esz == 2 ? 16 : 8;
+  if (d.D % g.UPB || d.B * g.UPB > PT) return false;
+  g.NU = d.D / g.UPB;
+  g.NX = d.E / 16;
+  g.NR = d.B;
+  if (g.NU + g.NX + g.NR > 256) return false;
+  g.ldu = K4 + KY + pad;
+  g.ldx = K4 + pad;
+  const size_t red = (size_t)(PWV / mt) * 16 * mt * 20 * 4;
+  size_t o = align16(16 + (size_t)g.UPB * g.ldu * esz);
+  g.u_red = (int)o;
+  o = align16(o + red);
+  g.u_dg = (int)o;
+  o = align16(o + (size_t)d.B * 4 * g.UPB * esz);
+  const size_t u = o;
+  o = align16(16 + (size_t)16 * g.ldx * esz);
+  g.x_red = (int)o;
+  const size_t x = align16(o + red);
+  // R: att1[b] always, enc[b] when it fits
+  const int GA = PT / (d.A / 8);
+  size_t r = 0;
+  for (int enc_in = 1; enc_in >= 0; --enc_in) {
+    o = align16(16 + (size_t)d.P * d.A * esz);
+    g.r_enc = enc_in ? (int)o : -1;
+    if (enc_in) o = align16(o + (size_t)d.P * d.E * esz);
+    g.r_dz = (int)o;
+    o = align16(o + (size_t)d.E * 4);
+    g.r_dawe = (int)o;
+    o = align16(o + (size_t)d.E * 4);
+    g.r_red = (int)o;
+    o = align16(o + (size_t)GA * d.A * 4);
+    g.r_al = (int)o;
+    o = align16(o + 64 * 4);
+    g.r_dal = (int)o;
+    o = align16(o + 64 * 4);
+    g.r_dtt = (int)o;
+    o = align16(o + (size_t)d.A * esz);
+    r = o;
+    if (r <= LDS_MAX) break;
+  }
+  lds = std::max(std::max(std::max(u, x), r), (size_t)81 * 1024);  // one workgroup per CU
+  if (lds > LDS_MAX) return false;
+  g.gran_off = (SYNC_HDR + g.NU + g.NR + 63) / 64 * 64;
+  words = g.gran_off + d.B * d.E * 2;
+  return true;
+}
+
+template <typename T, int MT>
+static int launch_bwd_persist(const imgcap_lstm_desc& d, const BGeo& g, size_t lds, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)lstm_bwd_persist_kernel<T, MT>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return fail(IMGCAP_EINVAL, "lstm persistent backward: cannot raise the dynamic LDS limit");
+    attr = true;
+  }
+  hipLaunchKernelGGL((lstm_bwd_persist_kernel<T, MT>), dim3(g.NU + g.NX + g.NR), dim3(PT), lds, st, d, g);
+  IMGCAP_CHECK_LAUNCH("lstm persistent backward");
+  return 0;
+}
+
+// Runs the whole backward recurrence in one launch when the shape fits (outputs: dcat, de,
+// dawe, dh, dc); *used = false leaves the call to the per-step path.
+int lstm_bwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
+  *used = false;
+  static const int env = [] {
+    const char* e = getenv("IMGCAP_LSTM_BWD_PERSIST");
+    return e ? atoi(e) : 1;
+  }();
+  if (!env || d.T < 2 || !d.sync) return 0;
+  const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
+  BGeo g;
   size_t lds;
   int mt, words;
+  if (!bwd_plan(d, esz, g, lds, mt, words)) return 0;
+  if (d.sync_words < words) return 0;  // a buffer sized by an older query: per-step path
+  IMGCAP_REQUIRE(aligned16(d.sync) && aligned16(d.dcat), "lstm persistent backward: 16-byte aligned sync / dcat");
+  if (hipMemsetAsync(d.sync, 0, align16((size_t)words * 4), st) != hipSuccess)
+    return fail(IMGCAP_EINVAL, "lstm persistent backward: memset of the sync words failed");
+  *used = true;
+  if (esz == 2) return mt == 1 ? launch_bwd_persist<bf16, 1>(d, g, lds, st) : launch_bwd_persist<bf16, 2>(d, g, lds, st);
+  return mt == 1 ? launch_bwd_persist<float, 1>(d, g, lds, st) : launch_bwd_persist<float, 2>(d, g, lds, st);
+}
+
+int lstm_persist_sync_words(const imgcap_lstm_desc& d) {
+  Geo g;
+  BGeo bg;
+  size_t lds;
+  int mt, words = 0, bwords = 0;
   const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
-  return persist_plan(d, esz, g, lds, mt, words) ? words : 0;
+  if (!persist_plan(d, esz, g, lds, mt, words)) words = 0;
+  if (!bwd_plan(d, esz, bg, lds, mt, bwords)) bwords = 0;
+  return std::max(words, bwords);
 }
 
 }  // namespace imgcap

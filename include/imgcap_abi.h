@@ -294,7 +294,7 @@ int imgcap_ce_bwd(int dtype, int n, int V, const void* logits, int64_t ld, const
  * target) is computed first and written, then lse / loss / hit5 as imgcap_ce_fwd and
  * dlogits = (softmax - onehot) * scale[0] as imgcap_ce_bwd; one read + one write of [n, V]
  * (train.py:266-276 -- the loss, its gradient and utils.py:248-250's top-5 of one step).
- * Rows: 16-byte aligned, pitches multiples of 8 (bf16) / 4 (fp32) elements, V <= 16384 / 8192;
+ * Rows: 16-byte aligned, pitches multiples of 8 (bf16) / 4 (fp32) elements, V <= 24576 / 12288;
  * dlogits' padding columns up to the next multiple of 8 / 4 are written as 0. */
 int imgcap_ce_fused(int dtype, int n, int V, const void* logits, int64_t ld, const int64_t* targets,
                     float* scale, float* lse, float* loss, float* hit5, void* dlogits, int64_t ldd,

@@ -180,3 +180,47 @@ def test_lstm_persistent_recurrence_matches_per_step(hip_device, dtype, B):
         assert _rel(a[:, :tm + lo], b[:, :tm + lo]) < tol, k
         assert torch.all(a[:, tm + lo:] == 0), k
     assert _rel(g1[:, :tm], s["g1"][:, :tm, :A + E]) < tol
+
+
+@pytest.mark.parametrize("dtype,B", [(torch.float32, 5), (torch.bfloat16, 32), (torch.float32, 24),
+                                     (torch.bfloat16, 13)])
+def test_lstm_persistent_backward_matches_per_step(hip_device, dtype, B):
+    """The one-launch backward recurrence (lstm_bwd_persist_kernel) against the per-step launches
+    on the same descriptor: dcat ([d att2 | d gate_pre | dgates] per step), de, dawe, dL/dh0,
+    dL/dc0 and the attention-parameter partials computed from them; zeros past max(dl)."""
+    import ctypes
+    from imagecaptioningconvnext_amd import _abi
+    from imagecaptioningconvnext_amd import kernels as K
+    E, A, D, Em, V, L = (768, 512, 512, 512, 300, 24) if B == 32 else (64, 32, 48, 32, 100, 14)
+    p = make_params(shapes.lstm_decoder_shapes(E, A, D, Em, V), 8)
+    dec = _decoder(dict(E=E, A=A, D=D, Em=Em, V=V), p, dtype, hip_device)
+    eng = dec.engine()
+    enc = make_features((B, 7, 7, E), 9).to(hip_device).to(dtype)
+    lens = [L - 3 - (i * 5) % (L - 6) for i in range(B)]  # maximum L - 3 < L: skipped tail steps
+    caps, caplens = make_captions(B, L, lens, V, 10)
+    s = eng.forward(enc, caps.to(hip_device), caplens.to(hip_device), fixed_T=True)
+    eng.backward(s, want_denc=True)
+    torch.cuda.synchronize()
+    d = s["desc"]
+    assert d.sync and eng.sync_error() == 0
+    bufs = s["bwd_bufs"]
+    names = ("dcat", "de", "dh", "dc", "datt1", "dwf", "dbea")
+    got = {k: bufs[k].clone() for k in names}
+    T = s["T"]
+    got["dawe"] = bufs["dawe"][:, :T].clone()
+    for k in names:
+        bufs[k].fill_(float("nan"))
+    bufs["dawe"][:, :T].fill_(float("nan"))
+    d.sync, d.sync_words = None, 0
+    _abi.call("imgcap_lstm_tf_bwd", ctypes.byref(d), K.stream())
+    torch.cuda.synchronize()
+    tm = max(lens) - 1
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    for k in names + ("dawe",):
+        a, b = got[k].float(), (bufs[k][:, :T] if k == "dawe" else bufs[k]).float()
+        assert torch.isfinite(a).all(), k
+        if k in ("dcat", "de", "dawe"):
+            assert _rel(a[:, :tm], b[:, :tm]) < tol, k
+            assert torch.all(a[:, tm:] == 0), k
+        else:
+            assert _rel(a, b) < tol, k
