@@ -449,7 +449,12 @@ static int glds_stages() {
 }
 
 // 64x64 tile stages (IMGCAP_GLDS64_STAGES, 2-4) and the XCD tile order of the LDS-DMA tiles
-// (IMGCAP_GEMM_ORDER: 0 row-major bands, 1 grouped rectangles; glds_tile_order)
+// (IMGCAP_GEMM_ORDER: 0 row-major bands, 1 grouped rectangles, 2 = auto (default): grouped for
+// wide grids, nx >= 1.5 ny; glds_tile_order).  Measured at C2 (tools/gpu/gemm_knobs.sh, 64x64
+// tiles): grouped 149x26 (vocab logits) 43.1 -> 35.2 us, 48x25 20.1 -> 18.9; on tall grids
+// (6x98, 12x25, 24x98) row-major bands are already the better order (each XCD reads its own
+// rows once and the narrow B whole): grouped 19.0 -> 20.3, 23.1 -> 24.0, 22.7 -> 23.1.  More
+// 64x64 stages lose: 3 stages 703 -> 734 us over the step's GEMMs, 4 stages 887 us.
 static int glds64_stages() {
   static const int s = [] {
     const char* e = getenv("IMGCAP_GLDS64_STAGES");
@@ -461,14 +466,15 @@ static int glds64_stages() {
 static int gemm_order() {
   static const int o = [] {
     const char* e = getenv("IMGCAP_GEMM_ORDER");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   return o;
 }
 // band height in tile rows for a grid of nx x ny tiles (glds_tile_order): each XCD's run of
 // ~nx*ny/8 tiles as a square-ish rectangle; 0 = row-major
 static int glds_group(int nx, int ny) {
-  if (gemm_order() == 0 || nx * ny < 64) return 0;
+  const int o = gemm_order();
+  if (o == 0 || nx * ny < 64 || (o == 2 && 2 * nx < 3 * ny)) return 0;
   const double run = (double)nx * ny / 8.0;
   int g = (int)(std::sqrt(run) + 0.5);
   return std::max(1, std::min(g, ny));
