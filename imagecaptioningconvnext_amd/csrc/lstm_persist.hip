@@ -658,7 +658,15 @@ struct BGeo {
   int u_red, u_dg, x_red;       // byte offsets (U / X)
   int r_enc, r_dz, r_dawe, r_red, r_al, r_dal, r_dtt;  // byte offsets (R); r_enc < 0: enc from global
   int gran_off;                 // sync word offset of the [B][E] dz granules
+  long long* stamps;            // diagnostics (IMGCAP_LSTM_STAMPS=1): [role U/X/R][step][16]
 };
+
+// thread 0 of the first U, X and R block records s_memrealtime at phase edges of step t
+DEV void bstamp(const BGeo& g, int role, int t, int k) {
+  const int b0 = role == 0 ? 0 : role == 1 ? g.NU : g.NU + g.NX;
+  if (g.stamps && threadIdx.x == 0 && (int)blockIdx.x == b0 && t < 64)
+    g.stamps[(role * 64 + t) * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
 
 struct CellIn {
   float gi, gf, gg, go, c, cp, dhs;
@@ -745,9 +753,11 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
     if (iok && Tmax > 0 && Tmax - 1 < dlb) cin = cell_in_load<T>(d, Tmax - 1, ib, ij);
     const bool bok = fr < nrows;  // B fragment rows past UPB are zero
     __syncthreads();
+    const int role = isU ? 0 : 1;
     for (int t = Tmax - 1; t >= 0; --t) {
       const int ep = Tmax - t;
       const long mbt = (long)m * Tn + t;
+      bstamp(g, role, t, 0);
       if (isU) {
         // ---- LSTMCell backward of step t (cell_bwd_apply of lstm.hip) ----
         if (iok) {
@@ -777,11 +787,13 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
           st_wt(r_dcat, (uint32_t)(off * sizeof(T)), v);
         }
         block_publish(fdg + blk, ep);
+        bstamp(g, 0, t, 1);
         // cell inputs of the next (earlier) step: independent of every hand-off
         if (iok && t > 0 && t - 1 < dlb) cin = cell_in_load<T>(d, t - 1, ib, ij);
       }
       // ---- dgates_t . W[:, cols]  (U: W_hh part of dh_{t-1}; X: dz_t) ----
       if (!block_wait(fdg, g.NU, ep, err, s_ok + 2)) return;
+      bstamp(g, role, t, 2);
       f32x4 acc[2];
       acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
       {
@@ -802,9 +814,11 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
           }
         }
       }
+      bstamp(g, role, t, 3);
       if (isU) {
         // ---- + [d att2 | d gate_pre]_t . [W_da; W_fb][:, units]: after the R blocks ----
         if (!block_wait(fdt, g.NR, ep, err, s_ok + 3)) return;
+        bstamp(g, 0, t, 4);
         const int ks0 = kp * per2, ks1 = min(nk2, ks0 + per2);
         for (int ks = ks0; ks < ks1; ks += KCH) {
           Frag<T> fa[KCH];
@@ -850,6 +864,7 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
         }
       }
       __syncthreads();  // red is rewritten next step
+      bstamp(g, role, t, 5);
     }
     if (isU) {
       if (iok) d.dc[(long)ib * D + ij] = dc;  // dL/dc0
@@ -903,6 +918,7 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
       block_publish(fdt + b, ep);
       continue;
     }
+    bstamp(g, 2, t, 0);
     // ---- operands independent of the hand-off, requested first ----
     const float* g1 = d.g1 + bt * W3;
     float gp[8], aw[8], a2[8];
@@ -944,6 +960,7 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
       __syncthreads();
       if (s_ok[2] == 0) return;
     }
+    bstamp(g, 2, t, 1);
     // ---- d awe = dz * sigmoid(gate), d gate_pre = dz * awe * s (1 - s) ----
     if (vth) {
       float da[8], dg[8];
@@ -970,8 +987,45 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
       dal[tid] = dalpha_in;  // upstream d alpha
     }
     __syncthreads();
+    bstamp(g, 2, t, 2);
     // ---- d alpha_p += enc_p . d awe: wave w takes pixels w, w + 8, ..; lane = 8-channel vectors ----
-    {
+    if (enc_lds && sizeof(T) == 2) {
+      // enc rows resident in LDS (bf16): per 64-channel-vector slot, every pixel's 16-byte piece
+      // is requested before the first product, the dot partials of the wave's <= 8 pixels are
+      // kept in registers and reduced by DPP at the end (one round trip, no serial chain)
+      const T* el = (const T*)(smem + g.r_enc);
+      constexpr int PPW = 64 / PWV;  // pixels per wave (P <= 64)
+      float part[PPW];
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) part[i] = 0.f;
+      for (int v0 = 0; v0 < NVE; v0 += 64) {  // wave-uniform
+        const int v = v0 + lane;
+        const bool vok = v < NVE;
+        float dv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dv[j] = vok ? dawes[v * 8 + j] : 0.f;
+        uint4 ev[PPW];
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+          const int p = min(w + PWV * i, P - 1);
+          ev[i] = vok ? *(const uint4*)(el + p * E + v * 8) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+          const bf16x8 x = __builtin_bit_cast(bf16x8, ev[i]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) part[i] += (float)x[j] * dv[j];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        const int p = w + PWV * i;
+        if (p < P) {  // wave-uniform
+          const float s = wave_sum_dpp(part[i]);
+          if (lane == 0) dal[p] += s;
+        }
+      }
+    } else {
       for (int p = w; p < P; p += PWV) {
         float s = 0.f;
         for (int v = lane; v < NVE; v += 64) {
@@ -985,6 +1039,7 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
       }
     }
     __syncthreads();
+    bstamp(g, 2, t, 3);
     if (w == 0) {  // softmax backward -> d score
       const float a = lane < P ? als[lane] : 0.f;
       const float da = lane < P ? dal[lane] : 0.f;
@@ -999,12 +1054,30 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
     // ---- d att2[a] = w_f[a] * sum_p de_p [att1[p, a] + att2[a] > 0] ----
     if (pga < GA) {
       float sacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int p = pga; p < P; p += GA) {
-        float x[8];
-        ld_g<T, 8>(att1s + p * A + va * 8, x);
-        const float de = dal[p];
+      if (sizeof(T) == 2 && GA == PWV) {  // A = 512: <= 8 pixels per thread, loads issued first
+        constexpr int PPT = 64 / PWV;
+        uint4 xv[PPT];
+        float dep[PPT];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sacc[j] += (x[j] + a2[j] > 0.f) ? de : 0.f;
+        for (int i = 0; i < PPT; ++i) {
+          const int p = pga + GA * i;
+          xv[i] = *(const uint4*)(att1s + min(p, P - 1) * A + va * 8);
+          dep[i] = p < P ? dal[min(p, P - 1)] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) {
+          const bf16x8 x = __builtin_bit_cast(bf16x8, xv[i]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sacc[j] += ((float)x[j] + a2[j] > 0.f) ? dep[i] : 0.f;
+        }
+      } else {
+        for (int p = pga; p < P; p += GA) {
+          float x[8];
+          ld_g<T, 8>(att1s + p * A + va * 8, x);
+          const float de = dal[p];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sacc[j] += (x[j] + a2[j] > 0.f) ? de : 0.f;
+        }
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) red[pga * A + va * 8 + j] = sacc[j];
@@ -1016,9 +1089,11 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
       dtt[tid] = from_f<T>(s * wf_a);
     }
     __syncthreads();
+    bstamp(g, 2, t, 4);
     for (int i = tid; i < A / VEC; i += PT)
       st_wt(r_dcat, (uint32_t)((bt * W3 + i * VEC) * sizeof(T)), *(const uint4*)(dtt + i * VEC));
     block_publish(fdt + b, ep);
+    bstamp(g, 2, t, 5);
   }
   // steps past every decode length: zero outputs
   for (int t = Tmax; t < Tn; ++t) {
@@ -1232,6 +1307,16 @@ int lstm_bwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   int mt, words;
   if (!bwd_plan(d, esz, g, lds, mt, words)) return 0;
   if (d.sync_words < words) return 0;  // a buffer sized by an older query: per-step path
+  static const bool stamps = getenv("IMGCAP_LSTM_STAMPS") && atoi(getenv("IMGCAP_LSTM_STAMPS"));
+  g.stamps = nullptr;
+  if (stamps && d.T <= 64) {  // same diagnostics area as the forward's: after max(fwd, bwd) words
+    Geo fg;
+    size_t fl;
+    int fmt, fwords = 0;
+    if (!persist_plan(d, esz, fg, fl, fmt, fwords)) fwords = 0;
+    const int base = (std::max(words, fwords) + 63) / 64 * 64 + 64;
+    if (d.sync_words >= base + 3 * 64 * 16 * 2) g.stamps = (long long*)(d.sync + base);
+  }
   IMGCAP_REQUIRE(aligned16(d.sync) && aligned16(d.dcat), "lstm persistent backward: 16-byte aligned sync / dcat");
   if (hipMemsetAsync(d.sync, 0, align16((size_t)words * 4), st) != hipSuccess)
     return fail(IMGCAP_EINVAL, "lstm persistent backward: memset of the sync words failed");

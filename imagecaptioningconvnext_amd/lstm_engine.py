@@ -90,7 +90,7 @@ class LstmEngine:
         if words <= 0:
             return
         if self._sync is None or self._sync.numel() < words or self._sync.device != dev:
-            self._sync = torch.zeros(max(words + 4608, 8192), dtype=torch.int32, device=dev)  # + diagnostics stamps
+            self._sync = torch.zeros(max(words + 6400, 8192), dtype=torch.int32, device=dev)  # + diagnostics stamps
         d.sync, d.sync_words = self._sync.data_ptr(), self._sync.numel()
 
     def sync_error(self):

@@ -148,6 +148,27 @@ def lstm():
         print(f"shader clock during the recurrence: {clk:.0f} MHz")
         print("cross: G published -> R got g %.0f ns; R published -> U got z %.0f ns; U published -> U got h %.0f" % (
             (r[:, 1] - u[:, 3]).mean(), (u[:, 4] - r[:, 4]).mean(), (st[0, 2:T, 1] - u[:, 7]).mean()))
+        # the persistent backward (lstm_bwd_persist_kernel, bstamp()): steps run T-1 .. 0
+        eng._launch("imgcap_lstm_tf_bwd", d, ws)
+        torch.cuda.synchronize()
+        sb = eng._sync[off:off + 3 * 64 * 16 * 2].view(torch.int64).view(3, 64, 16).cpu().double() * 10.0
+        U, X, R = sb[0, 1:T - 1], sb[1, 1:T - 1], sb[2, 1:T - 1]
+        nxtU = sb[0, 0:T - 2, 0]  # the next step processed is t - 1
+        un = ["cell+publish", "wait dgates", "dgates mma", "wait datt", "datt mma+reduce", "->next"]
+        us = [U[:, 1] - U[:, 0], U[:, 2] - U[:, 1], U[:, 3] - U[:, 2], U[:, 4] - U[:, 3], U[:, 5] - U[:, 4],
+              nxtU - U[:, 5]]
+        print("bwd U block 0, mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(un, us)))
+        xn = ["wait dgates", "loads+mma", "reduce+granules"]
+        xs = [X[:, 2] - X[:, 0], X[:, 3] - X[:, 2], X[:, 5] - X[:, 3]]
+        print("bwd X block 0, mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(xn, xs)))
+        rn = ["wait dz", "dawe", "dalpha", "softmax+datt2", "store+publish", "->next"]
+        rs = [R[:, 1] - R[:, 0], R[:, 2] - R[:, 1], R[:, 3] - R[:, 2], R[:, 4] - R[:, 3], R[:, 5] - R[:, 4],
+              sb[2, 0:T - 2, 0] - R[:, 5]]
+        print("bwd R block 0, mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(rn, rs)))
+        print("bwd cross: U published dgates -> X got %.0f ns, X got -> X done %.0f, R got dz - X done %.0f, "
+              "R published -> U got datt %.0f, U done -> next U published %.0f" % (
+                  (X[:, 2] - U[:, 1]).mean(), (X[:, 5] - X[:, 2]).mean(), (R[:, 1] - X[:, 5]).mean(),
+                  (U[:, 4] - R[:, 5]).mean(), (sb[0, 0:T - 2, 1] - U[:, 5]).mean()))
 
 
 def misc():
