@@ -50,6 +50,13 @@ def _trainable(encoder):
     return bool(fn()) if callable(fn) else False
 
 
+class _SeqGraphs:
+    """The sequential-schedule step as two captured graphs (encoder half, decoder half)."""
+
+    def __init__(self, enc, dec):
+        self.enc, self.dec = enc, dec
+
+
 class TeacherForcedTrainer:
     def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, encoder_lr=1e-4, grad_clip=5.0, alphaC=1.0,
                  pad_id=0, process_group=None, graph=False, pipeline=False):
@@ -75,6 +82,9 @@ class TeacherForcedTrainer:
         self._pipe = None
         # bucketed gradient all-reduce (world > 1): early bucket [lo, hi) of the decoder's flat
         # grads, reduced on self._comm while the rest of the backward runs
+        self._feat_slot = None   # sequential graph: encoder features between the two graphs
+        self._feat_meta = None
+        self._enc_saved = None
         self._bucket = None
         self._hook_mode = None   # None | "eager" (issue the bucket now) | "split" (capture split)
         self._split = None
@@ -109,14 +119,17 @@ class TeacherForcedTrainer:
         with torch.no_grad(), K.workspace_slot(1 if self.pipeline else 0):
             return self.encoder(imgs)
 
-    def _fwd_bwd(self, imgs, caps, caplens):
+    def _enc_part(self, imgs):
+        """Encoder half of the step: (features, saved state of the fine-tuned children or None)."""
         self.encoder.train()
         self.decoder.train()
-        es = None
         if self.enc_eng is not None:
-            feats, es = self.enc_eng.forward(imgs)
-        else:
-            feats = self._encode(imgs)
+            return self.enc_eng.forward(imgs)
+        return self._encode(imgs), None
+
+    def _fwd_bwd(self, imgs, caps, caplens):
+        feats, es = self._enc_part(imgs)
+        self._feat_meta = (tuple(feats.shape), feats.dtype)
         return self._dec(feats, caps, caplens, es)
 
     def _dec(self, feats, caps, caplens, es=None, mid=None):
@@ -179,6 +192,10 @@ class TeacherForcedTrainer:
         g2.capture_end()
 
     def _replay(self, g):
+        if isinstance(g, _SeqGraphs):  # encoder half, then decoder half
+            g.enc.replay()
+            self._replay(g.dec)
+            return
         if isinstance(g, tuple):  # split step: early bucket reduced between the two halves
             g[0].replay()
             self._reduce_early()
@@ -197,23 +214,35 @@ class TeacherForcedTrainer:
             for _ in range(warmup):
                 self._fwd_bwd(*self._inputs)
         torch.cuda.current_stream(dev).wait_stream(side)
-        if self._bucket is not None:
+        # the encoder half as its own graph, writing the features into a buffer allocated
+        # outside the captures; the decoder half (+ the fine-tuned encoder's backward) reads it.
+        # One graph of the whole step, the decoder reading the encoder's output tensor inside
+        # the graph's own pool, faulted on replays that followed allocator activity (C4
+        # --no-pipeline, C5; tools/probe/capture_bisect.py: the encoder-only, decoder-only and
+        # two-graph captures replay cleanly after the regular pool is overwritten)
+        shape, dtype = self._feat_meta
+        self._feat_slot = torch.empty(shape, dtype=dtype, device=dev)
+        ge = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ge):
+            self._seed_ctr.add_(1)
+            feats, es = self._enc_part(self._inputs[0])
+            self._feat_slot.copy_(feats)
+        self._enc_saved = es  # the fine-tuned children's activations live in ge's pool
+        if self._bucket is not None:  # decoder half split at the early-bucket hook (DDP)
             cap = torch.cuda.Stream(device=dev)
             cap.wait_stream(torch.cuda.current_stream(dev))
             torch.cuda.synchronize(dev)
             with torch.cuda.stream(cap):
                 g1, g2 = self._begin_split_capture()
-                self._seed_ctr.add_(1)
-                self._metrics = self._fwd_bwd(*self._inputs)
+                self._metrics = self._dec(self._feat_slot, self._inputs[1], self._inputs[2], es)
                 self._end_split_capture(g2)
             torch.cuda.current_stream(dev).wait_stream(cap)
-            self._graph = (g1, g2)
+            self._graph = _SeqGraphs(ge, (g1, g2))
             return
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._seed_ctr.add_(1)
-            self._metrics = self._fwd_bwd(*self._inputs)
-        self._graph = g
+        gd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gd):
+            self._metrics = self._dec(self._feat_slot, self._inputs[1], self._inputs[2], es)
+        self._graph = _SeqGraphs(ge, gd)
 
     # ---- encoder / decoder pipeline ------------------------------------------------------------
     def _pipe_capture(self, imgs, caps, caplens, warmup=2):

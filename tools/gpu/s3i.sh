@@ -1,0 +1,11 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for c in C4 C5; do
+EXTRA=""; [ "$c" = "C4" ] && EXTRA="--no-pipeline"
+timeout -k 10 300 python bench.py --config $c $EXTRA --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_${c}_s3i.log 2>&1 || { grep -v "^frame" gpurun_out/bench_${c}_s3i.log | tail -8; exit 1; }
+tail -1 gpurun_out/bench_${c}_s3i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['config']['workload'][:3], d['value'], d['ms_per_step'])"
+done
+timeout -k 10 400 python -u -m pytest tests/test_train_step_gpu.py tests/test_encoder_train_gpu.py tests/test_trainer_fullsize_gpu.py -q -x --timeout 200 --timeout-method thread > gpurun_out/s3i_t.log 2>&1 || { tail -20 gpurun_out/s3i_t.log; exit 1; }
+tail -1 gpurun_out/s3i_t.log
