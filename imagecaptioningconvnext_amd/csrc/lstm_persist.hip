@@ -1271,8 +1271,7 @@ int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
 // ---- backward ------------------------------------------------------------------------------
 static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, int& mt, int& words) {
   const size_t LDS_MAX = 160 * 1024;
-  if (d.B < 1 || d.B > 32 || d.P > 64 || d.A > 512 || d.A % 8 || d.E % 16 || d.D % 16 || !d.w_zh_t || !d.w_att_t)
-    return false;
+  if (d.B < 1 || d.B > 32 || d.P > 64 || d.A > 512 || d.A % 8 || d.E % 16 || d.D % 16) return false;
   mt = d.B <= 16 ? 1 : 2;
   const int KY = d.A + d.E, K4 = 4 * d.D;
   if (KY % 8) return false;
@@ -1355,7 +1354,8 @@ int lstm_bwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   size_t lds;
   int mt, words;
   if (!bwd_plan(d, esz, g, lds, mt, words)) return 0;
-  if (d.sync_words < words) return 0;  // a buffer sized by an older query: per-step path
+  IMGCAP_REQUIRE(d.w_zh_t && d.w_att_t, "lstm persistent backward: transposed weights needed");
+  IMGCAP_REQUIRE(d.sync_words >= words, "lstm persistent backward: sync workspace smaller than imgcap_lstm_sync_words");
   static const bool stamps = getenv("IMGCAP_LSTM_STAMPS") && atoi(getenv("IMGCAP_LSTM_STAMPS"));
   g.stamps = nullptr;
   if (stamps && d.T <= 64) {  // same diagnostics area as the forward's: after max(fwd, bwd) words

@@ -208,12 +208,12 @@ class TeacherForcedTrainer:
         self._seed_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         K.set_seed_counter(self._seed_ctr)
         self._inputs = (imgs.clone(), caps.clone(), caplens.clone())
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):  # first-touch allocations and one-time kernel setup
-            for _ in range(warmup):
-                self._fwd_bwd(*self._inputs)
-        torch.cuda.current_stream(dev).wait_stream(side)
+        # first-touch allocations and one-time kernel setup, on the capturing stream itself: with
+        # the warm-up on a separate stream the captured sequential step faulted on replays after
+        # allocator activity (C4 --no-pipeline, C5)
+        for _ in range(warmup):
+            self._fwd_bwd(*self._inputs)
+        torch.cuda.synchronize(dev)
         # the encoder half as its own graph, writing the features into a buffer allocated
         # outside the captures; the decoder half (+ the fine-tuned encoder's backward) reads it.
         # One graph of the whole step, the decoder reading the encoder's output tensor inside
