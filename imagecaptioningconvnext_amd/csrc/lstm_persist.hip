@@ -59,11 +59,6 @@ DEV uint4 ld_wt(rsrc_t r, uint32_t off) {
 DEV void st_wt(rsrc_t r, uint32_t off, uint4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, r, off, 0, 16);
 }
-typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-// one 8-byte {value, epoch} granule, write-through (sc1), written whole by one store
-DEV void st_wt8(rsrc_t r, uint32_t off, float v, unsigned ep) {
-  __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(v), ep}, r, off, 0, 16);
-}
 
 struct Geo {
   int NU, NG, NUG, RS, Ec, NR, UPB, KU, ldu, ldg, rc;
@@ -660,10 +655,9 @@ template <> DEV void pack8<float>(const float (&v)[8], uint4& lo, uint4& hi) {
 struct BGeo {
   int NU, UPB, NX, NR;
   int ldu, ldx;                 // LDS row pitches (elements) of the resident weights
-  int u_red, u_dg;              // byte offsets (U)
+  int u_red, u_dg, x_red;       // byte offsets (U / X)
   int r_enc, r_dz, r_dawe, r_red, r_al, r_dal, r_dtt;  // byte offsets (R); r_enc < 0: enc from global
-  int gran_off;                 // sync word offset of the [B][SX][E] dz partial granules
-  int XC, KSX, SX;              // X blocks: columns per block, k per slice, slices of 4D
+  int gran_off;                 // sync word offset of the [B][E] dz granules
   long long* stamps;            // diagnostics (IMGCAP_LSTM_STAMPS=1): [role U/X/R][step][16]
 };
 
@@ -715,7 +709,7 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
   constexpr int KP = PWV / MT;                      // K parts: wave w -> row tile w % MT, K part w / MT
   constexpr int KCH = sizeof(T) == 2 ? 16 : 8;      // A fragments requested per round trip
   const rsrc_t r_dcat = make_rsrc(d.dcat, (uint32_t)((long)B * Tn * W3 * sizeof(T)));
-  const rsrc_t r_gr = make_rsrc(d.sync + g.gran_off, (uint32_t)((long)B * g.SX * E * 8));
+  const rsrc_t r_gr = make_rsrc(d.sync + g.gran_off, (uint32_t)((long)B * E * 8));
   const int mi = w % MT, kp = w / MT;
   const int fr = lane & 15, fk = 8 * (lane >> 4);
   const int m = mi * 16 + fr;
@@ -724,124 +718,82 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
   const int per1 = (nk1 + KP - 1) / KP, per2 = (nk2 + KP - 1) / KP;
   const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
 
-  if (blk >= g.NU && blk < g.NU + g.NX) {
-    // ======================= X workgroup: partial dz_t over one K slice ==================
-    // dz_t[:, x0 : x0 + XC] restricted to k in [kx0, kx0 + KSX) of dgates_t: the A operand is
-    // 32 x KSX (16 KB at C2) instead of all 4D columns, and every wave owns whole output tiles
-    // (no cross-wave reduction); the R blocks sum the SX slice partials in slice order.
-    const int xb = blk - g.NU;
-    const int ncg = (E + g.XC - 1) / g.XC;
-    const int x0 = (xb % ncg) * g.XC, sl = xb / ncg, kx0 = sl * g.KSX;
-    const int klen = min(g.KSX, K4 - kx0);
-    const int ldx = g.ldx;
-    T* wx = (T*)(smem + 16);  // [XC][ldx]
+  if (blk < g.NU + g.NX) {
+    // ======================= U and X workgroups ==========================================
+    const bool isU = blk < g.NU;
+    const int UPB = g.UPB, u0 = blk * UPB;
+    const int x0 = (blk - g.NU) * 16;
+    const int ld = isU ? g.ldu : g.ldx;
+    const int KW = isU ? K4 + KY : K4;  // resident k per weight row
+    const int nrows = isU ? UPB : 16;
+    T* wr = (T*)(smem + 16);
+    float* red = (float*)(smem + (isU ? g.u_red : g.x_red));  // [KP][16 * MT][20]
+    T* dgs = (T*)(smem + g.u_dg);                              // U: [B][4][UPB] staged dgates
     {
-      const int cpr = g.KSX / VEC;
-      for (int i = tid; i < g.XC * cpr; i += PT) {
+      const int cpr = KW / VEC;
+      for (int i = tid; i < nrows * cpr; i += PT) {
         const int c = i / cpr, k = (i % cpr) * VEC;
         uint4 v = zero4;
-        if (x0 + c < E && k < klen) v = *(const uint4*)((const T*)d.w_zh_t + (long)(x0 + c) * K4 + kx0 + k);
-        *(uint4*)(wx + c * ldx + k) = v;
-      }
-    }
-    __syncthreads();
-    const int ntile = MT * (g.XC / 16);
-    const int nks = klen / 32;
-    constexpr int KSM = 8;  // k-steps per slice (KSX = 256)
-    for (int t = Tmax - 1; t >= 0; --t) {
-      const int ep = Tmax - t;
-      const long mbt = (long)m * Tn + t;
-      bstamp(g, 1, t, 0);
-      if (!block_wait(fdg, g.NU, ep, err, s_ok + 2)) return;
-      bstamp(g, 1, t, 2);
-      Frag<T> fa[KSM];
-#pragma unroll
-      for (int i = 0; i < KSM; ++i) {
-        const int k0 = kx0 + i * 32 + fk;
-        fa[i] = frag_wt<T>(r_dcat, (uint32_t)((mbt * W3 + KY + k0) * sizeof(T)), mok && i < nks);
-      }
-      for (int tt = w; tt < ntile; tt += PWV) {  // wave-uniform; tiles tt, tt + 8 share row tile w % MT
-        const int ni = tt / MT;
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < KSM; ++i)
-          if (i < nks) mma(acc, fa[i], lds_frag<T>(wx + (ni * 16 + fr) * ldx + i * 32 + fk));
-        const int col = x0 + ni * 16 + fr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = mi * 16 + 4 * (lane >> 4) + r;
-          if (b < B && col < E)
-            st_wt8(r_gr, (uint32_t)((((long)b * g.SX + sl) * E + col) * 8), acc[r], (unsigned)ep);
+        if (isU) {
+          const int j = u0 + c;
+          v = k < K4 ? *(const uint4*)((const T*)d.w_zh_t + (long)(E + j) * K4 + k)
+                     : *(const uint4*)((const T*)d.w_att_t + (long)j * KY + (k - K4));
+        } else if (x0 + c < E) {
+          v = *(const uint4*)((const T*)d.w_zh_t + (long)(x0 + c) * K4 + k);
         }
-      }
-      bstamp(g, 1, t, 3);
-    }
-    return;
-  }
-
-  if (blk < g.NU) {
-    // ======================= U workgroup ==================================================
-    const int UPB = g.UPB, u0 = blk * UPB;
-    const int ld = g.ldu;
-    T* wr = (T*)(smem + 16);                   // [UPB][ldu]: W_hh[:, unit] | [W_da; W_fb][:, unit]
-    float* red = (float*)(smem + g.u_red);     // [KP][16 * MT][20]
-    T* dgs = (T*)(smem + g.u_dg);              // [B][4][UPB] staged dgates
-    {
-      const int cpr = (K4 + KY) / VEC;
-      for (int i = tid; i < UPB * cpr; i += PT) {
-        const int c = i / cpr, k = (i % cpr) * VEC;
-        const int j = u0 + c;
-        *(uint4*)(wr + c * ld + k) = k < K4 ? *(const uint4*)((const T*)d.w_zh_t + (long)(E + j) * K4 + k)
-                                            : *(const uint4*)((const T*)d.w_att_t + (long)j * KY + (k - K4));
+        *(uint4*)(wr + c * ld + k) = v;
       }
     }
-    // this thread's (row, unit) item of the cell backward
+    // this thread's (row, unit) item of the cell backward (U)
     const int ib = tid / UPB, ijj = tid % UPB, ij = u0 + ijj;
-    const bool iok = tid < B * UPB;
+    const bool iok = isU && tid < B * UPB;
     const int dlb = iok ? d.dl[ib] : 0;
     float dc = 0.f, dh_rec = 0.f;
     CellIn cin{};
     if (iok && Tmax > 0 && Tmax - 1 < dlb) cin = cell_in_load<T>(d, Tmax - 1, ib, ij);
-    const bool bok = fr < UPB;  // B fragment rows past UPB are zero
+    const bool bok = fr < nrows;  // B fragment rows past UPB are zero
     __syncthreads();
+    const int role = isU ? 0 : 1;
     for (int t = Tmax - 1; t >= 0; --t) {
       const int ep = Tmax - t;
       const long mbt = (long)m * Tn + t;
-      bstamp(g, 0, t, 0);
-      // ---- LSTMCell backward of step t (cell_bwd_apply of lstm.hip) ----
-      if (iok) {
-        float dg[4] = {0.f, 0.f, 0.f, 0.f};
-        if (t < dlb) {
-          const float dh = cin.dhs + dh_rec;
-          const float tc = tanhf(cin.c);
-          const float dct = dc + dh * cin.go * (1.f - tc * tc);
-          dg[0] = dct * cin.gg * cin.gi * (1.f - cin.gi);
-          dg[1] = dct * cin.cp * cin.gf * (1.f - cin.gf);
-          dg[2] = dct * cin.gi * (1.f - cin.gg * cin.gg);
-          dg[3] = dh * tc * cin.go * (1.f - cin.go);
-          dc = dct * cin.gf;
-        } else {
-          dc = 0.f;
-        }
+      bstamp(g, role, t, 0);
+      if (isU) {
+        // ---- LSTMCell backward of step t (cell_bwd_apply of lstm.hip) ----
+        if (iok) {
+          float dg[4] = {0.f, 0.f, 0.f, 0.f};
+          if (t < dlb) {
+            const float dh = cin.dhs + dh_rec;
+            const float tc = tanhf(cin.c);
+            const float dct = dc + dh * cin.go * (1.f - tc * tc);
+            dg[0] = dct * cin.gg * cin.gi * (1.f - cin.gi);
+            dg[1] = dct * cin.cp * cin.gf * (1.f - cin.gf);
+            dg[2] = dct * cin.gi * (1.f - cin.gg * cin.gg);
+            dg[3] = dh * tc * cin.go * (1.f - cin.go);
+            dc = dct * cin.gf;
+          } else {
+            dc = 0.f;
+          }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dgs[(ib * 4 + q) * UPB + ijj] = from_f<T>(dg[q]);
+          for (int q = 0; q < 4; ++q) dgs[(ib * 4 + q) * UPB + ijj] = from_f<T>(dg[q]);
+        }
+        __syncthreads();
+        // dgates_t rows of this block's units -> dcat (write-through): row b, gate q, UPB elements
+        const int pieces = UPB * (int)sizeof(T) / 16;
+        for (int i = tid; i < B * 4 * pieces; i += PT) {
+          const int pc = i % pieces, bq = i / pieces, b = bq / 4, q = bq % 4;
+          const uint4 v = *(const uint4*)(dgs + bq * UPB + pc * VEC);
+          const long off = ((long)b * Tn + t) * W3 + KY + (long)q * D + u0 + pc * VEC;
+          st_wt(r_dcat, (uint32_t)(off * sizeof(T)), v);
+        }
+        block_publish(fdg + blk, ep);
+        bstamp(g, 0, t, 1);
+        // cell inputs of the next (earlier) step: independent of every hand-off
+        if (iok && t > 0 && t - 1 < dlb) cin = cell_in_load<T>(d, t - 1, ib, ij);
       }
-      __syncthreads();
-      // dgates_t rows of this block's units -> dcat (write-through): row b, gate q, UPB elements
-      const int pieces = UPB * (int)sizeof(T) / 16;
-      for (int i = tid; i < B * 4 * pieces; i += PT) {
-        const int pc = i % pieces, bq = i / pieces, b = bq / 4, q = bq % 4;
-        const uint4 v = *(const uint4*)(dgs + bq * UPB + pc * VEC);
-        const long off = ((long)b * Tn + t) * W3 + KY + (long)q * D + u0 + pc * VEC;
-        st_wt(r_dcat, (uint32_t)(off * sizeof(T)), v);
-      }
-      block_publish(fdg + blk, ep);
-      bstamp(g, 0, t, 1);
-      // cell inputs of the next (earlier) step: independent of every hand-off
-      if (iok && t > 0 && t - 1 < dlb) cin = cell_in_load<T>(d, t - 1, ib, ij);
-      // ---- dgates_t . W_hh[:, units]: requested as soon as every U block has published ----
+      // ---- dgates_t . W[:, cols]  (U: W_hh part of dh_{t-1}; X: dz_t) ----
       if (!block_wait(fdg, g.NU, ep, err, s_ok + 2)) return;
-      bstamp(g, 0, t, 2);
+      bstamp(g, role, t, 2);
       f32x4 acc[2];
       acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
       {
@@ -862,11 +814,11 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
           }
         }
       }
-      bstamp(g, 0, t, 3);
-      // ---- + [d att2 | d gate_pre]_t . [W_da; W_fb][:, units]: after the R blocks ----
-      if (!block_wait(fdt, g.NR, ep, err, s_ok + 3)) return;
-      bstamp(g, 0, t, 4);
-      {
+      bstamp(g, role, t, 3);
+      if (isU) {
+        // ---- + [d att2 | d gate_pre]_t . [W_da; W_fb][:, units]: after the R blocks ----
+        if (!block_wait(fdt, g.NR, ep, err, s_ok + 3)) return;
+        bstamp(g, 0, t, 4);
         const int ks0 = kp * per2, ks1 = min(nk2, ks0 + per2);
         for (int ks = ks0; ks < ks1; ks += KCH) {
           Frag<T> fa[KCH];
@@ -888,25 +840,43 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
       for (int r = 0; r < 4; ++r)
         red[(kp * 16 * MT + mi * 16 + 4 * (lane >> 4) + r) * 20 + fr] = acc[0][r] + acc[1][r];
       __syncthreads();
-      if (iok) {
-        float sum = 0.f;
+      if (isU) {
+        if (iok) {
+          float s = 0.f;
 #pragma unroll
-        for (int q = 0; q < KP; ++q) sum += red[(q * 16 * MT + ib) * 20 + ijj];
-        dh_rec = sum;
-        if (t == 0) d.dh[(long)ib * D + ij] = sum;  // dL/dh0
+          for (int q = 0; q < KP; ++q) s += red[(q * 16 * MT + ib) * 20 + ijj];
+          dh_rec = s;
+          if (t == 0) d.dh[(long)ib * D + ij] = s;  // dL/dh0
+        }
+      } else {
+        // dz_t granules {value, epoch} of this block's 16 columns, two per 16-byte store
+        for (int i = tid; i < B * 8; i += PT) {
+          const int b = i / 8, c = (i % 8) * 2;
+          float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+          for (int q = 0; q < KP; ++q) {
+            v0 += red[(q * 16 * MT + b) * 20 + c];
+            v1 += red[(q * 16 * MT + b) * 20 + c + 1];
+          }
+          if (x0 + c < E)
+            st_wt(r_gr, (uint32_t)(((long)b * E + x0 + c) * 8),
+                  make_uint4(__float_as_uint(v0), (unsigned)ep, __float_as_uint(v1), (unsigned)ep));
+        }
       }
       __syncthreads();  // red is rewritten next step
-      bstamp(g, 0, t, 5);
+      bstamp(g, role, t, 5);
     }
-    if (iok) d.dc[(long)ib * D + ij] = dc;  // dL/dc0
-    // steps past every decode length: zero dgates rows (as the per-step path leaves them)
-    for (int i = tid; i < B * (Tn - Tmax) * 4 * UPB; i += PT) {
-      const int jj = i % UPB, rest = i / UPB, q = rest % 4, rest2 = rest / 4, b = rest2 % B, t = Tmax + rest2 / B;
-      ((T*)d.dcat)[((long)b * Tn + t) * W3 + KY + (long)q * D + u0 + jj] = from_f<T>(0.f);
-    }
-    if (Tmax == 0 && iok) {
-      d.dh[(long)ib * D + ij] = 0.f;
-      d.dc[(long)ib * D + ij] = 0.f;
+    if (isU) {
+      if (iok) d.dc[(long)ib * D + ij] = dc;  // dL/dc0
+      // steps past every decode length: zero dgates rows (as the per-step path leaves them)
+      for (int i = tid; i < B * (Tn - Tmax) * 4 * UPB; i += PT) {
+        const int jj = i % UPB, rest = i / UPB, q = rest % 4, rest2 = rest / 4, b = rest2 % B, t = Tmax + rest2 / B;
+        ((T*)d.dcat)[((long)b * Tn + t) * W3 + KY + (long)q * D + u0 + jj] = from_f<T>(0.f);
+      }
+      if (Tmax == 0 && iok) {
+        d.dh[(long)ib * D + ij] = 0.f;
+        d.dc[(long)ib * D + ij] = 0.f;
+      }
     }
     return;
   }
@@ -966,30 +936,13 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
     // ---- dz_t[b] from the X blocks' granules ----
     {
       bool bad = false;
-      // columns (2j, 2j+1): the SX slice partials, all requested at once per poll, summed in
-      // slice order once every tag is this step's epoch
-      constexpr int SXM = 16;
       for (int j = tid; j < E / 2; j += PT) {
-        const uint32_t off0 = (uint32_t)(((long)b * g.SX * E + 2 * j) * 8);
+        const uint32_t off = (uint32_t)(((long)b * E + 2 * j) * 8);
         for (int spins = 0;; ++spins) {
-          uint4 q[SXM];
-          bool ready = true;
-#pragma unroll
-          for (int sl = 0; sl < SXM; ++sl)
-            if (sl < g.SX) {
-              q[sl] = ld_wt(r_gr, off0 + (uint32_t)(sl * E * 8));
-              ready = ready && q[sl].y == (unsigned)ep && q[sl].w == (unsigned)ep;
-            }
-          if (ready) {
-            float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-            for (int sl = 0; sl < SXM; ++sl)
-              if (sl < g.SX) {
-                s0 += __uint_as_float(q[sl].x);
-                s1 += __uint_as_float(q[sl].z);
-              }
-            dzs[2 * j] = s0;
-            dzs[2 * j + 1] = s1;
+          const uint4 q = ld_wt(r_gr, off);
+          if (q.y == (unsigned)ep && q.w == (unsigned)ep) {
+            dzs[2 * j] = __uint_as_float(q.x);
+            dzs[2 * j + 1] = __uint_as_float(q.z);
             break;
           }
           if ((spins & 255) == 255 &&
@@ -1280,15 +1233,11 @@ static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, i
   g.UPB = esz == 2 ? 16 : 8;
   if (d.D % g.UPB || d.B * g.UPB > PT) return false;
   g.NU = d.D / g.UPB;
-  g.XC = d.E >= 128 ? 128 : d.E;  // X blocks: 128 dz columns x one 256-deep slice of 4D
-  g.KSX = 256;
-  g.SX = (K4 + g.KSX - 1) / g.KSX;
-  if (g.SX > 16) return false;
-  g.NX = ((d.E + g.XC - 1) / g.XC) * g.SX;
+  g.NX = d.E / 16;
   g.NR = d.B;
   if (g.NU + g.NX + g.NR > 256) return false;
   g.ldu = K4 + KY + pad;
-  g.ldx = g.KSX + pad;
+  g.ldx = K4 + pad;
   const size_t red = (size_t)(PWV / mt) * 16 * mt * 20 * 4;
   size_t o = align16(16 + (size_t)g.UPB * g.ldu * esz);
   g.u_red = (int)o;
@@ -1296,7 +1245,9 @@ static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, i
   g.u_dg = (int)o;
   o = align16(o + (size_t)d.B * 4 * g.UPB * esz);
   const size_t u = o;
-  const size_t x = align16(16 + (size_t)g.XC * g.ldx * esz);
+  o = align16(16 + (size_t)16 * g.ldx * esz);
+  g.x_red = (int)o;
+  const size_t x = align16(o + red);
   // R: att1[b] always, enc[b] when it fits
   const int GA = PT / (d.A / 8);
   size_t r = 0;
@@ -1322,7 +1273,7 @@ static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, i
   lds = std::max(std::max(std::max(u, x), r), (size_t)81 * 1024);  // one workgroup per CU
   if (lds > LDS_MAX) return false;
   g.gran_off = (SYNC_HDR + g.NU + g.NR + 63) / 64 * 64;
-  words = g.gran_off + d.B * g.SX * d.E * 2;
+  words = g.gran_off + d.B * d.E * 2;
   return true;
 }
 

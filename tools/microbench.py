@@ -158,8 +158,8 @@ def lstm():
         us = [U[:, 1] - U[:, 0], U[:, 2] - U[:, 1], U[:, 3] - U[:, 2], U[:, 4] - U[:, 3], U[:, 5] - U[:, 4],
               nxtU - U[:, 5]]
         print("bwd U block 0, mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(un, us)))
-        xn = ["wait dgates", "loads+mma+granules"]
-        xs = [X[:, 2] - X[:, 0], X[:, 3] - X[:, 2]]
+        xn = ["wait dgates", "loads+mma", "reduce+granules"]
+        xs = [X[:, 2] - X[:, 0], X[:, 3] - X[:, 2], X[:, 5] - X[:, 3]]
         print("bwd X block 0, mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(xn, xs)))
         rn = ["wait dz", "dawe", "dalpha", "softmax+datt2", "store+publish", "->next"]
         rs = [R[:, 1] - R[:, 0], R[:, 2] - R[:, 1], R[:, 3] - R[:, 2], R[:, 4] - R[:, 3], R[:, 5] - R[:, 4],
@@ -167,7 +167,7 @@ def lstm():
         print("bwd R block 0, mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(rn, rs)))
         print("bwd cross: U published dgates -> X got %.0f ns, X got -> X done %.0f, R got dz - X done %.0f, "
               "R published -> U got datt %.0f, U done -> next U published %.0f" % (
-                  (X[:, 2] - U[:, 1]).mean(), (X[:, 3] - X[:, 2]).mean(), (R[:, 1] - X[:, 3]).mean(),
+                  (X[:, 2] - U[:, 1]).mean(), (X[:, 5] - X[:, 2]).mean(), (R[:, 1] - X[:, 5]).mean(),
                   (U[:, 4] - R[:, 5]).mean(), (sb[0, 0:T - 2, 1] - U[:, 5]).mean()))
 
 
