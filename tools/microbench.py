@@ -108,7 +108,7 @@ def lstm():
     import ctypes
     from imagecaptioningconvnext_amd import _abi
     from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
-    B, L, V = 32, 52, 9490
+    B, L, V = int(os.environ.get("IMGCAP_MB_B", "32")), 52, 9490
     dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=dev,
                                encoder_dim=768, dropout=0.5, compute_dtype=bf).to(dev)
     eng = dec.engine()
@@ -121,7 +121,7 @@ def lstm():
     T = s["T"]
     ws = s["bwd_bufs"]["chain_ws"]
     t = time_launch(lambda: eng._launch("imgcap_lstm_tf_fwd", d), reps=5, warm=2)
-    print(f"lstm fwd recurrence ({eng.CHAINS} chains): {t * 1e6:8.1f} us total, {t * 1e6 / T:6.2f} us/step")
+    print(f"lstm fwd recurrence B={B} ({eng.CHAINS} chains): {t * 1e6:8.1f} us total, {t * 1e6 / T:6.2f} us/step")
     te = time_launch(lambda: eng._launch("imgcap_lstm_tf_fwd", d), reps=5, warm=2, graph=False)
     print(f"lstm fwd recurrence ({eng.CHAINS} chains, eager streams): {te * 1e6:8.1f} us total")
     t = time_launch(lambda: eng._launch("imgcap_lstm_tf_bwd", d, ws), reps=5, warm=2)
@@ -340,7 +340,7 @@ def overlap():
     from imagecaptioningconvnext_amd import _abi
     from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
     from imagecaptioningconvnext_amd.models.encoder import Encoder
-    B, L, V = 32, 52, 9490
+    B, L, V = int(os.environ.get("IMGCAP_MB_B", "32")), 52, 9490
     dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=dev,
                                encoder_dim=768, dropout=0.5, compute_dtype=bf).to(dev)
     enc = Encoder(variant="tiny", compute_dtype=bf).to(dev)
@@ -449,7 +449,7 @@ def cumask():
     keep the CUs the encoder may not use."""
     from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
     from imagecaptioningconvnext_amd.models.encoder import Encoder
-    B, L, V = 32, 52, 9490
+    B, L, V = int(os.environ.get("IMGCAP_MB_B", "32")), 52, 9490
     dec = DecoderWithAttention(attention_dim=512, embed_dim=512, decoder_dim=512, vocab_size=V, device=dev,
                                encoder_dim=768, dropout=0.5, compute_dtype=bf).to(dev)
     enc = Encoder(variant="tiny", compute_dtype=bf).to(dev)
