@@ -37,7 +37,7 @@ class LstmDesc(ctypes.Structure):
                                 "awe", "zs", "gates", "cs", "hs", "hprev", "w_zh_t", "w_att_t", "dhs", "dalpha",
                                 "dcat", "dz", "ws_y", "y_cnt", "dh", "dc", "de", "datt1", "dwf", "dbea")] + [
         ("x_slices", ctypes.c_int32), ("y_slices", ctypes.c_int32), ("dawe", c_void_p), ("sync", c_void_p),
-        ("sync_words", ctypes.c_int32)]
+        ("sync_words", ctypes.c_int32), ("row_groups", ctypes.c_int32)]
 
 
 class MhaDesc(ctypes.Structure):

@@ -66,6 +66,7 @@ struct Geo {
   long long* stamps;  // diagnostics (IMGCAP_LSTM_STAMPS=1): per step, s_memrealtime at phase edges
   int gran_off;       // sync word offset of the [B][A + E] {epoch, value} granules (G -> R hand-off)
   int r_gv;           // R: LDS offset of the row's [att2 | gate_pre chunk] values
+  int* err;           // the launch's error word (shared by the row groups)
 };
 
 // thread 0 of block 0 (U+G) and of the first R block records [role][t][k]
@@ -179,13 +180,13 @@ DEV Frag<T> frag_wt(rsrc_t r, uint32_t off, bool ok) {
 }
 
 template <typename T, int MT>
-__global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d, Geo g) {
+DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* s_ok = (int*)smem;
   const int B = d.B, P = d.P, E = d.E, A = d.A, D = d.D, M = d.M, Tn = d.T;
   const int W3 = A + E + 4 * D;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int* err = d.sync;
+  int* err = g.err;
   int* fh = d.sync + SYNC_HDR;
   int* fg = fh + g.NU;
   int* fz = fg + g.NG;
@@ -199,7 +200,6 @@ __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d
   }
   __syncthreads();
   const int Tmax = max(0, min(Tn, s_ok[1]));
-  const int blk = blockIdx.x;
   constexpr int VEC = VecOf<T>::N;
   const rsrc_t r_hs = make_rsrc(d.hs, (uint32_t)((long)B * Tn * D * sizeof(T)));
   const rsrc_t r_h0 = make_rsrc(d.hprev, (uint32_t)((long)B * Tn * D * sizeof(T)));
@@ -610,6 +610,18 @@ __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d
   }
 }
 
+// Row groups: rows [0, B0) and [B0, B) are independent recurrences (no term couples two batch
+// rows), run side by side in ONE launch -- each group with its own blocks, descriptor view
+// (row-offset pointers) and flag / granule area; blocks [0, nb0) are group 0.  Halving the
+// rows per chain shortens each step's payload loads and MFMA work (measured per step at
+// B = 16 vs 32: forward 15.7 vs 17.4 us, backward 17.8 vs 21.2 us).
+template <typename T, int MT>
+__global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d0, Geo g0, imgcap_lstm_desc d1,
+                                                              Geo g1, int nb0) {
+  if ((int)blockIdx.x < nb0) lstm_fwd_body<T, MT>(d0, g0, blockIdx.x);
+  else lstm_fwd_body<T, MT>(d1, g1, blockIdx.x - nb0);
+}
+
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 DEV void ldf8(const float* p, float (&v)[8]) {
@@ -659,6 +671,7 @@ struct BGeo {
   int r_enc, r_dz, r_dawe, r_red, r_al, r_dal, r_dtt;  // byte offsets (R); r_enc < 0: enc from global
   int gran_off;                 // sync word offset of the [B][E] dz granules
   long long* stamps;            // diagnostics (IMGCAP_LSTM_STAMPS=1): [role U/X/R][step][16]
+  int* err;                     // the launch's error word (shared by the row groups)
 };
 
 // thread 0 of the first U, X and R block records s_memrealtime at phase edges of step t
@@ -686,13 +699,13 @@ DEV CellIn cell_in_load(const imgcap_lstm_desc& d, int t, int b, int j) {
 }
 
 template <typename T, int MT>
-__global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d, BGeo g) {
+DEV void lstm_bwd_body(const imgcap_lstm_desc& d, const BGeo& g, const int blk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* s_ok = (int*)smem;
   const int B = d.B, P = d.P, E = d.E, A = d.A, D = d.D, Tn = d.T;
   const int KY = A + E, K4 = 4 * D, W3 = KY + K4;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int* err = d.sync;
+  int* err = g.err;
   int* fdg = d.sync + SYNC_HDR;  // U blocks: dgates_t published
   int* fdt = fdg + g.NU;         // R blocks: [d att2 | d gate_pre]_t published
   if (tid < 64) {
@@ -704,7 +717,6 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
   }
   __syncthreads();
   const int Tmax = max(0, min(Tn, s_ok[1]));
-  const int blk = blockIdx.x;
   constexpr int VEC = VecOf<T>::N;
   constexpr int KP = PWV / MT;                      // K parts: wave w -> row tile w % MT, K part w / MT
   constexpr int KCH = sizeof(T) == 2 ? 16 : 8;      // A fragments requested per round trip
@@ -1105,13 +1117,21 @@ __global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d
   }
 }
 
+template <typename T, int MT>
+__global__ __launch_bounds__(PT) void lstm_bwd_persist_kernel(imgcap_lstm_desc d0, BGeo g0, imgcap_lstm_desc d1,
+                                                              BGeo g1, int nb0) {
+  if ((int)blockIdx.x < nb0) lstm_bwd_body<T, MT>(d0, g0, blockIdx.x);
+  else lstm_bwd_body<T, MT>(d1, g1, blockIdx.x - nb0);
+}
+
 }  // namespace
 
 // Geometry + LDS plan; false when the shape is outside what the persistent kernel covers.
-static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds, int& mt, int& words) {
+static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds, int& mt, int& words,
+                         int force_mt = 0) {
   const size_t LDS_MAX = 160 * 1024;
   if (d.B < 1 || d.B > 32 || d.P > 64 || d.A > 512 || d.A % 8 || d.E % 8 || d.D % 8 || d.M % 8) return false;
-  mt = d.B <= 16 ? 1 : 2;
+  mt = force_mt ? force_mt : d.B <= 16 ? 1 : 2;
   g.UPB = 8;
   const int UC = 4 * g.UPB;
   g.NU = d.D / g.UPB;
@@ -1170,8 +1190,98 @@ static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds
   return true;
 }
 
+// The descriptor restricted to rows [r0, r0 + nb) (every per-row array is batch-major) with its
+// own flag area at sync word `soff`.
+static imgcap_lstm_desc rows_view(const imgcap_lstm_desc& d, int r0, int nb, int esz, int soff) {
+  imgcap_lstm_desc v = d;
+  const long T = d.T, P = d.P, E = d.E, A = d.A, D = d.D, W3 = A + E + 4 * D, r = r0;
+  const auto cb = [&](const void* p, long elems) { return p ? (const char*)p + r * elems * esz : nullptr; };
+  const auto mb = [&](void* p, long elems) { return p ? (char*)p + r * elems * esz : nullptr; };
+  const auto cf = [&](const float* p, long elems) { return p ? p + r * elems : nullptr; };
+  const auto mf = [&](float* p, long elems) { return p ? p + r * elems : nullptr; };
+  v.B = nb;
+  v.enc = cb(d.enc, P * E);
+  v.att1 = cb(d.att1, P * A);
+  v.xe = cf(d.xe, T * 4 * D);
+  v.c0 = cf(d.c0, D);
+  v.dl = d.dl + r0;
+  v.g1 = mf(d.g1, T * W3);
+  v.alphas = mf(d.alphas, T * P);
+  v.awe = mf(d.awe, T * E);
+  v.zs = mb(d.zs, T * E);
+  v.gates = mf(d.gates, T * 4 * D);
+  v.cs = mf(d.cs, T * D);
+  v.hs = mb(d.hs, T * D);
+  v.hprev = mb(d.hprev, T * D);
+  v.dhs = cb(d.dhs, T * D);
+  v.dalpha = cf(d.dalpha, T * P);
+  v.dcat = mb(d.dcat, T * W3);
+  v.dh = mf(d.dh, D);
+  v.dc = mf(d.dc, D);
+  v.de = mf(d.de, T * P);
+  v.dawe = mf(d.dawe, (T + 1) * E);
+  v.sync = d.sync + soff;
+  v.sync_words = d.sync_words - soff;
+  return v;
+}
+
+// Row-group split: two groups when every row group still has a persistent plan and the two
+// fit on the chip.  Mask (d.row_groups when bit 2 is set, else IMGCAP_LSTM_GROUPS, else 0):
+// bit 0 splits the forward, bit 1 the backward.  Measured (C2 bench, 1x MI355X): the
+// encoder / decoder pipeline, whose encoder branch runs on the CUs the recurrence leaves,
+// 11.8k img/s unsplit, 12.1k forward-only, 12.1k backward-only, 11.5k both; the sequential
+// schedule 7.9k unsplit, 8.3k both.  Returns the first group's row count (B when not split).
+static int split_rows(const imgcap_lstm_desc& d, bool fwd) {
+  static const int env = [] {
+    const char* e = getenv("IMGCAP_LSTM_GROUPS");
+    return e ? atoi(e) : 0;
+  }();
+  const int mask = (d.row_groups & 4) ? d.row_groups : env;
+  if (!(mask & (fwd ? 1 : 2)) || d.B <= 16 || d.B > 64) return d.B;
+  return (d.B + 1) / 2;
+}
+
+struct FwdLaunch {
+  imgcap_lstm_desc d[2];
+  Geo g[2];
+  int groups = 0, nb0 = 0, nblk = 0, mt = 0, words = 0;
+  size_t lds = 0;
+};
+
+// Plans the forward launch (two row groups, else one); false = the per-step path.
+static bool fwd_launch_plan(const imgcap_lstm_desc& d, int esz, FwdLaunch& L) {
+  const int b0 = split_rows(d, true);
+  for (int groups = b0 < d.B ? 2 : 1; groups >= 1; --groups) {
+    L = FwdLaunch();
+    L.groups = groups;
+    const int rows[2] = {groups == 2 ? b0 : d.B, d.B - b0};
+    L.mt = rows[0] <= 16 ? 1 : 2;
+    int soff = 0;
+    bool ok = true;
+    for (int i = 0; i < groups && ok; ++i) {
+      L.d[i] = groups == 2 ? rows_view(d, i ? b0 : 0, rows[i], esz, soff) : d;
+      size_t lds;
+      int m, words;
+      ok = persist_plan(L.d[i], esz, L.g[i], lds, m, words, L.mt);
+      L.lds = std::max(L.lds, lds);
+      if (i == 0) L.nb0 = L.g[0].NUG + L.g[0].NR;
+      L.nblk += L.g[i].NUG + L.g[i].NR;
+      soff += (words + 63) / 64 * 64;
+      L.words = groups == 2 ? soff : words;
+    }
+    if (!ok || L.nblk > 256) continue;
+    for (int i = 0; i < groups; ++i) L.g[i].err = d.sync;
+    if (groups == 1) {
+      L.d[1] = L.d[0];
+      L.g[1] = L.g[0];
+    }
+    return true;
+  }
+  return false;
+}
+
 template <typename T, int MT>
-static int launch_persist(const imgcap_lstm_desc& d, const Geo& g, size_t lds, hipStream_t st) {
+static int launch_persist(const FwdLaunch& L, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)lstm_fwd_persist_kernel<T, MT>,
@@ -1179,10 +1289,13 @@ static int launch_persist(const imgcap_lstm_desc& d, const Geo& g, size_t lds, h
       return fail(IMGCAP_EINVAL, "lstm persistent: cannot raise the dynamic LDS limit");
     attr = true;
   }
-  hipLaunchKernelGGL((lstm_fwd_persist_kernel<T, MT>), dim3(g.NUG + g.NR), dim3(PT), lds, st, d, g);
+  hipLaunchKernelGGL((lstm_fwd_persist_kernel<T, MT>), dim3(L.nblk), dim3(PT), L.lds, st, L.d[0], L.g[0], L.d[1],
+                     L.g[1], L.nb0);
   IMGCAP_CHECK_LAUNCH("lstm persistent forward");
   return 0;
 }
+
+int lstm_persist_sync_words(const imgcap_lstm_desc& d);
 
 // Runs the whole forward recurrence in one launch when the shape fits; *used = false leaves
 // the call to the per-step path.
@@ -1194,38 +1307,37 @@ int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   }();
   if (!env || d.T < 2 || !d.sync) return 0;
   const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
-  Geo g;
-  size_t lds;
-  int mt, words;
-  if (!persist_plan(d, esz, g, lds, mt, words)) return 0;
+  FwdLaunch L;
+  if (!fwd_launch_plan(d, esz, L)) return 0;
   static const bool stamps = getenv("IMGCAP_LSTM_STAMPS") && atoi(getenv("IMGCAP_LSTM_STAMPS"));
-  g.stamps = nullptr;
-  if (stamps && d.T <= 64 && d.sync_words >= words + 64 + 2 * 64 * 16 * 2)
-    g.stamps = (long long*)(d.sync + ((words + 63) / 64 * 64 + 64));
-  IMGCAP_REQUIRE(d.sync_words >= words, "lstm persistent: sync workspace too small");
+  L.g[0].stamps = L.g[1].stamps = nullptr;
+  if (stamps && d.T <= 64) {  // group 0 only, after every group's sync words (fwd and bwd)
+    const int base = (lstm_persist_sync_words(d) + 63) / 64 * 64 + 64;
+    if (d.sync_words >= base + 2 * 64 * 16 * 2) L.g[0].stamps = (long long*)(d.sync + base);
+  }
+  IMGCAP_REQUIRE(d.sync_words >= L.words, "lstm persistent: sync workspace too small");
   IMGCAP_REQUIRE(aligned16(d.sync), "lstm persistent: sync workspace must be 16-byte aligned");
   // zero the error word and every flag (a memset node when captured)
-  if (hipMemsetAsync(d.sync, 0, align16((size_t)words * 4), st) != hipSuccess)
+  if (hipMemsetAsync(d.sync, 0, align16((size_t)L.words * 4), st) != hipSuccess)
     return fail(IMGCAP_EINVAL, "lstm persistent: memset of the sync words failed");
   *used = true;
-  int rc;
 #define LP_CASE(TT, M_) \
-  if (mt == M_) return launch_persist<TT, M_>(d, g, lds, st);
+  if (L.mt == M_) return launch_persist<TT, M_>(L, st);
   if (esz == 2) {
     LP_CASE(bf16, 1) LP_CASE(bf16, 2)
   } else {
     LP_CASE(float, 1) LP_CASE(float, 2)
   }
 #undef LP_CASE
-  rc = fail(IMGCAP_EINVAL, "lstm persistent: no instantiation");
-  return rc;
+  return fail(IMGCAP_EINVAL, "lstm persistent: no instantiation");
 }
 
 // ---- backward ------------------------------------------------------------------------------
-static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, int& mt, int& words) {
+static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, int& mt, int& words,
+                     int force_mt = 0) {
   const size_t LDS_MAX = 160 * 1024;
   if (d.B < 1 || d.B > 32 || d.P > 64 || d.A > 512 || d.A % 8 || d.E % 16 || d.D % 16) return false;
-  mt = d.B <= 16 ? 1 : 2;
+  mt = force_mt ? force_mt : d.B <= 16 ? 1 : 2;
   const int KY = d.A + d.E, K4 = 4 * d.D;
   if (KY % 8) return false;
   const int pad = 16 / esz;
@@ -1277,8 +1389,46 @@ static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, i
   return true;
 }
 
+struct BwdLaunch {
+  imgcap_lstm_desc d[2];
+  BGeo g[2];
+  int groups = 0, nb0 = 0, nblk = 0, mt = 0, words = 0;
+  size_t lds = 0;
+};
+
+static bool bwd_launch_plan(const imgcap_lstm_desc& d, int esz, BwdLaunch& L) {
+  const int b0 = split_rows(d, false);
+  for (int groups = b0 < d.B ? 2 : 1; groups >= 1; --groups) {
+    L = BwdLaunch();
+    L.groups = groups;
+    const int rows[2] = {groups == 2 ? b0 : d.B, d.B - b0};
+    L.mt = rows[0] <= 16 ? 1 : 2;
+    int soff = 0;
+    bool ok = true;
+    for (int i = 0; i < groups && ok; ++i) {
+      L.d[i] = groups == 2 ? rows_view(d, i ? b0 : 0, rows[i], esz, soff) : d;
+      size_t lds;
+      int m, words;
+      ok = bwd_plan(L.d[i], esz, L.g[i], lds, m, words, L.mt) && aligned16(L.d[i].dcat);
+      L.lds = std::max(L.lds, lds);
+      if (i == 0) L.nb0 = L.g[0].NU + L.g[0].NX + L.g[0].NR;
+      L.nblk += L.g[i].NU + L.g[i].NX + L.g[i].NR;
+      soff += (words + 63) / 64 * 64;
+      L.words = groups == 2 ? soff : words;
+    }
+    if (!ok || L.nblk > 256) continue;
+    for (int i = 0; i < groups; ++i) L.g[i].err = d.sync;
+    if (groups == 1) {
+      L.d[1] = L.d[0];
+      L.g[1] = L.g[0];
+    }
+    return true;
+  }
+  return false;
+}
+
 template <typename T, int MT>
-static int launch_bwd_persist(const imgcap_lstm_desc& d, const BGeo& g, size_t lds, hipStream_t st) {
+static int launch_bwd_persist(const BwdLaunch& L, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)lstm_bwd_persist_kernel<T, MT>,
@@ -1286,7 +1436,8 @@ static int launch_bwd_persist(const imgcap_lstm_desc& d, const BGeo& g, size_t l
       return fail(IMGCAP_EINVAL, "lstm persistent backward: cannot raise the dynamic LDS limit");
     attr = true;
   }
-  hipLaunchKernelGGL((lstm_bwd_persist_kernel<T, MT>), dim3(g.NU + g.NX + g.NR), dim3(PT), lds, st, d, g);
+  hipLaunchKernelGGL((lstm_bwd_persist_kernel<T, MT>), dim3(L.nblk), dim3(PT), L.lds, st, L.d[0], L.g[0], L.d[1],
+                     L.g[1], L.nb0);
   IMGCAP_CHECK_LAUNCH("lstm persistent backward");
   return 0;
 }
@@ -1301,39 +1452,31 @@ int lstm_bwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   }();
   if (!env || d.T < 2 || !d.sync) return 0;
   const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
-  BGeo g;
-  size_t lds;
-  int mt, words;
-  if (!bwd_plan(d, esz, g, lds, mt, words)) return 0;
+  BwdLaunch L;
+  if (!bwd_launch_plan(d, esz, L)) return 0;
   IMGCAP_REQUIRE(d.w_zh_t && d.w_att_t, "lstm persistent backward: transposed weights needed");
-  IMGCAP_REQUIRE(d.sync_words >= words, "lstm persistent backward: sync workspace smaller than imgcap_lstm_sync_words");
+  IMGCAP_REQUIRE(d.sync_words >= L.words, "lstm persistent backward: sync workspace smaller than imgcap_lstm_sync_words");
   static const bool stamps = getenv("IMGCAP_LSTM_STAMPS") && atoi(getenv("IMGCAP_LSTM_STAMPS"));
-  g.stamps = nullptr;
+  L.g[0].stamps = L.g[1].stamps = nullptr;
   if (stamps && d.T <= 64) {  // same diagnostics area as the forward's: after max(fwd, bwd) words
-    Geo fg;
-    size_t fl;
-    int fmt, fwords = 0;
-    if (!persist_plan(d, esz, fg, fl, fmt, fwords)) fwords = 0;
-    const int base = (std::max(words, fwords) + 63) / 64 * 64 + 64;
-    if (d.sync_words >= base + 3 * 64 * 16 * 2) g.stamps = (long long*)(d.sync + base);
+    const int base = (lstm_persist_sync_words(d) + 63) / 64 * 64 + 64;
+    if (d.sync_words >= base + 3 * 64 * 16 * 2) L.g[0].stamps = (long long*)(d.sync + base);
   }
   IMGCAP_REQUIRE(aligned16(d.sync) && aligned16(d.dcat), "lstm persistent backward: 16-byte aligned sync / dcat");
-  if (hipMemsetAsync(d.sync, 0, align16((size_t)words * 4), st) != hipSuccess)
+  if (hipMemsetAsync(d.sync, 0, align16((size_t)L.words * 4), st) != hipSuccess)
     return fail(IMGCAP_EINVAL, "lstm persistent backward: memset of the sync words failed");
   *used = true;
-  if (esz == 2) return mt == 1 ? launch_bwd_persist<bf16, 1>(d, g, lds, st) : launch_bwd_persist<bf16, 2>(d, g, lds, st);
-  return mt == 1 ? launch_bwd_persist<float, 1>(d, g, lds, st) : launch_bwd_persist<float, 2>(d, g, lds, st);
+  if (esz == 2) return L.mt == 1 ? launch_bwd_persist<bf16, 1>(L, st) : launch_bwd_persist<bf16, 2>(L, st);
+  return L.mt == 1 ? launch_bwd_persist<float, 1>(L, st) : launch_bwd_persist<float, 2>(L, st);
 }
 
 int lstm_persist_sync_words(const imgcap_lstm_desc& d) {
-  Geo g;
-  BGeo bg;
-  size_t lds;
-  int mt, words = 0, bwords = 0;
   const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
-  if (!persist_plan(d, esz, g, lds, mt, words)) words = 0;
-  if (!bwd_plan(d, esz, bg, lds, mt, bwords)) bwords = 0;
-  return std::max(words, bwords);
+  FwdLaunch f;
+  BwdLaunch b;
+  const int fw = fwd_launch_plan(d, esz, f) ? f.words : 0;
+  const int bw = bwd_launch_plan(d, esz, b) ? b.words : 0;
+  return std::max(fw, bw);
 }
 
 }  // namespace imgcap

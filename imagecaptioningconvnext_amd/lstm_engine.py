@@ -71,6 +71,10 @@ class LstmEngine:
     # With the persistent forward (one launch per chain, own flag words) two chains are also
     # serialised: 1.80 ms vs 0.96 ms for one (tools/gpu/lp2.sh).
     CHAINS = int(os.environ.get("IMGCAP_LSTM_CHAINS", "1"))
+    # Row groups of the persistent recurrences inside their one launch (imgcap_lstm_desc.row_groups:
+    # 0 = library default, 4 | mask = bit 0 forward, bit 1 backward split); the trainer picks
+    # it per schedule (train_step.TeacherForcedTrainer).
+    row_groups = 0
 
     def _per_row_bytes(self, T, P):
         """Byte stride per batch row of every row-indexed imgcap_lstm_desc pointer."""
@@ -227,6 +231,7 @@ class LstmEngine:
                          xe=xe, c0=c0, dl=dl, g1=g1, alphas=alphas, awe=awe, zs=zs, gates=gates, cs=cs, hs=hs,
                          hprev=hprev).items():
             setattr(d, k, v.data_ptr())
+        d.row_groups = self.row_groups
         self._sync_words(d, dev)
         # k-major copies of the weights the backward recurrence multiplies by, made on a side
         # stream under the forward recurrence (they only depend on the weights)

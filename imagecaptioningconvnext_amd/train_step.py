@@ -80,6 +80,11 @@ class TeacherForcedTrainer:
         # parameter updates are exactly the sequential ones (the encoder is frozen).
         self.pipeline = pipeline
         self._pipe = None
+        if lstm and not os.environ.get("IMGCAP_LSTM_GROUPS"):
+            # LSTM recurrences as two row groups in their one launch (lstm_persist.hip,
+            # split_rows): beside the pipelined encoder branch only the forward is split (the
+            # encoder needs the CUs the backward would take); the sequential schedule splits both
+            self.eng.row_groups = 4 | (1 if pipeline else 3)
         # bucketed gradient all-reduce (world > 1): early bucket [lo, hi) of the decoder's flat
         # grads, reduced on self._comm while the rest of the backward runs
         self._feat_slot = None   # sequential graph: encoder features between the two graphs

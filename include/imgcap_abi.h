@@ -366,6 +366,10 @@ typedef struct imgcap_lstm_desc {
                            hand-off flags, zeroed by the library (a memset on the stream) before
                            each launch; word 0 is left non-zero if a hand-off timed out. */
   int32_t sync_words;
+  int32_t row_groups;   /* persistent recurrences: 0 = library default (IMGCAP_LSTM_GROUPS, else
+                           one chain); 4 | mask = explicit, mask bit 0 runs the forward, bit 1 the
+                           backward as two row groups [0, ceil(B/2)), [ceil(B/2), B) side by side in
+                           the one launch (B > 16; more CUs, shorter steps) */
 } imgcap_lstm_desc;
 
 /* fwd: with d->sync set and T >= 2, the whole recurrence is ONE persistent launch when the

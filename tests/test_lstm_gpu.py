@@ -146,6 +146,12 @@ def test_lstm_medium_vs_oracle_with_dropout_determinism(hip_device):
     assert abs(s1["metrics"][0].item() - loss.item()) > 1e-4
 
 
+def _live_mask(lens, T, dev):
+    """[B, T] True where step t < the decode length of sorted row b (caption length - 1)"""
+    dls = torch.tensor(sorted((n - 1 for n in lens), reverse=True), device=dev)
+    return torch.arange(T, device=dev)[None, :] < dls[:, None]
+
+
 @pytest.mark.parametrize("dtype,B", [(torch.float32, 5), (torch.bfloat16, 32), (torch.float32, 24)])
 def test_lstm_persistent_recurrence_matches_per_step(hip_device, dtype, B):
     """The one-launch forward recurrence (csrc/lstm_persist.hip) against the per-step launches
@@ -174,12 +180,16 @@ def test_lstm_persistent_recurrence_matches_per_step(hip_device, dtype, B):
     torch.cuda.synchronize()
     T, tm = s["T"], max(lens) - 1
     tol = 1e-5 if dtype == torch.float32 else 2e-2
+    # rows past their own decode length are don't-care (decoder.py:95 runs batch_size_t rows):
+    # with row groups (B > 16) a group stops at its own longest row
+    live = _live_mask(lens, T, hip_device)
     for k in names:
         a, b = got[k].float(), s[k].float()
         lo = 1 if k == "hprev" else 0  # hprev slot t holds h_{t-1}
-        assert _rel(a[:, :tm + lo], b[:, :tm + lo]) < tol, k
+        assert _rel(a[live], b[live]) < tol, k
         assert torch.all(a[:, tm + lo:] == 0), k
-    assert _rel(g1[:, :tm], s["g1"][:, :tm, :A + E]) < tol
+    assert torch.equal(got["alphas"], s["alphas"]) or _rel(got["alphas"], s["alphas"]) < tol
+    assert _rel(g1[live], s["g1"][..., :A + E][live]) < tol
 
 
 @pytest.mark.parametrize("dtype,B", [(torch.float32, 5), (torch.bfloat16, 32), (torch.float32, 24),
@@ -216,11 +226,12 @@ def test_lstm_persistent_backward_matches_per_step(hip_device, dtype, B):
     torch.cuda.synchronize()
     tm = max(lens) - 1
     tol = 1e-5 if dtype == torch.float32 else 2e-2
+    live = _live_mask(lens, T, hip_device)
     for k in names + ("dawe",):
         a, b = got[k].float(), (bufs[k][:, :T] if k == "dawe" else bufs[k]).float()
         assert torch.isfinite(a).all(), k
         if k in ("dcat", "de", "dawe"):
-            assert _rel(a[:, :tm], b[:, :tm]) < tol, k
+            assert _rel(a[live], b[live]) < tol, k
             assert torch.all(a[:, tm:] == 0), k
         else:
             assert _rel(a, b) < tol, k
