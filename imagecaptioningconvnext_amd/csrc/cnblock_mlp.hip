@@ -15,6 +15,8 @@
 // tile through LDS, 8 columns per thread (16-byte residual loads and stores).
 #include "mfma.h"
 
+#include <algorithm>
+
 namespace imgcap {
 
 #ifndef MLP_GELU
@@ -256,6 +258,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
       for (int tm = 0; tm < G::TM; ++tm) {
         bf16x4 hv;
 #if MLP_GELU == 2
+        // (gelu_sig here measured slower: C = 192 59 -> 71 us, tools/kbench)
         const f32x2 g01 = gelu_fast2(f32x2{acc1[tm][tn][0] + bb[0], acc1[tm][tn][1] + bb[1]});
         const f32x2 g23 = gelu_fast2(f32x2{acc1[tm][tn][2] + bb[2], acc1[tm][tn][3] + bb[3]});
         hv[0] = (bf16)g01[0]; hv[1] = (bf16)g01[1]; hv[2] = (bf16)g23[0]; hv[3] = (bf16)g23[1];
@@ -337,9 +340,258 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   MLP_STAMP(41);
 }
 
+// ---- narrow stages (C = 96): both weight matrices resident in LDS ---------------------------
+// The chunked kernel above re-streams W1 and W2 (2 * 4C * C bf16 = 144 KB at C = 96) from L2
+// into LDS for every 128-row block: 115 MB of L2 -> LDS traffic per launch at the Tiny stage-1
+// shape, at the per-CU LDS-fill rate that is most of its time.  Here one 512-thread workgroup per
+// CU fills LDS with W1, W2 (and b1) ONCE and then its waves walk 32-row units.  The hidden activation never touches LDS either: GEMM1 runs with the
+// operands swapped (H^T = W1 Z^T), so a lane ends with hidden units {32j + 4q .. +3} and
+// {32j + 16 + 4q .. +3} of row fr -- after bias + GELU these 8 values ARE the lane's B fragment of
+// GEMM2's k-step j, provided W2's k order inside each 32-wide step is permuted the same way (done
+// once while filling LDS).  GEMM2 is swapped as well (O^T = W2 H^T): each lane ends with 4
+// consecutive output channels of one row, so the residual update is 8-byte loads and stores
+// straight from the accumulators.  Per row: z read once, x read and written once (6C bytes).
+#ifndef MLP_RES_TM
+#define MLP_RES_TM 2
+#endif
+#ifndef MLP_RES_GELU
+#define MLP_RES_GELU 1  // 1 = gelu_sig (common.h), 0 = gelu_fast2 (kernel-bench variants)
+#endif
+namespace {
+template <int C>
+struct ResCfg {
+  static constexpr int HID = 4 * C;
+  static constexpr int LD1 = C + 8;    // W1 image [HID][C]: 208-B rows, 16 rows of one fragment hit distinct banks
+  static constexpr int LD2 = HID + 8;  // W2 image [C][HID] (k permuted per 32-step): 784-B rows
+  static constexpr int W1E = HID * LD1;
+  static constexpr int W2E = C * LD2;
+  static constexpr int SMEM = (W1E + W2E) * 2 + HID * 4;
+  static constexpr int KS1 = C / 32;   // GEMM1 k-steps
+  static constexpr int NJ = HID / 32;  // GEMM2 k-steps (hidden chunks of 32)
+  static constexpr int TN2 = C / 16;   // output-channel fragments
+  static constexpr int TM = MLP_RES_TM;  // 16-row slabs per unit
+  static constexpr int UR = 16 * TM;   // rows per unit
+  static constexpr int WAVES = 8;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(C % 32 == 0, "C");
+};
+}  // namespace
+
+
+template <int C>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void cnblock_mlp_res_kernel(
+    int M, const bf16* __restrict__ z, const bf16* __restrict__ w1, const float* __restrict__ b1,
+    const bf16* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ gamma,
+    const float* __restrict__ sd, int rows_per_sample, const float* __restrict__ lnw,
+    const float* __restrict__ lnb, bf16* __restrict__ x) {
+  using G = ResCfg<C>;
+  extern __shared__ __attribute__((aligned(16))) char smem_dyn[];
+  bf16* w1s = (bf16*)smem_dyn;
+  bf16* w2s = w1s + G::W1E;
+  float* b1s = (float*)(w2s + G::W2E);
+  const int lane = threadIdx.x & 63;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nunits = (M + G::UR - 1) / G::UR;
+
+  // 32-row units dealt round robin over the waves of the grid.  (A launch-wide counter that
+  // waves pull units from measured 92 us against 40 us for this static deal at the Tiny stage-1
+  // shape: same-address returning atomics from 2048 waves serialise.)
+  const int nw = gridDim.x * G::WAVES;
+  int unit = blockIdx.x * G::WAVES + (threadIdx.x >> 6);
+
+  // every load of the fill issued before the first LDS store (one memory round trip)
+  constexpr int NV = G::HID * C / 8 / 512;
+  static_assert(NV * 512 * 8 == G::HID * C, "fill split");
+  uint4 f1[NV], f2[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = threadIdx.x + i * 512;
+    f1[i] = *(const uint4*)(w1 + (long)v * 8);
+    f2[i] = *(const uint4*)(w2 + (long)v * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int v = threadIdx.x + i * 512;
+    {
+      const int r = v / (C / 8), c = (v % (C / 8)) * 8;
+      *(uint4*)(w1s + r * G::LD1 + c) = f1[i];
+    }
+    const int n = v / (G::HID / 8), c = (v % (G::HID / 8)) * 8;  // 8 hidden = pieces 2a, 2a+1
+    const int j = c / 32, p = (c % 32) / 4;                        // p even
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int pp = p + e, s = pp / 4, q = pp % 4;
+      const uint2 h = e ? make_uint2(f2[i].z, f2[i].w) : make_uint2(f2[i].x, f2[i].y);
+      *(uint2*)(w2s + n * G::LD2 + 32 * j + 8 * q + 4 * s) = h;
+    }
+  }
+  for (int v = threadIdx.x; v < G::HID; v += 512) b1s[v] = b1[v];
+  MLP_STAMP(1);
+  __syncthreads();
+  MLP_STAMP(2);
+  int nu = 0;
+
+  // Z fragments of a unit (B operand of GEMM1: column fr = row, k = 32 ks + 8 fq), LayerNorm'd
+  auto load_z = [&](int u, bf16x8 (&zf)[G::TM][G::KS1]) {
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm) {
+      const int row = u * G::UR + tm * 16 + fr;
+      const bool ok = row < M;
+      const bf16* zp = z + (long)(ok ? row : 0) * C + 8 * fq;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const uint4 q = *(const uint4*)(zp + ks * 32);
+        zf[tm][ks] = __builtin_bit_cast(bf16x8, ok ? q : make_uint4(0u, 0u, 0u, 0u));
+      }
+    }
+  };
+  auto norm_z = [&](bf16x8 (&zf)[G::TM][G::KS1]) {
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm) {
+      float s = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += (float)zf[tm][ks][j];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mean = s * (1.f / C);
+      float q = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float dd = (float)zf[tm][ks][j] - mean; q += dd * dd; }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      const float rstd = rsqrtf(q * (1.f / C) + 1e-6f);
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const int k = ks * 32 + 8 * fq;
+        const f32x4 g0 = *(const f32x4*)(lnw + k), g1 = *(const f32x4*)(lnw + k + 4);
+        const f32x4 c0 = *(const f32x4*)(lnb + k), c1 = *(const f32x4*)(lnb + k + 4);
+        const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) zf[tm][ks][j] = (bf16)(((float)zf[tm][ks][j] - mean) * rstd * gg[j] + cc[j]);
+      }
+    }
+  };
+
+  bf16x8 zf[G::TM][G::KS1];
+  if (unit < nunits) load_z(unit, zf);
+  while (unit < nunits) {
+    // next unit's index and Z rows, and this unit's residual rows, in flight under the MFMAs
+    const int next = unit + nw;
+    const int r0 = unit * G::UR;
+    uint2 xres[G::TM][G::TN2];
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm) {
+      const int row = min(r0 + tm * 16 + fr, M - 1);
+#pragma unroll
+      for (int tn = 0; tn < G::TN2; ++tn) xres[tm][tn] = *(const uint2*)(x + (long)row * C + tn * 16 + 4 * fq);
+    }
+    if (lnw) norm_z(zf);
+    bf16x8 zc[G::TM][G::KS1];
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) zc[tm][ks] = zf[tm][ks];
+    if (next < nunits) load_z(next, zf);
+
+    f32x4 acc2[G::TM][G::TN2];
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < G::TN2; ++tn) acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (nu < 4) MLP_STAMP(3 + 3 * nu);
+
+    for (int j = 0; j < G::NJ; ++j) {
+      // GEMM1 (swapped): acc1[t][tm] = b1 + W1[32j + 16t + .., :] Z^T -> hidden 32j+16t+4fq+r of row fr
+      const f32x4 bb0 = *(const f32x4*)(b1s + 32 * j + 4 * fq);
+      const f32x4 bb1 = *(const f32x4*)(b1s + 32 * j + 16 + 4 * fq);
+      f32x4 acc1[2][G::TM];
+#pragma unroll
+      for (int tm = 0; tm < G::TM; ++tm) {
+        acc1[0][tm] = bb0;
+        acc1[1][tm] = bb1;
+      }
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 a = *(const bf16x8*)(w1s + (32 * j + 16 * t + fr) * G::LD1 + ks * 32 + 8 * fq);
+#pragma unroll
+          for (int tm = 0; tm < G::TM; ++tm)
+            acc1[t][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, zc[tm][ks], acc1[t][tm], 0, 0, 0);
+        }
+      // GELU -> the lane's GEMM2 B fragment (hidden 32j+4fq+{0..3}, 32j+16+4fq+{0..3})
+      bf16x8 hf[G::TM];
+#pragma unroll
+      for (int tm = 0; tm < G::TM; ++tm) {
+#if MLP_RES_GELU
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hf[tm][4 * t + r] = (bf16)gelu_sig(acc1[t][tm][r]);
+#else
+        const f32x2 g0 = gelu_fast2(f32x2{acc1[0][tm][0], acc1[0][tm][1]});
+        const f32x2 g1 = gelu_fast2(f32x2{acc1[0][tm][2], acc1[0][tm][3]});
+        const f32x2 g2 = gelu_fast2(f32x2{acc1[1][tm][0], acc1[1][tm][1]});
+        const f32x2 g3 = gelu_fast2(f32x2{acc1[1][tm][2], acc1[1][tm][3]});
+        hf[tm] = bf16x8{(bf16)g0[0], (bf16)g0[1], (bf16)g1[0], (bf16)g1[1],
+                        (bf16)g2[0], (bf16)g2[1], (bf16)g3[0], (bf16)g3[1]};
+#endif
+      }
+      // GEMM2 (swapped): acc2[tm][tn] += W2[16tn + .., step j] H^T -> channels 16tn+4fq+r of row fr
+#pragma unroll
+      for (int tn = 0; tn < G::TN2; ++tn) {
+        const bf16x8 a = *(const bf16x8*)(w2s + (tn * 16 + fr) * G::LD2 + 32 * j + 8 * fq);
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+          acc2[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hf[tm], acc2[tm][tn], 0, 0, 0);
+      }
+    }
+
+    if (nu < 4) MLP_STAMP(4 + 3 * nu);
+    // x += gamma * sd * (o + b2): 4 consecutive channels of row fr per fragment
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm) {
+      const int row = r0 + tm * 16 + fr;
+      if (row < M) {
+        const float s = sd ? sd[row / rows_per_sample] : 1.f;
+#pragma unroll
+        for (int tn = 0; tn < G::TN2; ++tn) {
+          const int c = tn * 16 + 4 * fq;
+          const f32x4 g = *(const f32x4*)(gamma + c), bb = *(const f32x4*)(b2 + c);
+          const bf16x4 xv = __builtin_bit_cast(bf16x4, xres[tm][tn]);
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)((float)xv[r] + (acc2[tm][tn][r] + bb[r]) * g[r] * s);
+          *(bf16x4*)(x + (long)row * C + c) = o;
+        }
+      }
+    }
+    if (nu < 4) MLP_STAMP(5 + 3 * nu);
+    ++nu;
+    unit = next;
+  }
+  MLP_STAMP(20);
+}
+
 }  // namespace imgcap
 
 using namespace imgcap;
+
+namespace {
+bool mlp_res_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("IMGCAP_MLP_RES");  // A/B switch for kernel benchmarks (default on)
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+}  // namespace
 
 extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const float* ln_w, const float* ln_b, const void* w1,
                                   const float* b1, const void* w2, const float* b2, const float* gamma, const float* sd,
@@ -352,6 +604,28 @@ extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const float* ln_w
   IMGCAP_REQUIRE((ln_w == nullptr) == (ln_b == nullptr) && (ln_w == nullptr || (aligned16(ln_w) && aligned16(ln_b))),
                  "imgcap_cnblock_mlp: ln_w / ln_b");
   hipStream_t st = (hipStream_t)stream;
+  if (C == 96 && mlp_res_enabled()) {
+    using G = ResCfg<96>;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)cnblock_mlp_res_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+      attr = true;
+    }
+    int dev = 0;
+    IMGCAP_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "imgcap_cnblock_mlp: device");
+    static int ncu_of[64];
+    if (!ncu_of[dev]) {
+      ncu_of[dev] = 256;
+      (void)hipDeviceGetAttribute(&ncu_of[dev], hipDeviceAttributeMultiprocessorCount, dev);
+    }
+    const int ncu = ncu_of[dev];
+    const int units = (M + G::UR - 1) / G::UR;
+    const int grid = std::max(1, std::min(ncu, (units + G::WAVES - 1) / G::WAVES));
+    hipLaunchKernelGGL(cnblock_mlp_res_kernel<96>, dim3(grid), dim3(512), G::SMEM, st, M, (const bf16*)z,
+                       (const bf16*)w1, b1, (const bf16*)w2, b2, gamma, sd, rows_per_sample, ln_w, ln_b, (bf16*)x);
+    IMGCAP_CHECK_LAUNCH("imgcap_cnblock_mlp");
+    return 0;
+  }
 #define MLP_(CC, BM, HC, ZL, WPE)                                                                            \
   hipLaunchKernelGGL((cnblock_mlp_kernel<CC, BM, HC, ZL, WPE>), dim3((M + BM - 1) / BM), dim3(256), 0, st, M,         \
                      (const bf16*)z, (const bf16*)w1, b1, (const bf16*)w2, b2, gamma, sd, rows_per_sample, ln_w, \

@@ -156,6 +156,18 @@ DEV f32x2 gelu_fast2(f32x2 x) {
   return 0.5f * x * (1.f + se);
 }
 DEV float gelu_fast(float x) { return gelu_fast2(f32x2{x, 0.f})[0]; }
+// erf-form GELU as x * sigmoid(x p(min(x^2, 25))): p is the weighted minimax fit (degree 2 in x^2
+// over |x| <= 5) of logit(Phi(x)) / x; |GELU error| <= 5.5e-5 over all of R (fp32, checked
+// against the exact form on 6e5 points in [-30, 30]; the tails saturate to x / -0), i.e. far
+// below the bf16 rounding of a stored hidden value.  Seven plain VALU operations + v_exp_f32 +
+// v_rcp_f32 (~40 issue cycles) against ~70 for the polynomial-erf form -- the VALU side of the
+// fused MLP is what bounds it (cnblock_mlp.hip).  Kept scalar: packed f32 VALU issues slower
+// beside MFMAs.  The coefficients carry the -log2(e) of the sigmoid's exp.
+DEV float gelu_sig(float x) {
+  const float s = fminf(x * x, 25.f);
+  const float p = fmaf(fmaf(s, 9.117902926e-04f, -1.061791434e-01f), s, -2.301726884e+00f);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * p));
+}
 DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 
 }  // namespace imgcap

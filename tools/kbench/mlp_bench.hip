@@ -51,6 +51,13 @@ int main() {
       for (int b = 0; b < 64; ++b)
         for (int k = 1; k < 42; ++k)
           if (h[b * 64 + k] && h[b * 64 + k - 1]) acc[k] += (double)(h[b * 64 + k] - h[b * 64 + k - 1]) / 64;
+#ifdef MLP_RES_STAMPS
+      if (C == 96) {  // resident kernel: fill, barrier, then per unit: loads+LN, MFMA loop, epilogue
+        printf("  C=96 res stamps (cycles, mean of 64 blocks' wave 0):");
+        for (int k = 1; k < 21; ++k) printf(" %d:%.0f", k, acc[k]);
+        printf("\n");
+      } else
+#endif
       printf("  C=%d stamps (cycles, mean of 64 blocks): zload %.0f w0 %.0f |", C, acc[1], acc[2]);
       for (int c = 0; c < 8; ++c) printf(" c%d: g1 %.0f gelu %.0f g2 %.0f st %.0f |", c, acc[3 + 4 * c], acc[4 + 4 * c], acc[5 + 4 * c], acc[6 + 4 * c]);
       printf(" epi-tile %.0f epi %.0f total %.0f\n", acc[40], acc[41], (double)0);
