@@ -340,6 +340,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
   MLP_STAMP(41);
 }
 
+// z = LayerNorm(y) (torchvision LayerNorm2d, eps 1e-6) on GEMM-operand fragments, two-pass in
+// fp32: row fr of slab tm sits in lanes fr, fr+16, fr+32, fr+48 (k = 32 ks + 8 fq ..); the result
+// is rounded to bf16 like a stored z
+template <int C, int TM, int KS>
+DEV void mlp_ln_frags(bf16x8 (&zf)[TM][KS], const float* __restrict__ lnw, const float* __restrict__ lnb, int fq) {
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (float)zf[tm][ks][j];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.f / C);
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float dd = (float)zf[tm][ks][j] - mean; q += dd * dd; }
+    q += __shfl_xor(q, 16, 64);
+    q += __shfl_xor(q, 32, 64);
+    const float rstd = rsqrtf(q * (1.f / C) + 1e-6f);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ks * 32 + 8 * fq;
+      const f32x4 g0 = *(const f32x4*)(lnw + k), g1 = *(const f32x4*)(lnw + k + 4);
+      const f32x4 c0 = *(const f32x4*)(lnb + k), c1 = *(const f32x4*)(lnb + k + 4);
+      const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+      const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) zf[tm][ks][j] = (bf16)(((float)zf[tm][ks][j] - mean) * rstd * gg[j] + cc[j]);
+    }
+  }
+}
+
+// W2 k order inside a 32-wide hidden step, as GEMM1's swapped output leaves the hidden values in a
+// lane: 4-element piece p = 4s + q (hidden 16s + 4q .. +3) sits at position 8q + 4s.  Stores the
+// 16-byte source vector holding hidden [c, c + 8) of one W2 row (c % 8 == 0) into `row`.
+DEV void w2_store_permuted(bf16* row, int c, const uint4& u) {
+  const int j = c / 32, p = (c % 32) / 4;  // p even
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int pp = p + e, s = pp / 4, q = pp % 4;
+    *(uint2*)(row + 32 * j + 8 * q + 4 * s) = e ? make_uint2(u.z, u.w) : make_uint2(u.x, u.y);
+  }
+}
+
 // ---- narrow stages (C = 96): both weight matrices resident in LDS ---------------------------
 // The chunked kernel above re-streams W1 and W2 (2 * 4C * C bf16 = 144 KB at C = 96) from L2
 // into LDS for every 128-row block: 115 MB of L2 -> LDS traffic per launch at the Tiny stage-1
@@ -416,14 +464,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int r = v / (C / 8), c = (v % (C / 8)) * 8;
       *(uint4*)(w1s + r * G::LD1 + c) = f1[i];
     }
-    const int n = v / (G::HID / 8), c = (v % (G::HID / 8)) * 8;  // 8 hidden = pieces 2a, 2a+1
-    const int j = c / 32, p = (c % 32) / 4;                        // p even
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int pp = p + e, s = pp / 4, q = pp % 4;
-      const uint2 h = e ? make_uint2(f2[i].z, f2[i].w) : make_uint2(f2[i].x, f2[i].y);
-      *(uint2*)(w2s + n * G::LD2 + 32 * j + 8 * q + 4 * s) = h;
-    }
+    const int n = v / (G::HID / 8), c = (v % (G::HID / 8)) * 8;
+    w2_store_permuted(w2s + n * G::LD2, c, f2[i]);
   }
   for (int v = threadIdx.x; v < G::HID; v += 512) b1s[v] = b1[v];
   MLP_STAMP(1);
@@ -445,38 +487,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     }
   };
-  auto norm_z = [&](bf16x8 (&zf)[G::TM][G::KS1]) {
-#pragma unroll
-    for (int tm = 0; tm < G::TM; ++tm) {
-      float s = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += (float)zf[tm][ks][j];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      const float mean = s * (1.f / C);
-      float q = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { const float dd = (float)zf[tm][ks][j] - mean; q += dd * dd; }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      const float rstd = rsqrtf(q * (1.f / C) + 1e-6f);
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks) {
-        const int k = ks * 32 + 8 * fq;
-        const f32x4 g0 = *(const f32x4*)(lnw + k), g1 = *(const f32x4*)(lnw + k + 4);
-        const f32x4 c0 = *(const f32x4*)(lnb + k), c1 = *(const f32x4*)(lnb + k + 4);
-        const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
-        const float cc[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) zf[tm][ks][j] = (bf16)(((float)zf[tm][ks][j] - mean) * rstd * gg[j] + cc[j]);
-      }
-    }
-  };
-
   bf16x8 zf[G::TM][G::KS1];
   if (unit < nunits) load_z(unit, zf);
   while (unit < nunits) {
@@ -490,7 +500,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int tn = 0; tn < G::TN2; ++tn) xres[tm][tn] = *(const uint2*)(x + (long)row * C + tn * 16 + 4 * fq);
     }
-    if (lnw) norm_z(zf);
+    if (lnw) mlp_ln_frags<C, G::TM, G::KS1>(zf, lnw, lnb, fq);
     bf16x8 zc[G::TM][G::KS1];
 #pragma unroll
     for (int tm = 0; tm < G::TM; ++tm)
@@ -578,6 +588,155 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   MLP_STAMP(20);
 }
 
+// ---- wider stages (C = 128, 192): weights streamed through LDS, hidden chained in registers ----
+// W1/W2 (2 * 4C * C bf16: 256 / 576 KB) do not fit in LDS.  One 512-thread workgroup per 128 rows
+// (8 waves x one 16-row slab); the hidden dimension is walked in 32-unit steps whose W1 rows and
+// (k-permuted) W2 columns pass through a 3-deep LDS ring, loaded two steps ahead into alternating
+// register sets, so one barrier per step and a step's load has two steps of compute to land.
+// GEMM1 -> GELU -> GEMM2 run on the registers exactly as in the resident kernel above.
+namespace {
+template <int C>
+struct StrCfg {
+  static constexpr int HID = 4 * C;
+  static constexpr int LD1 = C + 8;   // W1 chunk image [32][C]: row stride 16 B past a bank multiple
+  static constexpr int LD2 = 40;      // W2 chunk image [C][32] (+8): 80-B rows, 16 rows on distinct banks
+  static constexpr int STE = 32 * LD1 + C * LD2;  // one ring stage (bf16 elements)
+  static constexpr int NS = 3;
+  static constexpr int SMEM = NS * STE * 2;
+  static constexpr int KS1 = C / 32;
+  static constexpr int NJ = HID / 32;
+  static constexpr int TN2 = C / 16;
+  static constexpr int WAVES = 8;
+  static constexpr int BM = 16 * WAVES;
+  static constexpr int NW1 = 32 * C / 8;        // 16-byte W1 vectors per step (as many of W2)
+  static constexpr int NV = 2 * NW1 / 512;      // per thread (index v < NW1: W1, else W2)
+  static_assert(NV * 512 == 2 * NW1 && NW1 % 512 % 64 == 0, "step split (wave-uniform matrix choice)");
+  static_assert(SMEM <= 160 * 1024 && NJ % 2 == 0, "ring");
+};
+template <int C>
+DEV void str_load(uint4 (&r)[StrCfg<C>::NV], const bf16* __restrict__ w1, const bf16* __restrict__ w2, int j) {
+  using G = StrCfg<C>;
+#pragma unroll
+  for (int i = 0; i < G::NV; ++i) {
+    const int v = threadIdx.x + i * 512;
+    if (v < G::NW1) {
+      const int h = v / (C / 8), c = (v % (C / 8)) * 8;
+      r[i] = *(const uint4*)(w1 + (long)(32 * j + h) * C + c);
+    } else {
+      const int n = (v - G::NW1) / 4, c = ((v - G::NW1) % 4) * 8;
+      r[i] = *(const uint4*)(w2 + (long)n * G::HID + 32 * j + c);
+    }
+  }
+}
+template <int C>
+DEV void str_store(bf16* st, const uint4 (&r)[StrCfg<C>::NV]) {
+  using G = StrCfg<C>;
+#pragma unroll
+  for (int i = 0; i < G::NV; ++i) {
+    const int v = threadIdx.x + i * 512;
+    if (v < G::NW1) {
+      const int h = v / (C / 8), c = (v % (C / 8)) * 8;
+      *(uint4*)(st + h * G::LD1 + c) = r[i];
+    } else {
+      const int n = (v - G::NW1) / 4, c = ((v - G::NW1) % 4) * 8;
+      w2_store_permuted(st + 32 * G::LD1 + n * G::LD2, c, r[i]);
+    }
+  }
+}
+}  // namespace
+
+template <int C>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void cnblock_mlp_str_kernel(
+    int M, const bf16* __restrict__ z, const bf16* __restrict__ w1, const float* __restrict__ b1,
+    const bf16* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ gamma,
+    const float* __restrict__ sd, int rows_per_sample, const float* __restrict__ lnw,
+    const float* __restrict__ lnb, bf16* __restrict__ x) {
+  using G = StrCfg<C>;
+  extern __shared__ __attribute__((aligned(16))) char smem_dyn[];
+  bf16* ring = (bf16*)smem_dyn;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int row = blockIdx.x * G::BM + w * 16 + fr;
+  const bool ok = row < M;
+
+  uint4 ra[G::NV], rb[G::NV];
+  str_load<C>(ra, w1, w2, 0);
+  str_load<C>(rb, w1, w2, 1);
+  // this wave's slab: Z as GEMM1 B fragments, the residual as 4-channel pieces
+  bf16x8 zf[1][G::KS1];
+  {
+    const bf16* zp = z + (long)(ok ? row : 0) * C + 8 * fq;
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks) {
+      const uint4 q = *(const uint4*)(zp + ks * 32);
+      zf[0][ks] = __builtin_bit_cast(bf16x8, ok ? q : make_uint4(0u, 0u, 0u, 0u));
+    }
+  }
+  uint2 xres[G::TN2];
+#pragma unroll
+  for (int tn = 0; tn < G::TN2; ++tn) xres[tn] = *(const uint2*)(x + (long)(ok ? row : M - 1) * C + tn * 16 + 4 * fq);
+  str_store<C>(ring, ra);
+  str_store<C>(ring + G::STE, rb);
+  str_load<C>(ra, w1, w2, 2);
+  str_load<C>(rb, w1, w2, 3);
+  if (lnw) mlp_ln_frags<C, 1, G::KS1>(zf, lnw, lnb, fq);
+  __syncthreads();
+
+  f32x4 acc2[G::TN2];
+#pragma unroll
+  for (int tn = 0; tn < G::TN2; ++tn) acc2[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto step = [&](int j, uint4 (&rn)[G::NV]) {
+    const bf16* st = ring + (j % G::NS) * G::STE;
+    const f32x4 bb0 = *(const f32x4*)(b1 + 32 * j + 4 * fq);
+    const f32x4 bb1 = *(const f32x4*)(b1 + 32 * j + 16 + 4 * fq);
+    f32x4 acc1[2] = {bb0, bb1};
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16x8 a = *(const bf16x8*)(st + (16 * t + fr) * G::LD1 + ks * 32 + 8 * fq);
+        acc1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, zf[0][ks], acc1[t], 0, 0, 0);
+      }
+    bf16x8 hf;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hf[4 * t + r] = (bf16)gelu_sig(acc1[t][r]);
+    const bf16* w2c = st + 32 * G::LD1;
+#pragma unroll
+    for (int tn = 0; tn < G::TN2; ++tn) {
+      const bf16x8 a = *(const bf16x8*)(w2c + (tn * 16 + fr) * G::LD2 + 8 * fq);
+      acc2[tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hf, acc2[tn], 0, 0, 0);
+    }
+    // step j + 2 into the stage step j - 1 used (every wave passed the last barrier after it),
+    // then request step j + 4 into the same registers
+    if (j + 2 < G::NJ) {
+      str_store<C>(ring + ((j + 2) % G::NS) * G::STE, rn);
+      if (j + 4 < G::NJ) str_load<C>(rn, w1, w2, j + 4);
+    }
+    __syncthreads();
+  };
+  for (int j = 0; j < G::NJ; j += 2) {
+    step(j, ra);
+    step(j + 1, rb);
+  }
+
+  if (ok) {
+    const float s = sd ? sd[row / rows_per_sample] : 1.f;
+#pragma unroll
+    for (int tn = 0; tn < G::TN2; ++tn) {
+      const int c = tn * 16 + 4 * fq;
+      const f32x4 g = *(const f32x4*)(gamma + c), bb = *(const f32x4*)(b2 + c);
+      const bf16x4 xv = __builtin_bit_cast(bf16x4, xres[tn]);
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)((float)xv[r] + (acc2[tn][r] + bb[r]) * g[r] * s);
+      *(bf16x4*)(x + (long)row * C + c) = o;
+    }
+  }
+}
+
 }  // namespace imgcap
 
 using namespace imgcap;
@@ -623,6 +782,17 @@ extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const float* ln_w
     const int grid = std::max(1, std::min(ncu, (units + G::WAVES - 1) / G::WAVES));
     hipLaunchKernelGGL(cnblock_mlp_res_kernel<96>, dim3(grid), dim3(512), G::SMEM, st, M, (const bf16*)z,
                        (const bf16*)w1, b1, (const bf16*)w2, b2, gamma, sd, rows_per_sample, ln_w, ln_b, (bf16*)x);
+    IMGCAP_CHECK_LAUNCH("imgcap_cnblock_mlp");
+    return 0;
+  }
+  if ((C == 128 || C == 192) && mlp_res_enabled()) {
+    auto launch = [&](auto kern, int smem) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+      hipLaunchKernelGGL(kern, dim3((M + 127) / 128), dim3(512), smem, st, M, (const bf16*)z, (const bf16*)w1, b1,
+                         (const bf16*)w2, b2, gamma, sd, rows_per_sample, ln_w, ln_b, (bf16*)x);
+    };
+    if (C == 128) launch(cnblock_mlp_str_kernel<128>, StrCfg<128>::SMEM);
+    else launch(cnblock_mlp_str_kernel<192>, StrCfg<192>::SMEM);
     IMGCAP_CHECK_LAUNCH("imgcap_cnblock_mlp");
     return 0;
   }

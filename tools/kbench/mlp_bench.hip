@@ -7,7 +7,7 @@
 
 int main() {
   const int B = 32;
-  const int shapes[2][2] = {{56, 96}, {28, 192}};
+  const int shapes[3][2] = {{56, 96}, {28, 192}, {56, 128}};
   for (auto& sh : shapes) {
     const int H = sh[0], C = sh[1];
     const int M = B * H * H;
