@@ -402,8 +402,8 @@ DEV void w2_store_permuted(bf16* row, int c, const uint4& u) {
 #ifndef MLP_RES_TM
 #define MLP_RES_TM 2
 #endif
-#ifndef MLP_RES_GELU
-#define MLP_RES_GELU 1  // 1 = gelu_sig (common.h), 0 = gelu_fast2 (kernel-bench variants)
+#ifndef MLP_RES_PIPE
+#define MLP_RES_PIPE 0  // 1: GEMM1 of step j+1 issued before step j's GELU (measured 34.4 vs 32.7 us at C = 96)
 #endif
 namespace {
 template <int C>
@@ -421,7 +421,7 @@ struct ResCfg {
   static constexpr int UR = 16 * TM;   // rows per unit
   static constexpr int WAVES = 8;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
-  static_assert(C % 32 == 0, "C");
+  static_assert(C % 32 == 0 && NJ % 2 == 0, "C");
 };
 }  // namespace
 
@@ -515,52 +515,67 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int tn = 0; tn < G::TN2; ++tn) acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (nu < 4) MLP_STAMP(3 + 3 * nu);
 
-    for (int j = 0; j < G::NJ; ++j) {
-      // GEMM1 (swapped): acc1[t][tm] = b1 + W1[32j + 16t + .., :] Z^T -> hidden 32j+16t+4fq+r of row fr
+    // GEMM1 (swapped): a1[t][tm] = b1 + W1[32j + 16t + .., :] Z^T -> hidden 32j+16t+4fq+r of row fr
+    auto gemm1 = [&](int j, f32x4 (&a1)[2][G::TM]) {
       const f32x4 bb0 = *(const f32x4*)(b1s + 32 * j + 4 * fq);
       const f32x4 bb1 = *(const f32x4*)(b1s + 32 * j + 16 + 4 * fq);
-      f32x4 acc1[2][G::TM];
 #pragma unroll
       for (int tm = 0; tm < G::TM; ++tm) {
-        acc1[0][tm] = bb0;
-        acc1[1][tm] = bb1;
+        a1[0][tm] = bb0;
+        a1[1][tm] = bb1;
       }
+      bf16x8 a[G::KS1][2];  // every fragment requested before the first MFMA (the compiler
+                            // otherwise pairs each LDS read with its MFMA and waits it out)
 #pragma unroll
       for (int ks = 0; ks < G::KS1; ++ks)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const bf16x8 a = *(const bf16x8*)(w1s + (32 * j + 16 * t + fr) * G::LD1 + ks * 32 + 8 * fq);
+        for (int t = 0; t < 2; ++t) a[ks][t] = *(const bf16x8*)(w1s + (32 * j + 16 * t + fr) * G::LD1 + ks * 32 + 8 * fq);
+      asm volatile("" ::: "memory");
 #pragma unroll
-          for (int tm = 0; tm < G::TM; ++tm)
-            acc1[t][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, zc[tm][ks], acc1[t][tm], 0, 0, 0);
-        }
-      // GELU -> the lane's GEMM2 B fragment (hidden 32j+4fq+{0..3}, 32j+16+4fq+{0..3})
-      bf16x8 hf[G::TM];
-#pragma unroll
-      for (int tm = 0; tm < G::TM; ++tm) {
-#if MLP_RES_GELU
+      for (int ks = 0; ks < G::KS1; ++ks)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) hf[tm][4 * t + r] = (bf16)gelu_sig(acc1[t][tm][r]);
-#else
-        const f32x2 g0 = gelu_fast2(f32x2{acc1[0][tm][0], acc1[0][tm][1]});
-        const f32x2 g1 = gelu_fast2(f32x2{acc1[0][tm][2], acc1[0][tm][3]});
-        const f32x2 g2 = gelu_fast2(f32x2{acc1[1][tm][0], acc1[1][tm][1]});
-        const f32x2 g3 = gelu_fast2(f32x2{acc1[1][tm][2], acc1[1][tm][3]});
-        hf[tm] = bf16x8{(bf16)g0[0], (bf16)g0[1], (bf16)g1[0], (bf16)g1[1],
-                        (bf16)g2[0], (bf16)g2[1], (bf16)g3[0], (bf16)g3[1]};
-#endif
-      }
-      // GEMM2 (swapped): acc2[tm][tn] += W2[16tn + .., step j] H^T -> channels 16tn+4fq+r of row fr
+          for (int tm = 0; tm < G::TM; ++tm)
+            a1[t][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][t], zc[tm][ks], a1[t][tm], 0, 0, 0);
+    };
+    // GELU -> the lane's GEMM2 B fragment (hidden 32j+4fq+{0..3}, 32j+16+4fq+{0..3}), then
+    // GEMM2 (swapped): acc2[tm][tn] += W2[16tn + .., step j] H^T -> channels 16tn+4fq+r of row fr
+    auto gemm2 = [&](int j, const f32x4 (&a1)[2][G::TM]) {
+      bf16x8 hf[G::TM];
 #pragma unroll
-      for (int tn = 0; tn < G::TN2; ++tn) {
-        const bf16x8 a = *(const bf16x8*)(w2s + (tn * 16 + fr) * G::LD2 + 32 * j + 8 * fq);
+      for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hf[tm][4 * t + r] = (bf16)gelu_sig(a1[t][tm][r]);
+      bf16x8 a[G::TN2];
+#pragma unroll
+      for (int tn = 0; tn < G::TN2; ++tn) a[tn] = *(const bf16x8*)(w2s + (tn * 16 + fr) * G::LD2 + 32 * j + 8 * fq);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int tn = 0; tn < G::TN2; ++tn)
 #pragma unroll
         for (int tm = 0; tm < G::TM; ++tm)
-          acc2[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hf[tm], acc2[tm][tn], 0, 0, 0);
-      }
+          acc2[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tn], hf[tm], acc2[tm][tn], 0, 0, 0);
+    };
+    // software-pipelined by one step: step j+1's GEMM1 MFMAs are issued before step j's GELU, so
+    // the matrix core works under the VALU (a wave's GELU otherwise waits on its own GEMM1)
+    f32x4 a1a[2][G::TM], a1b[2][G::TM];
+#if MLP_RES_PIPE
+    gemm1(0, a1a);
+    for (int j = 0; j < G::NJ; j += 2) {
+      gemm1(j + 1, a1b);
+      gemm2(j, a1a);
+      if (j + 2 < G::NJ) gemm1(j + 2, a1a);
+      gemm2(j + 1, a1b);
     }
+#else
+    for (int j = 0; j < G::NJ; ++j) {
+      gemm1(j, a1a);
+      gemm2(j, a1a);
+    }
+#endif
 
     if (nu < 4) MLP_STAMP(4 + 3 * nu);
     // x += gamma * sd * (o + b2): 4 consecutive channels of row fr per fragment
@@ -602,7 +617,8 @@ struct StrCfg {
   static constexpr int LD2 = 40;      // W2 chunk image [C][32] (+8): 80-B rows, 16 rows on distinct banks
   static constexpr int STE = 32 * LD1 + C * LD2;  // one ring stage (bf16 elements)
   static constexpr int NS = 3;
-  static constexpr int SMEM = NS * STE * 2;
+  static constexpr int SMEM = NS * STE * 2 + HID * 4;  // + b1 (a global bias load in the loop
+                                                        // would wait out every weight load before it)
   static constexpr int KS1 = C / 32;
   static constexpr int NJ = HID / 32;
   static constexpr int TN2 = C / 16;
@@ -613,19 +629,18 @@ struct StrCfg {
   static_assert(NV * 512 == 2 * NW1 && NW1 % 512 % 64 == 0, "step split (wave-uniform matrix choice)");
   static_assert(SMEM <= 160 * 1024 && NJ % 2 == 0, "ring");
 };
+// Branch-free (addresses selected, not code paths): a conditional load or store here makes the
+// compiler's vmcnt bookkeeping conservative, and the store of step j + 2 would wait out the loads
+// of step j + 3 as well.
 template <int C>
 DEV void str_load(uint4 (&r)[StrCfg<C>::NV], const bf16* __restrict__ w1, const bf16* __restrict__ w2, int j) {
   using G = StrCfg<C>;
 #pragma unroll
   for (int i = 0; i < G::NV; ++i) {
-    const int v = threadIdx.x + i * 512;
-    if (v < G::NW1) {
-      const int h = v / (C / 8), c = (v % (C / 8)) * 8;
-      r[i] = *(const uint4*)(w1 + (long)(32 * j + h) * C + c);
-    } else {
-      const int n = (v - G::NW1) / 4, c = ((v - G::NW1) % 4) * 8;
-      r[i] = *(const uint4*)(w2 + (long)n * G::HID + 32 * j + c);
-    }
+    const int v = threadIdx.x + i * 512, u = v - G::NW1;
+    const bf16* p1 = w1 + (long)(32 * j + v / (C / 8)) * C + (v % (C / 8)) * 8;
+    const bf16* p2 = w2 + (long)(u / 4) * G::HID + 32 * j + (u % 4) * 8;
+    r[i] = *(const uint4*)(v < G::NW1 ? p1 : p2);
   }
 }
 template <int C>
@@ -633,14 +648,16 @@ DEV void str_store(bf16* st, const uint4 (&r)[StrCfg<C>::NV]) {
   using G = StrCfg<C>;
 #pragma unroll
   for (int i = 0; i < G::NV; ++i) {
-    const int v = threadIdx.x + i * 512;
-    if (v < G::NW1) {
-      const int h = v / (C / 8), c = (v % (C / 8)) * 8;
-      *(uint4*)(st + h * G::LD1 + c) = r[i];
-    } else {
-      const int n = (v - G::NW1) / 4, c = ((v - G::NW1) % 4) * 8;
-      w2_store_permuted(st + 32 * G::LD1 + n * G::LD2, c, r[i]);
-    }
+    const int v = threadIdx.x + i * 512, u = v - G::NW1;
+    // W1: 8 elements at [h][c]; W2: hidden pieces 2a, 2a+1 of row n to their permuted slots
+    const int o1 = (v / (C / 8)) * G::LD1 + (v % (C / 8)) * 8;
+    const int p = (u % 4) * 2;  // first 4-element piece of the 8 (within the 32-wide step)
+    const int o2 = 32 * G::LD1 + (u / 4) * G::LD2;
+    const bool a = v < G::NW1;
+    const int lo = a ? o1 : o2 + 8 * (p % 4) + 4 * (p / 4);
+    const int hi = a ? o1 + 4 : o2 + 8 * ((p + 1) % 4) + 4 * ((p + 1) / 4);
+    *(uint2*)(st + lo) = make_uint2(r[i].x, r[i].y);
+    *(uint2*)(st + hi) = make_uint2(r[i].z, r[i].w);
   }
 }
 }  // namespace
@@ -654,9 +671,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   using G = StrCfg<C>;
   extern __shared__ __attribute__((aligned(16))) char smem_dyn[];
   bf16* ring = (bf16*)smem_dyn;
+  float* b1s = (float*)(ring + G::NS * G::STE);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int row = blockIdx.x * G::BM + w * 16 + fr;
+  for (int v = threadIdx.x; v < G::HID; v += 512) b1s[v] = b1[v];
   const bool ok = row < M;
 
   uint4 ra[G::NV], rb[G::NV];
@@ -686,41 +705,65 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int tn = 0; tn < G::TN2; ++tn) acc2[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto step = [&](int j, uint4 (&rn)[G::NV]) {
+  auto gemm1 = [&](int j, f32x4 (&a1)[2]) {
     const bf16* st = ring + (j % G::NS) * G::STE;
-    const f32x4 bb0 = *(const f32x4*)(b1 + 32 * j + 4 * fq);
-    const f32x4 bb1 = *(const f32x4*)(b1 + 32 * j + 16 + 4 * fq);
-    f32x4 acc1[2] = {bb0, bb1};
+    a1[0] = *(const f32x4*)(b1s + 32 * j + 4 * fq);
+    a1[1] = *(const f32x4*)(b1s + 32 * j + 16 + 4 * fq);
+    bf16x8 a[G::KS1][2];  // every fragment requested before the first MFMA (see the resident kernel)
 #pragma unroll
     for (int ks = 0; ks < G::KS1; ++ks)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const bf16x8 a = *(const bf16x8*)(st + (16 * t + fr) * G::LD1 + ks * 32 + 8 * fq);
-        acc1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, zf[0][ks], acc1[t], 0, 0, 0);
-      }
+      for (int t = 0; t < 2; ++t) a[ks][t] = *(const bf16x8*)(st + (16 * t + fr) * G::LD1 + ks * 32 + 8 * fq);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < G::KS1; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][t], zf[0][ks], a1[t], 0, 0, 0);
+  };
+  auto gemm2 = [&](int j, const f32x4 (&a1)[2]) {
     bf16x8 hf;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) hf[4 * t + r] = (bf16)gelu_sig(acc1[t][r]);
-    const bf16* w2c = st + 32 * G::LD1;
+      for (int r = 0; r < 4; ++r) hf[4 * t + r] = (bf16)gelu_sig(a1[t][r]);
+    const bf16* w2c = ring + (j % G::NS) * G::STE + 32 * G::LD1;
+    bf16x8 a[G::TN2];
 #pragma unroll
-    for (int tn = 0; tn < G::TN2; ++tn) {
-      const bf16x8 a = *(const bf16x8*)(w2c + (tn * 16 + fr) * G::LD2 + 8 * fq);
-      acc2[tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hf, acc2[tn], 0, 0, 0);
-    }
-    // step j + 2 into the stage step j - 1 used (every wave passed the last barrier after it),
-    // then request step j + 4 into the same registers
-    if (j + 2 < G::NJ) {
-      str_store<C>(ring + ((j + 2) % G::NS) * G::STE, rn);
-      if (j + 4 < G::NJ) str_load<C>(rn, w1, w2, j + 4);
-    }
-    __syncthreads();
+    for (int tn = 0; tn < G::TN2; ++tn) a[tn] = *(const bf16x8*)(w2c + (tn * 16 + fr) * G::LD2 + 8 * fq);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int tn = 0; tn < G::TN2; ++tn) acc2[tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tn], hf, acc2[tn], 0, 0, 0);
   };
-  for (int j = 0; j < G::NJ; j += 2) {
-    step(j, ra);
-    step(j + 1, rb);
+  // Software-pipelined as in the resident kernel: step j+1's GEMM1 (its stage landed before the
+  // barrier that closed step j-1) is issued before step j's GELU.  After step j: step j+2 goes
+  // into the stage step j-1 used (every wave passed the barrier after it), then step j+4 is
+  // requested into the same registers.  The loop body is unconditional (the tail is peeled) so
+  // the vmcnt waits count the register sets exactly.
+  f32x4 a1a[2], a1b[2];
+  gemm1(0, a1a);
+  for (int j = 0; j < G::NJ - 4; j += 2) {
+    gemm1(j + 1, a1b);
+    gemm2(j, a1a);
+    str_store<C>(ring + ((j + 2) % G::NS) * G::STE, ra);
+    str_load<C>(ra, w1, w2, j + 4);
+    __syncthreads();
+    gemm1(j + 2, a1a);
+    gemm2(j + 1, a1b);
+    str_store<C>(ring + ((j + 3) % G::NS) * G::STE, rb);
+    str_load<C>(rb, w1, w2, j + 5);
+    __syncthreads();
   }
+  gemm1(G::NJ - 3, a1b);
+  gemm2(G::NJ - 4, a1a);
+  str_store<C>(ring + ((G::NJ - 2) % G::NS) * G::STE, ra);
+  __syncthreads();
+  gemm1(G::NJ - 2, a1a);
+  gemm2(G::NJ - 3, a1b);
+  str_store<C>(ring + ((G::NJ - 1) % G::NS) * G::STE, rb);
+  __syncthreads();
+  gemm1(G::NJ - 1, a1b);
+  gemm2(G::NJ - 2, a1a);
+  gemm2(G::NJ - 1, a1b);
 
   if (ok) {
     const float s = sd ? sd[row / rows_per_sample] : 1.f;

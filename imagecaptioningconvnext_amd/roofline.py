@@ -124,8 +124,9 @@ def _encoder_groups(trainer, B, dev):
             def mlp(blk=blk, z=z, x2=x2):
                 K.cnblock_mlp(z, blk["w1"], blk["b1"], blk["w2"], blk["b2"], blk["gamma"], x2, ln_w=blk["lnw"],
                               ln_b=blk["lnb"])
-            out.append(dict(name=f"cnblock_mlp_kernel<{C}> (stage {st + 1} fused MLP)", bound="mfma",
-                            symbol=f"cnblock_mlp_kernel<{C},", bytes=3.0 * M * C * 2 + 2 * 4 * C * C * 2,
+            kname = "cnblock_mlp_res_kernel" if C == 96 else "cnblock_mlp_str_kernel"  # csrc/cnblock_mlp.hip
+            out.append(dict(name=f"{kname}<{C}> (stage {st + 1} fused MLP)", bound="mfma",
+                            symbol=f"{kname}<{C}>", bytes=3.0 * M * C * 2 + 2 * 4 * C * C * 2,
                             per_step=len(blocks), t=time_launch(mlp, reps=20), flops=2.0 * 2 * M * C * 4 * C,
                             note=f"M={M} C={C}: LN + Linear C->4C + GELU + Linear 4C->C + scale + residual"))
         if hw <= 64:
