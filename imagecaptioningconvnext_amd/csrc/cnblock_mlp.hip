@@ -808,11 +808,8 @@ extern "C" int imgcap_cnblock_mlp(int M, int C, const void* z, const float* ln_w
   hipStream_t st = (hipStream_t)stream;
   if (C == 96 && mlp_res_enabled()) {
     using G = ResCfg<96>;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)cnblock_mlp_res_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
-      attr = true;
-    }
+    (void)hipFuncSetAttribute((const void*)cnblock_mlp_res_kernel<96>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              G::SMEM);  // per device, so on every call
     int dev = 0;
     IMGCAP_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "imgcap_cnblock_mlp: device");
     static int ncu_of[64];

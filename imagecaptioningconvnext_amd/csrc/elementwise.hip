@@ -248,12 +248,22 @@ __global__ __launch_bounds__(256) void sort_gather_kernel(int B, int P, int E, i
     float acc[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
-    for (int p = 0; p < P; ++p) {
-      const uint4 u = *(const uint4*)(in + (long)p * E + v * VEC);
-      *(uint4*)(out + (long)p * E + v * VEC) = u;
-      const T* x = (const T*)&u;
+    // pixels in batches of PB independent loads (one memory round trip per batch instead of one
+    // per pixel: 35 -> a few us at B = 32, P = 49), summed in p order
+    constexpr int PB = 16;
+    for (int p0 = 0; p0 < P; p0 += PB) {
+      uint4 u[PB];
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) acc[k] += to_f(x[k]);
+      for (int i = 0; i < PB; ++i)
+        if (p0 + i < P) u[i] = *(const uint4*)(in + (long)(p0 + i) * E + v * VEC);
+#pragma unroll
+      for (int i = 0; i < PB; ++i)
+        if (p0 + i < P) {
+          *(uint4*)(out + (long)(p0 + i) * E + v * VEC) = u[i];
+          const T* x = (const T*)&u[i];
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) acc[k] += to_f(x[k]);
+        }
     }
 #pragma unroll
     for (int k = 0; k < VEC; ++k) mean_out[(long)r * E + v * VEC + k] = from_f<T>(acc[k] / P);
