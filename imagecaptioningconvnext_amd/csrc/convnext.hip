@@ -527,11 +527,22 @@ int dw_nc_override() {
   }();
   return v == 4 || v == 8 ? v : 0;
 }
+// IMGCAP_DW_NARROW=0|1 (A/B timing of the late-stage lane mapping)
+bool dw_narrow() {
+  static const int v = [] {
+    const char* e = getenv("IMGCAP_DW_NARROW");
+    return e ? atoi(e) : 0;
+  }();
+  return v == 1;
+}
 template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
                    hipStream_t st, const void* res = nullptr, int flip = 0) {
-  // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups
-  const int PW = W % 7 == 0 ? 7 : W % 8 == 0 ? 8 : W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 1;
+  // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups.
+  // Narrow mode (dw_narrow): the 28 / 14 / 7-wide stages with 4 / 2 / 1 pixels per lane -- 7
+  // lanes per image row, so 2-4x the lanes and blocks of the late stages' small grids
+  const bool narrow = dw_narrow() && (W == 28 || W == 14 || W == 7);
+  const int PW = narrow ? W / 7 : W % 7 == 0 ? 7 : W % 8 == 0 ? 8 : W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 1;
   const int GW = W / PW, TR = 64 / GW;
   const long R = (long)B * H;
   const int RS = dw_row_slots(W, PW, (int)sizeof(T));
@@ -552,9 +563,9 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
   } while (0)
   switch (W) {  // the encoder's stage widths at 224 and 256 pixel inputs
     case 56: DW_(7, 56); break;
-    case 28: DW_(7, 28); break;
-    case 14: DW_(7, 14); break;
-    case 7: DW_(7, 7); break;
+    case 28: if (narrow) DW_(4, 28); else DW_(7, 28); break;
+    case 14: if (narrow) DW_(2, 14); else DW_(7, 14); break;
+    case 7: if (narrow) DW_(1, 7); else DW_(7, 7); break;
     case 64: DW_(8, 64); break;
     case 32: DW_(8, 32); break;
     case 16: DW_(8, 16); break;
