@@ -409,6 +409,31 @@ def test_cnblock_mlp_fused(hip_device, C, M, with_sd):
     assert _rel(got, delta) < 2e-2
 
 
+@pytest.mark.parametrize("C,M", [(96, 70001), (192, 40000)])
+def test_cnblock_mlp_large_grids(hip_device, C, M):
+    """Stage-sized row counts: the resident C = 96 kernel deals more 32-row units than the grid
+    has waves (each wave walks several), the streamed C = 192 kernel runs hundreds of blocks; LN in
+    the prologue and drop path on, vs torch fp32 on the bf16-rounded operands (gate as above)."""
+    g = torch.Generator(device="cpu").manual_seed(M)
+    y = (torch.randn(M, C, generator=g) * 2 + 0.5).bfloat16()
+    x = torch.randn(M, C, generator=g).bfloat16()
+    w1 = (torch.randn(4 * C, C, generator=g) / math.sqrt(C)).bfloat16()
+    w2 = (torch.randn(C, 4 * C, generator=g) / math.sqrt(4 * C)).bfloat16()
+    b1, b2, gamma, lw, lb = (torch.randn(n, generator=g) for n in (4 * C, C, C, C, C))
+    rps = 3136
+    sd = (torch.rand((M + rps - 1) // rps, generator=g) > 0.3).float() / 0.7
+    z = F.layer_norm(y.float(), (C,), lw, lb, 1e-6).bfloat16().float()
+    hid = F.gelu(z @ w1.float().t() + b1).bfloat16().float()
+    delta = (hid @ w2.float().t() + b2) * gamma * sd.repeat_interleave(rps)[:M].view(M, 1)
+    d = lambda t: t.to(hip_device)  # noqa: E731
+    xd = d(x)
+    K.cnblock_mlp(d(y), d(w1), d(b1), d(w2), d(b2), d(gamma), xd, sd=d(sd), rows_per_sample=rps, ln_w=d(lw),
+                  ln_b=d(lb))
+    got = xd.cpu().float() - x.float()
+    assert _rel(got, delta) < 2e-2
+    assert torch.isfinite(got).all()
+
+
 def test_gemm_grouped_weight_gradients(hip_device):
     """GemmBatch / imgcap_gemm_grouped: many dW = dY^T X products (ragged M, N, K, strided
     outputs, alpha/beta) in one grouped launch vs torch fp32 on the bf16-rounded operands."""
