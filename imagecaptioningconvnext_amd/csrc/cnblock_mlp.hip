@@ -379,12 +379,13 @@ DEV void mlp_ln_frags(bf16x8 (&zf)[TM][KS], const float* __restrict__ lnw, const
 // W2 k order inside a 32-wide hidden step, as GEMM1's swapped output leaves the hidden values in a
 // lane: 4-element piece p = 4s + q (hidden 16s + 4q .. +3) sits at position 8q + 4s.  Stores the
 // 16-byte source vector holding hidden [c, c + 8) of one W2 row (c % 8 == 0) into `row`.
-DEV void w2_store_permuted(bf16* row, int c, const uint4& u) {
+// swz: XOR applied to the 16-byte granule index (4j + q) of the destination (0: none).
+DEV void w2_store_permuted(bf16* row, int c, const uint4& u, int swz = 0) {
   const int j = c / 32, p = (c % 32) / 4;  // p even
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int pp = p + e, s = pp / 4, q = pp % 4;
-    *(uint2*)(row + 32 * j + 8 * q + 4 * s) = e ? make_uint2(u.z, u.w) : make_uint2(u.x, u.y);
+    *(uint2*)(row + 8 * ((4 * j + q) ^ swz) + 4 * s) = e ? make_uint2(u.z, u.w) : make_uint2(u.x, u.y);
   }
 }
 
@@ -409,8 +410,12 @@ namespace {
 template <int C>
 struct ResCfg {
   static constexpr int HID = 4 * C;
-  static constexpr int LD1 = C + 8;    // W1 image [HID][C]: 208-B rows, 16 rows of one fragment hit distinct banks
-  static constexpr int LD2 = HID + 8;  // W2 image [C][HID] (k permuted per 32-step): 784-B rows
+  // ds_read_b128 serves a wave in 4 fixed groups of 16 lanes (MI355X_MICROARCH.md §LDS): the 16
+  // lanes of a fragment group (rows fr, granules fq) must cover the 64 banks once.  W1 rows padded
+  // by 32 B (C + 8 was 2-way: SQ_LDS_BANK_CONFLICT 3.3 per LDS instruction); W2 rows unpadded with
+  // the 16-byte granule index XOR'ed by (row & 15) (tools: the bank model in DESIGN.md §3d)
+  static constexpr int LD1 = C + 16;   // W1 image [HID][C]
+  static constexpr int LD2 = HID;      // W2 image [C][HID]: k permuted per 32-step, granules swizzled
   static constexpr int W1E = HID * LD1;
   static constexpr int W2E = C * LD2;
   static constexpr int SMEM = (W1E + W2E) * 2 + HID * 4;
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       *(uint4*)(w1s + r * G::LD1 + c) = f1[i];
     }
     const int n = v / (G::HID / 8), c = (v % (G::HID / 8)) * 8;
-    w2_store_permuted(w2s + n * G::LD2, c, f2[i]);
+    w2_store_permuted(w2s + n * G::LD2, c, f2[i], n & 15);
   }
   for (int v = threadIdx.x; v < G::HID; v += 512) b1s[v] = b1[v];
   MLP_STAMP(1);
@@ -551,7 +556,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           for (int r = 0; r < 4; ++r) hf[tm][4 * t + r] = (bf16)gelu_sig(a1[t][tm][r]);
       bf16x8 a[G::TN2];
 #pragma unroll
-      for (int tn = 0; tn < G::TN2; ++tn) a[tn] = *(const bf16x8*)(w2s + (tn * 16 + fr) * G::LD2 + 32 * j + 8 * fq);
+      for (int tn = 0; tn < G::TN2; ++tn) a[tn] = *(const bf16x8*)(w2s + (tn * 16 + fr) * G::LD2 + 8 * ((4 * j + fq) ^ fr));
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int tn = 0; tn < G::TN2; ++tn)
@@ -613,8 +618,8 @@ namespace {
 template <int C>
 struct StrCfg {
   static constexpr int HID = 4 * C;
-  static constexpr int LD1 = C + 8;   // W1 chunk image [32][C]: row stride 16 B past a bank multiple
-  static constexpr int LD2 = 40;      // W2 chunk image [C][32] (+8): 80-B rows, 16 rows on distinct banks
+  static constexpr int LD1 = C + 16;  // W1 chunk image [32][C]: rows padded by 32 B (see ResCfg: +16 B was 2-way)
+  static constexpr int LD2 = 48;      // W2 chunk image [C][32] (+16): 96-B rows
   static constexpr int STE = 32 * LD1 + C * LD2;  // one ring stage (bf16 elements)
   static constexpr int NS = 3;
   static constexpr int SMEM = NS * STE * 2 + HID * 4;  // + b1 (a global bias load in the loop
