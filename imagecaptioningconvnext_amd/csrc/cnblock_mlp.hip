@@ -452,6 +452,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int nw = gridDim.x * G::WAVES;
   int unit = blockIdx.x * G::WAVES + (threadIdx.x >> 6);
 
+  auto load_z = [&](int u, bf16x8 (&zf)[G::TM][G::KS1]) {
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm) {
+      const int row = u * G::UR + tm * 16 + fr;
+      const bool ok = row < M;
+      const bf16* zp = z + (long)(ok ? row : 0) * C + 8 * fq;
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) {
+        const uint4 q = *(const uint4*)(zp + ks * 32);
+        zf[tm][ks] = __builtin_bit_cast(bf16x8, ok ? q : make_uint4(0u, 0u, 0u, 0u));
+      }
+    }
+  };
+  // the first unit's Z rows requested ahead of the fill, so they land under it
+  bf16x8 zf[G::TM][G::KS1];
+  if (unit < nunits) load_z(unit, zf);
+
   // every load of the fill issued before the first LDS store (one memory round trip)
   constexpr int NV = G::HID * C / 8 / 512;
   static_assert(NV * 512 * 8 == G::HID * C, "fill split");
@@ -479,21 +496,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   int nu = 0;
 
   // Z fragments of a unit (B operand of GEMM1: column fr = row, k = 32 ks + 8 fq), LayerNorm'd
-  auto load_z = [&](int u, bf16x8 (&zf)[G::TM][G::KS1]) {
-#pragma unroll
-    for (int tm = 0; tm < G::TM; ++tm) {
-      const int row = u * G::UR + tm * 16 + fr;
-      const bool ok = row < M;
-      const bf16* zp = z + (long)(ok ? row : 0) * C + 8 * fq;
-#pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks) {
-        const uint4 q = *(const uint4*)(zp + ks * 32);
-        zf[tm][ks] = __builtin_bit_cast(bf16x8, ok ? q : make_uint4(0u, 0u, 0u, 0u));
-      }
-    }
-  };
-  bf16x8 zf[G::TM][G::KS1];
-  if (unit < nunits) load_z(unit, zf);
   while (unit < nunits) {
     // next unit's index and Z rows, and this unit's residual rows, in flight under the MFMAs
     const int next = unit + nw;
