@@ -252,9 +252,13 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    progress = os.environ.get("IMGCAP_BENCH_PROGRESS") == "1"  # diagnostics: a synchronised mark per 10 steps
     t0 = time.perf_counter()
     for i in range(args.steps):
         trainer.step(*batches[i % 4])
+        if progress and i % 10 == 9:
+            torch.cuda.synchronize()
+            print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -271,7 +275,11 @@ def main(argv=None):
     fp8_fpi = fp8_flops_per_image(cfg, enc)
     if rank == 0:
         from imagecaptioningconvnext_amd import roofline
+        if progress:
+            print("[bench] roofline", file=sys.stderr, flush=True)
         roof = roofline.measure(cfg, trainer, batches[0], cfgname=args.config)
+        if progress:
+            print("[bench] roofline done", file=sys.stderr, flush=True)
         out = {
             "metric": "images/sec (train step, teacher-forced)",
             "value": round(imgs_per_s, 2),
