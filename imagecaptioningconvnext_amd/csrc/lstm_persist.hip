@@ -171,11 +171,11 @@ DEV Frag<T> lds_frag_k(const T* row, int k0, int K) {
 // A fragment (8 k of one row) from a write-through buffer; zero outside [0, rows) x [0, K)
 template <typename T>
 DEV Frag<T> frag_wt(rsrc_t r, uint32_t off, bool ok) {
-  uint4 lo = make_uint4(0u, 0u, 0u, 0u), hi = lo;
-  if (ok) {
-    lo = ld_wt(r, off);
-    if (sizeof(T) == 4) hi = ld_wt(r, off + 16);
-  }
+  // branch-free: a masked fragment reads past the buffer's range, which the buffer load returns
+  // as zeros (a conditional load leaves the compiler's vmcnt waits conservative)
+  const uint32_t o = ok ? off : 0x80000000u;
+  const uint4 lo = ld_wt(r, o);
+  const uint4 hi = sizeof(T) == 4 ? ld_wt(r, o + 16) : lo;
   return frag_from<T>(lo, hi);
 }
 
@@ -279,7 +279,11 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
         for (int q = 0; q < 4; ++q) xe[k][q] = isU && b < B ? d.xe[((long)b * Tn + t) * 4 * D + q * D + j] : 0.f;
       }
       // A = [z_t | h_{t-1}]: the h part is available now, the z part after the R blocks'
-      // hand-off; every fragment of this wave's K range is requested in one round trip each
+      // hand-off; every fragment of this wave's K range is requested in one round trip each.
+      // The G product (h_{t-1} [W_da; W_fb]^T) multiplies the SAME h fragments, so G blocks
+      // (U blocks or not) request them too and G runs on them: one 32 KB round trip of h per
+      // block instead of two (G's own copy used to queue behind this prefetch: "G h loads"
+      // 2.0 us per step in the stamps)
       const int nks = (KU + 31) / 32, per = (nks + KP - 1) / KP;
       const int ks0 = kp * per, ks1 = min(nks, ks0 + per);
       const long zrow = (long)m * Tn + t;
@@ -288,27 +292,21 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
       for (int i = 0; i < MAXKS; ++i) {
         const int k0 = (ks0 + i) * 32 + fk;
         fa[i] = frag_wt<T>(rh, (uint32_t)((hrow * D + (k0 - E)) * sizeof(T)),
-                           isU && mok && ks0 + i < ks1 && k0 >= E && k0 < KU);
+                           (isU || isG) && mok && ks0 + i < ks1 && k0 >= E && k0 < KU);
       }
       // ---------------- G: [att2 | gate_pre]_t ----------------
       if (isG) {
         f32x4 acc[2];
         acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int nks = (D + 31) / 32, per = (nks + KP - 1) / KP;
-        const int ks0 = kp * per, ks1 = min(nks, ks0 + per);
-        for (int ks = ks0; ks < ks1; ks += 8) {
-          Frag<T> fa[8];
+        stamp(g, 0, t, 9, true);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int k0 = (ks + i) * 32 + fk;
-            fa[i] = frag_wt<T>(rh, (uint32_t)((hrow * D + k0) * sizeof(T)), mok && ks + i < ks1 && k0 < D);
-          }
-          stamp(g, 0, t, 9, true);
+        for (int i = 0; i < MAXKS; ++i) {
+          const int kb = (ks0 + i) * 32;
+          if (ks0 + i < ks1 && kb + 32 > E) {  // uniform: the k-step holds h columns
+            // lanes left of E carry zero A fragments; their B read is clamped to a valid column
+            const int kg = max(kb + fk - E, 0);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {  // steps past ks1 have zero A fragments: no branch
-            const int k0 = (ks + i) * 32 + fk;
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni) mma(acc[ni], fa[i], lds_frag_k<T>(wg + (ni * 16 + fr) * ldg, k0, D));
+            for (int ni = 0; ni < 2; ++ni) mma(acc[ni], fa[i], lds_frag_k<T>(wg + (ni * 16 + fr) * ldg, kg, D));
           }
         }
 #pragma unroll
