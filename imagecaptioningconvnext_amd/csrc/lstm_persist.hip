@@ -66,6 +66,7 @@ struct Geo {
   long long* stamps;  // diagnostics (IMGCAP_LSTM_STAMPS=1): per step, s_memrealtime at phase edges
   int gran_off;       // sync word offset of the [B][A + E] {epoch, value} granules (G -> R hand-off)
   int r_gv;           // R: LDS offset of the row's [att2 | gate_pre chunk] values
+  int ldE;            // R: LDS pitch (elements) of the enc rows: Ec + 32, see lstm_fwd_body
   int* err;           // the launch's error word (shared by the row groups)
 };
 
@@ -448,7 +449,11 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
   const int rr = blk - g.NUG, b = rr / g.RS, s = rr % g.RS;
   const int Ec = g.Ec, e0 = s * Ec;
   T* att1s = (T*)(smem + 16);                   // [P][A]
-  T* encs = (T*)(smem + g.r_enc);               // [P][Ec]
+  // [P][ldE]: a lane quad reads 4 consecutive pixels of one 8-channel vector in the context
+  // loop; with rows of Ec (a multiple of 128 elements) the quad hit one bank group (4-way,
+  // SQ_LDS_BANK_CONFLICT 3.3 per LDS instruction), rows padded by 64 B spread them over the 64 banks
+  const int ldE = g.ldE;
+  T* encs = (T*)(smem + g.r_enc);
   float* red2 = (float*)(smem + g.r_red2);      // [64] scores
   float* es = (float*)(smem + g.r_es);          // [64] alpha
   float* gv = (float*)(smem + g.r_gv);          // [A + Ec] att2 | gate_pre chunk of this step
@@ -460,7 +465,7 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
     const int cpr = Ec / VEC;
     for (int i = tid; i < P * cpr; i += PT) {
       const int p = i / cpr, k = (i % cpr) * VEC;
-      *(uint4*)(encs + p * Ec + k) = *(const uint4*)(en + (long)p * E + k);
+      *(uint4*)(encs + p * ldE + k) = *(const uint4*)(en + (long)p * E + k);
     }
   }
   const int dlb = d.dl[b];
@@ -565,7 +570,7 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
         for (int i = 0; i < 8; ++i) {
           const int p = min(p0 + 4 * i, P - 1);
 #pragma unroll
-          for (int h = 0; h < H; ++h) xr[i][h] = *(const uint4*)(encs + p * Ec + v * 8 + h * VEC);
+          for (int h = 0; h < H; ++h) xr[i][h] = *(const uint4*)(encs + p * ldE + v * 8 + h * VEC);
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -1156,7 +1161,7 @@ static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds
     if (Ec > 2048) continue;
     size_t q = align16(16 + (size_t)d.P * d.A * esz);
     const size_t enc = q;
-    q = align16(q + (size_t)d.P * Ec * esz);
+    q = align16(q + (size_t)d.P * (Ec + 32) * esz);
     const size_t rd = q;
     q = align16(q + 16);
     const size_t rd2 = q;
@@ -1169,6 +1174,7 @@ static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds
       g.r_gv = (int)gvo;
       g.RS = rs;
       g.Ec = Ec;
+      g.ldE = Ec + 32;
       g.r_enc = (int)enc;
       g.r_red = (int)rd;
       g.r_red2 = (int)rd2;
