@@ -154,6 +154,22 @@ DEV float quad_sum_dpp(float v) {
   v += IMGCAP_DPP(v, 0x4E, 0xF);
   return v;
 }
+// Eight wave sums at once: lane l returns the sum over all 64 lanes of v[(l >> 3) & 7].  Each
+// exchange halves the values a lane carries (32 -> 4, 16 -> 2, 8 -> 1 values), then three more
+// for the last one: 10 shuffles instead of 8 x (6 DPP steps + readlane).
+DEV float wave_sum8_t(const float (&v)[8], int lane) {
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8;
+  float a[4], b[2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a[k] = (h5 ? v[4 + k] : v[k]) + __shfl_xor(h5 ? v[k] : v[4 + k], 32, 64);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) b[k] = (h4 ? a[2 + k] : a[k]) + __shfl_xor(h4 ? a[k] : a[2 + k], 16, 64);
+  float c = (h3 ? b[1] : b[0]) + __shfl_xor(h3 ? b[0] : b[1], 8, 64);
+  c += __shfl_xor(c, 4, 64);
+  c += __shfl_xor(c, 2, 64);
+  c += __shfl_xor(c, 1, 64);
+  return c;
+}
 
 DEV void unpack8(const uint4& a, const uint4& b, float (&v)[8]) {
   v[0] = __uint_as_float(a.x); v[1] = __uint_as_float(a.y); v[2] = __uint_as_float(a.z); v[3] = __uint_as_float(a.w);
@@ -533,16 +549,31 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
 #pragma unroll
         for (int h = 0; h < H; ++h) xr[i][h] = *(const uint4*)(att1s + p * A + (aok ? lane * 8 : 0) + h * VEC);
       }
+      if constexpr (NPW == 8) {  // every pixel's partial first, then one transposed reduction
+        float part[8];
 #pragma unroll
-      for (int i = 0; i < NPW; ++i) {
-        const int p = w + PWV * i;
-        if (p < P) {
+        for (int i = 0; i < 8; ++i) {
           const T* x8 = (const T*)&xr[i][0];
           float sc = 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) sc += wf[j] * fmaxf(to_f(x8[j]) + a2[j], 0.f);
-          sc = wave_sum_dpp(aok ? sc : 0.f);
-          if (lane == 0) red2[p] = sc;
+          part[i] = aok ? sc : 0.f;
+        }
+        const float sum = wave_sum8_t(part, lane);
+        const int p = w + PWV * ((lane >> 3) & 7);
+        if ((lane & 7) == 0 && p < P) red2[p] = sum;
+      } else {
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) {
+          const int p = w + PWV * i;
+          if (p < P) {
+            const T* x8 = (const T*)&xr[i][0];
+            float sc = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sc += wf[j] * fmaxf(to_f(x8[j]) + a2[j], 0.f);
+            sc = wave_sum_dpp(aok ? sc : 0.f);
+            if (lane == 0) red2[p] = sc;
+          }
         }
       }
     }
@@ -1032,14 +1063,22 @@ DEV void lstm_bwd_body(const imgcap_lstm_desc& d, const BGeo& g, const int blk) 
           for (int j = 0; j < 8; ++j) part[i] += (float)x[j] * dv[j];
         }
       }
+      bstamp(g, 2, t, 6);
+      if constexpr (PPW == 8) {  // all eight pixel sums in one transposed reduction
+        const float sum = wave_sum8_t(part, lane);
+        const int p = w + PWV * ((lane >> 3) & 7);
+        if ((lane & 7) == 0 && p < P) dal[p] += sum;
+      } else {
 #pragma unroll
-      for (int i = 0; i < PPW; ++i) {
-        const int p = w + PWV * i;
-        if (p < P) {  // wave-uniform
-          const float s = wave_sum_dpp(part[i]);
-          if (lane == 0) dal[p] += s;
+        for (int i = 0; i < PPW; ++i) {
+          const int p = w + PWV * i;
+          if (p < P) {  // wave-uniform
+            const float s = wave_sum_dpp(part[i]);
+            if (lane == 0) dal[p] += s;
+          }
         }
       }
+      bstamp(g, 2, t, 7);
     } else {
       for (int p = w; p < P; p += PWV) {
         float s = 0.f;
@@ -1055,7 +1094,7 @@ DEV void lstm_bwd_body(const imgcap_lstm_desc& d, const BGeo& g, const int blk) 
     }
     __syncthreads();
     bstamp(g, 2, t, 3);
-    if (w == 0) {  // softmax backward -> d score
+    if (w == 0) {  // softmax backward -> d score (stamps 8-10: the d att2 sub-phases)
       const float a = lane < P ? als[lane] : 0.f;
       const float da = lane < P ? dal[lane] : 0.f;
       const float dot = wave_sum_dpp(a * da);
@@ -1066,6 +1105,7 @@ DEV void lstm_bwd_body(const imgcap_lstm_desc& d, const BGeo& g, const int blk) 
       }
     }
     __syncthreads();
+    bstamp(g, 2, t, 8);
     // ---- d att2[a] = w_f[a] * sum_p de_p [att1[p, a] + att2[a] > 0] ----
     if (pga < GA) {
       float sacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1097,7 +1137,9 @@ DEV void lstm_bwd_body(const imgcap_lstm_desc& d, const BGeo& g, const int blk) 
 #pragma unroll
       for (int j = 0; j < 8; ++j) red[pga * A + va * 8 + j] = sacc[j];
     }
+    bstamp(g, 2, t, 9);
     __syncthreads();
+    bstamp(g, 2, t, 10);
     if (tid < A) {
       float s = 0.f;
       for (int q = 0; q < GA; ++q) s += red[q * A + tid];

@@ -165,6 +165,11 @@ def lstm():
         rs = [R[:, 1] - R[:, 0], R[:, 2] - R[:, 1], R[:, 3] - R[:, 2], R[:, 4] - R[:, 3], R[:, 5] - R[:, 4],
               sb[2, 0:T - 2, 0] - R[:, 5]]
         print("bwd R block 0, mean ns per step: " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(rn, rs)))
+        sn = ["dalpha products", "dalpha reductions", "dalpha barrier", "softmax bwd", "datt2 sums", "barrier",
+              "datt2 reduce+barrier"]
+        ss = [R[:, 6] - R[:, 2], R[:, 7] - R[:, 6], R[:, 3] - R[:, 7], R[:, 8] - R[:, 3], R[:, 9] - R[:, 8],
+              R[:, 10] - R[:, 9], R[:, 4] - R[:, 10]]
+        print("bwd R block 0 sub-phases (ns): " + ", ".join(f"{n} {x.mean():.0f}" for n, x in zip(sn, ss)))
         print("bwd cross: U published dgates -> X got %.0f ns, X got -> X done %.0f, R got dz - X done %.0f, "
               "R published -> U got datt %.0f, U done -> next U published %.0f" % (
                   (X[:, 2] - U[:, 1]).mean(), (X[:, 5] - X[:, 2]).mean(), (R[:, 1] - X[:, 5]).mean(),
