@@ -6,7 +6,7 @@
 // workgroup keeps its operands resident in LDS for the whole sequence and the steps are chained
 // by in-launch hand-offs.
 //
-// Roles (one 256-thread workgroup per CU; the LDS request keeps it that way):
+// Roles (one 512-thread workgroup per CU; the LDS request keeps it that way):
 //   UG blocks [0, NUG):   U role (blk < NU): UPB LSTM units = UC = 4*UPB gate columns (all four
 //                         gates of each unit), rows of [W_ih[:, M:] | W_hh] resident in LDS;
 //                         gates = xe + [z_t | h_{t-1}] . W^T + b_hh, then the LSTMCell -> h_t.
@@ -35,6 +35,8 @@
 #include "mfma.h"
 
 namespace imgcap {
+
+static int device_cus();
 
 namespace {
 
@@ -68,6 +70,7 @@ struct Geo {
   int r_gv;           // R: LDS offset of the row's [att2 | gate_pre chunk] values
   int ldE;            // R: LDS pitch (elements) of the enc rows: Ec + 32, see lstm_fwd_body
   int* err;           // the launch's error word (shared by the row groups)
+  int fault_step;     // test knob (IMGCAP_LSTM_FAULT_FWD): U block 0 never publishes h of this step
 };
 
 // thread 0 of block 0 (U+G) and of the first R block records [role][t][k]
@@ -418,7 +421,7 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
           st_wt(r_hs, (uint32_t)(off * sizeof(T)), v);
         }
         stamp(g, 0, t, 6);
-        block_publish(fh + blk, t + 1);
+        if (t != g.fault_step || blk != 0) block_publish(fh + blk, t + 1);
         stamp(g, 0, t, 7);
         // outputs nobody in this launch reads: after the hand-off
 #pragma unroll
@@ -708,6 +711,7 @@ struct BGeo {
   int gran_off;                 // sync word offset of the [B][E] dz granules
   long long* stamps;            // diagnostics (IMGCAP_LSTM_STAMPS=1): [role U/X/R][step][16]
   int* err;                     // the launch's error word (shared by the row groups)
+  int fault_step;               // test knob (IMGCAP_LSTM_FAULT_BWD): U block 0 never publishes dgates of this step
 };
 
 // thread 0 of the first U, X and R block records s_memrealtime at phase edges of step t
@@ -834,7 +838,7 @@ DEV void lstm_bwd_body(const imgcap_lstm_desc& d, const BGeo& g, const int blk) 
           const long off = ((long)b * Tn + t) * W3 + KY + (long)q * D + u0 + pc * VEC;
           st_wt(r_dcat, (uint32_t)(off * sizeof(T)), v);
         }
-        block_publish(fdg + blk, ep);
+        if (t != g.fault_step || blk != 0) block_publish(fdg + blk, ep);
         bstamp(g, 0, t, 1);
         // cell inputs of the next (earlier) step: independent of every hand-off
         if (iok && t > 0 && t - 1 < dlb) cin = cell_in_load<T>(d, t - 1, ib, ij);
@@ -1231,7 +1235,7 @@ static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds
   }
   if (!g.RS) return false;
   g.NR = d.B * g.RS;
-  if (g.NUG + g.NR > 256) return false;
+  if (g.NUG + g.NR > device_cus()) return false;
   // at least 81 KB: one workgroup per CU (the visibility form used here is the one measured so)
   lds = std::max(std::max(ug, r), (size_t)81 * 1024);
   if (lds > LDS_MAX) return false;
@@ -1291,6 +1295,41 @@ static int split_rows(const imgcap_lstm_desc& d, bool fwd) {
   return (d.B + 1) / 2;
 }
 
+// Compute units of the current device (every persistent workgroup must be resident at once: one
+// per CU, the LDS request keeps it that way).  Cached per device.
+static int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// Test knob: a step index from the environment (read at every launch), -1 when unset.
+static int env_step(const char* name) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : -1;
+}
+
+// Whether `kernel` with `lds` bytes of dynamic LDS gets at least one resident workgroup per CU
+// (raises the dynamic LDS limit first; the answer is cached per kernel and LDS size).
+static bool resident_one_per_cu(const void* kernel, size_t lds) {
+  struct Entry { const void* k; size_t lds; int ok; };
+  static Entry seen[64];
+  static int n_seen = 0;
+  for (int i = 0; i < n_seen; ++i)
+    if (seen[i].k == kernel && seen[i].lds == lds) return seen[i].ok;
+  int blocks = 0;
+  const bool ok = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess &&
+                  hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kernel, PT, lds) == hipSuccess && blocks >= 1;
+  if (n_seen < 64) seen[n_seen++] = Entry{kernel, lds, ok ? 1 : 0};
+  return ok;
+}
+
 struct FwdLaunch {
   imgcap_lstm_desc d[2];
   Geo g[2];
@@ -1319,7 +1358,7 @@ static bool fwd_launch_plan(const imgcap_lstm_desc& d, int esz, FwdLaunch& L) {
       soff += (words + 63) / 64 * 64;
       L.words = groups == 2 ? soff : words;
     }
-    if (!ok || L.nblk > 256) continue;
+    if (!ok || L.nblk > device_cus()) continue;
     for (int i = 0; i < groups; ++i) L.g[i].err = d.sync;
     if (groups == 1) {
       L.d[1] = L.d[0];
@@ -1330,15 +1369,13 @@ static bool fwd_launch_plan(const imgcap_lstm_desc& d, int esz, FwdLaunch& L) {
   return false;
 }
 
+static const void* fwd_kernel_of(int esz, int mt) {
+  if (esz == 2) return mt == 1 ? (const void*)lstm_fwd_persist_kernel<bf16, 1> : (const void*)lstm_fwd_persist_kernel<bf16, 2>;
+  return mt == 1 ? (const void*)lstm_fwd_persist_kernel<float, 1> : (const void*)lstm_fwd_persist_kernel<float, 2>;
+}
+
 template <typename T, int MT>
 static int launch_persist(const FwdLaunch& L, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)lstm_fwd_persist_kernel<T, MT>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      return fail(IMGCAP_EINVAL, "lstm persistent: cannot raise the dynamic LDS limit");
-    attr = true;
-  }
   hipLaunchKernelGGL((lstm_fwd_persist_kernel<T, MT>), dim3(L.nblk), dim3(PT), L.lds, st, L.d[0], L.g[0], L.d[1],
                      L.g[1], L.nb0);
   IMGCAP_CHECK_LAUNCH("lstm persistent forward");
@@ -1359,6 +1396,9 @@ int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
   FwdLaunch L;
   if (!fwd_launch_plan(d, esz, L)) return 0;
+  // every workgroup resident at once (the hand-offs spin on each other): else the per-step path
+  if (!resident_one_per_cu(fwd_kernel_of(esz, L.mt), L.lds)) return 0;
+  L.g[0].fault_step = L.g[1].fault_step = env_step("IMGCAP_LSTM_FAULT_FWD");
   static const bool stamps = getenv("IMGCAP_LSTM_STAMPS") && atoi(getenv("IMGCAP_LSTM_STAMPS"));
   L.g[0].stamps = L.g[1].stamps = nullptr;
   if (stamps && d.T <= 64) {  // group 0 only, after every group's sync words (fwd and bwd)
@@ -1397,7 +1437,7 @@ static bool bwd_plan(const imgcap_lstm_desc& d, int esz, BGeo& g, size_t& lds, i
   g.NU = d.D / g.UPB;
   g.NX = d.E / 16;
   g.NR = d.B;
-  if (g.NU + g.NX + g.NR > 256) return false;
+  if (g.NU + g.NX + g.NR > device_cus()) return false;
   g.ldu = K4 + KY + pad;
   g.ldx = K4 + pad;
   const size_t red = (size_t)(PWV / mt) * 16 * mt * 20 * 4;
@@ -1466,7 +1506,7 @@ static bool bwd_launch_plan(const imgcap_lstm_desc& d, int esz, BwdLaunch& L) {
       soff += (words + 63) / 64 * 64;
       L.words = groups == 2 ? soff : words;
     }
-    if (!ok || L.nblk > 256) continue;
+    if (!ok || L.nblk > device_cus()) continue;
     for (int i = 0; i < groups; ++i) L.g[i].err = d.sync;
     if (groups == 1) {
       L.d[1] = L.d[0];
@@ -1477,15 +1517,13 @@ static bool bwd_launch_plan(const imgcap_lstm_desc& d, int esz, BwdLaunch& L) {
   return false;
 }
 
+static const void* bwd_kernel_of(int esz, int mt) {
+  if (esz == 2) return mt == 1 ? (const void*)lstm_bwd_persist_kernel<bf16, 1> : (const void*)lstm_bwd_persist_kernel<bf16, 2>;
+  return mt == 1 ? (const void*)lstm_bwd_persist_kernel<float, 1> : (const void*)lstm_bwd_persist_kernel<float, 2>;
+}
+
 template <typename T, int MT>
 static int launch_bwd_persist(const BwdLaunch& L, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)lstm_bwd_persist_kernel<T, MT>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      return fail(IMGCAP_EINVAL, "lstm persistent backward: cannot raise the dynamic LDS limit");
-    attr = true;
-  }
   hipLaunchKernelGGL((lstm_bwd_persist_kernel<T, MT>), dim3(L.nblk), dim3(PT), L.lds, st, L.d[0], L.g[0], L.d[1],
                      L.g[1], L.nb0);
   IMGCAP_CHECK_LAUNCH("lstm persistent backward");
@@ -1504,6 +1542,8 @@ int lstm_bwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   const int esz = d.dtype == IMGCAP_BF16 ? 2 : 4;
   BwdLaunch L;
   if (!bwd_launch_plan(d, esz, L)) return 0;
+  if (!resident_one_per_cu(bwd_kernel_of(esz, L.mt), L.lds)) return 0;
+  L.g[0].fault_step = L.g[1].fault_step = env_step("IMGCAP_LSTM_FAULT_BWD");
   IMGCAP_REQUIRE(d.w_zh_t && d.w_att_t, "lstm persistent backward: transposed weights needed");
   IMGCAP_REQUIRE(d.sync_words >= L.words, "lstm persistent backward: sync workspace smaller than imgcap_lstm_sync_words");
   static const bool stamps = getenv("IMGCAP_LSTM_STAMPS") && atoi(getenv("IMGCAP_LSTM_STAMPS"));

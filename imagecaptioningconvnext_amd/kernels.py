@@ -328,6 +328,29 @@ def ce_fused(logits, targets, V, scale, lse, loss, hit5, dlogits):
               scale.data_ptr(), lse.data_ptr(), ptr(loss), ptr(hit5), dlogits.data_ptr(), dlogits.stride(0), stream())
 
 
+def ce_fused_fits(logits, dlogits, V):
+    """Whether imgcap_ce_fused takes these rows (its per-lane register row: V <= 24576 in bf16,
+    12288 in fp32; 16-byte aligned rows whose pitch covers the vectorised row)."""
+    vec = 8 if logits.dtype == torch.bfloat16 else 4
+    nvec = (V + vec - 1) // vec
+    return ((nvec + 255) // 256 <= 12 and logits.stride(0) % vec == 0 and dlogits.stride(0) % vec == 0
+            and dlogits.stride(0) >= nvec * vec and logits.data_ptr() % 16 == 0 and dlogits.data_ptr() % 16 == 0)
+
+
+def ce_train(logits, targets, V, metrics, lse, loss, hit5, dlogits, finalize):
+    """Training-step CE (train.py:266-276): loss rows, top-5 hits, metrics (via ``finalize``, the
+    caller's loss_finalize launch) and dlogits = (softmax - onehot) / tokens.  One fused pass over
+    the logits when imgcap_ce_fused takes the rows, else ce_fwd -> finalize -> ce_bwd (the scale
+    1/tokens is metrics[3], written by loss_finalize)."""
+    if ce_fused_fits(logits, dlogits, V):
+        ce_fused(logits, targets, V, metrics[3:4], lse, loss, hit5, dlogits)
+        finalize()
+    else:
+        ce_fwd(logits, targets, V, lse, loss, hit5)
+        finalize()
+        ce_bwd(logits, targets, V, lse, metrics[3:4], dlogits)
+
+
 def loss_finalize(loss_rows, hit5, targets, extra, out):
     _abi.call("imgcap_loss_finalize", targets.numel(), loss_rows.data_ptr(), hit5.data_ptr(), targets.data_ptr(),
               ptr(extra), out.data_ptr(), stream())

@@ -57,6 +57,7 @@ class LstmEngine:
         self._y_cnt = None
         self._sync = None
         self._chain_sync = []
+        self._retired_sync = []  # superseded hand-off word buffers (captured graphs may point at them)
 
     # K-slices of the backward step GEMMs (imgcap_lstm_desc.x_slices / y_slices).  Measured at
     # the C2 shape (B=32, D=512, tools/gpu/lstm_sweep.sh): x 2 / y 3 (80 x 2 and 32 x 3 blocks)
@@ -94,12 +95,26 @@ class LstmEngine:
         if words <= 0:
             return
         if self._sync is None or self._sync.numel() < words or self._sync.device != dev:
+            if self._sync is not None:  # a captured graph may still point at it: keep it alive
+                self._retired_sync.append(self._sync)
             self._sync = torch.zeros(max(words + 6400, 8192), dtype=torch.int32, device=dev)  # + diagnostics stamps
         d.sync, d.sync_words = self._sync.data_ptr(), self._sync.numel()
 
     def sync_error(self):
         """Non-zero when the last persistent recurrence gave up on a hand-off (bounded spin)."""
         return 0 if self._sync is None else int(self._sync[0].item())
+
+    def _fold_status(self, dst, init=False):
+        """dst[0] (= / +=) the persistent recurrences' error words (word 0 of every sync buffer in
+        use), on the stream: a timed-out hand-off leaves that step's outputs invalid, and the
+        trainer raises on it instead of training on them (train_step._update / drain_metrics)."""
+        words = [self._sync] if self._sync is not None else []
+        if self.CHAINS > 1:
+            words += list(self._chain_sync)
+        if init:
+            dst.zero_()
+        for w in words:
+            dst.add_(w[0:1])
 
     def _chain_rows(self, B):
         n = max(1, min(self.CHAINS, B))
@@ -132,10 +147,14 @@ class LstmEngine:
             if d.sync:  # persistent recurrence per chain: each chain its own flag words
                 words = _abi.lib().imgcap_lstm_sync_words(ctypes.byref(sd))
                 if words > 0:
-                    if len(self._chain_sync) <= i or self._chain_sync[i].device != main.device:
-                        self._chain_sync = self._chain_sync[:i] + [torch.zeros(8192, dtype=torch.int32,
-                                                                               device=main.device)]
-                    sd.sync, sd.sync_words = self._chain_sync[i].data_ptr(), 8192
+                    cur = self._chain_sync[i] if len(self._chain_sync) > i else None
+                    if cur is None or cur.device != main.device or cur.numel() < words:
+                        # grown during warm-up, before any capture (a captured graph keeps its own)
+                        new = torch.zeros(max(words, 8192), dtype=torch.int32, device=main.device)
+                        if cur is not None:
+                            self._retired_sync.append(cur)
+                        self._chain_sync = self._chain_sync[:i] + [new] + self._chain_sync[i + 1:]
+                    sd.sync, sd.sync_words = self._chain_sync[i].data_ptr(), self._chain_sync[i].numel()
             if ws:
                 for k, v in ws[i].items():
                     setattr(sd, k, v.data_ptr())
@@ -262,16 +281,19 @@ class LstmEngine:
             lse = torch.empty(B * T, **f32)
             lrow = torch.empty(B * T, **f32)
             hit = torch.empty(B * T, **f32)
-            metrics = torch.empty(4, **f32)  # loss, tokens, top5 hits, 1/tokens
+            metrics = torch.empty(5, **f32)  # loss, tokens, top5 hits, 1/tokens, hand-off errors
             # loss, top-5 and the loss gradient in one pass over the logits (train.py:266-276);
             # backward() starts from these dlogits
             dlogits = torch.empty(B * T, self.Vpad, **ctd)
-            K.ce_fused(logits, targets, V, metrics[3:4], lse, lrow, hit, dlogits)
             dalpha = torch.empty(B, T, P, **f32)
             reg = torch.empty(1, **f32)
-            _abi.call("imgcap_attn_reg", B, T, P, alphas.data_ptr(), dl.data_ptr(), alphaC, dalpha.data_ptr(),
-                      reg.data_ptr(), K.stream())
-            K.loss_finalize(lrow, hit, targets, reg, metrics)
+
+            def finalize():
+                _abi.call("imgcap_attn_reg", B, T, P, alphas.data_ptr(), dl.data_ptr(), alphaC, dalpha.data_ptr(),
+                          reg.data_ptr(), K.stream())
+                K.loss_finalize(lrow, hit, targets, reg, metrics)
+            K.ce_train(logits, targets, V, metrics, lse, lrow, hit, dlogits, finalize)
+            self._fold_status(metrics[4:5], init=True)  # the forward recurrence's error word
             s.update(logits=logits, targets=targets, lse=lse, dalpha=dalpha, metrics=metrics, dlogits=dlogits)
         return s
 
@@ -409,10 +431,13 @@ class LstmEngine:
         chain_ws = []
         rows = self._chain_rows(B)
         if self._y_cnt is None or len(self._y_cnt) != len(rows) or self._y_cnt[0].device != dev:
+            self._retired_sync += [c for c in (self._y_cnt or []) if c is not None]
             self._y_cnt = [None] * len(rows)
         for i, (b0, b1) in enumerate(rows):
             nrg = (b1 - b0 + 31) // 32
             if self._y_cnt[i] is None or self._y_cnt[i].numel() < nrg * (D // 16):
+                if self._y_cnt[i] is not None:  # captured graphs may point at the old counters
+                    self._retired_sync.append(self._y_cnt[i])
                 self._y_cnt[i] = torch.zeros(nrg * (D // 16), device=dev, dtype=torch.int32)
             chain_ws.append(dict(dz=torch.empty(xs, b1 - b0, E + D, **f32),
                                  ws_y=torch.empty(ys * nrg * (D // 16) * 512, **f32), y_cnt=self._y_cnt[i]))
@@ -434,6 +459,8 @@ class LstmEngine:
         bufs["chain_ws"] = chain_ws
         s["bwd_bufs"] = bufs  # the descriptor points into these: keep them alive as long as `s`
         self._launch("imgcap_lstm_tf_bwd", d, chain_ws)
+        if "metrics" in s:
+            self._fold_status(s["metrics"][4:5])  # the backward recurrence's error word
         dc2 = dcat.view(BT, W3)
         dgates = dc2[:, A + E:]
         # W_hcat / b_hcat grads (batched over all B*T rows)

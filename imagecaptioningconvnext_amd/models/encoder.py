@@ -130,6 +130,9 @@ class Encoder(nn.Module):
         self.sd_seed = 0
         self._packed = None
         self._packed_key = None
+        # superseded packs stay referenced: a captured HIP graph holds raw pointers into them
+        # (train_step drops them when it re-captures)
+        self._retired_packs = []
         self._engine = None
         self.fine_tune()
 
@@ -151,6 +154,8 @@ class Encoder(nn.Module):
         key = self._pack_key()
         if self._packed is not None and self._packed_key == key:
             return self._packed
+        if self._packed is not None:
+            self._retired_packs.append(self._packed)
         ct = self.compute_dtype
         f = self.convnext
         with torch.no_grad():
@@ -266,6 +271,10 @@ class Encoder(nn.Module):
                 x = torch.empty(B, h // 2, w // 2, C2, device=dev, dtype=ct)
                 K.gemm(patches, down["w"], trans_b=True, bias=down["b"], out=x.view(-1, C2))
         return x, bid
+
+    def release_retired(self):
+        """Drop the superseded weight packs (no captured graph refers to them any more)."""
+        self._retired_packs = []
 
     def trainable(self):
         return any(p.requires_grad for p in self.convnext.parameters())

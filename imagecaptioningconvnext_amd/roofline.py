@@ -1,143 +1,234 @@
 """Live roofline of the bench step's dominant kernel (bench.py ``roofline`` field).
 
-Candidates are timed on the current HIP stream with HIP events around back-to-back launches
-replayed from a HIP graph (so host launch cost does not hide short kernels), each with its
-algorithmic work per launch:
-
-  * every GEMM of one train step: the step runs once eagerly with ``kernels.record_gemms``
-    collecting each ``imgcap_gemm`` call; the calls are grouped by the kernel that serves them
-    (``imgcap_gemm_plan``: one group per kernel symbol, as rocprofv3 lists them) and each call
-    is re-timed in isolation.  Work = 2*M*N*K per call; a group's achieved rate is
-    sum(work) / sum(time), i.e. its average launch's work over its average launch duration.
-  * the fused ConvNeXt MLP (cnblock_mlp) per stage width: 2 * 2 * M * C * 4C per launch.
-  * the depthwise 7x7 per stage: HBM bytes = read x + write y (+ weights).
-
-The dominant kernel is the group with the largest time per step; its rate is reported against
-the MI355X peak (bf16 dense MFMA 2.5 PFLOP/s, HBM 8 TB/s; MI355X_MICROARCH.md).
+Every library call of one train step is timed where it runs: the step is launched eagerly (the
+sequential schedule: encoder forward, decoder forward + loss, backward, clamp + Adam) and each
+``imgcap_*`` call is bracketed by two HIP events on the stream it is launched on, with a short
+device-side sleep queued in front of the first event so that the GPU runs behind the host and the
+events bracket only that call's kernels (no host launch gap inside the interval).  Three such
+steps; the median per call.  Calls are grouped by the kernel symbol rocprofv3 lists for them
+(GEMMs by the kernel ``imgcap_gemm_plan`` picks; the persistent LSTM recurrences, the attention,
+the fused MLP, the depthwise conv, CE, LayerNorm, Adam ... by their own symbols) and ranked by
+time per step; the top group is the step's dominant kernel.  Its algorithmic work per launch
+(DESIGN.md §5 lists the per-call formulas: 2*M*N*K for GEMMs, the recurrences' MACs per row and
+step, bytes read + written once for the HBM-bound kernels) over its average launch duration is
+reported against the MI355X peak (bf16 dense MFMA 2.5 PFLOP/s, MX-FP8 5 PFLOP/s, fp32 157 TF/s,
+HBM 8 TB/s; MI355X_MICROARCH.md).
 """
 import collections
+import statistics
 
 import torch
 
+from . import _abi
 from . import kernels as K
 
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_FP8_TFLOPS = 5000.0  # dense block-scaled (MX) e4m3 MFMA
+PEAK_F32_TFLOPS = 157.3   # f32 MFMA = f32 vector rate
+SLEEP_CYCLES = 400_000    # device sleep in front of each timed call (> the host's launch time)
 
 _KIND_NAME = {1: "gemm_skinny_kernel", 2: "gemm_kernel<64,64,64>", 3: "gemm_kernel<128,128,64>",
               4: "gemm_glds_kernel<128,128>", 5: "gemm256_kernel<256,256>", 6: "gemm_glds_kernel<64,64>",
               7: "gemm_glds_kernel<128,64>"}
 
+# calls that launch nothing
+_NO_KERNEL = {"imgcap_workspace_slot", "imgcap_set_seed_counter", "imgcap_gemm_set_policy", "imgcap_workspace_attach",
+              "imgcap_workspace_needed", "imgcap_version"}
 
-def time_launch(fn, reps=50, warm=5, graph=True):
-    """Seconds per launch of ``fn``, HIP events around ``reps`` back-to-back launches.  With
-    graph=True the launches are captured into one HIP graph and replayed, so host launch cost
-    (~10 us per ctypes call) does not hide short kernels -- the per-launch figure then matches
-    the kernel durations rocprofv3 reports for the step (which also replays a graph)."""
-    for _ in range(warm):
-        fn()
-    torch.cuda.synchronize()
-    g = None
-    if graph:
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for _ in range(reps):
-                fn()
-        g.replay()
-        torch.cuda.synchronize()
-    st = torch.cuda.current_stream()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(st)
-    if g is not None:
-        g.replay()
-    else:
-        for _ in range(reps):
-            fn()
-    b.record(st)
-    b.synchronize()
-    return a.elapsed_time(b) / reps * 1e-3  # seconds per launch
+# ABI entry point -> the kernel symbol rocprofv3 reports for it (substring)
+_SYMBOL = {
+    "imgcap_lstm_tf_fwd": "lstm_fwd_persist_kernel", "imgcap_lstm_tf_bwd": "lstm_bwd_persist_kernel",
+    "imgcap_mha_fwd": "mha_fwd_kernel", "imgcap_mha_bwd": "mha_bwd_kernel",
+    "imgcap_dwconv7": "dwconv7_kernel", "imgcap_dwconv7_ln": "dwconv7_ln_kernel",
+    "imgcap_dwconv7_bwd_data": "dwconv7_kernel", "imgcap_dwconv7_wgrad": "dwconv7_wgrad_kernel",
+    "imgcap_ce_fused": "ce_fused_kernel", "imgcap_ce_fwd": "ce_fwd_kernel", "imgcap_ce_bwd": "ce_bwd_kernel",
+    "imgcap_add_layernorm_fwd": "add_ln_fwd_kernel", "imgcap_add_layernorm_bwd": "add_ln_bwd_kernel",
+    "imgcap_clamp_adam": "clamp_adam_kernel", "imgcap_convnext_stem": "stem_kernel",
+    "imgcap_convnext_stem_u8": "stem_kernel", "imgcap_ln_patchify2": "ln_patchify2_kernel",
+    "imgcap_ln_patchify2_bwd": "ln_patchify2_bwd_kernel", "imgcap_transpose": "transpose_kernel",
+    "imgcap_embedding_fwd": "embedding_fwd_kernel", "imgcap_embedding_bwd": "emb_segsum_kernel",
+    "imgcap_colsum_multi": "colsum_multi_kernel", "imgcap_colsum": "colsum_kernel",
+    "imgcap_mx_quant_rows": "mx_quant_rows_kernel", "imgcap_sort_gather_rows": "sort_gather_kernel",
+    "imgcap_dropout": "dropout_kernel", "imgcap_cast": "cast_kernel", "imgcap_rowscale": "rowscale_kernel",
+    "imgcap_layer_scale_grad": "layer_scale_grad_kernel", "imgcap_lstm_denc": "lstm_denc_kernel",
+    "imgcap_attn_reg": "attn_reg_kernel", "imgcap_loss_finalize": "loss_finalize_kernel",
+    "imgcap_stochastic_depth_scales": "sd_scales_kernel", "imgcap_adaptive_pool_nhwc": "adaptive_pool_kernel",
+    "imgcap_adaptive_pool_bwd_nhwc": "adaptive_pool_bwd_kernel", "imgcap_mean_mid": "mean_mid_kernel",
+    "imgcap_fill": "fill_kernel", "imgcap_slice_reduce": "slice_reduce_kernel",
+}
 
 
-def _gemm_groups(trainer, batch):
+def _esz(dtype_id):
+    return 4 if dtype_id == _abi.F32 else 2
+
+
+def _mfma_peak(dtype_id):
+    return PEAK_BF16_TFLOPS if dtype_id == _abi.BF16 else PEAK_F32_TFLOPS
+
+
+def _gemm_group(a):
+    dtype, ak, bk, M, N, K_ = a[0], a[1], a[2], a[3], a[4], a[5]
+    lda, ldb, ep = a[7], a[10], a[16]._obj
+    kind, splits = K.gemm_plan(dtype, ak, bk, M, N, K_, lda, ldb, a[15], ep.split_k)
+    name = _KIND_NAME.get(kind, f"gemm kind {kind}")
+    if kind in (2, 3, 4, 5, 6, 7):
+        name += f"<ak={ak},bk={bk}>" + (" (split-K)" if splits > 1 else "")
+    tf = lambda v: "true" if v else "false"  # noqa: E731
+    sym = {4: f"gemm_glds_kernel<128, 128, {tf(ak)}, {tf(bk)}, ",  # any stage count
+           5: f"gemm256_kernel<64, 2, {tf(ak)}, {tf(bk)}>",
+           6: f"gemm_glds_kernel<64, 64, {tf(ak)}, {tf(bk)}, ",
+           7: f"gemm_glds_kernel<128, 64, {tf(ak)}, {tf(bk)}, "}.get(kind, _KIND_NAME.get(kind, ""))
+    return name, sym
+
+
+def _work(fn, a):
+    """(group key, symbol, bound, work, peak, shape) of one call: work in FLOP (bound "mfma") or
+    bytes read + written once (bound "hbm"); work None = no model (ranked by time only)."""
+    sym = _SYMBOL.get(fn, fn)
+    if fn == "imgcap_gemm":
+        name, gsym = _gemm_group(a)
+        M, N, K_, batch = a[3], a[4], a[5], a[15]
+        return name, gsym, "mfma", 2.0 * M * N * K_ * batch, _mfma_peak(a[0]), (M, N, K_)
+    if fn == "imgcap_gemm_grouped":
+        arr = (_abi.GemmProblem * a[2]).from_address(a[3].value)
+        f = sum(2.0 * p.M * p.N * p.K for p in arr)
+        ak, bk = a[0], a[1]
+        nm = f"gemm_glds_grouped_kernel<{'true' if ak else 'false'}, {'true' if bk else 'false'}>"
+        return nm, nm, "mfma", f, PEAK_BF16_TFLOPS, (a[2], "problems")
+    if fn == "imgcap_gemm_mx":
+        M, N, K_ = a[0], a[1], a[2]
+        return "gemm_mx_kernel (MX-FP8)", "gemm_mx", "mfma", 2.0 * M * N * K_, PEAK_FP8_TFLOPS, (M, N, K_)
+    if fn in ("imgcap_lstm_tf_fwd", "imgcap_lstm_tf_bwd"):
+        d = a[0]._obj
+        B, P, E, A, D, T = d.B, d.P, d.E, d.A, d.D, d.T
+        if fn.endswith("fwd"):  # G: h [W_da; W_fb]; U: [z | h] [W_ih_z | W_hh]^T; R: scores + context
+            macs = D * (A + E) + (E + D) * 4 * D + P * A + P * E
+        else:  # U: dgates W_hh + d att [W_da; W_fb]; X: dgates W_ih_z; R: d alpha, d att1 / de
+            macs = 4 * D * D + (A + E) * D + 4 * D * E + P * E + 2 * P * A
+        return sym, sym, "mfma", 2.0 * B * T * macs, _mfma_peak(d.dtype), (B, T, E, D)
+    if fn in ("imgcap_mha_fwd", "imgcap_mha_bwd"):
+        m = a[0]._obj
+        f = 2.0 * m.B * m.H * m.Lq * m.Lk * m.dh * (2 if fn.endswith("fwd") else 5)
+        if m.causal:
+            f *= 0.5
+        return sym, sym, "mfma", f, _mfma_peak(m.dtype), (m.B, m.H, m.Lq, m.Lk)
+    if fn == "imgcap_cnblock_mlp":
+        M, C = a[0], a[1]
+        nm = f"cnblock_mlp_{'res' if C == 96 else 'str'}_kernel<{C}>"
+        return nm, nm, "mfma", 16.0 * M * C * C, PEAK_BF16_TFLOPS, (M, C)
+    if fn in ("imgcap_dwconv7", "imgcap_dwconv7_ln", "imgcap_dwconv7_wgrad"):
+        e = _esz(a[0])
+        n = a[1] * a[2] * a[3] * a[4]
+        return sym, sym, "hbm", 2.0 * n * e + 50 * a[4] * 4, PEAK_HBM_GBS, (a[1], a[2], a[3], a[4])
+    if fn == "imgcap_dwconv7_bwd_data":
+        e = _esz(a[0])
+        n = a[1] * a[2] * a[3] * a[4]
+        res = a[7] is not None and a[7] != 0
+        return sym, sym, "hbm", (3.0 if res else 2.0) * n * e + 49 * a[4] * 4, PEAK_HBM_GBS, (a[1], a[2], a[3], a[4])
+    if fn in ("imgcap_ce_fused", "imgcap_ce_bwd"):
+        return sym, sym, "hbm", 2.0 * a[1] * a[2] * _esz(a[0]), PEAK_HBM_GBS, (a[1], a[2])
+    if fn == "imgcap_ce_fwd":
+        return sym, sym, "hbm", 1.0 * a[1] * a[2] * _esz(a[0]), PEAK_HBM_GBS, (a[1], a[2])
+    if fn == "imgcap_add_layernorm_fwd":  # x (+ r) read, y (+ s_out) written
+        n = a[1] * a[2] * _esz(a[0])
+        return sym, sym, "hbm", n * (2 + (a[4] is not None) + (a[11] is not None)), PEAK_HBM_GBS, (a[1], a[2])
+    if fn == "imgcap_add_layernorm_bwd":  # dy, s read, dx (+ dr) written (+ fp32 dy*xhat)
+        n = a[1] * a[2]
+        b = n * _esz(a[0]) * (3 + (a[12] is not None)) + (n * 4 if a[15] is not None else 0)
+        return sym, sym, "hbm", b, PEAK_HBM_GBS, (a[1], a[2])
+    if fn == "imgcap_clamp_adam":  # p, g, m, v read; p, m, v written (fp32) + bf16 shadow written
+        n = a[0]
+        return sym, sym, "hbm", n * (7 * 4 + (2 if a[5] is not None else 0)), PEAK_HBM_GBS, (n,)
+    if fn in ("imgcap_convnext_stem", "imgcap_convnext_stem_u8"):
+        B, H, W, C0 = a[1], a[2], a[3], a[4]
+        src = 1 if fn.endswith("u8") else 4
+        return sym, sym, "hbm", B * 3 * H * W * src + B * (H // 4) * (W // 4) * C0 * _esz(a[0]), PEAK_HBM_GBS, \
+            (B, H, W, C0)
+    if fn in ("imgcap_ln_patchify2", "imgcap_ln_patchify2_bwd"):
+        n = a[1] * a[2] * a[3] * a[4]
+        return sym, sym, "hbm", (2.0 if fn == "imgcap_ln_patchify2" else 3.0) * n * _esz(a[0]), PEAK_HBM_GBS, \
+            (a[1], a[2], a[3], a[4])
+    if fn == "imgcap_transpose":
+        return sym, sym, "hbm", 2.0 * a[1] * a[2] * _esz(a[0]), PEAK_HBM_GBS, (a[1], a[2])
+    if fn == "imgcap_embedding_fwd":
+        return sym, sym, "hbm", a[1] * a[2] * (4.0 + _esz(a[0])), PEAK_HBM_GBS, (a[1], a[2])
+    if fn == "imgcap_embedding_bwd":
+        return sym, sym, "hbm", a[1] * a[2] * (4.0 + _esz(a[0])), PEAK_HBM_GBS, (a[1], a[2])
+    if fn == "imgcap_colsum_multi":
+        arr = (_abi.ColsumItem * a[0]).from_address(a[1].value)
+        return sym, sym, "hbm", float(sum(it.rows * it.cols * _esz(it.dtype) for it in arr)), PEAK_HBM_GBS, \
+            (a[0], "items")
+    if fn == "imgcap_mx_quant_rows":
+        return sym, sym, "hbm", a[1] * a[2] * (_esz(a[0]) + 1 + 1 / 32), PEAK_HBM_GBS, (a[1], a[2])
+    if fn == "imgcap_sort_gather_rows":
+        return sym, sym, "hbm", 2.0 * a[1] * a[2] * a[3] * _esz(a[0]), PEAK_HBM_GBS, (a[1], a[2], a[3])
+    if fn == "imgcap_dropout":
+        return sym, sym, "hbm", 2.0 * a[1] * _esz(a[0]), PEAK_HBM_GBS, (a[1],)
+    if fn == "imgcap_cast":
+        return sym, sym, "hbm", a[2] * (_esz(a[0]) + _esz(a[1])), PEAK_HBM_GBS, (a[2],)
+    return sym, sym, "latency", None, None, ()
+
+
+def _timed_step(trainer, batch):
+    """[(fn, args, seconds)] of every library call of one eager sequential train step."""
     rec = []
-    K.record_gemms(rec)
+    orig = _abi.call
+
+    def call(fn, *a):
+        if fn in _NO_KERNEL:
+            return orig(fn, *a)
+        st = torch.cuda.current_stream()
+        torch.cuda._sleep(SLEEP_CYCLES)  # the device waits here while the host queues the call
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        r = orig(fn, *a)
+        e1.record(st)
+        rec.append((fn, a, e0, e1))
+        return r
+
+    _abi.call = call
     try:
         trainer._fwd_bwd(*batch)
+        # clip + Adam (the collectives of _update are left out: rank 0 alone runs this)
+        trainer.eng.fp.adam_step(trainer.decoder_lr, trainer.grad_clip)
+        if trainer.enc_eng is not None:
+            trainer.enc_eng.fp.adam_step(trainer.encoder_lr, trainer.grad_clip)
     finally:
-        K.record_gemms(None)
+        _abi.call = orig
     torch.cuda.synchronize()
+    return [(fn, a, e0.elapsed_time(e1) * 1e-3) for fn, a, e0, e1 in rec]
+
+
+def kernel_table(trainer, batch, passes=3):
+    """Per-kernel-symbol rows of one train step, ranked by time per step."""
+    runs = [_timed_step(trainer, batch) for _ in range(passes)]
+    base = runs[0]
+    if any(len(r) != len(base) or any(x[0] != y[0] for x, y in zip(r, base)) for r in runs):
+        raise RuntimeError("roofline: the step's library calls differ between passes")
     groups = collections.OrderedDict()
-    for c in rec:
-        if c.get("mx"):  # block-scaled fp8 (frozen encoder Linears of C5)
-            g = groups.setdefault("gemm_mx_kernel (MX-FP8)", dict(name="gemm_mx_kernel (MX-FP8)", calls=[],
-                                                                   bound="mfma", symbol="gemm_mx_kernel", mx=True))
-            g["calls"].append(c)
-            continue
-        kind, splits = K.gemm_plan(c["dtype"], c["ak"], c["bk"], c["M"], c["N"], c["K"], c["lda"], c["ldb"], 1,
-                                   c["split_k"])
-        name = _KIND_NAME.get(kind, f"gemm kind {kind}")
-        if kind in (2, 3, 4, 5, 6, 7):
-            name += f"<ak={c['ak']},bk={c['bk']}>" + (" (split-K)" if splits > 1 else "")
-        tf = lambda v: "true" if v else "false"  # noqa: E731
-        sym = {4: f"gemm_glds_kernel<128, 128, {tf(c['ak'])}, {tf(c['bk'])}, ",  # any stage count
-               5: f"gemm256_kernel<64, 2, {tf(c['ak'])}, {tf(c['bk'])}>",
-               6: f"gemm_glds_kernel<64, 64, {tf(c['ak'])}, {tf(c['bk'])}, ",
-               7: f"gemm_glds_kernel<128, 64, {tf(c['ak'])}, {tf(c['bk'])}, "}.get(kind, _KIND_NAME.get(kind, ""))
-        g = groups.setdefault(name, dict(name=name, calls=[], bound="mfma", symbol=sym))
-        g["calls"].append(c)
-    out = []
-    for g in groups.values():
-        t_tot, f_tot, b_tot = 0.0, 0.0, 0.0
-        for c in g["calls"]:
-            t_tot += time_launch(c["call"], reps=20, warm=2)
-            f_tot += 2.0 * c["M"] * c["N"] * c["K"]
-            ct = c["keep"][-1].c_dtype
-            cb = 4 if ct == 0 else 2 if ct == 1 else 1 + 1 / 32
-            ab = (1 + 1 / 32) if c.get("mx") else 2.0  # operand bytes per element (MX: + its scale)
-            b_tot += ab * (c["M"] + c["N"]) * c["K"] + cb * c["M"] * c["N"]  # A + B read, C written once
-        n = len(g["calls"])
-        shapes = sorted({(c["M"], c["N"], c["K"]) for c in g["calls"]})
-        out.append(dict(name=g["name"], bound="mfma", per_step=n, t=t_tot / n, flops=f_tot / n, symbol=g["symbol"],
-                        bytes=b_tot / n, peak=PEAK_FP8_TFLOPS if g.get("mx") else PEAK_BF16_TFLOPS,
-                        note=f"{n} launches/step, shapes (M,N,K) {shapes[:6]}{' ...' if len(shapes) > 6 else ''}"))
-    return out
-
-
-def _encoder_groups(trainer, B, dev):
-    enc = trainer.encoder
-    if enc.compute_dtype != torch.bfloat16:
-        return []
-    pk = enc._pack()
-    out = []
-    hw = 56
-    for st, (blocks, _) in enumerate(pk["stages"]):
-        blk = blocks[0]
-        C = blk["w1"].shape[1]
-        M = B * hw * hw
-        x = torch.randn(B, hw, hw, C, device=dev).to(torch.bfloat16)
-        y = torch.empty_like(x)
-        if C in K.CNBLOCK_MLP_CHANNELS:
-            x2 = x.view(M, C)
-            z = y.view(M, C)
-
-            def mlp(blk=blk, z=z, x2=x2):
-                K.cnblock_mlp(z, blk["w1"], blk["b1"], blk["w2"], blk["b2"], blk["gamma"], x2, ln_w=blk["lnw"],
-                              ln_b=blk["lnb"])
-            kname = "cnblock_mlp_res_kernel" if C == 96 else "cnblock_mlp_str_kernel"  # csrc/cnblock_mlp.hip
-            out.append(dict(name=f"{kname}<{C}> (stage {st + 1} fused MLP)", bound="mfma",
-                            symbol=f"{kname}<{C}>", bytes=3.0 * M * C * 2 + 2 * 4 * C * C * 2,
-                            per_step=len(blocks), t=time_launch(mlp, reps=20), flops=2.0 * 2 * M * C * 4 * C,
-                            note=f"M={M} C={C}: LN + Linear C->4C + GELU + Linear 4C->C + scale + residual"))
-        if hw <= 64:
-            def dw(blk=blk, x=x, y=y):
-                K.dwconv7(x, blk["w49"], blk["dwb"], y)
-            out.append(dict(name=f"dwconv7_kernel (stage {st + 1}, C={C})", bound="hbm", per_step=len(blocks),
-                            symbol="dwconv7_kernel",
-                            t=time_launch(dw, reps=20), bytes=2.0 * M * C * 2 + 49 * C * 4,
-                            note=f"B*H*W={M} C={C}: read x + write y (bf16)"))
-        hw //= 2
-    return out
+    for i, (fn, a, _) in enumerate(base):
+        t = statistics.median(r[i][2] for r in runs)
+        key, sym, bound, work, peak, shape = _work(fn, a)
+        g = groups.setdefault(key, dict(name=key, symbol=sym, bound=bound, peak=peak, t=0.0, work=0.0, n=0,
+                                         shapes=set(), fns=set()))
+        g["t"] += t
+        g["n"] += 1
+        g["fns"].add(fn)
+        if work is None or g["work"] is None:
+            g["work"] = None
+        else:
+            g["work"] += work
+        if len(g["shapes"]) < 8:
+            g["shapes"].add(shape)
+    rows = sorted(groups.values(), key=lambda g: -g["t"])
+    step_t = sum(g["t"] for g in rows)
+    for g in rows:
+        g["share"] = g["t"] / step_t if step_t else 0.0
+        if g["work"] is not None and g["t"] > 0:
+            g["achieved"] = g["work"] / g["t"] / (1e9 if g["bound"] == "hbm" else 1e12)
+            g["frac"] = g["achieved"] / g["peak"]
+    return rows, step_t
 
 
 def pmc_traffic(symbol, cfgname):
@@ -182,27 +273,24 @@ def pmc_sq(symbol, cfgname):
 
 
 def measure(cfg, trainer, batch, cfgname=None):
-    dev = batch[0].device
-    B = batch[0].shape[0]
-    cands = _gemm_groups(trainer, batch) + _encoder_groups(trainer, B, dev)
-    for c in cands:
-        c["share"] = c["t"] * c["per_step"]
-    best = max(cands, key=lambda c: c["share"])
-    t = best["t"]
-    if best["bound"] == "hbm":
-        achieved = best["bytes"] / t / 1e9
-        peak, unit = PEAK_HBM_GBS, "GB/s"
-    else:
-        achieved = best["flops"] / t / 1e12
-        peak, unit = best.get("peak", PEAK_BF16_TFLOPS), "TFLOP/s"
-    ranked = sorted(cands, key=lambda c: -c["share"])
-    traffic = pmc_traffic(best.get("symbol"), cfgname) if cfgname else None
-    return {"bound": best["bound"], "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": None if traffic is None else round(traffic),
+    rows, step_t = kernel_table(trainer, batch)
+    modelled = [g for g in rows if g["work"] is not None]
+    best = rows[0] if rows[0]["work"] is not None else modelled[0]
+    t = best["t"] / best["n"]
+    unit = "GB/s" if best["bound"] == "hbm" else "TFLOP/s"
+    traffic = pmc_traffic(best["symbol"], cfgname) if cfgname else None
+    return {"bound": best["bound"], "achieved": round(best["achieved"], 2), "peak": best["peak"], "unit": unit,
+            "frac": round(best["frac"], 4), "traffic": None if traffic is None else round(traffic),
             "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/)",
-            "algorithmic_bytes": round(best["bytes"]) if "bytes" in best else None,
-            "kernel": best["name"],
-            # SIMD-cycle share of the matrix pipe while the kernel ran (rocprofv3 SQ counters)
-            "sq": pmc_sq(best.get("symbol"), cfgname) if cfgname else None,
-            "avg_launch_us": round(t * 1e6, 2), "launches_per_step": best["per_step"], "shape": best["note"],
-            "others_us_per_step": {c["name"]: round(c["share"] * 1e6, 1) for c in ranked[1:8]}}
+            "algorithmic": round(best["work"] / best["n"]),
+            "algorithmic_unit": "bytes/launch" if best["bound"] == "hbm" else "FLOP/launch",
+            "kernel": best["name"], "symbol": best["symbol"],
+            "sq": pmc_sq(best["symbol"], cfgname) if cfgname else None,
+            "avg_launch_us": round(t * 1e6, 2), "launches_per_step": best["n"],
+            "share_of_kernel_time": round(best["share"], 4),
+            "shape": f"{best['n']} launches/step, shapes {sorted(best['shapes'], key=str)[:6]}",
+            "method": "every library call of one eager sequential step between HIP events on its own stream "
+                      "(median of 3 steps), grouped by kernel symbol, ranked by time per step",
+            "kernel_time_per_step_us": round(step_t * 1e6, 1),
+            "ranked_us_per_step": {g["name"]: [round(g["t"] * 1e6, 1)] +
+                                   ([round(g["frac"], 4)] if "frac" in g else []) for g in rows[:12]}}

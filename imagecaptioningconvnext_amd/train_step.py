@@ -118,6 +118,9 @@ class TeacherForcedTrainer:
         self.enc_eng = self.encoder.engine() if _trainable(self.encoder) else None
         self._graph = None
         self._pipe = None
+        rel = getattr(self.encoder, "release_retired", None)
+        if rel is not None:  # the graphs that pointed into superseded weight packs are gone
+            rel()
 
     def _encode(self, imgs):
         self.encoder.train()
@@ -436,7 +439,12 @@ class TeacherForcedTrainer:
             if self.world > 1:
                 dist.all_reduce(efp.grad, op=dist.ReduceOp.SUM, group=self.pg)
             efp.adam_step(self.encoder_lr, self.grad_clip, grad_div=float(self.world))
-        red = torch.stack([m[0] * m[1], m[1], m[2]])
+        # m[4]: error words of the persistent LSTM recurrences (a hand-off that timed out); such
+        # a step's loss is reported as NaN and drain_metrics() raises (decoder.py:100-111 must
+        # never degrade silently)
+        bad = m[4] if m.numel() > 4 else torch.zeros((), device=m.device)
+        loss_tok = torch.where(bad > 0, torch.full_like(m[0], float("nan")), m[0] * m[1])
+        red = torch.stack([loss_tok, m[1], m[2], bad])
         if self.world > 1:
             dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)
         self._metric_log.append(red)
@@ -471,4 +479,8 @@ class TeacherForcedTrainer:
             return []
         r = torch.stack(self._metric_log).double().cpu()
         self._metric_log = []
-        return [(float(a / b), float(b), float(c / b * 100.0)) for a, b, c in r]
+        failed = int((r[:, 3] > 0).sum())
+        if failed:
+            raise RuntimeError(f"persistent LSTM recurrence: a workgroup hand-off timed out in {failed} of the "
+                               f"{r.shape[0]} logged steps (error word set); their updates are invalid")
+        return [(float(a / b), float(b), float(c / b * 100.0)) for a, b, c, _ in r]

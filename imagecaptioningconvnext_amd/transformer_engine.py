@@ -169,11 +169,11 @@ class TransformerEngine:
             lse = torch.empty(BL, **f32)
             lrow = torch.empty(BL, **f32)
             hit = torch.empty(BL, **f32)
-            metrics = torch.empty(4, **f32)  # loss, tokens, top5 hits, 1/tokens
+            metrics = torch.zeros(5, **f32)  # loss, tokens, top5 hits, 1/tokens, hand-off errors (none here)
             # loss, top-5 and the loss gradient in one pass over the logits (train.py:266-276)
             dlogits = torch.empty(BL, self.Vpad, **ctd)
-            K.ce_fused(logits, targets, V, metrics[3:4], lse, lrow, hit, dlogits)
-            K.loss_finalize(lrow, hit, targets, None, metrics)
+            K.ce_train(logits, targets, V, metrics, lse, lrow, hit, dlogits,
+                       lambda: K.loss_finalize(lrow, hit, targets, None, metrics))
             s.update(logits=logits, targets=targets, lse=lse, metrics=metrics, dlogits=dlogits)
         return s
 

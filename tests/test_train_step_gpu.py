@@ -6,31 +6,34 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _models(dev, decoder, dropout, sd_off):
+def _models(dev, decoder, dropout, sd_off, dtype=torch.float32, starting_layer=None):
     from imagecaptioningconvnext_amd.models.decoder import DecoderWithAttention
     from imagecaptioningconvnext_amd.models.encoder import Encoder
     from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
     torch.manual_seed(5)
-    enc = Encoder(variant="tiny", compute_dtype=torch.float32)
-    enc.fine_tune(False)
+    enc = Encoder(variant="tiny", compute_dtype=dtype)
+    if starting_layer is None:
+        enc.fine_tune(False)
+    else:
+        enc.fine_tune(True, startingLayer=starting_layer)
     if sd_off:
         for m in enc.modules():
             if hasattr(m, "sd_prob"):
                 m.sd_prob = 0.0
     if decoder == "lstm":
         dec = DecoderWithAttention(attention_dim=64, embed_dim=64, decoder_dim=64, vocab_size=120, device=dev,
-                                   encoder_dim=768, dropout=dropout, compute_dtype=torch.float32)
+                                   encoder_dim=768, dropout=dropout, compute_dtype=dtype)
     else:
         dec = TransformerDecoder(embed_dim=128, decoder_dim=128, vocab_size=120, maxLen=20, device=dev,
                                  wordMap=None, pretrained_embeddings_path=None, fine_tune_embeddings=True,
                                  dropout=dropout, encoder_dim=768, num_heads=2, num_layers=2,
-                                 compute_dtype=torch.float32)
+                                 compute_dtype=dtype)
     return enc.to(dev), dec.to(dev)
 
 
-def _batch(dev, i, B=4, L=20, V=120):
+def _batch(dev, i, B=4, L=20, V=120, hw=64):
     g = torch.Generator().manual_seed(100 + i)
-    img = torch.randn(B, 3, 64, 64, generator=g)
+    img = torch.randn(B, 3, hw, hw, generator=g)
     caps = torch.randint(1, V - 2, (B, L), generator=g)
     caps[:, 0] = V - 2
     lens = torch.tensor([L, 15, 11, 7])[:B]
@@ -147,3 +150,63 @@ def test_bucketed_allreduce_matches_single_collective_over_steps(hip_device, tmp
     for ra, rb in zip(a, b):
         assert torch.equal(ra["flat"], rb["flat"]) and torch.equal(ra["metrics"], rb["metrics"])
     assert torch.equal(a[0]["flat"], a[1]["flat"])
+
+
+def _churn(dev, i):
+    """Regular-pool allocator activity between replays: blocks of many sizes allocated, filled
+    with 0xFF, freed; a few kept (so the next step sees a different layout)."""
+    ts = [torch.empty((mb << 20) + 4096 * i, dtype=torch.uint8, device=dev).fill_(255) for mb in (1, 2, 5, 13, 34)]
+    ts += [torch.full((n,), -1, dtype=torch.int64, device=dev) for n in (1, 7, 100, 5000) * 4]
+    torch.cuda.synchronize(dev)
+    return ts[i % 3::3]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_captured_finetune_step_survives_allocator_churn(hip_device, dtype):
+    """The captured sequential schedule (encoder graph + decoder graph, the fine-tuned children's
+    backward inside the second; what train.py / trainMultiGPU.py run with a fine-tuned encoder,
+    and C5) replayed over several steps with deliberate allocator activity between the replays
+    (and the eager Adam / metric update): bitwise the parameters, Adam moments and metrics of the
+    same steps launched eagerly.  Tiny, fine_tune(True, 7), Transformer decoder, 224x224."""
+    from imagecaptioningconvnext_amd import kernels as K
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    runs = []
+    for graph in (False, True):
+        enc, dec = _models(hip_device, "transformer", dropout=0.0, sd_off=True, dtype=dtype, starting_layer=7)
+        tr = TeacherForcedTrainer(enc, dec, lstm=False, graph=graph)
+        assert tr.enc_eng is not None
+        keep = []
+        for i in range(5):
+            keep = _churn(hip_device, i)
+            tr.step(*_batch(hip_device, i % 2, B=2, hw=224))
+        torch.cuda.synchronize()
+        del keep
+        e, d = tr.enc_eng.fp, tr.eng.fp
+        runs.append((tr.drain_metrics(), d.flat.clone(), d.m.clone(), e.flat.clone(), e.m.clone(), e.v.clone()))
+        K.set_seed_counter(None)
+    (m_e, *a), (m_g, *b) = runs
+    assert m_e == m_g
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("direction", ["FWD", "BWD"])
+def test_persistent_lstm_handoff_timeout_raises(hip_device, monkeypatch, direction):
+    """A hand-off of the persistent LSTM recurrence that never completes (test knob: U block 0
+    skips one publish, csrc/lstm_persist.hip) must not train silently on half-written outputs
+    (decoder.py:100-111): the step's loss is NaN and drain_metrics() raises."""
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    enc, dec = _models(hip_device, "lstm", dropout=0.0, sd_off=True)
+    tr = TeacherForcedTrainer(enc, dec, lstm=True, graph=False)
+    tr.step(*_batch(hip_device, 0))  # healthy step first
+    assert tr.eng._sync is not None  # the persistent recurrences ran
+    assert len(tr.drain_metrics()) == 1
+    monkeypatch.setenv(f"IMGCAP_LSTM_FAULT_{direction}", "2")
+    tr.step(*_batch(hip_device, 1))
+    monkeypatch.delenv(f"IMGCAP_LSTM_FAULT_{direction}")
+    red = tr._metric_log[-1].cpu()
+    assert red[3] > 0 and torch.isnan(red[0])
+    with pytest.raises(RuntimeError, match="hand-off timed out"):
+        tr.drain_metrics()
+    tr.step(*_batch(hip_device, 1))  # the knob is read per launch: clean again
+    assert len(tr.drain_metrics()) == 1

@@ -184,3 +184,31 @@ def test_transformer_medium_vs_oracle_and_dropout(hip_device):
     eng.step_id = 0
     b = eng.forward(enc.to(hip_device), caps.to(hip_device), caplens.to(hip_device))["metrics"].clone()
     assert torch.equal(a, b) and abs(a[0].item() - loss.item()) > 1e-3
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-4), (torch.bfloat16, 3e-2)])
+def test_transformer_vocab_past_fused_ce_limit_vs_oracle(hip_device, dtype, tol):
+    """V = 30000 is past imgcap_ce_fused's register row (24576 bf16 / 12288 fp32): the training
+    CE falls back to ce_fwd -> loss_finalize -> ce_bwd (kernels.ce_train); loss and gradients
+    against the oracle as for the fused path (train.py:266-276)."""
+    from imagecaptioningconvnext_amd import kernels as K
+    E, d, ff, V, layers, B, L = 64, 128, 128, 30000, 1, 3, 14
+    p = make_params(shapes.transformer_decoder_shapes(E, d, ff, V, layers), 71)
+    enc = make_features((B, 7, 7, E), 72)
+    caps, caplens = make_captions(B, L, [14, 9, 5], V, 73)
+    pr = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    preds, cs, dls = decoders.transformer_tf_forward(pr, enc, caps, caplens, caps == 0, 2, layers)
+    loss, _, _ = train_step.transformer_loss(preds, cs, dls)
+    loss.backward()
+    dec = _decoder(dict(E=E, d=d, ff=ff, V=V, layers=layers, H=2, L=L), p, dtype, hip_device)
+    eng = dec.engine()
+    s = eng.forward(enc.to(hip_device), caps.to(hip_device), caplens.to(hip_device), pad_id=0)
+    assert not K.ce_fused_fits(s["logits"], s["dlogits"], V)
+    assert abs(s["metrics"][0].item() - loss.item()) < tol * loss.item()
+    assert int(s["metrics"][1].item()) == sum(dls)
+    eng.backward(s)
+    for n in eng.fp.params:
+        g = pr[n].grad
+        if g.norm() < 1e-6:
+            continue
+        assert _rel(eng.fp.g(n), g) < tol * (1 if dtype == torch.float32 else 3), n
