@@ -162,6 +162,19 @@ def flops_per_image(cfg, enc):
     return 2 * enc_macs + 3 * 2 * dec_macs
 
 
+def cpu_model():
+    """The host CPU's model name (lscpu's "Model name", read from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or None
+
+
 def cpu_baseline(seconds):
     """Oracle (plain PyTorch CPU restatement) of the C1 train step: Tiny + LSTM, B=4, fp32."""
     from oracle import convnext, decoders, shapes, train_step
@@ -192,7 +205,7 @@ def cpu_baseline(seconds):
             n += 1
         if (t_steps >= seconds and n >= 2) or step >= 50:
             break
-    return dict(value=round(B * n / t_steps, 3), unit="images/s", cores=nthreads, kind="port",
+    return dict(value=round(B * n / t_steps, 3), unit="images/s", cores=nthreads, kind="port", cpu=cpu_model(),
                 sample=f"oracle C1 train step (ConvNeXt-Tiny + LSTM-attention, B=4, fp32, 224x224, L=52, "
                        f"V={V}), {n} timed steps after 1 warm-up, {t_steps:.1f} s")
 

@@ -15,6 +15,8 @@ reported against the MI355X peak (bf16 dense MFMA 2.5 PFLOP/s, MX-FP8 5 PFLOP/s,
 HBM 8 TB/s; MI355X_MICROARCH.md).
 """
 import collections
+import json
+import os
 import statistics
 
 import torch
@@ -274,6 +276,11 @@ def pmc_sq(symbol, cfgname):
 
 def measure(cfg, trainer, batch, cfgname=None):
     rows, step_t = kernel_table(trainer, batch)
+    dump = os.environ.get("IMGCAP_ROOFLINE_TABLE")
+    if dump:  # the whole ranked table (profiles/*_kernel_table.json)
+        with open(dump, "w") as f:
+            json.dump([{k: (sorted(map(str, v)) if isinstance(v, set) else v) for k, v in g.items()} for g in rows],
+                      f, indent=1)
     modelled = [g for g in rows if g["work"] is not None]
     best = rows[0] if rows[0]["work"] is not None else modelled[0]
     t = best["t"] / best["n"]

@@ -97,6 +97,8 @@ class TeacherForcedTrainer:
         self._comm = None
         if self.world > 1 and hasattr(self.eng, "early_bucket"):
             self._bucket = self.eng.early_bucket()
+            if _trainable(encoder):  # the whole decoder, reduced beside the encoder backward
+                self._bucket = (0, self.eng.fp.grad.numel())
             if torch.cuda.is_available() and self.eng.fp.grad.is_cuda:
                 self._comm = torch.cuda.Stream(device=self.eng.fp.grad.device)
         if self.world > 1:
@@ -116,6 +118,8 @@ class TeacherForcedTrainer:
         self.encoder.fine_tune(fine_tune=True, startingLayer=startingLayer)
         self.flush()
         self.enc_eng = self.encoder.engine() if _trainable(self.encoder) else None
+        if self._bucket is not None and self.enc_eng is not None:
+            self._bucket = (0, self.eng.fp.grad.numel())
         self._graph = None
         self._pipe = None
         rel = getattr(self.encoder, "release_retired", None)
@@ -148,14 +152,18 @@ class TeacherForcedTrainer:
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
         if mid is not None:
             mid()
-        kw = {}
-        if self._bucket is not None and self._hook_mode is not None:
-            kw["bucket_hook"] = self._bucket_hook
+        hook = self._bucket is not None and self._hook_mode is not None
         if es is not None:
-            self.eng.backward(s, want_denc=True, **kw)
+            # fine-tuned encoder: the decoder's gradients are all final once its backward is done;
+            # their all-reduce (one bucket, the whole decoder) runs on the comm stream while the
+            # encoder children's backward runs (trainMultiGPU.py:233-235,256,384: DDP's reducer
+            # overlaps the buckets with the rest of the backward)
+            self.eng.backward(s, want_denc=True)
+            if hook:
+                self._bucket_hook()
             self.enc_eng.backward(es, s["denc"].reshape(feats.shape))
         else:
-            self.eng.backward(s, **kw)
+            self.eng.backward(s, **({"bucket_hook": self._bucket_hook} if hook else {}))
         return s["metrics"]
 
     # ---- bucketed gradient all-reduce --------------------------------------------------------
@@ -348,10 +356,13 @@ class TeacherForcedTrainer:
             self._pipe_capture(imgs, caps, caplens)
         P = self._pipe
         k = P["i"] % 2
+        if any(d.shape != s_.shape or d.dtype != s_.dtype for d, s_ in ((P["img"], imgs), (P["caps"][k], caps),
+                                                                        (P["lens"][k], caplens))):
+            # a batch of another shape (the last, partial batch of an epoch): finish the batch in
+            # flight, then this one with eager launches, sequentially
+            self.flush()
+            return self._eager(imgs, caps, caplens)
         for dst, src in ((P["img"], imgs), (P["caps"][k], caps), (P["lens"][k], caplens)):
-            if dst.shape != src.shape:
-                raise ValueError("graph mode needs a fixed batch shape; got %s, captured %s"
-                                 % (tuple(src.shape), tuple(dst.shape)))
             dst.copy_(src, non_blocking=True)
         m = None
         if P["i"] == 0:
@@ -439,14 +450,19 @@ class TeacherForcedTrainer:
             if self.world > 1:
                 dist.all_reduce(efp.grad, op=dist.ReduceOp.SUM, group=self.pg)
             efp.adam_step(self.encoder_lr, self.grad_clip, grad_div=float(self.world))
-        # m[4]: error words of the persistent LSTM recurrences (a hand-off that timed out); such
-        # a step's loss is reported as NaN and drain_metrics() raises (decoder.py:100-111 must
-        # never degrade silently)
-        bad = m[4] if m.numel() > 4 else torch.zeros((), device=m.device)
-        loss_tok = torch.where(bad > 0, torch.full_like(m[0], float("nan")), m[0] * m[1])
-        red = torch.stack([loss_tok, m[1], m[2], bad])
-        if self.world > 1:
-            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)
+        # m = [loss, tokens, top-5 hits, 1/tokens, hand-off errors]; m[4] counts the persistent
+        # LSTM recurrences' timed-out hand-offs: such a step's loss reads NaN and drain_metrics()
+        # raises (decoder.py:100-111 must never degrade silently).  One rank: the step's metric
+        # vector is logged as is (one copy, reduced on the host at drain time); DDP: the
+        # reduceLossAndTokens / accuracy sums across ranks (trainMultiGPU.py:96-108, 398-403).
+        if self.world == 1:
+            red = m.clone()
+            self._metric_log.append(red)
+            return red
+        zero = torch.zeros((), device=m.device, dtype=m.dtype)
+        red = torch.stack([m[0] * m[1], m[1], m[2], zero, m[4] if m.numel() > 4 else zero])
+        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)
+        red[0] = red[0] / red[1]  # global token-weighted mean loss, back in m's layout
         self._metric_log.append(red)
         return red
 
@@ -477,10 +493,11 @@ class TeacherForcedTrainer:
         """(globalLoss, tokens, top5 %) per logged step, like reduceLossAndTokens + accuracy."""
         if not self._metric_log:
             return []
-        r = torch.stack(self._metric_log).double().cpu()
+        r = torch.stack([m if m.numel() > 4 else torch.cat([m, m.new_zeros(5 - m.numel())])
+                         for m in self._metric_log]).double().cpu()
         self._metric_log = []
-        failed = int((r[:, 3] > 0).sum())
+        failed = int((r[:, 4] > 0).sum())
         if failed:
             raise RuntimeError(f"persistent LSTM recurrence: a workgroup hand-off timed out in {failed} of the "
                                f"{r.shape[0]} logged steps (error word set); their updates are invalid")
-        return [(float(a / b), float(b), float(c / b * 100.0)) for a, b, c, _ in r]
+        return [(float(a), float(b), float(c / b * 100.0)) for a, b, c in r[:, :3]]

@@ -67,6 +67,9 @@ class _FakeTrainer:
     def step(self, *a):
         pass
 
+    def flush(self):
+        pass
+
     def drain_metrics(self):
         self.log.append((self.decoder_lr, self.encoder_lr, self.enc_eng is not None))
         return [(1.0, 1.0, 1.0)]

@@ -194,7 +194,7 @@ def test_captured_finetune_step_survives_allocator_churn(hip_device, dtype):
 def test_persistent_lstm_handoff_timeout_raises(hip_device, monkeypatch, direction):
     """A hand-off of the persistent LSTM recurrence that never completes (test knob: U block 0
     skips one publish, csrc/lstm_persist.hip) must not train silently on half-written outputs
-    (decoder.py:100-111): the step's loss is NaN and drain_metrics() raises."""
+    (decoder.py:100-111): the step's error count is set and drain_metrics() raises."""
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
     enc, dec = _models(hip_device, "lstm", dropout=0.0, sd_off=True)
     tr = TeacherForcedTrainer(enc, dec, lstm=True, graph=False)
@@ -204,9 +204,28 @@ def test_persistent_lstm_handoff_timeout_raises(hip_device, monkeypatch, directi
     monkeypatch.setenv(f"IMGCAP_LSTM_FAULT_{direction}", "2")
     tr.step(*_batch(hip_device, 1))
     monkeypatch.delenv(f"IMGCAP_LSTM_FAULT_{direction}")
-    red = tr._metric_log[-1].cpu()
-    assert red[3] > 0 and torch.isnan(red[0])
+    red = tr._metric_log[-1].cpu()  # [loss, tokens, top-5 hits, 1/tokens, hand-off errors]
+    assert red[4] > 0
     with pytest.raises(RuntimeError, match="hand-off timed out"):
         tr.drain_metrics()
     tr.step(*_batch(hip_device, 1))  # the knob is read per launch: clean again
     assert len(tr.drain_metrics()) == 1
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_ddp2_transformer_finetuned_encoder_hip(hip_device, tmp_path, graph):
+    """Transformer decoder + ConvNeXt-Tiny children[7:] trainable, 2 gloo ranks on the one GPU
+    (trainMultiGPU.py:233-235, 256, 384-394): the whole decoder reduced as one bucket beside the
+    encoder backward (eager: from the hook on the comm stream; graph: between the decoder-half
+    graph and the encoder-backward graph), the encoder gradients after it; bitwise equal to one
+    collective after the backward, and to a single process summing the two shards' gradients."""
+    import ddp_ft_util
+    a = ddp_ft_util.run_hip(tmp_path / "a", graph, True)
+    b = ddp_ft_util.run_hip(tmp_path / "b", graph, False)
+    for ra, rb in zip(a, b):
+        for k in ra:
+            assert torch.equal(ra[k], rb[k]), k
+    for k in a[0]:
+        assert torch.equal(a[0][k], a[1][k]), k
+    dec, enc = ddp_ft_util.expected_hip(hip_device)
+    assert torch.equal(a[0]["dec"], dec) and torch.equal(a[0]["enc"], enc)

@@ -70,6 +70,8 @@ def make_parser(multi_gpu=False):
     p.add_argument('--dataFolder', type=str, default=None,
                    help="the reference's input files (train.py:35); synthetic batches when not given")
     p.add_argument('--workers', type=int, default=6)
+    p.add_argument('--noPipeline', action='store_true',
+                   help='frozen encoder: run encoder and decoder of a step back to back (no two-stream pipeline)')
     return p
 
 
@@ -172,6 +174,7 @@ def trainWithTeacherForcing(trainDataLoader, encoder, decoder, trainer, epoch, l
         n += 1
         batchTime.update(time.time() - start)
         start = time.time()
+    trainer.flush()  # pipelined schedule: the last batch of the epoch is still in flight
     if torch.cuda.is_initialized():
         torch.cuda.synchronize()
     for loss, tokens, top5 in trainer.drain_metrics():
@@ -262,8 +265,11 @@ def main(argv=None):
     device = torch.device("cuda")
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
     encoder, decoder, ck = build_models(args, device)
+    # pipeline: while the encoder is frozen its forward of batch i+1 runs beside the decoder step of
+    # batch i (the schedule bench.py measures; parameter updates identical to the sequential one)
     trainer = TeacherForcedTrainer(encoder, decoder, lstm=args.lstmDecoder, decoder_lr=decoderLr,
-                                   encoder_lr=args.encoderLr, grad_clip=gradClip, alphaC=alphaC, graph=True)
+                                   encoder_lr=args.encoderLr, grad_clip=gradClip, alphaC=alphaC, graph=True,
+                                   pipeline=not args.noPipeline)
     run_epochs(args, encoder, decoder, trainer, ck, device)
 
 

@@ -62,7 +62,7 @@ def main(argv=None):
     encoder, decoder, ck = train.build_models(args, device)
     trainer = TeacherForcedTrainer(encoder, decoder, lstm=args.lstmDecoder, decoder_lr=train.decoderLr,
                                    encoder_lr=args.encoderLr, grad_clip=train.gradClip, alphaC=train.alphaC,
-                                   graph=True)
+                                   graph=True, pipeline=not args.noPipeline)
     log = print if rank == 0 else (lambda *a, **k: None)
     # trainMultiGPU.py: encoder fine-tuned (and DDP-averaged) from epoch 20; rank 0 checkpoints
     train.run_epochs(args, encoder, decoder, trainer, ck, device, rank=rank, log=log, world=world,
