@@ -319,9 +319,10 @@ def test_c5_large_fp8_finetune_vs_emulating_oracle(hip_device):
     worst = max(g_errs, key=g_errs.get)
     print(f"C5: features rel {f_err:.2e}, loss rel {abs(g_loss.item() / loss.item() - 1):.2e}, "
           f"worst stage-4 grad {worst} {g_errs[worst]:.2e}")
+    # measured (MI355X, round 2): features 1.3e-2, loss 6e-7, worst stage-4 gradient 3.5e-3
     assert f_err < 2.5e-2
-    assert abs(g_loss.item() - loss.item()) < 1e-2 * abs(loss.item())
-    assert g_errs[worst] < 5e-2
+    assert abs(g_loss.item() - loss.item()) < 1e-4 * abs(loss.item())
+    assert g_errs[worst] < 1e-2
     # the fused step (MX prefix, bf16 stage-4 forward/backward, encoder Adam at encoderLr)
     for p_ in list(enc.parameters()) + list(dec.parameters()):
         p_.grad = None
@@ -329,5 +330,6 @@ def test_c5_large_fp8_finetune_vs_emulating_oracle(hip_device):
     assert tr.enc_eng is not None
     tr.step(img.to(dev), caps.to(dev), caplens.to(dev))
     (t_loss, t_tok, _), = tr.drain_metrics()
+    print(f"C5 fused step: loss rel {abs(t_loss / loss.item() - 1):.2e}")
     assert t_tok == sum(dls)
-    assert abs(t_loss - loss.item()) < 1e-2 * abs(loss.item())
+    assert abs(t_loss - loss.item()) < 1e-4 * abs(loss.item())

@@ -81,10 +81,13 @@ def test_lstm_trainer_b32_tied_lengths_vs_oracle(hip_device):
     _check_post_adam(dict(dec.named_parameters()), p, {k: v.grad for k, v in pr.items()}, 1e-4)
 
 
-def test_transformer_trainer_b64_tied_lengths_vs_oracle(hip_device):
+@pytest.mark.parametrize("B,E", [(64, 768), (32, 1024)])
+def test_transformer_trainer_tied_lengths_vs_oracle(hip_device, B, E):
+    """C3 (Tiny features, E = 768, B = 64) and C4's decoder width (Base features, E = 1024 through
+    encoder_proj, 32 per GPU)."""
     from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
-    B, d, ff, layers, H = 64, 512, 512, 6, 8
+    d, ff, layers, H = 512, 512, 6, 8
     p = make_params(shapes.transformer_decoder_shapes(E, d, ff, V, layers), 51)
     feats = make_features((B, 7, 7, E), 52)
     lens = _tied_lengths(B, 53)
