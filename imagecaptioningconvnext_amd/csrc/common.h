@@ -27,6 +27,10 @@ int fail(int code, const std::string& msg);
 // imgcap_workspace_attach); abi.cpp
 void* workspace(size_t bytes, hipStream_t stream);
 std::string last_error();
+// zero `bytes` (a multiple of 16, 16-byte aligned) with a kernel on `stream` -- a kernel node
+// when captured, not a memset node (elementwise.hip; DESIGN.md §2b: the captured split step
+// faulted with the runtime's graph packet capture on while a memset node sat in the first half)
+hipError_t zero_async(void* p, size_t bytes, hipStream_t stream);
 
 #define IMGCAP_CHECK_LAUNCH(what)                                                   \
   do {                                                                             \

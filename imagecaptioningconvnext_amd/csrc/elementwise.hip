@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(int n, int dim, cons
 // Deterministic embedding backward (nn.Embedding, decoder.py:84 / transformerDecoder.py:94):
 // dtable[id] += sum over the positions r with ids[r] == id, IN POSITION ORDER, of dout[r]
 // (times the dropout mask of the Transformer path).  No float atomics, so the result is
-// bitwise the same on every run.  Three launches after a memset of the rank words:
+// bitwise the same on every run.  Three launches after zeroing the rank words:
 //   emb_rank:    rank of position i in the (id, position) order, counted against one chunk of
 //                EMB_CHUNK ids per workgroup (chunk in LDS, broadcast reads); the chunk counts
 //                are summed with integer atomics (exact, order-free)
@@ -270,11 +270,23 @@ __global__ __launch_bounds__(256) void sort_gather_kernel(int B, int P, int E, i
   }
 }
 
+__global__ __launch_bounds__(256) void zero16_kernel(uint4* p, long n16) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n16; i += (long)gridDim.x * 256) p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 static dim3 grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 4096) b = 4096;
   if (b < 1) b = 1;
   return dim3((unsigned)b);
+}
+
+hipError_t zero_async(void* p, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return hipSuccess;
+  if ((bytes & 15) || !aligned16(p)) return hipErrorInvalidValue;
+  const long n16 = (long)(bytes / 16);
+  hipLaunchKernelGGL(zero16_kernel, grid_for(n16), dim3(256), 0, stream, (uint4*)p, n16);
+  return hipGetLastError();
 }
 
 }  // namespace imgcap
@@ -323,8 +335,7 @@ extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* id
   if (!rank) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_embedding_bwd: ") + last_error());
   int* spos = rank + rank_bytes / sizeof(int);
   int* sid = spos + n;
-  if (hipMemsetAsync(rank, 0, rank_bytes, st) != hipSuccess)
-    return fail(IMGCAP_EINVAL, "imgcap_embedding_bwd: memset failed");
+  if (zero_async(rank, rank_bytes, st) != hipSuccess) return fail(IMGCAP_EINVAL, "imgcap_embedding_bwd: zeroing failed");
   const int nb = (n + 255) / 256;
   hipLaunchKernelGGL(emb_rank_kernel, dim3(nb, (n + EMB_CHUNK - 1) / EMB_CHUNK), dim3(256), 0, st, n, ids, rank);
   hipLaunchKernelGGL(emb_scatter_kernel, dim3(nb), dim3(256), 0, st, n, ids, rank, spos, sid);

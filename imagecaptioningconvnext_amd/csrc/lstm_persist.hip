@@ -22,7 +22,7 @@
 // workgroup barrier, ONE lane stores the block's flag (relaxed agent-scope atomic store =
 // sc1); the consumer's wave 0 polls the producers' flags with sc1 loads, then a workgroup
 // barrier, then every load of the payload is an sc1 buffer load.  No fences.  Flags are
-// per producer (no contended counter), epoch = step + 1, zeroed by a memset before the launch.
+// per producer (no contended counter), epoch = step + 1, zeroed by a kernel before the launch.
 // Every spin is bounded: on timeout (or when another block already gave up) the block writes
 // the error word and returns, so the grid always drains.
 //
@@ -1407,9 +1407,9 @@ int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   }
   IMGCAP_REQUIRE(d.sync_words >= L.words, "lstm persistent: sync workspace too small");
   IMGCAP_REQUIRE(aligned16(d.sync), "lstm persistent: sync workspace must be 16-byte aligned");
-  // zero the error word and every flag (a memset node when captured)
-  if (hipMemsetAsync(d.sync, 0, align16((size_t)L.words * 4), st) != hipSuccess)
-    return fail(IMGCAP_EINVAL, "lstm persistent: memset of the sync words failed");
+  // zero the error word and every flag (a kernel node when captured)
+  if (zero_async(d.sync, align16((size_t)L.words * 4), st) != hipSuccess)
+    return fail(IMGCAP_EINVAL, "lstm persistent: zeroing of the sync words failed");
   *used = true;
 #define LP_CASE(TT, M_) \
   if (L.mt == M_) return launch_persist<TT, M_>(L, st);
@@ -1553,8 +1553,8 @@ int lstm_bwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
     if (d.sync_words >= base + 3 * 64 * 16 * 2) L.g[0].stamps = (long long*)(d.sync + base);
   }
   IMGCAP_REQUIRE(aligned16(d.sync) && aligned16(d.dcat), "lstm persistent backward: 16-byte aligned sync / dcat");
-  if (hipMemsetAsync(d.sync, 0, align16((size_t)L.words * 4), st) != hipSuccess)
-    return fail(IMGCAP_EINVAL, "lstm persistent backward: memset of the sync words failed");
+  if (zero_async(d.sync, align16((size_t)L.words * 4), st) != hipSuccess)
+    return fail(IMGCAP_EINVAL, "lstm persistent backward: zeroing of the sync words failed");
   *used = true;
   if (esz == 2) return L.mt == 1 ? launch_bwd_persist<bf16, 1>(L, st) : launch_bwd_persist<bf16, 2>(L, st);
   return L.mt == 1 ? launch_bwd_persist<float, 1>(L, st) : launch_bwd_persist<float, 2>(L, st);

@@ -229,3 +229,41 @@ def test_ddp2_transformer_finetuned_encoder_hip(hip_device, tmp_path, graph):
         assert torch.equal(a[0][k], a[1][k]), k
     dec, enc = ddp_ft_util.expected_hip(hip_device)
     assert torch.equal(a[0]["dec"], dec) and torch.equal(a[0]["enc"], enc)
+
+
+@pytest.mark.parametrize("decoder,pipeline,split", [("lstm", False, False), ("lstm", True, True),
+                                                    ("transformer", False, True), ("transformer", True, False)])
+def test_captured_step_graphs_hold_only_kernel_nodes(hip_device, monkeypatch, decoder, pipeline, split):
+    """Every library launch of the captured step is a KERNEL node: with a memset node in the
+    decoder's first half, the split (DDP) schedule faulted on that half's second replay while the
+    runtime's graph packet capture was on, and ran clean with it off or with the memsets turned
+    into a zeroing kernel (gpurun_out/r3split).  The only non-kernel node allowed
+    is torch's own device-to-device copy of the encoder features into the slot the decoder reads."""
+    import graph_nodes
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    kept = []
+    base = torch.cuda.CUDAGraph
+
+    class Kept(base):
+        def __new__(cls, keep_graph=False):
+            g = base.__new__(cls, True)
+            kept.append(g)
+            return g
+
+        def __init__(self, keep_graph=False):
+            super().__init__(True)
+    monkeypatch.setattr(torch.cuda, "CUDAGraph", Kept)
+    enc, dec = _models(hip_device, decoder, 0.1, False)
+    tr = TeacherForcedTrainer(enc, dec, lstm=decoder == "lstm", graph=True, pipeline=pipeline)
+    if split:  # the DDP split at the early bucket, reduced over no group (one rank)
+        tr._bucket = tr.eng.early_bucket()
+        tr._reduce_early = lambda: setattr(tr, "_early_issued", False)
+    for i in range(3):
+        tr.step(*_batch(hip_device, i))
+    torch.cuda.synchronize()
+    assert kept
+    for g in kept:
+        nodes = graph_nodes.describe(g.raw_cuda_graph())
+        other = [n for n in nodes if " kernel " not in n and " memcpy " not in n]
+        assert not other, other[:5]
+        assert sum(" memcpy " in n for n in nodes) <= 1, [n for n in nodes if " memcpy " in n]
