@@ -4,6 +4,8 @@ captions of TIED lengths (the length sort of decoder.py:79 must keep every row w
 caption; rows are compared per original sample), vs the CPU oracle: loss, top-5, logits (<= 1e-3 relative, the north-star bar) and post-Adam
 parameters.  The encoder is a pass-through (the batch is encoder features), as in the
 reference's own DDP golden (tests/ddp_util.py)."""
+import os
+
 import pytest
 import torch
 
@@ -31,13 +33,34 @@ def _tied_lengths(B, seed):
     return pool[torch.randint(0, len(pool), (B,), generator=g)].tolist()
 
 
-def _check_post_adam(named, p0, grads, lr):
+def _check_post_adam(named, p0, grads, lr, hip_grads=None, grad_rel=None):
     """Adam's first step moves an entry by lr * g / (|g| + eps): exactly sign(g) * lr unless g is
-    at round-off level, where only the 2 * lr bound means anything."""
-    new = train_step.adam_step({k: p0[k] for k in grads}, train_step.clip_gradient(grads, 5.0), {}, lr, 1)
+    at round-off level, where only the 2 * lr bound means anything.
+
+    With ``hip_grads`` (the trainer's own gradient buffer) the check is split in two: the HIP
+    gradients against the oracle's (per tensor, relative ``grad_rel``) and the update against
+    Adam applied to the HIP gradients (the optimizer kernel, exact up to round-off), with the
+    oracle's direction required wherever the two gradients agree in sign with margin.  A post-norm
+    Transformer's ReLU masks flip for pre-activations at round-off level between two fp32
+    implementations, which moves individual FFN gradients by ~1e-3 of the tensor norm (measured
+    1.2e-3 / 1.6e-3 worst at E = 768 / 1024)."""
+    clip = train_step.clip_gradient(grads, 5.0)
+    new = train_step.adam_step({k: p0[k] for k in grads}, clip, {}, lr, 1)
+    hg = {k: hip_grads(k).detach().float().cpu() for k in grads} if hip_grads is not None else None
+    if hg is not None and os.environ.get("IMGCAP_GRAD_REPORT"):
+        rel = sorted(((_rel(hg[k], grads[k]), k) for k in grads), reverse=True)
+        print("grad rel (worst 12):", [(f"{r:.1e}", k) for r, k in rel[:12]], flush=True)
+    mine = None
+    if hg is not None:
+        mine = train_step.adam_step({k: p0[k] for k in grads}, train_step.clip_gradient(hg, 5.0), {}, lr, 1)
     for k, want in new.items():
         got = named[k].detach().float().cpu()
+        if grad_rel is not None:
+            assert _rel(hg[k], grads[k]) <= grad_rel, (k, _rel(hg[k], grads[k]))
         sure = grads[k].abs() > 1e-5
+        if hg is not None:
+            assert (got - mine[k]).abs().max().item() <= 1e-3 * lr + 1e-7, k  # the Adam kernel
+            sure &= (hg[k] - grads[k]).abs() < 0.5 * grads[k].abs()
         if sure.any():
             assert (got - want)[sure].abs().max().item() <= 1e-3 * lr + 1e-7, k
         assert (got - want).abs().max().item() <= 2 * lr * 1.0001, k
@@ -114,4 +137,4 @@ def test_transformer_trainer_tied_lengths_vs_oracle(hip_device, B, E):
     assert abs(g_loss - loss.item()) <= 1e-4 * loss.item()
     assert g_tok == sum(dls) and abs(g_top5 - top5) < 1e-6
     grads = {k: v.grad for k, v in pr.items() if v.requires_grad}
-    _check_post_adam(dict(dec.named_parameters()), p, grads, 1e-4)
+    _check_post_adam(dict(dec.named_parameters()), p, grads, 1e-4, hip_grads=lambda k: tr.eng.fp.g(k), grad_rel=5e-3)
