@@ -16,13 +16,20 @@
 //                         resident in LDS; scores, softmax, context, sigmoid gate -> z_t[b]
 //                         (decoder.py:25-31, 102-105).
 // Per step three hand-offs: h_{t-1} (all U blocks) -> G and U;  [att2 | gate_pre] (all G
-// blocks) -> R;  z_t (all R blocks) -> U.  Each is the write-through form of the visibility
-// rules (MI355X_MICROARCH.md, inter-workgroup visibility, valid-forms table row 1): payload
-// stored sc1 (buffer stores, aux = sc1), every storing wave drains (s_waitcnt vmcnt(0)), a
-// workgroup barrier, ONE lane stores the block's flag (relaxed agent-scope atomic store =
-// sc1); the consumer's wave 0 polls the producers' flags with sc1 loads, then a workgroup
-// barrier, then every load of the payload is an sc1 buffer load.  No fences.  Flags are
-// per producer (no contended counter), epoch = step + 1, zeroed by a kernel before the launch.
+// blocks) -> R;  z_t (all R blocks) -> U.
+//   g and z: tagged granules -- every value travels in a naturally aligned 8-byte {value bits,
+//   epoch} granule written by one write-through (sc1) store (a 16-byte store carries two), and
+//   the consumer's sc1 loads of the granules are the poll: no drain, no separate flag, no second
+//   round trip (MI355X_MICROARCH.md handoff-1to1 vs handoff-flag; granules observed untorn on
+//   gfx950 / ROCm 7.2, also as 16-byte halves).  A U block polls one sentinel granule pair per
+//   lane before sweeping its 48 KB of z granules.  z granules live in two slots by step parity
+//   (a slot is rewritten two steps later, by which time every consumer has read it: the chain
+//   z_t -> h_t -> g_{t+1} -> z_{t+1} passes through every block), tag = step + 1.
+//   h: write-through hs rows + one flag per U block (drained sc1 stores, then a relaxed agent-
+//   scope flag store; the consumer's wave 0 polls the flags, a barrier, sc1 payload loads).  As
+//   granules (IMGCAP_LSTM_HGRAN=1, the HG instantiation) the h hop measured 3.3-3.4 us against 2.0
+//   (32 KB of granules per consumer instead of a 16 KB payload), the step 15.1 vs 14.6 us.
+// The flag / granule area is zeroed by a kernel before the launch.
 // Every spin is bounded: on timeout (or when another block already gave up) the block writes
 // the error word and returns, so the grid always drains.
 //
@@ -45,6 +52,9 @@ constexpr int PWV = PT / 64;       // waves
 constexpr int GCOLS = 32;          // G columns per workgroup
 constexpr int SPIN_LIMIT = 1 << 21;
 template <typename T> struct MaxKs { static constexpr int N = sizeof(T) == 2 ? 16 : 8; };  // U-phase k-steps per wave
+// forward: k-steps per wave by row tiles (the granule polls hold every step's loads in flight;
+// MT = 1 has 8 K parts, so 8 steps cover K = E + D <= 2048)
+template <typename T, int MT> struct MaxKsF { static constexpr int N = sizeof(T) == 2 && MT == 2 ? 16 : 8; };
 constexpr int SYNC_HDR = 16;       // words before the flags (word 0: error)
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
@@ -71,6 +81,9 @@ struct Geo {
   int ldE;            // R: LDS pitch (elements) of the enc rows: Ec + 32, see lstm_fwd_body
   int* err;           // the launch's error word (shared by the row groups)
   int fault_step;     // test knob (IMGCAP_LSTM_FAULT_FWD): U block 0 never publishes h of this step
+  int hg_off, zg_off; // sync word offsets of the h / z granule slots: [2][B][D or E / VPG] {value(s), epoch}
+  int hgran;          // h_t hand-off: 1 = tagged granules, 0 = write-through hs rows + per-block flags
+  int poll_sleep;     // s_sleep rounds after an incomplete granule poll pass (0 = spin)
 };
 
 // thread 0 of block 0 (U+G) and of the first R block records [role][t][k]
@@ -199,7 +212,89 @@ DEV Frag<T> frag_wt(rsrc_t r, uint32_t off, bool ok) {
   return frag_from<T>(lo, hi);
 }
 
-template <typename T, int MT>
+// Tagged granules: one naturally aligned 8-byte {value bits, epoch} pair written by ONE store (a
+// 16-byte write-through store carries two); the data is its own flag (no drain, no separate flag,
+// no second round trip; MI355X_MICROARCH.md handoff-1to1 vs handoff-flag).  Values per granule:
+// two bf16 or one fp32.  A fragment (8 consecutive values of one row) is 4 (bf16) / 8 (fp32)
+// granules = 2 / 4 sixteen-byte loads.
+template <typename T> struct GranOf {
+  static constexpr int VPG = sizeof(T) == 2 ? 2 : 1;  // values per granule
+  static constexpr int NL = 4 / VPG;                  // 16-byte loads per fragment
+};
+// One pass over a fragment's granules: the fragment and whether every tag is `ep` (an offset
+// past the buffer's range returns zeros without a memory access: the caller passes one for a
+// fragment it already holds or does not need)
+template <typename T>
+DEV bool frag_gran(rsrc_t r, uint32_t off, unsigned ep, Frag<T>& f) {
+  constexpr int NL = GranOf<T>::NL;
+  uint4 q[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) q[i] = ld_wt(r, off + 16 * i);
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) ok = ok && q[i].y == ep && q[i].w == ep;
+  const uint4 lo = make_uint4(q[0].x, q[0].z, q[1].x, q[1].z);
+  const uint4 hi = NL == 4 ? make_uint4(q[NL / 2].x, q[NL / 2].z, q[NL - 1].x, q[NL - 1].z) : lo;
+  f = frag_from<T>(lo, hi);
+  return ok;
+}
+// 8 values (one fragment's worth, packed as T in lo/hi) stored as tagged granules at byte `off`
+template <typename T>
+DEV void store_gran8(rsrc_t r, uint32_t off, const uint4& lo, const uint4& hi, unsigned ep) {
+  if constexpr (sizeof(T) == 2) {
+    st_wt(r, off, make_uint4(lo.x, ep, lo.y, ep));
+    st_wt(r, off + 16, make_uint4(lo.z, ep, lo.w, ep));
+  } else {
+    st_wt(r, off, make_uint4(lo.x, ep, lo.y, ep));
+    st_wt(r, off + 16, make_uint4(lo.z, ep, lo.w, ep));
+    st_wt(r, off + 32, make_uint4(hi.x, ep, hi.y, ep));
+    st_wt(r, off + 48, make_uint4(hi.z, ep, hi.w, ep));
+  }
+}
+// Wave-level poll of up to N fragments: fragment i is wanted where (want >> i) & 1, at byte
+// offset base + i * stride, tag ep.  Spins until every wanted fragment of every lane carries the
+// tag; a bounded spin (or an error word already set by another block) returns false.
+template <typename T, int N>
+DEV bool poll_frags(rsrc_t r, int base, int stride, unsigned want, unsigned ep, Frag<T> (&fa)[N], int* err,
+                    int sleep) {
+  // sentinel: until the first granule pair of each lane's first wanted fragment carries the tag,
+  // poll only that (16 bytes per lane per pass instead of every fragment); a producer writes all
+  // of a row's granules within one phase, so the full pass that follows usually completes at once
+  {
+    const uint32_t so = want ? (uint32_t)(base + __builtin_ctz(want) * stride) : 0x80000000u;
+    for (int spins = 0;; ++spins) {
+      const uint4 q = ld_wt(r, so);
+      if (__all(!want || q.y == ep)) break;
+      if ((spins & 255) == 255 &&
+          (spins >= SPIN_LIMIT || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
+  unsigned pending = want;
+  for (int spins = 0;; ++spins) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      Frag<T> f;
+      const bool need = (pending >> i) & 1u;
+      const bool ok = frag_gran<T>(r, need ? (uint32_t)(base + i * stride) : 0x80000000u, ep, f);
+      if (need && ok) {
+        fa[i] = f;
+        pending &= ~(1u << i);
+      }
+    }
+    if (__all(pending == 0u)) return true;
+    for (int q = 0; q < sleep; ++q) __builtin_amdgcn_s_sleep(2);
+    if ((spins & 63) == 63 &&
+        (spins >= SPIN_LIMIT / 8 || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+}
+
+template <typename T, int MT, bool HG>
 DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* s_ok = (int*)smem;
@@ -207,9 +302,6 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
   const int W3 = A + E + 4 * D;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int* err = g.err;
-  int* fh = d.sync + SYNC_HDR;
-  int* fg = fh + g.NU;
-  int* fz = fg + g.NG;
   // steps actually run: every row is past its decode length from max(dl) on
   if (tid < 64) {
     int m = 0;
@@ -221,9 +313,9 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
   __syncthreads();
   const int Tmax = max(0, min(Tn, s_ok[1]));
   constexpr int VEC = VecOf<T>::N;
-  const rsrc_t r_hs = make_rsrc(d.hs, (uint32_t)((long)B * Tn * D * sizeof(T)));
   const rsrc_t r_h0 = make_rsrc(d.hprev, (uint32_t)((long)B * Tn * D * sizeof(T)));
-  const rsrc_t r_zs = make_rsrc(d.zs, (uint32_t)((long)B * Tn * E * sizeof(T)));
+  const rsrc_t r_hs = make_rsrc(d.hs, (uint32_t)((long)B * Tn * D * sizeof(T)));
+  int* fh = d.sync + SYNC_HDR;  // per-U-block h flags (hgran == 0)
   const rsrc_t r_gr = make_rsrc(d.sync + g.gran_off, (uint32_t)((long)B * (A + E) * 8));
 
   if (blk < g.NUG) {
@@ -231,7 +323,7 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
     constexpr int KP = PWV / MT;         // K parts: wave w -> row tile w % MT, K part w / MT
     constexpr int NTU = 2;  // UPB = 8 units = 32 gate columns
     constexpr int UC = 16 * NTU;
-    constexpr int MAXKS = MaxKs<T>::N;
+    constexpr int MAXKS = MaxKsF<T, MT>::N;
     const int UPB = g.UPB;
     const bool isU = blk < g.NU, isG = blk < g.NG;
     const int u0 = blk * UPB;
@@ -278,18 +370,19 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
       const int col = blk * GCOLS + (tid % (GCOLS / 4)) * 4 + j;
       gb[j] = isG && col < A + E ? d.b_hcat[col] : 0.f;
     }
+    if (tid == 0) s_ok[2] = 1;  // cleared (for good) by a wave whose granule poll gave up
     __syncthreads();
     const int mi = w % MT, kp = w / MT;
     const int fr = lane & 15, fk = 8 * (lane >> 4);
     const int m = mi * 16 + fr;
     const bool mok = m < B;
+    constexpr int VPG = GranOf<T>::VPG;
+    const rsrc_t r_hg = make_rsrc(d.sync + g.hg_off, (uint32_t)(2L * B * (D / VPG) * 8));
+    const rsrc_t r_zg = make_rsrc(d.sync + g.zg_off, (uint32_t)(2L * B * (E / VPG) * 8));
     for (int t = 0; t < Tmax; ++t) {
       stamp(g, 0, t, 0);
-      if (t > 0 && !block_wait(fh, g.NU, t, err, s_ok + 2)) return;
-      stamp(g, 0, t, 1);
-      // h_{t-1} rows: h0 (hprev slot 0) at t = 0, else hs slot t-1
-      const rsrc_t rh = t == 0 ? r_h0 : r_hs;
-      const long hrow = (long)m * Tn + (t == 0 ? 0 : t - 1);
+      // h_{t-1} rows: h0 (hprev slot 0) at t = 0, else the U blocks' h granules of step t-1
+      const long hrow = (long)m * Tn;
       // U prefetch (issued before the G phase so its round trip overlaps it): xe, h part of A
       float xe[CPT][4];
 #pragma unroll
@@ -301,19 +394,43 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
       // A = [z_t | h_{t-1}]: the h part is available now, the z part after the R blocks'
       // hand-off; every fragment of this wave's K range is requested in one round trip each.
       // The G product (h_{t-1} [W_da; W_fb]^T) multiplies the SAME h fragments, so G blocks
-      // (U blocks or not) request them too and G runs on them: one 32 KB round trip of h per
-      // block instead of two (G's own copy used to queue behind this prefetch: "G h loads"
-      // 2.0 us per step in the stamps)
+      // (U blocks or not) request them too and G runs on them: one round trip of h per block.
       const int nks = (KU + 31) / 32, per = (nks + KP - 1) / KP;
       const int ks0 = kp * per, ks1 = min(nks, ks0 + per);
       const long zrow = (long)m * Tn + t;
       Frag<T> fa[MAXKS];
+      unsigned hwant = 0u, zwant = 0u;
 #pragma unroll
       for (int i = 0; i < MAXKS; ++i) {
         const int k0 = (ks0 + i) * 32 + fk;
-        fa[i] = frag_wt<T>(rh, (uint32_t)((hrow * D + (k0 - E)) * sizeof(T)),
-                           (isU || isG) && mok && ks0 + i < ks1 && k0 >= E && k0 < KU);
+        const bool in = mok && ks0 + i < ks1;
+        const bool hk = (isU || isG) && in && k0 >= E && k0 < KU;
+        fa[i] = frag_from<T>(make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u));
+        if (t == 0) {
+          fa[i] = frag_wt<T>(r_h0, (uint32_t)((hrow * D + (k0 - E)) * sizeof(T)), hk);
+        } else if (hk) {
+          hwant |= 1u << i;
+        }
+        if (isU && in && k0 < E) zwant |= 1u << i;
       }
+      // granule byte offsets of this wave's first k-step (affine in the step: 32 / VPG granules)
+      constexpr int GSTRIDE = 32 / VPG * 8;
+      const int k00 = ks0 * 32 + fk;
+      const int hbase = ((((t - 1) & 1) * B + m) * (D / VPG) + (k00 - E) / VPG) * 8;
+      const int zbase = (((t & 1) * B + m) * (E / VPG) + k00 / VPG) * 8;
+      if (t > 0 && HG) {
+        if (!poll_frags<T, MAXKS>(r_hg, hbase, GSTRIDE, hwant, (unsigned)t, fa, err, g.poll_sleep) && lane == 0)
+          s_ok[2] = 0;
+      } else if (t > 0) {  // every U block's flag, then the write-through hs rows of step t-1
+        if (!block_wait(fh, g.NU, t, err, s_ok + 3)) return;
+        const long hprow = (long)m * Tn + t - 1;
+#pragma unroll
+        for (int i = 0; i < MAXKS; ++i) {
+          const int k0 = (ks0 + i) * 32 + fk;
+          if ((hwant >> i) & 1u) fa[i] = frag_wt<T>(r_hs, (uint32_t)((hprow * D + (k0 - E)) * sizeof(T)), true);
+        }
+      }
+      stamp(g, 0, t, 1);
       // ---------------- G: [att2 | gate_pre]_t ----------------
       if (isG) {
         f32x4 acc[2];
@@ -334,6 +451,7 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) red[(kp * 16 * MT + mi * 16 + 4 * (lane >> 4) + r) * RC + ni * 16 + fr] = acc[ni][r];
         __syncthreads();
+        if (s_ok[2] == 0) return;
         // 16-byte write-through stores: row b, 4 consecutive columns per thread
         const int col0 = blk * GCOLS;
         for (int i = tid; i < 16 * MT * (GCOLS / 4); i += PT) {
@@ -361,13 +479,10 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
       }
       // ---------------- U: gates, LSTMCell -> h_t ----------------
       if (isU) {
-        if (!block_wait(fz, g.NR, t + 1, err, s_ok + 3)) return;
+        // the z part of A: the R blocks' z_t granules (slot t & 1, tag t + 1)
+        if (!poll_frags<T, MAXKS>(r_zg, zbase, GSTRIDE, zwant, (unsigned)(t + 1), fa, err, g.poll_sleep) && lane == 0)
+          s_ok[2] = 0;
         stamp(g, 0, t, 4);
-#pragma unroll
-        for (int i = 0; i < MAXKS; ++i) {
-          const int k0 = (ks0 + i) * 32 + fk;
-          if (mok && ks0 + i < ks1 && k0 < E) fa[i] = frag_wt<T>(r_zs, (uint32_t)((zrow * E + k0) * sizeof(T)), true);
-        }
         stamp(g, 0, t, 8, true);
         f32x4 acc[NTU][2];  // two K-interleaved chains per column tile
 #pragma unroll
@@ -390,6 +505,7 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
           for (int r = 0; r < 4; ++r)
             red[(kp * 16 * MT + mi * 16 + 4 * (lane >> 4) + r) * RC + ni * 16 + fr] = acc[ni][0][r] + acc[ni][1][r];
         __syncthreads();
+        if (s_ok[2] == 0) return;
         stamp(g, 0, t, 5);
         float cell[CPT][5];  // activated i, f, g, o and c_t, stored after the hand-off
 #pragma unroll
@@ -412,16 +528,33 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
           hst[b * UPB + jj] = from_f<T>(h);
         }
         __syncthreads();
-        // h_t of this block's units: one row per thread, write-through 16-byte pieces
+        // h_t of this block's units as granules (slot t & 1, tag t + 1): one row per thread; the
+        // saved hs / hprev copies with plain stores
         const int pieces = UPB * (int)sizeof(T) / 16;  // UPB * sizeof(T) is 16 or 32
-        for (int i = tid; i < B * pieces; i += PT) {
-          const int b = i / pieces, pc = i % pieces;
-          const uint4 v = *(const uint4*)(hst + b * UPB + pc * VEC);
-          const long off = ((long)b * Tn + t) * D + u0 + pc * VEC;
-          st_wt(r_hs, (uint32_t)(off * sizeof(T)), v);
+        const bool publish = t != g.fault_step || blk != 0;
+        if constexpr (HG) {
+          if (publish)
+            for (int b = tid; b < B; b += PT) {
+              const uint4 lo = *(const uint4*)(hst + b * UPB);
+              const uint4 hi = pieces == 2 ? *(const uint4*)(hst + b * UPB + VecOf<T>::N) : lo;
+              store_gran8<T>(r_hg, (uint32_t)((((long)(t & 1) * B + b) * (D / VPG) + u0 / VPG) * 8), lo, hi,
+                             (unsigned)(t + 1));
+            }
+          stamp(g, 0, t, 6);
+          for (int i = tid; i < B * pieces; i += PT) {
+            const int b = i / pieces, pc = i % pieces;
+            const uint4 v = *(const uint4*)(hst + b * UPB + pc * VEC);
+            *(uint4*)((T*)d.hs + ((long)b * Tn + t) * D + u0 + pc * VEC) = v;
+          }
+        } else {
+          for (int i = tid; i < B * pieces; i += PT) {
+            const int b = i / pieces, pc = i % pieces;
+            const uint4 v = *(const uint4*)(hst + b * UPB + pc * VEC);
+            st_wt(r_hs, (uint32_t)((((long)b * Tn + t) * D + u0 + pc * VEC) * sizeof(T)), v);
+          }
+          stamp(g, 0, t, 6);
+          if (publish) block_publish(fh + blk, t + 1);
         }
-        stamp(g, 0, t, 6);
-        if (t != g.fault_step || blk != 0) block_publish(fh + blk, t + 1);
         stamp(g, 0, t, 7);
         // outputs nobody in this launch reads: after the hand-off
 #pragma unroll
@@ -467,6 +600,8 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
   // ======================= R workgroup: attention of row b, channel chunk s ================
   const int rr = blk - g.NUG, b = rr / g.RS, s = rr % g.RS;
   const int Ec = g.Ec, e0 = s * Ec;
+  constexpr int VPG = GranOf<T>::VPG;
+  const rsrc_t r_zg = make_rsrc(d.sync + g.zg_off, (uint32_t)(2L * B * (E / VPG) * 8));
   T* att1s = (T*)(smem + 16);                   // [P][A]
   // [P][ldE]: a lane quad reads 4 consecutive pixels of one 8-channel vector in the context
   // loop; with rows of Ec (a multiple of 128 elements) the quad hit one bank group (4-way,
@@ -622,16 +757,18 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
         T* zt = (T*)zz;
 #pragma unroll
         for (int j = 0; j < 8; ++j) zt[j] = from_f<T>(sigmoidf_(gp[j]) * acc[j]);
-        const uint32_t off = (uint32_t)((bt * E + e0 + v * 8) * sizeof(T));
-        st_wt(r_zs, off, zz[0]);
-        if (sizeof(T) == 4) st_wt(r_zs, off + 16, zz[1]);
+        // z_t to the U blocks as tagged granules (slot t & 1, tag t + 1); the saved zs copy plain
+        store_gran8<T>(r_zg, (uint32_t)((((long)(t & 1) * B + b) * (E / VPG) + (e0 + v * 8) / VPG) * 8), zz[0],
+                       zz[1], (unsigned)(t + 1));
+        T* zsp = (T*)d.zs + bt * E + e0 + v * 8;
+        *(uint4*)zsp = zz[0];
+        if (sizeof(T) == 4) *(uint4*)(zsp + 4) = zz[1];
         float* aw = d.awe + bt * E + e0 + v * 8;  // saved context (nobody in this launch reads it)
         *(f32x4*)aw = f32x4{acc[0], acc[1], acc[2], acc[3]};
         *(f32x4*)(aw + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
       }
     }
     stamp(g, 1, t, 3);
-    block_publish(fz + rr, t + 1);
     stamp(g, 1, t, 4);
     if (s == 0 && tid < P) d.alphas[bt * P + tid] = t < dlb ? es[tid] : 0.f;
   }
@@ -652,13 +789,13 @@ DEV void lstm_fwd_body(const imgcap_lstm_desc& d, const Geo& g, const int blk) {
 // (row-offset pointers) and flag / granule area; blocks [0, nb0) are group 0.  Halving the
 // rows per chain shortens each step's payload loads and MFMA work (measured per step at
 // B = 16 vs 32: forward 15.7 vs 17.4 us, backward 17.8 vs 21.2 us).
-template <typename T, int MT>
+template <typename T, int MT, bool HG>
 __global__ __launch_bounds__(PT) void lstm_fwd_persist_kernel(imgcap_lstm_desc d0, Geo g0, imgcap_lstm_desc d1,
                                                               Geo g1, int nb0) {
   // one inlined body over the selected group's (kernel-argument) descriptor: two inlined copies
   // doubled the code and ran out of SGPRs (1,000+ SGPR spills to VGPR lanes)
   const bool second = (int)blockIdx.x >= nb0;
-  lstm_fwd_body<T, MT>(second ? d1 : d0, second ? g1 : g0, second ? (int)blockIdx.x - nb0 : (int)blockIdx.x);
+  lstm_fwd_body<T, MT, HG>(second ? d1 : d0, second ? g1 : g0, second ? (int)blockIdx.x - nb0 : (int)blockIdx.x);
 }
 
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -1196,7 +1333,8 @@ static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds
   g.ldg = d.D + pad;
   g.rc = std::max(UC, GCOLS) + 4;
   const int KP = PWV / mt;
-  if (((g.KU + 31) / 32 + KP - 1) / KP > (esz == 2 ? MaxKs<bf16>::N : MaxKs<float>::N)) return false;
+  const int maxks = esz == 2 ? (mt == 2 ? MaxKsF<bf16, 2>::N : MaxKsF<bf16, 1>::N) : MaxKsF<float, 1>::N;
+  if (((g.KU + 31) / 32 + KP - 1) / KP > maxks) return false;
   size_t o = 16 + (size_t)UC * g.ldu * esz + (size_t)GCOLS * g.ldg * esz;
   g.ug_red = (int)align16(o);
   o = g.ug_red + (size_t)KP * 16 * mt * g.rc * 4;
@@ -1240,7 +1378,10 @@ static bool persist_plan(const imgcap_lstm_desc& d, int esz, Geo& g, size_t& lds
   lds = std::max(std::max(ug, r), (size_t)81 * 1024);
   if (lds > LDS_MAX) return false;
   g.gran_off = (SYNC_HDR + g.NU + g.NG + g.NR + 63) / 64 * 64;  // 256-byte aligned granule block
-  words = g.gran_off + d.B * (d.A + d.E) * 2;
+  const int vpg = esz == 2 ? 2 : 1;
+  g.hg_off = (g.gran_off + d.B * (d.A + d.E) * 2 + 63) / 64 * 64;  // [2][B][D / vpg] h granules
+  g.zg_off = g.hg_off + 2 * d.B * (d.D / vpg) * 2;                 // [2][B][E / vpg] z granules
+  words = g.zg_off + 2 * d.B * (d.E / vpg) * 2;
   return true;
 }
 
@@ -1309,6 +1450,12 @@ static int device_cus() {
   return cache[dev];
 }
 
+// Integer knob from the environment (read once), `dflt` when unset.
+static int env_or(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
 // Test knob: a step index from the environment (read at every launch), -1 when unset.
 static int env_step(const char* name) {
   const char* e = getenv(name);
@@ -1369,14 +1516,18 @@ static bool fwd_launch_plan(const imgcap_lstm_desc& d, int esz, FwdLaunch& L) {
   return false;
 }
 
-static const void* fwd_kernel_of(int esz, int mt) {
-  if (esz == 2) return mt == 1 ? (const void*)lstm_fwd_persist_kernel<bf16, 1> : (const void*)lstm_fwd_persist_kernel<bf16, 2>;
-  return mt == 1 ? (const void*)lstm_fwd_persist_kernel<float, 1> : (const void*)lstm_fwd_persist_kernel<float, 2>;
+static const void* fwd_kernel_of(int esz, int mt, bool hg) {
+  if (esz == 2) {
+    if (hg) return mt == 1 ? (const void*)lstm_fwd_persist_kernel<bf16, 1, true> : (const void*)lstm_fwd_persist_kernel<bf16, 2, true>;
+    return mt == 1 ? (const void*)lstm_fwd_persist_kernel<bf16, 1, false> : (const void*)lstm_fwd_persist_kernel<bf16, 2, false>;
+  }
+  if (hg) return mt == 1 ? (const void*)lstm_fwd_persist_kernel<float, 1, true> : (const void*)lstm_fwd_persist_kernel<float, 2, true>;
+  return mt == 1 ? (const void*)lstm_fwd_persist_kernel<float, 1, false> : (const void*)lstm_fwd_persist_kernel<float, 2, false>;
 }
 
-template <typename T, int MT>
+template <typename T, int MT, bool HG>
 static int launch_persist(const FwdLaunch& L, hipStream_t st) {
-  hipLaunchKernelGGL((lstm_fwd_persist_kernel<T, MT>), dim3(L.nblk), dim3(PT), L.lds, st, L.d[0], L.g[0], L.d[1],
+  hipLaunchKernelGGL((lstm_fwd_persist_kernel<T, MT, HG>), dim3(L.nblk), dim3(PT), L.lds, st, L.d[0], L.g[0], L.d[1],
                      L.g[1], L.nb0);
   IMGCAP_CHECK_LAUNCH("lstm persistent forward");
   return 0;
@@ -1397,8 +1548,11 @@ int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
   FwdLaunch L;
   if (!fwd_launch_plan(d, esz, L)) return 0;
   // every workgroup resident at once (the hand-offs spin on each other): else the per-step path
-  if (!resident_one_per_cu(fwd_kernel_of(esz, L.mt), L.lds)) return 0;
+  static const int hgran = env_or("IMGCAP_LSTM_HGRAN", 0), psleep = env_or("IMGCAP_LSTM_POLL_SLEEP", 0);
+  if (!resident_one_per_cu(fwd_kernel_of(esz, L.mt, hgran != 0), L.lds)) return 0;
   L.g[0].fault_step = L.g[1].fault_step = env_step("IMGCAP_LSTM_FAULT_FWD");
+  L.g[0].hgran = L.g[1].hgran = hgran;
+  L.g[0].poll_sleep = L.g[1].poll_sleep = psleep;
   static const bool stamps = getenv("IMGCAP_LSTM_STAMPS") && atoi(getenv("IMGCAP_LSTM_STAMPS"));
   L.g[0].stamps = L.g[1].stamps = nullptr;
   if (stamps && d.T <= 64) {  // group 0 only, after every group's sync words (fwd and bwd)
@@ -1412,7 +1566,7 @@ int lstm_fwd_persistent(const imgcap_lstm_desc& d, hipStream_t st, bool* used) {
     return fail(IMGCAP_EINVAL, "lstm persistent: zeroing of the sync words failed");
   *used = true;
 #define LP_CASE(TT, M_) \
-  if (L.mt == M_) return launch_persist<TT, M_>(L, st);
+  if (L.mt == M_) return hgran ? launch_persist<TT, M_, true>(L, st) : launch_persist<TT, M_, false>(L, st);
   if (esz == 2) {
     LP_CASE(bf16, 1) LP_CASE(bf16, 2)
   } else {

@@ -10,10 +10,37 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
-from imagecaptioningconvnext_amd.roofline import time_launch  # noqa: E402
 
 dev = torch.device("cuda:0")
 bf = torch.bfloat16
+
+
+def time_launch(fn, reps=50, warm=5, graph=True):
+    """Seconds per launch of ``fn``, HIP events around ``reps`` back-to-back launches (captured
+    into one HIP graph and replayed with graph=True, so host launch cost does not hide short
+    kernels)."""
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    g = None
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    if g is not None:
+        g.replay()
+    else:
+        for _ in range(reps):
+            fn()
+    b.record(st)
+    b.synchronize()
+    return a.elapsed_time(b) / reps * 1e-3
 
 
 def gemm_case(name, M, N, Kd, ta=False, tb=True, act=0, out_dtype=bf, reps=30, split_k=0):
