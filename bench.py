@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run encoder and decoder of a step back to back (no two-stream overlap)")
     ap.add_argument("--no-fp8", action="store_true", help="C5: frozen encoder GEMMs in bf16 instead of MX-FP8")
+    ap.add_argument("--no-roofline", action="store_true",
+                    help="skip the per-call roofline pass (profiling the replays alone); roofline is then null")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="launcher check on CPU: gloo ranks time an empty step (tests/test_bench_cpu.py); "
                          "prints the rank layout, not a measurement")
@@ -290,7 +292,7 @@ def main(argv=None):
         from imagecaptioningconvnext_amd import roofline
         if progress:
             print("[bench] roofline", file=sys.stderr, flush=True)
-        roof = roofline.measure(cfg, trainer, batches[0], cfgname=args.config)
+        roof = None if args.no_roofline else roofline.measure(cfg, trainer, batches[0], cfgname=args.config)
         if progress:
             print("[bench] roofline done", file=sys.stderr, flush=True)
         out = {

@@ -262,22 +262,26 @@ class LstmEngine:
             K.transpose(w["wih"][:, M:], out=wzh_t[:E])
             K.transpose(w["hcat"][A + E:], out=wzh_t[E:])
             watt_t = K.transpose(w["hcat"][:A + E])                    # [D, A + E] = [W_da; W_fb]^T
+            # the loss rows' mask and targets only depend on the captions: built here, beside the
+            # recurrence, instead of between it and the vocab projection
+            tmask = torch.arange(T, device=dev).view(1, T) < dl.view(B, 1)
+            if loss:
+                targets = torch.where(tmask, caps_s[:, 1:T + 1],
+                                      torch.full_like(caps_s[:, 1:T + 1], -1)).reshape(-1)
         self._launch("imgcap_lstm_tf_fwd", d)
         main.wait_stream(side)
-        wzh_t.record_stream(main)
-        watt_t.record_stream(main)
+        for t_ in (wzh_t, watt_t, tmask) + ((targets,) if loss else ()):
+            t_.record_stream(main)
         # ---- fc(dropout(h)) over all B*T rows (decoder.py:109) ----------------------------------
         hd = hs.view(B * T, D)
         if p_drop > 0:
             hd = K.dropout(hd, p_drop, s["seed"], _STREAM_DROPOUT_H)
-        tmask = torch.arange(T, device=dev).view(1, T) < dl.view(B, 1)
         s.update(enc_s=enc_s, ids=ids, emb=emb, mean=mean, att1=att1, xe=xe, c0=c0, g1=g1, alphas=alphas, awe=awe,
                  zs=zs, gates=gates, cs=cs, hs=hs, hprev=hprev, hd=hd, tmask=tmask, desc=d, wzh_t=wzh_t,
                  watt_t=watt_t)
         if loss:
             logits = torch.empty(B * T, self.Vpad, **ctd)
             K.gemm(hd, w["wfc"], trans_b=True, bias=w["bfc"], out=logits, N=V)
-            targets = torch.where(tmask, caps_s[:, 1:T + 1], torch.full_like(caps_s[:, 1:T + 1], -1)).reshape(-1)
             lse = torch.empty(B * T, **f32)
             lrow = torch.empty(B * T, **f32)
             hit = torch.empty(B * T, **f32)
@@ -405,7 +409,6 @@ class LstmEngine:
         A, E, D, M, V, W3 = self.A, self.E, self.D, self.M, self.V, self.W3
         dev = s["hs"].device
         w = self.weights()
-        gbuf.zero_()
         cb = K.ColsumBatch()  # every bias gradient, reduced in one launch at the end
         wgb = K.GemmBatch()    # every weight gradient, grouped launches at the end
         if dlogits is None:
@@ -420,6 +423,9 @@ class LstmEngine:
         side = self._side_stream(dev)
         side.wait_stream(main)
         with torch.cuda.stream(side):  # no library scratch on this stream (no split-K, one-pass colsum)
+            # the gradient buffer is cleared here, beside the recurrence (60 MB at C2, not on the
+            # critical path); the main stream joins this stream before its first gradient write
+            gbuf.zero_()
             K.gemm(dlogits, s["hd"], trans_a=True, M=V, out=_G.g("fc.weight"), out_dtype=torch.float32)
             cbs = K.ColsumBatch()
             cbs.add(dlogits, _G.g("fc.bias"), cols=V)
@@ -473,6 +479,7 @@ class LstmEngine:
         cb.add(dgates, _G.g("decode_step.bias_ih"))
         # embedding: d_emb = dgates W_ih[:, :M]  -> scatter-add rows
         demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
+        torch.cuda.current_stream(dev).wait_stream(side)  # gbuf cleared, fc dW / db (beside the recurrence) done
         K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
         # init_h / init_c from dh0, dc0
         dinit = torch.cat([dh, dc], dim=1).to(ct)
@@ -483,7 +490,6 @@ class LstmEngine:
         cb.add(dbea, _G.g("attention.encoder_att.bias"))
         cb.add(dwf, _G.g("attention.full_att.weight", (A,)))
         # full_att.bias: exactly zero gradient (softmax is shift-invariant) -> left at 0
-        torch.cuda.current_stream(dev).wait_stream(side)  # fc dW / db (beside the recurrence) done
         if bucket_hook is not None:
             bucket_hook()
         wgb.run()
