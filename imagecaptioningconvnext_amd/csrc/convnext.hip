@@ -291,19 +291,46 @@ __global__ __launch_bounds__(256) void dwconv7_ln_kernel(int B, int H, int W, in
 // the 7 kernel rows (rows of another image than the lane's are skipped: image boundaries
 // inside a tile).  fp32 accumulation, packed two channels per FMA.
 // LDS layout: 16-byte slots; pixel px of patch row r at slot r*RS + 4*px + px/PW (one gap slot
-// after every PW pixels), slot s of the pixel = its channels 8s..8s+7.  A wave reads slot wv of
-// pixel g*PW + q across its lanes (groups g, rows lr): 4*PW + 1 is odd, so the GW groups of a
-// row land in distinct bank groups, and RS = 16/GW (mod 16) interleaves successive rows into
-// the remaining ones -- each 16-lane pass of a ds_read_b128 is conflict-free.
+// after every PW pixels), slot s of the pixel = its channels 8s..8s+7 (fp32: two slots per 8
+// channels).  A wave reads slot wv of pixel g*PW + q across its lanes (row lr = lane / GW, group
+// g = lane % GW); ds_read_b128 serves a wave in four 16-lane groups ({0-3,12-15,20-27},
+// {4-11,16-19,28-31}, {32-35,44-47,52-59}, {36-43,48-51,60-63}; MI355X_MICROARCH.md §LDS), one
+// cycle per group when its 16 lanes hit 16 distinct slots of the 256-byte bank row.  The row
+// stride RS is searched (dw_row_slots) so that lr * RS + g * (4*PW + 1) is distinct mod 16
+// within every group: RS = 8 (mod 16) at GW = 8, 4 at 4, 2 at 2, 1 at 1 for PW = 7 (round 2's
+// 16/GW rule gave 2-way conflicts at GW = 8 and 16-way at GW = 1: 6.8 / 34 extra cycles per
+// read in profiles/r02_C2_sq.json).
 constexpr int DW_CT = 32;  // channels per block
-// LDS row stride in 16-byte slots: >= the row's slots, = 16/GW (mod 16) (see above)
+constexpr int kDwGroups[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                  {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                  {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                  {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+// LDS row stride in 16-byte slots: the smallest >= the row's slots with the fewest bank
+// collisions in any ds_read_b128 lane group of the window reads (see above)
 __host__ __device__ constexpr int dw_row_slots(int W, int PW, int elem_bytes) {
   const int GW = W / PW;
-  const int base = (4 * (W + 6) + (W + 5) / PW + 1) * (elem_bytes / 2);
-  const int target = (GW == 1 || GW == 2 || GW == 4 || GW == 8 || GW == 16) ? (16 / GW) % 16 : 1;
-  int rs = base;
-  while (rs % 16 != target) ++rs;
-  return rs;
+  const int f = elem_bytes / 2;                       // slots per 8 channels (bf16 1, fp32 2)
+  const int base = (4 * (W + 6) + (W + 5) / PW + 1) * f;
+  const int gstep = (4 * PW + 1) * f;                 // slot distance between pixel groups
+  int best = base, best_m = 1 << 30;
+  for (int rs = base; rs < base + 16; ++rs) {
+    int worst = 0;
+    for (int grp = 0; grp < 4; ++grp) {
+      int cnt[16] = {0};
+      for (int i = 0; i < 16; ++i) {
+        const int l = kDwGroups[grp][i];
+        const int sl = ((l / GW) * rs + (l % GW) * gstep) % 16;
+        const int c = ++cnt[sl];
+        worst = c > worst ? c : worst;
+      }
+    }
+    if (worst < best_m) {
+      best_m = worst;
+      best = rs;
+    }
+    if (worst == 1) break;
+  }
+  return best;
 }
 // WC: the image width as a compile-time constant (0: runtime W) -- the staging index math
 // (patch row / column of each 16-byte load) then folds to multiplies by constants, which at
@@ -431,6 +458,140 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_kernel(int B, int H, 
 }
 
 // ---------------------------------------------------------------------------------------
+// The same depthwise conv over NTL consecutive row tiles per block (compile-time width): the
+// block keeps a ring of 2*TR + 6 input rows in LDS, so the 6 halo rows are fetched once per
+// NTL*TR rows instead of once per TR (stage 1 at W = 56: 1.75x -> 1.25x the input at NTL = 3),
+// and the TR new rows of tile k+1 are loaded into registers before tile k is computed and
+// written to the ring after it -- their latency hides behind tile k's arithmetic.  Ring row of
+// input row i (counted from the block's first output row - 3) = i mod (2*TR + 6): tile k reads
+// rows [k*TR, k*TR + TR + 6), its prefetch lands in rows [k*TR + TR + 6, k*TR + 2*TR + 6),
+// the slots of rows k*TR - TR .. k*TR - 1 that tile k-1 finished with before the barrier.
+template <typename T, int PW, int WC, int NC, int NTL>
+__global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, int H, int C, const T* __restrict__ x,
+                                                           const float* __restrict__ w,
+                                                           const float* __restrict__ bias, T* __restrict__ y,
+                                                           const T* res, int flip) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  static_assert(WC > 0 && NTL >= 1, "compile-time width");
+  constexpr int VE = 16 / sizeof(T);
+  constexpr int NV = DW_CT / VE;
+  constexpr int SPP = DW_CT * 2 / 16;
+  constexpr int NT = 64 * DW_CT / NC;
+  constexpr int W = WC, GW = W / PW, TR = 64 / GW, WP = W + 6;
+  constexpr int RS = dw_row_slots(WC, PW, (int)sizeof(T));
+  constexpr int RING = NTL > 1 ? 2 * TR + 6 : TR + 6;
+  constexpr int PSTEP = NT / NV;                      // pixels per load instruction of the block
+  constexpr int NPF = (TR * WP + PSTEP - 1) / PSTEP;  // loads per thread for TR new rows
+  const long R = (long)B * H;
+  const long rb = (long)blockIdx.x * (NTL * TR);      // the block's first output row
+  const int cb = blockIdx.y * DW_CT;
+  uint4* img = (uint4*)dsm;
+  auto slot = [&](int rr, int px, int s) { return rr * RS + (SPP * px + px / PW) * (NV / SPP) + s; };
+  const int v = threadIdx.x % NV;
+  const int p0 = threadIdx.x / NV;
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(R * W * C * (long)sizeof(T)), 0x00020000);
+  // TR input rows from relative row i0 (relative row i = global row rb - 3 + i) into registers;
+  // the zero halo and rows outside [0, R) come from the descriptor's range check
+  auto load_rows = [&](int i0, int nrows, uint4 (&val)[NPF]) {
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int px = p0 + u * PSTEP;
+      const int pr = px / WP, pc = px % WP;
+      const long gr = rb - 3 + i0 + pr;
+      const int gw = pc - 3;
+      const bool ok = pr < nrows && gr >= 0 && gr < R && gw >= 0 && gw < W;
+      const uint32_t off = ok ? (uint32_t)((((gr * W) + gw) * C + cb + v * VE) * (long)sizeof(T)) : 0x80000000u;
+      val[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+  };
+  auto store_rows = [&](int i0, int nrows, const uint4 (&val)[NPF]) {
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int px = p0 + u * PSTEP;
+      const int pr = px / WP;
+      if (pr < nrows) img[slot((i0 + pr) % RING, px % WP, v)] = val[u];
+    }
+  };
+  {  // prologue: the TR + 6 rows of tile 0
+    uint4 a[NPF], b[NPF];
+    load_rows(0, TR, a);
+    load_rows(TR, 6, b);
+    store_rows(0, TR, a);
+    store_rows(TR, 6, b);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = cb + wv * NC;
+  const int lr = lane / GW, g = lane % GW;
+  const int w0 = g * PW;
+  constexpr int NP = NC / 2;
+  const int cofs = wv * NC * (int)sizeof(T);
+  const char* imgb = (const char*)img;
+  float bv[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) bv[j] = 0.f;
+  if (bias) ldc<float, NC>(bias + c0, bv);
+  for (int k = 0; k < NTL; ++k) {
+    uint4 pf[NPF];
+    const bool more = k + 1 < NTL;
+    if (more) load_rows(k * TR + TR + 6, TR, pf);
+    const long orow = rb + (long)k * TR + lr;
+    if (orow < R) {
+      const int h = (int)(orow % H);
+      f32x2 acc[PW][NP];
+#pragma unroll
+      for (int p = 0; p < PW; ++p)
+#pragma unroll
+        for (int j = 0; j < NP; ++j) acc[p][j] = f32x2{bv[2 * j], bv[2 * j + 1]};
+      for (int kh = 0; kh < 7; ++kh) {
+        const int ih = h + kh - 3;
+        f32x2 wt[7][NP];
+#pragma unroll
+        for (int kw = 0; kw < 7; ++kw) {
+          float t[NC];
+          ldc<float, NC>(w + (flip ? 48 - (kh * 7 + kw) : kh * 7 + kw) * C + c0, t);
+#pragma unroll
+          for (int j = 0; j < NP; ++j) wt[kw][j] = f32x2{t[2 * j], t[2 * j + 1]};
+        }
+        if (ih < 0 || ih >= H) continue;  // outside this lane's image (zero padding)
+        const int rr = (k * TR + lr + kh) % RING;
+        f32x2 win[PW + 6][NP];
+#pragma unroll
+        for (int q = 0; q < PW + 6; ++q) {
+          float vv[NC];
+          ldc<T, NC>((const T*)(imgb + slot(rr, w0 + q, 0) * 16 + cofs), vv);
+#pragma unroll
+          for (int j = 0; j < NP; ++j) win[q][j] = f32x2{vv[2 * j], vv[2 * j + 1]};
+        }
+#pragma unroll
+        for (int kw = 0; kw < 7; ++kw)
+#pragma unroll
+          for (int p = 0; p < PW; ++p)
+#pragma unroll
+            for (int j = 0; j < NP; ++j) acc[p][j] = win[p + kw][j] * wt[kw][j] + acc[p][j];
+      }
+      T* out = y + (orow * W + w0) * C + c0;
+#pragma unroll
+      for (int p = 0; p < PW; ++p) {
+        float o[NC];
+#pragma unroll
+        for (int j = 0; j < NP; ++j) { o[2 * j] = acc[p][j][0]; o[2 * j + 1] = acc[p][j][1]; }
+        if (res) {
+          float r[NC];
+          ldc<T, NC>(res + (orow * W + w0 + p) * C + c0, r);
+#pragma unroll
+          for (int j = 0; j < NC; ++j) o[j] += r[j];
+        }
+        stc<T, NC>(out + (long)p * C, o);
+      }
+    }
+    if (more) store_rows(k * TR + TR + 6, TR, pf);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // LayerNorm2d + 2x2/s2 patch gather: one wave per input pixel.
 template <typename T>
 __global__ __launch_bounds__(256) void ln_patchify2_kernel(int B, int H, int W, int C, const T* __restrict__ x,
@@ -535,6 +696,34 @@ bool dw_narrow() {
   }();
   return v == 1;
 }
+// the rolling kernel's ring exceeds the default 64 KB of dynamic LDS: raise the limit once per
+// instantiation (first launch, before any capture)
+template <typename T, int P, int WC, int N>
+void dw_roll_attr() {
+  static const bool done = [] {
+    (void)hipFuncSetAttribute((const void*)dwconv7_roll_kernel<T, P, WC, 8, N>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)done;
+}
+
+// IMGCAP_DW_NTL=k forces k row tiles per block of the rolling kernel (0: the one-tile kernel)
+int dw_ntl_override() {  // read at every launch (tests switch it)
+  const char* e = getenv("IMGCAP_DW_NTL");
+  return e && *e ? atoi(e) : -1;
+}
+// Row tiles per block of the rolling kernel.  Measured (tools/microbench.py dw, B = 64, Tiny and
+// Large stage shapes, gpurun_out/r3dw): one tile per block (two blocks per CU) is the fastest at
+// every shape -- 2-4 tiles per block cut the halo re-fetch but hold one block per CU (the ring
+// exceeds 80 KB) and ran 1.2-3x slower; the kernel is VALU-bound (per tap row: 196 packed FMAs
+// + ~200 bf16 unpack / address operations per lane), not halo-bound.  IMGCAP_DW_NTL overrides.
+int dw_pick_ntl(long, int, size_t, size_t) {
+  const int ov = dw_ntl_override();
+  if (ov >= 0) return ov > 4 ? 4 : ov;
+  return 1;
+}
+
 template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
                    hipStream_t st, const void* res = nullptr, int flip = 0) {
@@ -552,6 +741,40 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
   // late-stage grids) measured slower at every encoder shape (tools/microbench.py dw): the
   // b64 reads of the 16-byte slot layout conflict 2-way and the staging is the same per block
   const int nc = dw_nc_override() ? dw_nc_override() : 8;
+  // the rolling kernel (compile-time widths, 8 channels per lane, bf16 / fp32)
+  const long tiles = (R + TR - 1) / TR;
+  const size_t shm_roll = (size_t)(2 * TR + 6) * RS * 16;
+  const int ntl = (nc == 8 && !narrow && shm_roll <= 160 * 1024) ? dw_pick_ntl(tiles, C / DW_CT, shm, shm_roll) : 0;
+#define DWR_(P, WC, N)                                                                                         \
+  dw_roll_attr<T, P, WC, N>();                                                                                 \
+  hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8, N>), dim3((unsigned)((tiles + N - 1) / N), C / DW_CT),  \
+                     dim3(256), N == 1 ? shm : shm_roll, st, B, H, C, (const T*)x, w, bias, (T*)y,             \
+                     (const T*)res, flip)
+#define DWR_ALL(P, WC)                 \
+  do {                                 \
+    switch (ntl) {                     \
+      case 1: DWR_(P, WC, 1); break;   \
+      case 2: DWR_(P, WC, 2); break;   \
+      case 3: DWR_(P, WC, 3); break;   \
+      default: DWR_(P, WC, 4); break;  \
+    }                                  \
+  } while (0)
+  if (ntl > 0 && !narrow && (W == 56 || W == 28 || W == 14 || W == 7 || W == 64 || W == 32 || W == 16 || W == 8)) {
+    switch (W) {
+      case 56: DWR_ALL(7, 56); break;
+      case 28: DWR_ALL(7, 28); break;
+      case 14: DWR_ALL(7, 14); break;
+      case 7: DWR_ALL(7, 7); break;
+      case 64: DWR_ALL(8, 64); break;
+      case 32: DWR_ALL(8, 32); break;
+      case 16: DWR_ALL(8, 16); break;
+      default: DWR_ALL(8, 8); break;
+    }
+    IMGCAP_CHECK_LAUNCH("imgcap_dwconv7");
+    return 0;
+  }
+#undef DWR_ALL
+#undef DWR_
 #define DW_(P, WC)                                                                                              \
   do {                                                                                                         \
     if (nc == 4)                                                                                               \

@@ -319,6 +319,34 @@ def test_dwconv7(hip_device, dtype, tol, B, H, C):
     assert _rel(out.cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("ntl", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,H,C", [(5, 56, 96), (3, 28, 64), (7, 14, 32), (11, 7, 64), (3, 16, 32)])
+def test_dwconv7_row_tiles(hip_device, monkeypatch, ntl, dtype, tol, B, H, C):
+    """The rolling depthwise kernel with 1-4 row tiles per block (IMGCAP_DW_NTL; 0 = the
+    one-tile kernel): ring rows reused across tiles, tiles crossing image boundaries and the
+    partial last block; forward, and the flipped (transposed) pass of the backward + residual."""
+    from imagecaptioningconvnext_amd import kernels as K
+    monkeypatch.setenv("IMGCAP_DW_NTL", str(ntl))
+    torch.manual_seed(B * H + C + ntl)
+    x = torch.randn(B, H, H, C)
+    w = torch.randn(C, 1, 7, 7) * 0.2
+    bias = torch.randn(C)
+    res = torch.randn(B, H, H, C)
+    xin = x.to(dtype).float()
+    ref = F.conv2d(xin.permute(0, 3, 1, 2), w, bias, padding=3, groups=C).permute(0, 2, 3, 1)
+    w49 = w.view(C, 49).t().contiguous().to(hip_device)
+    out = torch.empty(B, H, H, C, dtype=dtype, device=hip_device)
+    K.dwconv7(x.to(hip_device, dtype), w49, bias.to(hip_device), out)
+    assert _rel(out.cpu(), ref) < tol
+    # backward data: the transposed conv (flipped taps) of x, plus the residual
+    reft = F.conv_transpose2d(xin.permute(0, 3, 1, 2), w, padding=3, groups=C).permute(0, 2, 3, 1)
+    reft = reft + res.to(dtype).float()
+    dx = torch.empty(B, H, H, C, dtype=dtype, device=hip_device)
+    K.dwconv7_bwd_data(x.to(hip_device, dtype), w49, dx, res=res.to(hip_device, dtype))
+    assert _rel(dx.cpu(), reft) < tol
+
+
 @pytest.mark.parametrize("C,M", [(96, 700), (192, 300)])
 def test_cnblock_mlp_with_layernorm(hip_device, C, M):
     """LN (eps 1e-6) in the MLP prologue == LN kernel then MLP (z rounded to bf16 either way)."""
