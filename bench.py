@@ -53,6 +53,10 @@ def parse(argv=None):
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run encoder and decoder of a step back to back (no two-stream overlap)")
     ap.add_argument("--no-fp8", action="store_true", help="C5: frozen encoder GEMMs in bf16 instead of MX-FP8")
+    ap.add_argument("--lengths", choices=("full", "coco"), default="full",
+                    help="caption lengths of the synthetic batches: all 52 (default) or COCO-like")
+    ap.add_argument("--no-len-buckets", action="store_true",
+                    help="LSTM: always run L - 1 steps (no length buckets)")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the per-call roofline pass (profiling the replays alone); roofline is then null")
     ap.add_argument("--launch-selftest", action="store_true",
@@ -90,8 +94,11 @@ def spawn_ranks(n, argv):
     return rc
 
 
-def synthetic_batch(B, rank, step, device):
-    """U[0,1) images ImageNet-normalised; caps <start> w.. <end>, caplen 52."""
+def synthetic_batch(B, rank, step, device, lengths="full"):
+    """U[0,1) images ImageNet-normalised; caps <start> w.. <end>, caplen 52.
+    lengths="coco": caption lengths drawn like COCO's (about 10.5 +- 2.5 words + <start>/<end>,
+    clipped to [8, 52]; padded with 0 past the length, as dataLoader.py's encoded captions).
+    Returns (img, caps, caplens, max_caplen) -- the last known on the host."""
     g = torch.Generator(device="cpu").manual_seed(1234 + 7919 * rank + step)
     img = torch.rand(B, 3, 224, 224, generator=g)
     mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
@@ -99,9 +106,15 @@ def synthetic_batch(B, rank, step, device):
     img = (img - mean) / std
     caps = torch.randint(1, V - 3, (B, CAPLEN), generator=g)
     caps[:, 0] = V - 2
-    caps[:, CAPLEN - 1] = V - 1
-    caplens = torch.full((B, 1), CAPLEN, dtype=torch.int64)
-    return img.to(device), caps.to(device), caplens.to(device)
+    if lengths == "coco":
+        lens = (torch.randn(B, generator=g) * 2.5 + 12.5).round().clamp(8, CAPLEN).long()
+    else:
+        lens = torch.full((B,), CAPLEN, dtype=torch.int64)
+    for b in range(B):
+        caps[b, lens[b] - 1] = V - 1
+        caps[b, lens[b]:] = 0
+    caplens = lens.view(B, 1)
+    return img.to(device), caps.to(device), caplens.to(device), int(lens.max())
 
 
 def build(cfg, device):
@@ -187,7 +200,7 @@ def cpu_baseline(seconds):
     g = torch.Generator().manual_seed(0)
     p = {k: (torch.rand(s, generator=g) * 0.2 - 0.1) for k, s in shapes.lstm_decoder_shapes(E, 512, 512, 512, V).items()}
     state = {}
-    img, caps, caplens = synthetic_batch(B, 0, 0, "cpu")
+    img, caps, caplens, _ = synthetic_batch(B, 0, 0, "cpu")
     t_steps, n = 0.0, 0
     step = 0
     while True:
@@ -258,11 +271,11 @@ def main(argv=None):
     # streams in one graph); every timed step still does one encoder + one decoder pass
     pipeline = not args.no_pipeline and "starting_layer" not in cfg
     trainer = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm", graph=not args.no_graph,
-                                   pipeline=pipeline)
+                                   pipeline=pipeline, len_buckets=not args.no_len_buckets)
     B = cfg["batch"]
-    batches = [synthetic_batch(B, rank, i, device) for i in range(4)]
+    batches = [synthetic_batch(B, rank, i, device, args.lengths) for i in range(4)]
     for i in range(args.warmup):
-        trainer.step(*batches[i % 4])
+        trainer.step(*batches[i % 4][:3], max_caplen=batches[i % 4][3])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -270,7 +283,7 @@ def main(argv=None):
     progress = os.environ.get("IMGCAP_BENCH_PROGRESS") == "1"  # diagnostics: a synchronised mark per 10 steps
     t0 = time.perf_counter()
     for i in range(args.steps):
-        trainer.step(*batches[i % 4])
+        trainer.step(*batches[i % 4][:3], max_caplen=batches[i % 4][3])
         if progress and i % 10 == 9:
             torch.cuda.synchronize()
             print(f"[bench] step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
@@ -292,7 +305,7 @@ def main(argv=None):
         from imagecaptioningconvnext_amd import roofline
         if progress:
             print("[bench] roofline", file=sys.stderr, flush=True)
-        roof = None if args.no_roofline else roofline.measure(cfg, trainer, batches[0], cfgname=args.config)
+        roof = None if args.no_roofline else roofline.measure(cfg, trainer, batches[0][:3], cfgname=args.config)
         if progress:
             print("[bench] roofline done", file=sys.stderr, flush=True)
         out = {
@@ -310,7 +323,9 @@ def main(argv=None):
                                if fp8_fpi else ""),
             "pipeline": "encoder(batch i+1) || decoder fwd/bwd(batch i), two HIP streams in one graph"
                         if pipeline else "sequential",
-            "data": "synthetic (224x224x3 U[0,1) ImageNet-normalised, random captions len 52), random-init weights",
+            "data": "synthetic (224x224x3 U[0,1) ImageNet-normalised, random captions " +
+                    ("len 52" if args.lengths == "full" else "of COCO-like lengths (12.5 +- 2.5 tokens, <= 52)") +
+                    "), random-init weights",
             "config": {"workload": f"{args.config}: ConvNeXt-{cfg['encoder'].capitalize()} "
                                    f"({'fine-tuned from child %d' % cfg['starting_layer'] if 'starting_layer' in cfg else 'frozen'}) + "
                                    f"{'LSTM-attention' if cfg['decoder'] == 'lstm' else 'Transformer'} decoder, "

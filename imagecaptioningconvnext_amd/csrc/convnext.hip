@@ -4,6 +4,8 @@
 //   ln_patchify2  features[2,4,6] head: LayerNorm2d then 2x2/s2 patch rows for the MFMA GEMM
 //   adaptive_pool AdaptiveAvgPool2d (encoder.py:20,25)
 // The pointwise Linear pair / downsample conv run on imgcap_gemm (gemm.hip).
+#include <type_traits>
+
 #include "common.h"
 
 namespace imgcap {
@@ -457,6 +459,33 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_kernel(int B, int H, 
   }
 }
 
+// Row stride (16-byte slots) of the rolling kernel's image: pixel px at slot sppx*px + px/PW of
+// its row (one gap slot after every PW pixels), sppx = 16-byte slots per pixel (DW_CT channels
+// of the LDS element type); searched like dw_row_slots for conflict-free window reads.
+__host__ __device__ constexpr int dw_roll_row_slots(int W, int PW, int sppx) {
+  const int GW = W / PW;
+  const int base = sppx * (W + 6) + (W + 5) / PW + 1;
+  const int gstep = sppx * PW + 1;
+  int best = base, best_m = 1 << 30;
+  for (int rs = base; rs < base + 16; ++rs) {
+    int worst = 0;
+    for (int grp = 0; grp < 4; ++grp) {
+      int cnt[16] = {0};
+      for (int i = 0; i < 16; ++i) {
+        const int l = kDwGroups[grp][i];
+        const int c = ++cnt[((l / GW) * rs + (l % GW) * gstep) % 16];
+        worst = c > worst ? c : worst;
+      }
+    }
+    if (worst < best_m) {
+      best_m = worst;
+      best = rs;
+    }
+    if (worst == 1) break;
+  }
+  return best;
+}
+
 // ---------------------------------------------------------------------------------------
 // The same depthwise conv over NTL consecutive row tiles per block (compile-time width): the
 // block keeps a ring of 2*TR + 6 input rows in LDS, so the 6 halo rows are fetched once per
@@ -466,19 +495,22 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_kernel(int B, int H, 
 // input row i (counted from the block's first output row - 3) = i mod (2*TR + 6): tile k reads
 // rows [k*TR, k*TR + TR + 6), its prefetch lands in rows [k*TR + TR + 6, k*TR + 2*TR + 6),
 // the slots of rows k*TR - TR .. k*TR - 1 that tile k-1 finished with before the barrier.
-template <typename T, int PW, int WC, int NC, int NTL>
+template <typename T, int PW, int WC, int NC, int NTL, bool F32L>
 __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, int H, int C, const T* __restrict__ x,
                                                            const float* __restrict__ w,
                                                            const float* __restrict__ bias, T* __restrict__ y,
                                                            const T* res, int flip) {
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   static_assert(WC > 0 && NTL >= 1, "compile-time width");
+  // LDS element type: the input's, or fp32 (F32L: the bf16 -> fp32 unpack done once per staged
+  // element instead of once per window read, 7 kernel rows x 7 lanes later)
+  using LT = typename std::conditional<F32L, float, T>::type;
   constexpr int VE = 16 / sizeof(T);
   constexpr int NV = DW_CT / VE;
-  constexpr int SPP = DW_CT * 2 / 16;
+  constexpr int SPPX = DW_CT * (int)sizeof(LT) / 16;  // 16-byte slots per pixel
   constexpr int NT = 64 * DW_CT / NC;
   constexpr int W = WC, GW = W / PW, TR = 64 / GW, WP = W + 6;
-  constexpr int RS = dw_row_slots(WC, PW, (int)sizeof(T));
+  constexpr int RS = dw_roll_row_slots(WC, PW, SPPX);
   constexpr int RING = NTL > 1 ? 2 * TR + 6 : TR + 6;
   constexpr int PSTEP = NT / NV;                      // pixels per load instruction of the block
   constexpr int NPF = (TR * WP + PSTEP - 1) / PSTEP;  // loads per thread for TR new rows
@@ -486,7 +518,8 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, in
   const long rb = (long)blockIdx.x * (NTL * TR);      // the block's first output row
   const int cb = blockIdx.y * DW_CT;
   uint4* img = (uint4*)dsm;
-  auto slot = [&](int rr, int px, int s) { return rr * RS + (SPP * px + px / PW) * (NV / SPP) + s; };
+  auto slot = [&](int rr, int px, int s) { return rr * RS + SPPX * px + px / PW + s; };
+  constexpr int SPV = VE * (int)sizeof(LT) / 16;  // LDS slots per loaded 16-byte vector (1 or 2)
   const int v = threadIdx.x % NV;
   const int p0 = threadIdx.x / NV;
   const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(R * W * C * (long)sizeof(T)), 0x00020000);
@@ -509,7 +542,16 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, in
     for (int u = 0; u < NPF; ++u) {
       const int px = p0 + u * PSTEP;
       const int pr = px / WP;
-      if (pr < nrows) img[slot((i0 + pr) % RING, px % WP, v)] = val[u];
+      if (pr < nrows) {
+        uint4* d = img + slot((i0 + pr) % RING, px % WP, v * SPV);
+        if constexpr (SPV == 1) {
+          d[0] = val[u];
+        } else {  // 8 bf16 -> 8 fp32
+          const uint32_t q[4] = {val[u].x, val[u].y, val[u].z, val[u].w};
+          d[0] = make_uint4(q[0] << 16, q[0] & 0xFFFF0000u, q[1] << 16, q[1] & 0xFFFF0000u);
+          d[1] = make_uint4(q[2] << 16, q[2] & 0xFFFF0000u, q[3] << 16, q[3] & 0xFFFF0000u);
+        }
+      }
     }
   };
   {  // prologue: the TR + 6 rows of tile 0
@@ -526,7 +568,7 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, in
   const int lr = lane / GW, g = lane % GW;
   const int w0 = g * PW;
   constexpr int NP = NC / 2;
-  const int cofs = wv * NC * (int)sizeof(T);
+  const int cofs = wv * NC * (int)sizeof(LT);
   const char* imgb = (const char*)img;
   float bv[NC];
 #pragma unroll
@@ -560,7 +602,7 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, in
 #pragma unroll
         for (int q = 0; q < PW + 6; ++q) {
           float vv[NC];
-          ldc<T, NC>((const T*)(imgb + slot(rr, w0 + q, 0) * 16 + cofs), vv);
+          ldc<LT, NC>((const LT*)(imgb + slot(rr, w0 + q, 0) * 16 + cofs), vv);
 #pragma unroll
           for (int j = 0; j < NP; ++j) win[q][j] = f32x2{vv[2 * j], vv[2 * j + 1]};
         }
@@ -698,10 +740,10 @@ bool dw_narrow() {
 }
 // the rolling kernel's ring exceeds the default 64 KB of dynamic LDS: raise the limit once per
 // instantiation (first launch, before any capture)
-template <typename T, int P, int WC, int N>
+template <typename T, int P, int WC, int N, bool FL>
 void dw_roll_attr() {
   static const bool done = [] {
-    (void)hipFuncSetAttribute((const void*)dwconv7_roll_kernel<T, P, WC, 8, N>,
+    (void)hipFuncSetAttribute((const void*)dwconv7_roll_kernel<T, P, WC, 8, N, FL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
@@ -709,6 +751,11 @@ void dw_roll_attr() {
 }
 
 // IMGCAP_DW_NTL=k forces k row tiles per block of the rolling kernel (0: the one-tile kernel)
+// IMGCAP_DW_F32L=1: bf16 input staged as fp32 in LDS (read at every launch)
+bool dw_f32l() {
+  const char* e = getenv("IMGCAP_DW_F32L");
+  return e && *e == '1';
+}
 int dw_ntl_override() {  // read at every launch (tests switch it)
   const char* e = getenv("IMGCAP_DW_NTL");
   return e && *e ? atoi(e) : -1;
@@ -743,13 +790,24 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
   const int nc = dw_nc_override() ? dw_nc_override() : 8;
   // the rolling kernel (compile-time widths, 8 channels per lane, bf16 / fp32)
   const long tiles = (R + TR - 1) / TR;
-  const size_t shm_roll = (size_t)(2 * TR + 6) * RS * 16;
-  const int ntl = (nc == 8 && !narrow && shm_roll <= 160 * 1024) ? dw_pick_ntl(tiles, C / DW_CT, shm, shm_roll) : 0;
-#define DWR_(P, WC, N)                                                                                         \
-  dw_roll_attr<T, P, WC, N>();                                                                                 \
-  hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8, N>), dim3((unsigned)((tiles + N - 1) / N), C / DW_CT),  \
-                     dim3(256), N == 1 ? shm : shm_roll, st, B, H, C, (const T*)x, w, bias, (T*)y,             \
+  const bool f32l = sizeof(T) == 2 && dw_f32l();
+  const int sppx = DW_CT * (sizeof(T) == 4 || f32l ? 4 : 2) / 16;
+  const int rsr = dw_roll_row_slots(W, PW, sppx);
+  const size_t shm_r1 = (size_t)(TR + 6) * rsr * 16;
+  const size_t shm_roll = (size_t)(2 * TR + 6) * rsr * 16;
+  int ntl = (nc == 8 && !narrow) ? dw_pick_ntl(tiles, C / DW_CT, shm_r1, shm_roll) : 0;
+  if (ntl > 1 && shm_roll > 160 * 1024) ntl = 1;
+#define DWR1_(P, WC, N, FL)                                                                                   \
+  dw_roll_attr<T, P, WC, N, FL>();                                                                            \
+  hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8, N, FL>), dim3((unsigned)((tiles + N - 1) / N), C / DW_CT), \
+                     dim3(256), N == 1 ? shm_r1 : shm_roll, st, B, H, C, (const T*)x, w, bias, (T*)y,          \
                      (const T*)res, flip)
+#define DWR_(P, WC, N)          \
+  if (f32l) {                   \
+    DWR1_(P, WC, N, true);      \
+  } else {                      \
+    DWR1_(P, WC, N, false);     \
+  }
 #define DWR_ALL(P, WC)                 \
   do {                                 \
     switch (ntl) {                     \
@@ -775,6 +833,7 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
   }
 #undef DWR_ALL
 #undef DWR_
+#undef DWR1_
 #define DW_(P, WC)                                                                                              \
   do {                                                                                                         \
     if (nc == 4)                                                                                               \

@@ -191,8 +191,9 @@ class LstmEngine:
                 alphaC=1.0):
         """Runs decoder.py:69-113 (+ the train.py:265-269 loss when ``loss``).
 
-        fixed_T: run T = L-1 steps without reading decode lengths on the host (no sync; rows are
-        masked on device).  Otherwise T = max(decode_lengths) exactly as the reference.
+        fixed_T: run T = L-1 steps (True) or the given number of steps (an int >= every decode
+        length: the trainer's length buckets) without reading decode lengths on the host (no sync;
+        rows are masked on device).  Otherwise T = max(decode_lengths) exactly as the reference.
         Returns a dict of saved buffers (``s``) used by backward()."""
         ct, dev = self.ct, encoder_out.device
         A, E, D, M, V, W3 = self.A, self.E, self.D, self.M, self.V, self.W3
@@ -214,7 +215,9 @@ class LstmEngine:
             caps_s = encoded_captions.index_select(0, sort_ind)
             dl = (lens - 1).to(torch.int32)
         if fixed_T:
-            T = L - 1
+            # True: T = L - 1; an int: that many steps (a length bucket >= every decode length of
+            # the batch -- the rows past a caption's length are masked either way)
+            T = L - 1 if fixed_T is True else max(1, min(int(fixed_T), L - 1))
             dls = None
         else:
             dls = dl.tolist()  # decoder.py:91 (host list, part of the reference API)

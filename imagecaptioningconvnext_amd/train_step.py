@@ -59,7 +59,7 @@ class _SeqGraphs:
 
 class TeacherForcedTrainer:
     def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, encoder_lr=1e-4, grad_clip=5.0, alphaC=1.0,
-                 pad_id=0, process_group=None, graph=False, pipeline=False):
+                 pad_id=0, process_group=None, graph=False, pipeline=False, len_buckets=True):
         self.encoder = encoder
         self.decoder = decoder
         self.lstm = lstm
@@ -72,6 +72,15 @@ class TeacherForcedTrainer:
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.eng = decoder.engine()
         self._metric_log = []
+        # LSTM length buckets (decoder.py:91,100-111: steps t >= a caption's decode length do no
+        # work): a batch whose longest caption is known on the host (CPU caplens, or step()'s
+        # max_caplen) runs T = the next multiple of 8 >= its longest decode length instead of
+        # L - 1 -- the vocab projection, CE, dlogits, weight-gradient GEMMs and every per-step
+        # buffer shrink with it.  One captured graph set per bucket; None = L - 1.
+        self.len_buckets = bool(len_buckets) and lstm
+        self._cur_T = None
+        self._seq_T = None
+        self._seq_store = {}
         self.graph = graph
         self._graph = None
         # pipeline: the frozen encoder's forward of batch i runs on a second stream beside the
@@ -122,9 +131,37 @@ class TeacherForcedTrainer:
             self._bucket = (0, self.eng.fp.grad.numel())
         self._graph = None
         self._pipe = None
+        self._seq_store = {}
+        self._seq_T = None
         rel = getattr(self.encoder, "release_retired", None)
         if rel is not None:  # the graphs that pointed into superseded weight packs are gone
             rel()
+
+    _SEQ_FIELDS = ("_graph", "_inputs", "_metrics", "_feat_slot", "_enc_saved", "_feat_meta", "_seed_ctr")
+
+    def bucket_T(self, caps, caplens, max_caplen=None):
+        """Steps the LSTM runs for this batch: the next multiple of 8 >= its longest decode length
+        (caplen - 1), or None (= L - 1) when that is not known on the host or length buckets are off."""
+        if not self.len_buckets:
+            return None
+        if max_caplen is None:
+            if caplens.device.type != "cpu":
+                return None
+            max_caplen = int(caplens.max())
+        L = caps.size(1)
+        T = max(8, (int(max_caplen) - 1 + 7) // 8 * 8)
+        return None if T >= L - 1 else T
+
+    def _select_seq(self, T):
+        """Make bucket T's captured sequential step (graph, static inputs, metrics) current."""
+        if T == self._seq_T:
+            return
+        self._seq_store[self._seq_T] = {f: getattr(self, f, None) for f in self._SEQ_FIELDS}
+        for f, v in self._seq_store.get(T, {f: None for f in self._SEQ_FIELDS}).items():
+            setattr(self, f, v)
+        if self._seed_ctr is not None:  # that bucket's graphs advance their own counter
+            K.set_seed_counter(self._seed_ctr)
+        self._seq_T = T
 
     def _encode(self, imgs):
         self.encoder.train()
@@ -147,7 +184,7 @@ class TeacherForcedTrainer:
     def _dec(self, feats, caps, caplens, es=None, mid=None):
         self.decoder.train()
         if self.lstm:
-            s = self.eng.forward(feats, caps, caplens, fixed_T=True, alphaC=self.alphaC)
+            s = self.eng.forward(feats, caps, caplens, fixed_T=self._cur_T if self._cur_T else True, alphaC=self.alphaC)
         else:
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
         if mid is not None:
@@ -261,27 +298,40 @@ class TeacherForcedTrainer:
         self._graph = _SeqGraphs(ge, gd)
 
     # ---- encoder / decoder pipeline ------------------------------------------------------------
-    def _pipe_capture(self, imgs, caps, caplens, warmup=2):
+    def _pipe_buffers(self, imgs, caps, caplens):
+        """Static inputs of the pipelined schedule, shared by every length bucket's graphs: the
+        image batch being encoded, two caption / length slots and (on the first capture) two
+        feature slots; one device seed counter."""
         dev = imgs.device
         self._seed_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         K.set_seed_counter(self._seed_ctr)
-        side = torch.cuda.Stream(device=dev)
+        self._pipe = dict(side=torch.cuda.Stream(device=dev), i=0, img=imgs.clone(),
+                          caps=[caps.clone(), caps.clone()], lens=[caplens.clone(), caplens.clone()],
+                          T=[None, None], feats=None, sets={})
+
+    def _pipe_capture(self, T, warmup=2):
+        """Graphs of the pipelined step that decode a batch of length bucket T (slot parity k:
+        encode the new batch into slot k, train on slot 1 - k)."""
+        P = self._pipe
+        dev = P["img"].device
+        side = P["side"]
         main = torch.cuda.current_stream(dev)
-        P = dict(side=side, i=0, img=imgs.clone(), caps=[caps.clone(), caps.clone()],
-                 lens=[caplens.clone(), caplens.clone()])
+        self._cur_T = T
         side.wait_stream(main)
         with torch.cuda.stream(side):  # first-touch allocations and one-time kernel setup
             for _ in range(warmup):
                 f = self._encode(P["img"])
                 self._dec(f, P["caps"][0], P["lens"][0])
         main.wait_stream(side)
-        P["feats"] = [torch.empty_like(f), torch.empty_like(f)]
-        P["graphs"], P["metrics"] = [], []
+        if P["feats"] is None:
+            P["feats"] = [torch.empty_like(f), torch.empty_like(f)]
+        S = dict(graphs=[], metrics=[])
+        P["sets"][T] = S
         if PIPE_SPLIT:
             # one graph per branch and slot, replayed on their own streams (under rocprofv3 the
             # second branch of a two-branch graph starts late; unprofiled the single graph is as
             # fast or faster, see PIPE_SPLIT).  Separate memory pools: the two run concurrently.
-            P["genc"], P["gdec"] = [], []
+            S["genc"], S["gdec"] = [], []
             pool_e = pool_d = None
             for k in (0, 1):  # encode the new batch into slot k / train on slot 1-k
                 ge = torch.cuda.CUDAGraph()
@@ -295,10 +345,9 @@ class TeacherForcedTrainer:
                 with torch.cuda.graph(gd, pool=pool_d):
                     m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k])
                 pool_d = gd.pool()
-                P["genc"].append(ge)
-                P["gdec"].append(gd)
-                P["metrics"].append(m)
-            self._pipe = P
+                S["genc"].append(ge)
+                S["gdec"].append(gd)
+                S["metrics"].append(m)
             return
         pool = None
         for k in (0, 1):  # graph k: encode the new batch into slot k, train on slot 1-k
@@ -331,12 +380,12 @@ class TeacherForcedTrainer:
                     g.capture_end()
             main.wait_stream(cap)
             pool = g[0].pool() if split else g.pool()
-            P["graphs"].append(g)
-            P["metrics"].append(m)
-        self._pipe = P
+            S["graphs"].append(g)
+            S["metrics"].append(m)
 
-    def _pipe_step(self, imgs, caps, caplens):
-        """Returns the metrics tensor of the previous batch (None on the first call)."""
+    def _pipe_step(self, imgs, caps, caplens, T=None):
+        """Returns the metrics tensor of the previous batch (None on the first call).  T: this
+        batch's length bucket (decoded on the next call)."""
         if not self.graph:
             main = torch.cuda.current_stream()
             if self._pipe is None:
@@ -346,14 +395,17 @@ class TeacherForcedTrainer:
             with torch.cuda.stream(P["side"]):
                 feats = self._encode(imgs)
             self._hook_mode = "eager"
-            m = self._dec(*P["pending"]) if P["pending"] is not None else None
+            m = None
+            if P["pending"] is not None:
+                self._cur_T = P["pending"][3]
+                m = self._dec(*P["pending"][:3])
             self._hook_mode = None
             main.wait_stream(P["side"])
             feats.record_stream(main)
-            P["pending"] = (feats, caps, caplens)
+            P["pending"] = (feats, caps, caplens, T)
             return m
         if self._pipe is None:
-            self._pipe_capture(imgs, caps, caplens)
+            self._pipe_buffers(imgs, caps, caplens)
         P = self._pipe
         k = P["i"] % 2
         if any(d.shape != s_.shape or d.dtype != s_.dtype for d, s_ in ((P["img"], imgs), (P["caps"][k], caps),
@@ -361,24 +413,32 @@ class TeacherForcedTrainer:
             # a batch of another shape (the last, partial batch of an epoch): finish the batch in
             # flight, then this one with eager launches, sequentially
             self.flush()
+            self._cur_T = T
             return self._eager(imgs, caps, caplens)
+        m = None
+        if P["i"] > 0 and P["T"][1 - k] not in P["sets"]:
+            self._pipe_capture(P["T"][1 - k])  # first batch of this length bucket to be decoded
         for dst, src in ((P["img"], imgs), (P["caps"][k], caps), (P["lens"][k], caplens)):
             dst.copy_(src, non_blocking=True)
-        m = None
         if P["i"] == 0:
-            P["feats"][k].copy_(self._encode(P["img"]))
-        elif "genc" in P:
-            main = torch.cuda.current_stream()
-            self._seed_ctr.add_(1)  # before both branches read it (masks drawn at kernel run time)
-            P["side"].wait_stream(main)
-            P["gdec"][k].replay()
-            with torch.cuda.stream(P["side"]):
-                P["genc"][k].replay()
-            main.wait_stream(P["side"])
-            m = P["metrics"][k]
+            f = self._encode(P["img"])
+            if P["feats"] is None:
+                P["feats"] = [torch.empty_like(f), torch.empty_like(f)]
+            P["feats"][k].copy_(f)
         else:
-            self._replay(P["graphs"][k])
-            m = P["metrics"][k]
+            S = P["sets"][P["T"][1 - k]]
+            if "genc" in S:
+                main = torch.cuda.current_stream()
+                self._seed_ctr.add_(1)  # before both branches read it (masks drawn at kernel run time)
+                P["side"].wait_stream(main)
+                S["gdec"][k].replay()
+                with torch.cuda.stream(P["side"]):
+                    S["genc"][k].replay()
+                main.wait_stream(P["side"])
+            else:
+                self._replay(S["graphs"][k])
+            m = S["metrics"][k]
+        P["T"][k] = T
         P["i"] += 1
         return m
 
@@ -392,25 +452,32 @@ class TeacherForcedTrainer:
             if P["pending"] is None:
                 self._hook_mode = None
                 return None
-            m = self._dec(*P["pending"])
+            self._cur_T = P["pending"][3]
+            m = self._dec(*P["pending"][:3])
             P["pending"] = None
         else:
             if P["i"] == 0:
                 self._hook_mode = None
                 return None
             j = (P["i"] - 1) % 2
+            self._cur_T = P["T"][j]
             m = self._dec(P["feats"][j], P["caps"][j], P["lens"][j])
             P["i"] = 0
         self._hook_mode = None
         return self._update(m)
 
-    def step(self, imgs, caps, caplens):
+    def step(self, imgs, caps, caplens, max_caplen=None):
+        """One train step on a batch.  ``max_caplen``: the batch's longest caption length when
+        the caller knows it on the host (else read from CPU caplens, else L is assumed)."""
+        T = self.bucket_T(caps, caplens, max_caplen)
         if self.pipeline and self.enc_eng is None:
-            m = self._pipe_step(imgs, caps, caplens)
+            m = self._pipe_step(imgs, caps, caplens, T)
             return None if m is None else self._update(m)
+        self._cur_T = T
         if not self.graph:
             m = self._eager(imgs, caps, caplens)
         else:
+            self._select_seq(T)
             if self._graph is None:
                 self._capture(imgs, caps, caplens)
             if any(d.shape != s_.shape or d.dtype != s_.dtype for d, s_ in zip(self._inputs, (imgs, caps, caplens))):

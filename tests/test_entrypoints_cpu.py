@@ -64,7 +64,7 @@ class _FakeTrainer:
     def enable_encoder_finetune(self, startingLayer):
         self.enc_eng = object()
 
-    def step(self, *a):
+    def step(self, *a, **k):
         pass
 
     def flush(self):

@@ -267,3 +267,41 @@ def test_captured_step_graphs_hold_only_kernel_nodes(hip_device, monkeypatch, de
         kind = [n.split("] ", 1)[1].split()[0] for n in nodes]
         assert set(kind) <= {"kernel", "memcpy"}, [n for n, k in zip(nodes, kind) if k not in ("kernel", "memcpy")]
         assert kind.count("memcpy") <= 1, [n for n, k in zip(nodes, kind) if k == "memcpy"]
+
+
+def _len_batch(dev, i, lens, L=40, V=120, hw=64):
+    g = torch.Generator().manual_seed(300 + i)
+    B = len(lens)
+    img = torch.randn(B, 3, hw, hw, generator=g)
+    caps = torch.randint(1, V - 2, (B, L), generator=g)
+    caps[:, 0] = V - 2
+    for b, n in enumerate(lens):
+        caps[b, n - 1] = V - 1
+        caps[b, n:] = 0
+    return img.to(dev), caps.to(dev), torch.tensor(lens).view(B, 1).to(dev), max(lens)
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_lstm_length_buckets_match_full_steps(hip_device, pipeline):
+    """decoder.py:91,100-111: the trainer's length buckets (T = next multiple of 8 >= the longest
+    decode length, host-known max caplen) train exactly what L - 1 steps train: the rows past a
+    caption's length are masked either way.  Buckets 24, 8, 32, 24 (the last replays the first's
+    graph), graphs + pipeline vs the same trainer without buckets."""
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    seqs = [[20, 15, 11, 7], [9, 8, 7, 6], [33, 20, 10, 5], [18, 18, 3, 3], [21, 2, 2, 2]]
+    out = []
+    for buckets in (False, True):
+        enc, dec = _models(hip_device, "lstm", 0.0, True)
+        tr = TeacherForcedTrainer(enc, dec, lstm=True, graph=True, pipeline=pipeline, len_buckets=buckets)
+        for i, lens in enumerate(seqs):
+            img, caps, caplens, mx = _len_batch(hip_device, i, lens)
+            assert tr.bucket_T(caps, caplens, mx) == ((mx - 1 + 7) // 8 * 8 if buckets else None)
+            tr.step(img, caps, caplens, max_caplen=mx)
+        tr.flush()
+        torch.cuda.synchronize()
+        out.append((tr.eng.fp.flat.detach().cpu().clone(), tr.drain_metrics()))
+    (p0, m0), (p1, m1) = out
+    assert len(m0) == len(m1) == len(seqs)
+    for a, b in zip(m0, m1):
+        assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]) and a[1] == b[1] and abs(a[2] - b[2]) < 1e-6
+    assert ((p0 - p1).norm() / p0.norm()).item() < 2e-5  # Adam sign flips at round-off-level grads

@@ -18,7 +18,7 @@ cfg = bench.CONFIGS[cfgname]
 dev = torch.device("cuda:0")
 enc, dec = bench.build(cfg, dev)
 tr = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm", graph=False)
-batch = bench.synthetic_batch(cfg["batch"], 0, 0, dev)
+batch = bench.synthetic_batch(cfg["batch"], 0, 0, dev)[:3]
 tr.step(*batch)
 rec = []
 K.record_gemms(rec)

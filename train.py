@@ -127,8 +127,10 @@ def data_loader(args, device, epoch, rank=0, world=1):
     for i, (imgs, caps, caplens) in enumerate(dl):
         if args.steps and i >= args.steps:
             break
+        # the batch's longest caption, read on the host before the copy: the trainer's LSTM
+        # length bucket (TeacherForcedTrainer.bucket_T) without a device sync
         yield (imgs.to(device, non_blocking=True), caps.to(device, non_blocking=True),
-               caplens.to(device, non_blocking=True))
+               caplens.to(device, non_blocking=True), int(caplens.max()))
 
 
 def build_models(args, device):
@@ -166,11 +168,11 @@ def trainWithTeacherForcing(trainDataLoader, encoder, decoder, trainer, epoch, l
     batchTime, dataTime, losses, top5accs = AverageMeter(), AverageMeter(), AverageMeter(), AverageMeter()
     start = time.time()
     n = 0
-    for i, (imgs, caps, caplens) in enumerate(trainDataLoader):
+    for i, (imgs, caps, caplens, *host) in enumerate(trainDataLoader):
         dataTime.update(time.time() - start)
         if i % 100 == 0:
             log(f"TF, Epoch {epoch}, Batch {i + 1}", flush=True)
-        trainer.step(imgs, caps, caplens)
+        trainer.step(imgs, caps, caplens, max_caplen=host[0] if host else None)
         n += 1
         batchTime.update(time.time() - start)
         start = time.time()
