@@ -22,3 +22,22 @@ def test_library_loads_and_exports_all():
     for name in _declared():
         assert hasattr(L, name), name
     assert L.imgcap_version() == 1
+
+
+def _declared_arity():
+    """name -> parameter count of every prototype in the header (comments stripped; `void` = 0)."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:int|const char\*)\s+(imgcap_\w+)\s*\(([^)]*)\)\s*;", src, re.M):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_binding_arity_matches_header():
+    """ctypes argtypes of every entry point have the header's parameter count (a missing or extra
+    argument would shift every later one at the call)."""
+    ar = _declared_arity()
+    assert set(ar) == set(_abi.exported_symbols())
+    bad = {n: (ar[n], len(_abi._SIGS[n])) for n in _abi._SIGS if ar[n] != len(_abi._SIGS[n])}
+    assert not bad, bad
