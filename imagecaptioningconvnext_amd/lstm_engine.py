@@ -111,6 +111,9 @@ class LstmEngine:
         words = [self._sync] if self._sync is not None else []
         if self.CHAINS > 1:
             words += list(self._chain_sync)
+        if init and len(words) == 1:
+            dst.copy_(words[0][0:1])  # one launch instead of zero + add
+            return
         if init:
             dst.zero_()
         for w in words:
@@ -234,8 +237,17 @@ class LstmEngine:
         if mean is None:
             mean = torch.empty(B, E, **ctd)
             K.mean_mid(enc_s, mean)                                           # decoder.py:64
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev)
+        # att1 = enc W_ea (decoder.py:61, hoisted out of the loop) on the side stream, beside the
+        # init_h / init_c and W_ih-embedding products (no library scratch: 64x64 tile, one pass)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            att1 = K.gemm(enc_s.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])
+            ev_att1 = torch.cuda.Event()
+            ev_att1.record(side)
+        att1.record_stream(main)
         h0c0 = K.gemm(mean, w["init"], trans_b=True, bias=w["binit"], out_dtype=torch.float32)  # :100-101
-        att1 = K.gemm(enc_s.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])             # :61 hoisted
         xe = K.gemm(emb, w["wih"][:, :M], trans_b=True, bias=w["bih"], out_dtype=torch.float32)  # W_ih emb half
         hprev = torch.empty(B, T, D, **ctd)
         hprev[:, 0].copy_(h0c0[:, :D])
@@ -257,9 +269,6 @@ class LstmEngine:
         self._sync_words(d, dev)
         # k-major copies of the weights the backward recurrence multiplies by, made on a side
         # stream under the forward recurrence (they only depend on the weights)
-        main = torch.cuda.current_stream(dev)
-        side = self._side_stream(dev)
-        side.wait_stream(main)
         with torch.cuda.stream(side):
             wzh_t = torch.empty(E + D, 4 * D, **ctd)                  # [W_ih[:, M:] | W_hh]^T
             K.transpose(w["wih"][:, M:], out=wzh_t[:E])
@@ -271,6 +280,7 @@ class LstmEngine:
             if loss:
                 targets = torch.where(tmask, caps_s[:, 1:T + 1],
                                       torch.full_like(caps_s[:, 1:T + 1], -1)).reshape(-1)
+        main.wait_event(ev_att1)
         self._launch("imgcap_lstm_tf_fwd", d)
         main.wait_stream(side)
         for t_ in (wzh_t, watt_t, tmask) + ((targets,) if loss else ()):
@@ -295,9 +305,17 @@ class LstmEngine:
             dalpha = torch.empty(B, T, P, **f32)
             reg = torch.empty(1, **f32)
 
-            def finalize():
+            # the attention regulariser (train.py:268: its value and d alpha, which the backward
+            # recurrence reads) on the side stream, beside the vocab projection and the CE
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
                 _abi.call("imgcap_attn_reg", B, T, P, alphas.data_ptr(), dl.data_ptr(), alphaC, dalpha.data_ptr(),
                           reg.data_ptr(), K.stream())
+                ev_reg = torch.cuda.Event()
+                ev_reg.record(side)
+
+            def finalize():
+                main.wait_event(ev_reg)
                 K.loss_finalize(lrow, hit, targets, reg, metrics)
             K.ce_train(logits, targets, V, metrics, lse, lrow, hit, dlogits, finalize)
             self._fold_status(metrics[4:5], init=True)  # the forward recurrence's error word
@@ -433,6 +451,8 @@ class LstmEngine:
             cbs = K.ColsumBatch()
             cbs.add(dlogits, _G.g("fc.bias"), cols=V)
             cbs.run()
+            ev_fc = torch.cuda.Event()  # gbuf cleared, fc dW / db written
+            ev_fc.record(side)
         f32 = dict(device=dev, dtype=torch.float32)
         dcat = torch.empty(B, T, W3, device=dev, dtype=ct)
         xs, ys = self.X_SLICES, self.Y_SLICES
@@ -468,10 +488,24 @@ class LstmEngine:
         bufs["chain_ws"] = chain_ws
         s["bwd_bufs"] = bufs  # the descriptor points into these: keep them alive as long as `s`
         self._launch("imgcap_lstm_tf_bwd", d, chain_ws)
-        if "metrics" in s:
-            self._fold_status(s["metrics"][4:5])  # the backward recurrence's error word
         dc2 = dcat.view(BT, W3)
         dgates = dc2[:, A + E:]
+        # one rank, bf16, no encoder gradient: the embedding gradient (d_emb = dgates W_ih[:, :M],
+        # then the rank / scatter / segmented row sums) runs on the side stream beside the grouped
+        # weight-gradient GEMMs and the bias column sums (it is the only library-scratch user of
+        # the two branches: the grouped GEMMs and colsum_multi take none).  With DDP the early
+        # bucket's all-reduce takes that window instead (the hook after the embedding gradient).
+        par_tail = bucket_hook is None and not want_denc and ct == torch.bfloat16
+        if par_tail:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                if "metrics" in s:
+                    self._fold_status(s["metrics"][4:5])  # the backward recurrence's error word
+                demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
+                K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
+            main.wait_event(ev_fc)
+        elif "metrics" in s:
+            self._fold_status(s["metrics"][4:5])
         # W_hcat / b_hcat grads (batched over all B*T rows)
         wgb.add(dc2, s["hprev"].view(BT, D), out=_G.g("attention.decoder_att.weight", (W3, D), W3 * D), trans_a=True)
         cb.add(dc2, _G.g("attention.decoder_att.bias", (W3,), W3))
@@ -480,10 +514,11 @@ class LstmEngine:
         wgb.add(dgates, s["emb"], out=gwih[:, :M], M=4 * D, trans_a=True)
         wgb.add(dgates, s["zs"].view(BT, E), out=gwih[:, M:], M=4 * D, trans_a=True)
         cb.add(dgates, _G.g("decode_step.bias_ih"))
-        # embedding: d_emb = dgates W_ih[:, :M]  -> scatter-add rows
-        demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
-        torch.cuda.current_stream(dev).wait_stream(side)  # gbuf cleared, fc dW / db (beside the recurrence) done
-        K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
+        if not par_tail:
+            # embedding: d_emb = dgates W_ih[:, :M]  -> scatter-add rows
+            demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
+            main.wait_stream(side)  # gbuf cleared, fc dW / db (beside the recurrence) done
+            K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
         # init_h / init_c from dh0, dc0
         dinit = torch.cat([dh, dc], dim=1).to(ct)
         wgb.add(dinit, s["mean"], out=_G.g("init_h.weight", (2 * D, E), 2 * D * E), trans_a=True)
@@ -497,6 +532,8 @@ class LstmEngine:
             bucket_hook()
         wgb.run()
         cb.run()
+        if par_tail:
+            main.wait_stream(side)  # the embedding gradient and the metrics' error word
         s["denc"] = None
         if want_denc:
             # decoder.py:26 (att1 = enc W_ea), :64-66 (mean -> init_h/c), :102-103 (context)
