@@ -322,6 +322,12 @@ int imgcap_ce_fused(int dtype, int n, int V, const void* logits, int64_t ld, con
 int imgcap_clamp_adam(int64_t n, float* param, const float* grad, float* m, float* v,
                       void* shadow_bf16, float lr, float beta1, float beta2, float eps,
                       int step, float clip, float grad_div, void* stream);
+/* The same with the step's scalars in device memory: scal[0] = (float)(lr / (1 - beta1^t)),
+ * scal[1] = (float)sqrt(1 - beta2^t) (beta1/beta2 as floats promoted to double, as above) -- a
+ * captured graph then carries the update of each replay's step. */
+int imgcap_clamp_adam_dev(int64_t n, float* param, const float* grad, float* m, float* v,
+                          void* shadow_bf16, float beta1, float beta2, float eps, const float* scal,
+                          float clip, float grad_div, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * LSTM + soft-attention decoder, teacher forced (decoder.py:69-113, Attention 25-31,
