@@ -771,9 +771,122 @@ int dw_pick_ntl(long, int, size_t, size_t) {
   return 1;
 }
 
+// ---------------------------------------------------------------------------------------
+// Depthwise 7x7 for the narrow late stages (W = 14 / 7: stages 3-4), bf16, C % 128 == 0: lane =
+// (channel pair, output image row), block = one output row x all C channels (wave g: channels
+// 128g .. 128g + 127).  The channel-tiled kernels above stage a patch in LDS and give each lane
+// 7 pixels x 8 channels; at these widths their grids are < 1 wave per SIMD and every window value
+// is re-unpacked per kernel row (≈ 1.1 VALU per MAC).  Here a lane keeps its channel pair's 49
+// weight pairs in registers for the whole row, reads each of the 7 input rows once as coalesced
+// 4-byte bf16 pairs (64 lanes = 256 contiguous bytes, the next row requested before the current
+// one is used), unpacks it once and applies all 7 taps of that kernel row with packed FMAs
+// (≈ 0.7 VALU per MAC), and the grid is B*H rows x C/128 waves.  flip / res: the backward data gradient (taps mirrored, residual added), as dwconv7_kernel.
+template <int W>
+__global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf16* __restrict__ x,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         bf16* __restrict__ y, const bf16* __restrict__ res, int flip) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long r = blockIdx.x;  // b * H + h
+  const int h = (int)(r % H);
+  const long b = r / H;
+  const int c = wv * 128 + 2 * lane;
+  // the 7 weight pairs of kernel row kh (requested with that row's input, one row ahead)
+  // buffer loads: per-lane byte offset in a VGPR, the wave-uniform pixel / tap offset in an SGPR
+  // (64-bit addresses per load cost two VGPRs each and spilled); rows outside the image read 0
+  // through the descriptor's range check
+  const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, 49 * C * 4, 0x00020000);
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)((b + 1) * H * W * (long)C * 2), 0x00020000);
+  f32x2 wb[2][7];
+  auto load_w = [&](int kh, f32x2 (&dst)[7]) {
+#pragma unroll
+    for (int kw = 0; kw < 7; ++kw) {
+      const int t = kh * 7 + kw;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(wr, c * 4, (flip ? 48 - t : t) * C * 4, 0);
+      dst[kw] = __builtin_bit_cast(f32x2, v);
+    }
+  };
+  f32x2 acc[W];
+  {
+    const f32x2 bb = bias ? *(const f32x2*)(bias + c) : f32x2{0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < W; ++p) acc[p] = bb;
+  }
+  uint32_t rb[2][W];
+  auto load_row = [&](int kh, uint32_t (&dst)[W]) {
+    const int ih = h + kh - 3;
+    const bool ok = ih >= 0 && ih < H;
+    const uint32_t vo = ok ? (uint32_t)(((b * H + ih) * W * (long)C + c) * 2) : 0x80000000u;
+#pragma unroll
+    for (int iw = 0; iw < W; ++iw) dst[iw] = __builtin_amdgcn_raw_buffer_load_b32(xr, vo, iw * C * 2, 0);
+  };
+  load_row(0, rb[0]);
+  load_w(0, wb[0]);
+#pragma unroll
+  for (int kh = 0; kh < 7; ++kh) {
+    asm volatile("" ::: "memory");  // one row of loads ahead, no further (registers)
+    if (kh < 6) {
+      load_row(kh + 1, rb[(kh + 1) & 1]);
+      load_w(kh + 1, wb[(kh + 1) & 1]);
+    }
+    f32x2 xin[W];
+#pragma unroll
+    for (int iw = 0; iw < W; ++iw) {
+      const uint32_t v = rb[kh & 1][iw];
+      xin[iw] = f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
+    }
+#pragma unroll
+    for (int kw = 0; kw < 7; ++kw)
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        const int q = p + kw - 3;
+        if (q >= 0 && q < W) acc[p] = xin[q] * wb[kh & 1][kw] + acc[p];
+      }
+  }
+  bf16* out = y + r * W * (long)C + c;
+  {
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      f32x2 o = acc[p];
+      if (res) {
+        const uint32_t v = *(const uint32_t*)(res + r * W * (long)C + c + (long)p * C);
+        o += f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
+      }
+      *(bf16x2*)(out + (long)p * C) = bf16x2{(bf16)o[0], (bf16)o[1]};
+    }
+  }
+}
+
+bool dw_cp_enabled() {  // IMGCAP_DW_CP=0: the channel-tiled kernels at W = 14 / 7 too (A/B)
+  const char* e = getenv("IMGCAP_DW_CP");
+  return !(e && *e == '0');
+}
+// Measured (tools/dw_ln_bench.py, us, vs the channel-tiled kernel): Tiny stage 3 B32 9.2 vs 12.2,
+// B64 15.7 vs 17.2; Base stage 3 B32 10.6 vs 13.1; Tiny stage 4 B64 10.3 vs 12.6; Base stage 4 B32
+// 9.5 vs 12.5; Large stage 3 B64 (W 14, C 768) 33.2 vs 30.6 -- so W = 14 only up to C = 512.  A
+// LayerNorm epilogue (per-pixel wave sums + the block's waves through LDS) measured 1.1-2.4x
+// slower than this kernel + add_layernorm and was dropped.
+bool dw_cp_fits(int W, int C) {
+  return dw_cp_enabled() && (W == 7 || (W == 14 && C <= 512)) && C % 128 == 0 && C <= 1024;
+}
+
+int dwconv7_cp_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
+                      const void* res, int flip, hipStream_t st) {
+  const dim3 grid((unsigned)((long)B * H)), block((unsigned)(C / 128 * 64));
+  if (W == 14)
+    hipLaunchKernelGGL((dwconv7_cp_kernel<14>), grid, block, 0, st, H, C, (const bf16*)x, w, bias, (bf16*)y,
+                       (const bf16*)res, flip);
+  else
+    hipLaunchKernelGGL((dwconv7_cp_kernel<7>), grid, block, 0, st, H, C, (const bf16*)x, w, bias, (bf16*)y,
+                       (const bf16*)res, flip);
+  IMGCAP_CHECK_LAUNCH("imgcap_dwconv7 (channel pairs)");
+  return 0;
+}
+
 template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
                    hipStream_t st, const void* res = nullptr, int flip = 0) {
+  if (sizeof(T) == 2 && dw_cp_fits(W, C))
+    return dwconv7_cp_launch(B, H, W, C, x, w, bias, y, res, flip, st);
   // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups.
   // Narrow mode (dw_narrow): the 28 / 14 / 7-wide stages with 4 / 2 / 1 pixels per lane -- 7
   // lanes per image row, so 2-4x the lanes and blocks of the late stages' small grids
