@@ -781,9 +781,10 @@ int dw_pick_ntl(long, int, size_t, size_t) {
 // 4-byte bf16 pairs (64 lanes = 256 contiguous bytes, the next row requested before the current
 // one is used), unpacks it once and applies all 7 taps of that kernel row with packed FMAs
 // (≈ 0.7 VALU per MAC), and the grid is B*H rows x C/128 waves.  flip / res: the backward data gradient (taps mirrored, residual added), as dwconv7_kernel.
-template <int W>
+template <int W, bool LN>
 __global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf16* __restrict__ x,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
+                                                         const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                          bf16* __restrict__ y, const bf16* __restrict__ res, int flip) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long r = blockIdx.x;  // b * H + h
@@ -843,7 +844,48 @@ __global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf1
       }
   }
   bf16* out = y + r * W * (long)C + c;
-  {
+  if constexpr (LN) {
+    // LayerNorm over C of each output pixel (eps 1e-6), two passes, fixed order: the lanes'
+    // partials go to LDS [wave][pixel][lane]; wave g reduces pixels g, g + nwv, .. (its lanes sum
+    // the waves' partials of one lane column, then a wave sum), the block reads the results back
+    __shared__ float part[8][W][64];
+    __shared__ float stat[2][W];
+    const int nwv = blockDim.x >> 6;
+    float mean[W];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int p = 0; p < W; ++p) {
+        float v;
+        if (pass == 0) {
+          v = acc[p][0] + acc[p][1];
+        } else {
+          const float d0 = acc[p][0] - mean[p], d1 = acc[p][1] - mean[p];
+          v = d0 * d0 + d1 * d1;
+        }
+        part[wv][p][lane] = v;
+      }
+      __syncthreads();
+      for (int p = wv; p < W; p += nwv) {
+        float v = 0.f;
+        for (int g = 0; g < nwv; ++g) v += part[g][p][lane];
+        v = wave_sum(v);
+        if (lane == 0) stat[pass][p] = v / C;
+      }
+      __syncthreads();
+      if (pass == 0) {
+#pragma unroll
+        for (int p = 0; p < W; ++p) mean[p] = stat[0][p];
+      }
+    }
+    const f32x2 g2 = *(const f32x2*)(lnw + c), b2 = *(const f32x2*)(lnb + c);
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      const float rstd = rsqrtf(stat[1][p] + 1e-6f);
+      *(bf16x2*)(out + (long)p * C) = bf16x2{(bf16)((acc[p][0] - mean[p]) * rstd * g2[0] + b2[0]),
+                                             (bf16)((acc[p][1] - mean[p]) * rstd * g2[1] + b2[1])};
+    }
+  } else {
 #pragma unroll
     for (int p = 0; p < W; ++p) {
       f32x2 o = acc[p];
@@ -862,22 +904,28 @@ bool dw_cp_enabled() {  // IMGCAP_DW_CP=0: the channel-tiled kernels at W = 14 /
 }
 // Measured (tools/dw_ln_bench.py, us, vs the channel-tiled kernel): Tiny stage 3 B32 9.2 vs 12.2,
 // B64 15.7 vs 17.2; Base stage 3 B32 10.6 vs 13.1; Tiny stage 4 B64 10.3 vs 12.6; Base stage 4 B32
-// 9.5 vs 12.5; Large stage 3 B64 (W 14, C 768) 33.2 vs 30.6 -- so W = 14 only up to C = 512.  A
-// LayerNorm epilogue (per-pixel wave sums + the block's waves through LDS) measured 1.1-2.4x
-// slower than this kernel + add_layernorm and was dropped.
+// 9.5 vs 12.5; Large stage 3 B64 (W 14, C 768) 33.2 vs 30.6 -- so W = 14 only up to C = 512.
+// LN (imgcap_dwconv7_ln): the LayerNorm in the epilogue (a first form with 2 x W wave sums per
+// lane measured 1.1-2.4x slower than this kernel + add_layernorm; the LDS form above reduces each
+// pixel once per block).
 bool dw_cp_fits(int W, int C) {
   return dw_cp_enabled() && (W == 7 || (W == 14 && C <= 512)) && C % 128 == 0 && C <= 1024;
 }
 
-int dwconv7_cp_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
-                      const void* res, int flip, hipStream_t st) {
+int dwconv7_cp_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, const float* lnw,
+                      const float* lnb, void* y, const void* res, int flip, hipStream_t st) {
   const dim3 grid((unsigned)((long)B * H)), block((unsigned)(C / 128 * 64));
-  if (W == 14)
-    hipLaunchKernelGGL((dwconv7_cp_kernel<14>), grid, block, 0, st, H, C, (const bf16*)x, w, bias, (bf16*)y,
-                       (const bf16*)res, flip);
-  else
-    hipLaunchKernelGGL((dwconv7_cp_kernel<7>), grid, block, 0, st, H, C, (const bf16*)x, w, bias, (bf16*)y,
-                       (const bf16*)res, flip);
+#define CP_(WW, L)                                                                                          \
+  hipLaunchKernelGGL((dwconv7_cp_kernel<WW, L>), grid, block, 0, st, H, C, (const bf16*)x, w, bias, lnw, lnb, \
+                     (bf16*)y, (const bf16*)res, flip)
+  if (W == 14) {
+    if (lnw) CP_(14, true);
+    else CP_(14, false);
+  } else {
+    if (lnw) CP_(7, true);
+    else CP_(7, false);
+  }
+#undef CP_
   IMGCAP_CHECK_LAUNCH("imgcap_dwconv7 (channel pairs)");
   return 0;
 }
@@ -886,7 +934,7 @@ template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
                    hipStream_t st, const void* res = nullptr, int flip = 0) {
   if (sizeof(T) == 2 && dw_cp_fits(W, C))
-    return dwconv7_cp_launch(B, H, W, C, x, w, bias, y, res, flip, st);
+    return dwconv7_cp_launch(B, H, W, C, x, w, bias, nullptr, nullptr, y, res, flip, st);
   // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups.
   // Narrow mode (dw_narrow): the 28 / 14 / 7-wide stages with 4 / 2 / 1 pixels per lane -- 7
   // lanes per image row, so 2-4x the lanes and blocks of the late stages' small grids
@@ -1076,6 +1124,8 @@ extern "C" int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const vo
   IMGCAP_REQUIRE(x != out, "imgcap_dwconv7_ln: in-place not supported");
   if ((long)B * H * W == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == IMGCAP_BF16 && dw_cp_fits(W, C))
+    return dwconv7_cp_launch(B, H, W, C, x, w, bias, ln_w, ln_b, out, nullptr, 0, st);
   if (dtype == IMGCAP_BF16) {
     if (W % 7 == 0) return launch_dw<bf16, 7>(B, H, W, C, x, w, bias, ln_w, ln_b, out, st);
     if (W % 8 == 0) return launch_dw<bf16, 8>(B, H, W, C, x, w, bias, ln_w, ln_b, out, st);

@@ -238,10 +238,11 @@ class Encoder(nn.Module):
             x2 = x.view(M, C)
             for blk in blocks:
                 rs = sd[bid] if (sd is not None and blk["sd"] > 0) else None
-                if w <= 64:  # channel-tiled depthwise; LayerNorm applied by the consumer
+                if w <= 64 and (mx or fused or not K.dw_ln_fused(w, C, ct)):
+                    # channel-tiled depthwise; LayerNorm applied by the consumer
                     K.dwconv7(x, blk["w49"], blk["dwb"], z)
                     ln = (blk["lnw"], blk["lnb"])
-                else:        # wide images: row kernel with the LayerNorm fused
+                else:  # the LayerNorm fused: late stages (channel-pair kernel) / wide images (rows)
                     K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], z)
                     ln = (None, None)
                 if mx:  # LN -> fp8 rows; fp8 Linear + GELU -> fp8 hidden; fp8 Linear + scale + residual
