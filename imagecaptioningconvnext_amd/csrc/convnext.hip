@@ -781,23 +781,23 @@ int dw_pick_ntl(long, int, size_t, size_t) {
 // 4-byte bf16 pairs (64 lanes = 256 contiguous bytes, the next row requested before the current
 // one is used), unpacks it once and applies all 7 taps of that kernel row with packed FMAs
 // (≈ 0.7 VALU per MAC), and the grid is B*H rows x C/128 waves.  flip / res: the backward data gradient (taps mirrored, residual added), as dwconv7_kernel.
-template <int W, bool LN>
+template <int W, bool LN, int R>
 __global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf16* __restrict__ x,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
                                                          const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                          bf16* __restrict__ y, const bf16* __restrict__ res, int flip) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long r = blockIdx.x;  // b * H + h
-  const int h = (int)(r % H);
-  const long b = r / H;
-  const int c = wv * 128 + 2 * lane;
+  const int HB = (H + R - 1) / R;  // R output rows per block (R = 2: each weight row loaded once for both)
+  const long r = blockIdx.x;       // b * HB + row block
+  const int h = (int)(r % HB) * R;
+  const long b = r / HB;
+  const int c = (blockIdx.y * (blockDim.x >> 6) + wv) * 128 + 2 * lane;
   // the 7 weight pairs of kernel row kh (requested with that row's input, one row ahead)
   // buffer loads: per-lane byte offset in a VGPR, the wave-uniform pixel / tap offset in an SGPR
   // (64-bit addresses per load cost two VGPRs each and spilled); rows outside the image read 0
   // through the descriptor's range check
   const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, 49 * C * 4, 0x00020000);
   const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)((b + 1) * H * W * (long)C * 2), 0x00020000);
-  f32x2 wb[2][7];
   auto load_w = [&](int kh, f32x2 (&dst)[7]) {
 #pragma unroll
     for (int kw = 0; kw < 7; ++kw) {
@@ -806,67 +806,105 @@ __global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf1
       dst[kw] = __builtin_bit_cast(f32x2, v);
     }
   };
-  f32x2 acc[W];
+  f32x2 acc[R][W];
   {
     const f32x2 bb = bias ? *(const f32x2*)(bias + c) : f32x2{0.f, 0.f};
 #pragma unroll
-    for (int p = 0; p < W; ++p) acc[p] = bb;
+    for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+      for (int p = 0; p < W; ++p) acc[rr][p] = bb;
   }
-  uint32_t rb[2][W];
-  auto load_row = [&](int kh, uint32_t (&dst)[W]) {
-    const int ih = h + kh - 3;
+  // input row h + i - 3
+  auto load_row = [&](int i, uint32_t (&dst)[W]) {
+    const int ih = h + i - 3;
     const bool ok = ih >= 0 && ih < H;
     const uint32_t vo = ok ? (uint32_t)(((b * H + ih) * W * (long)C + c) * 2) : 0x80000000u;
 #pragma unroll
     for (int iw = 0; iw < W; ++iw) dst[iw] = __builtin_amdgcn_raw_buffer_load_b32(xr, vo, iw * C * 2, 0);
   };
-  load_row(0, rb[0]);
-  load_w(0, wb[0]);
+  auto unpack = [&](const uint32_t (&src)[W], f32x2 (&xin)[W]) {
 #pragma unroll
-  for (int kh = 0; kh < 7; ++kh) {
-    asm volatile("" ::: "memory");  // one row of loads ahead, no further (registers)
-    if (kh < 6) {
-      load_row(kh + 1, rb[(kh + 1) & 1]);
-      load_w(kh + 1, wb[(kh + 1) & 1]);
-    }
-    f32x2 xin[W];
-#pragma unroll
-    for (int iw = 0; iw < W; ++iw) {
-      const uint32_t v = rb[kh & 1][iw];
-      xin[iw] = f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
-    }
+    for (int iw = 0; iw < W; ++iw)
+      xin[iw] = f32x2{__uint_as_float(src[iw] << 16), __uint_as_float(src[iw] & 0xFFFF0000u)};
+  };
+  auto row_fma = [&](f32x2 (&a)[W], const f32x2 (&xin)[W], const f32x2 (&wk)[7]) {
 #pragma unroll
     for (int kw = 0; kw < 7; ++kw)
 #pragma unroll
       for (int p = 0; p < W; ++p) {
         const int q = p + kw - 3;
-        if (q >= 0 && q < W) acc[p] = xin[q] * wb[kh & 1][kw] + acc[p];
+        if (q >= 0 && q < W) a[p] = xin[q] * wk[kw] + a[p];
       }
+  };
+  // rolled loops, one row of loads ahead: fully unrolled, the compiler hoisted later rows' loads
+  // to the top (200-255 VGPRs, two waves per SIMD)
+  if constexpr (R == 1) {
+    uint32_t rb[2][W];
+    f32x2 wb[2][7], xin[W];
+    load_row(0, rb[0]);
+    load_w(0, wb[0]);
+#pragma unroll 1
+    for (int kh = 0; kh < 6; kh += 2) {
+      load_row(kh + 1, rb[1]);
+      load_w(kh + 1, wb[1]);
+      unpack(rb[0], xin);
+      row_fma(acc[0], xin, wb[0]);
+      load_row(kh + 2, rb[0]);
+      load_w(kh + 2, wb[0]);
+      unpack(rb[1], xin);
+      row_fma(acc[0], xin, wb[1]);
+    }
+    unpack(rb[0], xin);
+    row_fma(acc[0], xin, wb[0]);
+  } else {
+    static_assert(R == 2, "one or two output rows per block");
+    // input row i feeds output row h with kernel row i and row h + 1 with kernel row i - 1
+    uint32_t rc[W], rn[W];
+    f32x2 wp[7], wc[7], wn[7], xin[W];
+    load_row(0, rc);
+    load_w(0, wc);
+#pragma unroll 1
+    for (int i = 0; i < 8; ++i) {
+      if (i < 7) load_row(i + 1, rn);
+      if (i < 6) load_w(i + 1, wn);
+      unpack(rc, xin);
+      if (i < 7) row_fma(acc[0], xin, wc);
+      if (i > 0) row_fma(acc[1], xin, wp);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        wp[k] = wc[k];
+        wc[k] = wn[k];
+      }
+#pragma unroll
+      for (int k = 0; k < W; ++k) rc[k] = rn[k];
+    }
   }
-  bf16* out = y + r * W * (long)C + c;
+  const long o0 = (b * H + h) * W * (long)C + c;  // output row h, channel pair c
   if constexpr (LN) {
     // LayerNorm over C of each output pixel (eps 1e-6), two passes, fixed order: the lanes'
     // partials go to LDS [wave][pixel][lane]; wave g reduces pixels g, g + nwv, .. (its lanes sum
     // the waves' partials of one lane column, then a wave sum), the block reads the results back
-    __shared__ float part[8][W][64];
-    __shared__ float stat[2][W];
+    constexpr int NP = R * W;
+    __shared__ float part[8][NP][64];
+    __shared__ float stat[2][NP];
     const int nwv = blockDim.x >> 6;
-    float mean[W];
+    float mean[NP];
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-      for (int p = 0; p < W; ++p) {
+      for (int p = 0; p < NP; ++p) {
+        const f32x2 a = acc[p / W][p % W];
         float v;
         if (pass == 0) {
-          v = acc[p][0] + acc[p][1];
+          v = a[0] + a[1];
         } else {
-          const float d0 = acc[p][0] - mean[p], d1 = acc[p][1] - mean[p];
+          const float d0 = a[0] - mean[p], d1 = a[1] - mean[p];
           v = d0 * d0 + d1 * d1;
         }
         part[wv][p][lane] = v;
       }
       __syncthreads();
-      for (int p = wv; p < W; p += nwv) {
+      for (int p = wv; p < NP; p += nwv) {
         float v = 0.f;
         for (int g = 0; g < nwv; ++g) v += part[g][p][lane];
         v = wave_sum(v);
@@ -875,25 +913,28 @@ __global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf1
       __syncthreads();
       if (pass == 0) {
 #pragma unroll
-        for (int p = 0; p < W; ++p) mean[p] = stat[0][p];
+        for (int p = 0; p < NP; ++p) mean[p] = stat[0][p];
       }
     }
     const f32x2 g2 = *(const f32x2*)(lnw + c), b2 = *(const f32x2*)(lnb + c);
 #pragma unroll
-    for (int p = 0; p < W; ++p) {
+    for (int p = 0; p < NP; ++p) {
+      if (p >= W && h + 1 >= H) break;  // odd H: the last block's second row is outside the image
+      const f32x2 a = acc[p / W][p % W];
       const float rstd = rsqrtf(stat[1][p] + 1e-6f);
-      *(bf16x2*)(out + (long)p * C) = bf16x2{(bf16)((acc[p][0] - mean[p]) * rstd * g2[0] + b2[0]),
-                                             (bf16)((acc[p][1] - mean[p]) * rstd * g2[1] + b2[1])};
+      *(bf16x2*)(y + o0 + (long)p * C) = bf16x2{(bf16)((a[0] - mean[p]) * rstd * g2[0] + b2[0]),
+                                                (bf16)((a[1] - mean[p]) * rstd * g2[1] + b2[1])};
     }
   } else {
 #pragma unroll
-    for (int p = 0; p < W; ++p) {
-      f32x2 o = acc[p];
+    for (int p = 0; p < R * W; ++p) {
+      if (p >= W && h + 1 >= H) break;
+      f32x2 o = acc[p / W][p % W];
       if (res) {
-        const uint32_t v = *(const uint32_t*)(res + r * W * (long)C + c + (long)p * C);
+        const uint32_t v = *(const uint32_t*)(res + o0 + (long)p * C);
         o += f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
       }
-      *(bf16x2*)(out + (long)p * C) = bf16x2{(bf16)o[0], (bf16)o[1]};
+      *(bf16x2*)(y + o0 + (long)p * C) = bf16x2{(bf16)o[0], (bf16)o[1]};
     }
   }
 }
@@ -902,29 +943,48 @@ bool dw_cp_enabled() {  // IMGCAP_DW_CP=0: the channel-tiled kernels at W = 14 /
   const char* e = getenv("IMGCAP_DW_CP");
   return !(e && *e == '0');
 }
-// Measured (tools/dw_ln_bench.py, us, vs the channel-tiled kernel): Tiny stage 3 B32 9.2 vs 12.2,
-// B64 15.7 vs 17.2; Base stage 3 B32 10.6 vs 13.1; Tiny stage 4 B64 10.3 vs 12.6; Base stage 4 B32
-// 9.5 vs 12.5; Large stage 3 B64 (W 14, C 768) 33.2 vs 30.6 -- so W = 14 only up to C = 512.
+// Measured (tools/dw_ln_bench.py, us, vs the channel-tiled kernel): Tiny stage 3 B32 9.0 vs 12.4,
+// B64 13.4 vs 17.2; Base stage 3 B32 9.9 vs 13.1; Tiny stage 4 B64 8.9 vs 12.6; Base stage 4 B32
+// 8.9 vs 12.5; Large stage 3 B64 (W 14, C 768) 19.3 vs 30.0 (two rows per block, 2-wave channel
+// groups; 6-wave blocks with the kernel rows unrolled ran 33.2 vs 30.6: 255 VGPRs, one block per CU).
 // LN (imgcap_dwconv7_ln): the LayerNorm in the epilogue (a first form with 2 x W wave sums per
 // lane measured 1.1-2.4x slower than this kernel + add_layernorm; the LDS form above reduces each
 // pixel once per block).
 bool dw_cp_fits(int W, int C) {
-  return dw_cp_enabled() && (W == 7 || (W == 14 && C <= 512)) && C % 128 == 0 && C <= 1024;
+  return dw_cp_enabled() && (W == 7 || W == 14) && C % 128 == 0 && C <= 1024;
+}
+
+// Output rows per block.  Measured (tools/dw_ln_bench.py, us, one vs two rows): without LN Large
+// stage 3 B64 23.7 vs 19.3, B32 14.6 vs 12.9, Tiny stage 4 B64 9.5 vs 8.9, C <= 512 equal; with LN
+// Large stage 3 B64 40.5 vs 35.4, Tiny stage 3 B32 14.6 vs 18.5, Base stage 3 15.0 vs 17.2, Base
+// stage 4 9.1 vs 10.9 (the LN pass over 2W pixels).  IMGCAP_DW_CP_R=1/2 overrides (A/B).
+int dw_cp_rows(int W, int C, bool ln) {
+  const char* e = getenv("IMGCAP_DW_CP_R");
+  if (e && *e) return *e == '2' ? 2 : 1;
+  return C >= 768 && (W == 14 || !ln) ? 2 : 1;
 }
 
 int dwconv7_cp_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, const float* lnw,
                       const float* lnb, void* y, const void* res, int flip, hipStream_t st) {
-  const dim3 grid((unsigned)((long)B * H)), block((unsigned)(C / 128 * 64));
-#define CP_(WW, L)                                                                                          \
-  hipLaunchKernelGGL((dwconv7_cp_kernel<WW, L>), grid, block, 0, st, H, C, (const bf16*)x, w, bias, lnw, lnb, \
+  // the LayerNorm form needs every channel of a pixel in one block; without it a block takes 4, 2
+  // or 1 waves of 128 channels (blockIdx.y: channel group) so blocks pack a CU's wave slots
+  const int nw = C / 128, wpb = lnw ? nw : (nw % 4 == 0 ? 4 : nw % 2 == 0 ? 2 : 1);
+  const int R = dw_cp_rows(W, C, lnw != nullptr);
+  const dim3 grid((unsigned)((long)B * ((H + R - 1) / R)), (unsigned)(nw / wpb)), block((unsigned)(wpb * 64));
+#define CP_(WW, L, RR)                                                                                          \
+  hipLaunchKernelGGL((dwconv7_cp_kernel<WW, L, RR>), grid, block, 0, st, H, C, (const bf16*)x, w, bias, lnw, lnb, \
                      (bf16*)y, (const bf16*)res, flip)
+#define CP_R(WW, L) \
+  if (R == 2) CP_(WW, L, 2); \
+  else CP_(WW, L, 1)
   if (W == 14) {
-    if (lnw) CP_(14, true);
-    else CP_(14, false);
+    if (lnw) CP_R(14, true);
+    else CP_R(14, false);
   } else {
-    if (lnw) CP_(7, true);
-    else CP_(7, false);
+    if (lnw) CP_R(7, true);
+    else CP_R(7, false);
   }
+#undef CP_R
 #undef CP_
   IMGCAP_CHECK_LAUNCH("imgcap_dwconv7 (channel pairs)");
   return 0;

@@ -427,10 +427,10 @@ def dwconv7(x, w49, bias, out):
 
 def dw_ln_fused(W, C, dtype):
     """Whether imgcap_dwconv7_ln runs the channel-pair kernel with the LayerNorm in its epilogue
-    here (convnext.hip dw_cp_fits: W = 7, or 14 up to C = 512; C % 128 == 0, C <= 1024; bf16) --
+    here (convnext.hip dw_cp_fits: W = 7 or 14, C % 128 == 0, C <= 1024, bf16) --
     the encoder then skips the separate add_layernorm pass."""
     return (os.environ.get("IMGCAP_DW_CP", "1") != "0" and dtype == torch.bfloat16 and C % 128 == 0 and C <= 1024
-            and (W == 7 or (W == 14 and C <= 512)))
+            and W in (7, 14))
 
 
 def dwconv7_ln(x, w49, bias, ln_w, ln_b, out):

@@ -1,7 +1,7 @@
-"""Depthwise 7x7 for the narrow late stages (the channel-pair kernel of convnext.hip: W = 7, and W =
-14 up to C = 512, bf16) against torch fp32 conv2d(groups=C) on the bf16-rounded input and against
+"""Depthwise 7x7 for the narrow late stages (the channel-pair kernel of convnext.hip: W = 7 and 14,
+C <= 1024, bf16; one or two output rows per block, IMGCAP_DW_CP_R) against torch fp32 conv2d(groups=C) on the bf16-rounded input and against
 the channel-tiled kernel (IMGCAP_DW_CP=0), plain and in the backward data-gradient form (flipped
-taps + residual); the shapes past its range (W 14, C 1024) check the dispatch, and imgcap_dwconv7_ln
+taps + residual, odd H with two rows per block); C = 768 runs 2-wave channel-group blocks, and imgcap_dwconv7_ln
 (row kernel) against torch LayerNorm of the same conv."""
 import os
 
@@ -27,8 +27,10 @@ def _ref(x, w49, bias, flip=False):
     return y.permute(0, 2, 3, 1)
 
 
-@pytest.mark.parametrize("B,H,C", [(3, 14, 384), (2, 14, 512), (2, 7, 768), (3, 7, 1024), (1, 14, 1024)])
-def test_dwconv_cp_matches_torch(hip_device, B, H, C):
+@pytest.mark.parametrize("rows", ["1", "2"])
+@pytest.mark.parametrize("B,H,C", [(3, 14, 384), (2, 14, 512), (2, 7, 768), (3, 7, 1024), (1, 14, 1024), (2, 14, 768)])
+def test_dwconv_cp_matches_torch(hip_device, monkeypatch, rows, B, H, C):
+    monkeypatch.setenv("IMGCAP_DW_CP_R", rows)
     g = torch.Generator(device="cpu").manual_seed(B * H + C)
     x = torch.randn(B, H, H, C, generator=g).bfloat16()
     w49 = torch.randn(49, C, generator=g) * 0.1
@@ -53,9 +55,12 @@ def test_dwconv_cp_matches_torch(hip_device, B, H, C):
     assert _rel(y.cpu(), y0.cpu()) < 1e-2
 
 
-def test_dwconv_cp_backward_data_form(hip_device):
+@pytest.mark.parametrize("rows", ["1", "2"])
+@pytest.mark.parametrize("H,C", [(14, 384), (7, 768)])
+def test_dwconv_cp_backward_data_form(hip_device, monkeypatch, rows, H, C):
     """Flipped taps + residual (imgcap_dwconv7_bwd_data's use of the forward kernel)."""
-    B, H, C = 2, 14, 384
+    monkeypatch.setenv("IMGCAP_DW_CP_R", rows)
+    B = 2
     g = torch.Generator(device="cpu").manual_seed(7)
     dz = torch.randn(B, H, H, C, generator=g).bfloat16()
     res = torch.randn(B, H, H, C, generator=g).bfloat16()

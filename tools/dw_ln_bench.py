@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
 
 SHAPES = [("Tiny s3 B32", 32, 14, 384), ("Tiny s3 B64", 64, 14, 384), ("Base s3 B32", 32, 14, 512),
-          ("Tiny s4 B64", 64, 7, 768), ("Base s4 B32", 32, 7, 1024), ("Large s3 B64", 64, 14, 768)]
+          ("Tiny s4 B64", 64, 7, 768), ("Base s4 B32", 32, 7, 1024), ("Large s3 B32", 32, 14, 768),
+          ("Large s3 B64", 64, 14, 768)]
 
 
 def main():
@@ -28,9 +29,19 @@ def main():
         M = B * H * H
 
         def cp_ln():
+            os.environ["IMGCAP_DW_CP_R"] = "1"
             K.dwconv7_ln(x, w49, b, lw, lb, zf)
 
         def cp_dw():
+            os.environ["IMGCAP_DW_CP_R"] = "1"
+            K.dwconv7(x, w49, b, y)
+
+        def cp2_ln():
+            os.environ["IMGCAP_DW_CP_R"] = "2"
+            K.dwconv7_ln(x, w49, b, lw, lb, zf)
+
+        def cp2_dw():
+            os.environ["IMGCAP_DW_CP_R"] = "2"
             K.dwconv7(x, w49, b, y)
 
         def old_dw_ln():
@@ -44,9 +55,12 @@ def main():
             K.dwconv7(x, w49, b, y)
             del os.environ["IMGCAP_DW_CP"]
 
-        fns = (("cp+ln", cp_ln), ("old dw+ln", old_dw_ln), ("cp dw", cp_dw), ("old dw", old_dw))
+        fns = (("cp+ln", cp_ln), ("cp2+ln", cp2_ln), ("old dw+ln", old_dw_ln), ("cp dw", cp_dw), ("cp2 dw", cp2_dw),
+               ("old dw", old_dw))
         for _, fn in fns:
             fn()
+        torch.cuda.synchronize()
+        cp_ln()
         torch.cuda.synchronize()
         err = float((zf.float() - z.float()).norm() / z.float().norm())
         res = {n: [] for n, _ in fns}
