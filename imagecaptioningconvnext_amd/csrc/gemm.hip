@@ -1002,15 +1002,14 @@ extern "C" int imgcap_gemm_mx(int M, int N, int K, const void* A, int64_t lda, c
     IMGCAP_REQUIRE(vec_ok && N % 32 == 0 && ldc % 32 == 0 && ep.c_scale && ep.res == nullptr,
                    "imgcap_gemm_mx: MX-FP8 output needs N, ldc % 32 == 0, 16-byte aligned C, c_scale, no res");
   hipStream_t st = (hipStream_t)stream;
-  // 256x256 tile when it fills at least one round of the 256 CUs and K is long enough for its
-  // main loop to matter (with K = 768 the 128-tile's second resident block hides the GELU + MX
-  // epilogue: 85 vs 98 us at C5's stage-3 shape, tools/microbench.py mx); IMGCAP_MX_TILE forces
-  static const int force = [] {
-    const char* e = getenv("IMGCAP_MX_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  const long tiles256 = (long)((M + 255) / 256) * ((N + 255) / 256);
-  const bool big = force ? force == 256 : (tiles256 >= 256 && K >= 1024);
+  // The 256x256 tile is opt-in (IMGCAP_MX_TILE=256).  In isolation it wins where it fills a
+  // round of the 256 CUs with K >= 1024 and at C5's K = 3072 stage-3 Linear (62.3 vs 65.9 us,
+  // tools/microbench.py mx), but in the C5 step the 128 tile everywhere measured 5.11k img/s
+  // against 5.05k with the 256 tile at those shapes (tools/gpu/r3_mx.sh: its one block per CU
+  // overlaps worse with the neighbouring kernels).  More stages for the 128 tile (3 / 4: one
+  // block per CU) measured 1.4-1.6x slower at both stage-3 shapes.
+  const char* fe = getenv("IMGCAP_MX_TILE");
+  const bool big = fe && atoi(fe) == 256;
   if (big) {
     dim3 grid((N + 255) / 256, (M + 255) / 256);
     hipLaunchKernelGGL((gemm_mx256_kernel<2>), grid, dim3(512), 0, st, (const uint8_t*)A, (long)lda, As,
