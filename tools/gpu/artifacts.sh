@@ -15,4 +15,5 @@ EXTRA=""; [ "$CFG" != "C2" ] && EXTRA="--no-cpu-baseline"
 timeout -k 10 400 python bench.py --config $CFG $EXTRA > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
 tail -1 $O/bench.log > $O/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python bench.py --config $CFG --no-cpu-baseline > $O/stats.log 2>&1 || { tail -30 $O/stats.log; exit 1; }
+rm -f $O/stats/run_kernel_trace.csv  # per-dispatch trace: tens of MB (gpurun copies back <= 64 MiB)
 cut -c1-600 $O/bench.json
