@@ -1,6 +1,7 @@
 # round 3: LSTM backward tail -- bias column sums beside the grouped GEMMs, optional inline Adam
 # with the fc range after the backward recurrence: LSTM / trainer suites (inline Adam on and off),
 # then C2 same-box A/B (default, IMGCAP_LSTM_CB_SIDE=0, IMGCAP_INLINE_ADAM=1), two rounds
+# (IMGCAP_LSTM_CB_SIDE was a knob of the measured variant; removed after the A/B, so "cbmain" is now the default path)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
