@@ -737,8 +737,10 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(int cols, int slices
 }
 
 // ---- many column sums in one launch (the bias gradients of a whole backward pass) ----------
-// Block = (item, 64-column group): 8 column vectors x 32 row lanes walk ALL rows of the item
-// (8 rows in flight per lane), fixed-order LDS reduction, out = beta*out + sum.
+// Block = (item, 64-column group): 8 column vectors x 128 row lanes walk ALL rows of the item
+// (8 rows in flight per lane: 128 KB per block -- with 32 row lanes the grid of a 9490-wide
+// dlogits sum, 149 blocks, held too few bytes in flight to reach HBM rate), fixed-order LDS
+// reduction, out = beta*out + sum.
 constexpr int COLSUM_MAX_ITEMS = 64;
 struct ColsumBatch {
   int n;
@@ -746,8 +748,9 @@ struct ColsumBatch {
   imgcap_colsum_item it[COLSUM_MAX_ITEMS];
 };
 
-__global__ __launch_bounds__(256) void colsum_multi_kernel(ColsumBatch b) {
-  __shared__ float red[32][65];
+constexpr int COLSUM_RL = 128;  // row lanes per block
+__global__ __launch_bounds__(1024) void colsum_multi_kernel(ColsumBatch b) {
+  __shared__ float red[COLSUM_RL][65];
   int k = 0;
   while (k + 1 < b.n && (int)blockIdx.x >= b.first_block[k + 1]) ++k;
   const imgcap_colsum_item& item = b.it[k];
@@ -763,37 +766,51 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(ColsumBatch b) {
     int r = rl;
     if (item.dtype == IMGCAP_BF16) {
       const bf16* x = (const bf16*)item.x;
-      for (; vec && r + 32 * (U - 1) < item.rows; r += 32 * U) {
+      for (; vec && r + COLSUM_RL * (U - 1) < item.rows; r += COLSUM_RL * U) {
         bf16x8 v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = *(const bf16x8*)(x + (long)(r + 32 * u) * item.ld + c0);
+        for (int u = 0; u < U; ++u) v[u] = *(const bf16x8*)(x + (long)(r + COLSUM_RL * u) * item.ld + c0);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
           for (int j = 0; j < 8; ++j) s[j] += (float)v[u][j];
       }
-      for (; r < item.rows; r += 32)
+      for (; r < item.rows; r += COLSUM_RL) {  // tail rows: one vector per lane and row
+        if (vec) {
+          const bf16x8 v = *(const bf16x8*)(x + (long)r * item.ld + c0);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (c0 + j < item.cols) s[j] += (float)x[(long)r * item.ld + c0 + j];
+          for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (c0 + j < item.cols) s[j] += (float)x[(long)r * item.ld + c0 + j];
+        }
+      }
     } else {
       const float* x = (const float*)item.x;
-      for (; vec && r + 32 * (U - 1) < item.rows; r += 32 * U) {
+      for (; vec && r + COLSUM_RL * (U - 1) < item.rows; r += COLSUM_RL * U) {
         f32x4 v[U][2];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          v[u][0] = *(const f32x4*)(x + (long)(r + 32 * u) * item.ld + c0);
-          v[u][1] = *(const f32x4*)(x + (long)(r + 32 * u) * item.ld + c0 + 4);
+          v[u][0] = *(const f32x4*)(x + (long)(r + COLSUM_RL * u) * item.ld + c0);
+          v[u][1] = *(const f32x4*)(x + (long)(r + COLSUM_RL * u) * item.ld + c0 + 4);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
           for (int j = 0; j < 4; ++j) { s[j] += v[u][0][j]; s[j + 4] += v[u][1][j]; }
       }
-      for (; r < item.rows; r += 32)
+      for (; r < item.rows; r += COLSUM_RL) {
+        if (vec) {
+          const f32x4 v0 = *(const f32x4*)(x + (long)r * item.ld + c0), v1 = *(const f32x4*)(x + (long)r * item.ld + c0 + 4);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (c0 + j < item.cols) s[j] += x[(long)r * item.ld + c0 + j];
+          for (int j = 0; j < 4; ++j) { s[j] += v0[j]; s[j + 4] += v1[j]; }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (c0 + j < item.cols) s[j] += x[(long)r * item.ld + c0 + j];
+        }
+      }
     }
   }
 #pragma unroll
@@ -802,7 +819,7 @@ __global__ __launch_bounds__(256) void colsum_multi_kernel(ColsumBatch b) {
   if (threadIdx.x < 64) {
     const int c = cg * 64 + threadIdx.x;
     float t = 0.f;
-    for (int i = 0; i < 32; ++i) t += red[i][threadIdx.x];
+    for (int i = 0; i < COLSUM_RL; ++i) t += red[i][threadIdx.x];
     if (c < item.cols) item.out[c] = (item.beta != 0.f ? item.beta * item.out[c] : 0.f) + t;
   }
 }
@@ -943,7 +960,7 @@ extern "C" int imgcap_colsum_multi(int n, const imgcap_colsum_item* items, void*
   }
   b.first_block[n] = blocks;
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL(colsum_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
+  hipLaunchKernelGGL(colsum_multi_kernel, dim3(blocks), dim3(COLSUM_RL * 8), 0, (hipStream_t)stream, b);
   IMGCAP_CHECK_LAUNCH("imgcap_colsum_multi");
   return 0;
 }

@@ -146,6 +146,25 @@ def test_colsum(hip_device, rows, cols):
     assert _rel(out.cpu(), x.sum(0) + 0.5) < 1e-6
 
 
+def test_colsum_multi(hip_device):
+    """The batched bias-gradient column sums (imgcap_colsum_multi: 128 row lanes x 8 column
+    vectors per block): bf16 and fp32 items, ragged widths (non-vector tails), row counts below,
+    at and past the 1024-row vector stride, beta accumulation, a row pitch wider than the item."""
+    g = torch.Generator().manual_seed(5)
+    cases = [(1632, 9490, torch.bfloat16, 0.0), (3264, 512, torch.bfloat16, 0.5), (1023, 77, torch.float32, 0.0),
+             (1025, 2048, torch.float32, 1.0), (32, 1024, torch.bfloat16, 0.0), (5000, 100, torch.bfloat16, 0.0)]
+    cb, refs = K.ColsumBatch(), []
+    for rows, cols, dtype, beta in cases:
+        x = torch.randn(rows, cols + 8, generator=g).to(dtype)
+        out0 = torch.randn(cols, generator=g)
+        out = out0.to(hip_device)
+        cb.add(x.to(hip_device)[:, :cols], out, beta=beta)
+        refs.append((out, x[:, :cols].float().sum(0) + beta * out0))
+    cb.run()
+    for out, ref in refs:
+        assert _rel(out.cpu(), ref) < 1e-5
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 def test_add_layernorm_fwd_bwd(hip_device, dtype, tol):
     torch.manual_seed(1)
