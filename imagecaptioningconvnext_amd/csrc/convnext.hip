@@ -990,11 +990,129 @@ int dwconv7_cp_launch(int B, int H, int W, int C, const void* x, const float* w,
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Depthwise 7x7 for the wide early stages (W = 56 / 28), bf16, any even C: lane = (channel pair,
+// segment of S output columns, output row), lanes flattened channel-pair-fastest (consecutive
+// lanes read consecutive 4-byte pairs of one pixel; C = 96 / 192 need no 128-channel groups).
+// Per kernel row a lane loads its S + 6 input pixels as 4-byte pairs (buffer loads: the
+// segment's row start in a VGPR, the column in an SGPR; rows outside the image read 0 through
+// the range check, the columns left / right of it are masked), unpacks each once and applies the 7 taps with
+// packed FMAs, one kernel row of loads ahead in a rolled loop -- no LDS, no staging barrier.
+template <int S>
+__global__ __launch_bounds__(256) void dwconv7_seg_kernel(int B, int H, int W, int C, const bf16* __restrict__ x,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias, bf16* __restrict__ y,
+                                                          const bf16* __restrict__ res, int flip) {
+  constexpr int NI = S + 6;
+  const int P = C >> 1, nseg = W / S;
+  const long L = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)B * H * nseg * P;
+  if (L >= total) return;
+  const int pr = (int)(L % P);
+  const long rest = L / P;
+  const int sg = (int)(rest % nseg);
+  const long row = rest / nseg;  // b * H + h
+  const int h = (int)(row % H);
+  const int c = 2 * pr;
+  const bool left = sg == 0, right = sg == nseg - 1;
+  const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, 49 * C * 4, 0x00020000);
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)((long)B * H * W * C * 2), 0x00020000);
+  auto load_w = [&](int kh, f32x2 (&dst)[7]) {
+#pragma unroll
+    for (int kw = 0; kw < 7; ++kw) {
+      const int t = kh * 7 + kw;
+      dst[kw] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(wr, c * 4, (flip ? 48 - t : t) * C * 4, 0));
+    }
+  };
+  // input row h + kh - 3, columns sg*S - 3 .. sg*S + S + 2
+  auto load_row = [&](int kh, uint32_t (&dst)[NI]) {
+    const int ih = h + kh - 3;
+    const bool ok = ih >= 0 && ih < H;
+    // segment 0 starts at column 0 (its 3 left columns are padding): no offset below the buffer
+    const uint32_t vo = ok ? (uint32_t)((((row - h + ih) * W + (left ? 0 : sg * S - 3)) * (long)C + c) * 2) : 0x80000000u;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) dst[j] = __builtin_amdgcn_raw_buffer_load_b32(xr, vo, j * C * 2, 0);
+  };
+  f32x2 acc[S];
+  {
+    const f32x2 bb = bias ? *(const f32x2*)(bias + c) : f32x2{0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < S; ++p) acc[p] = bb;
+  }
+  auto row_fma = [&](const uint32_t (&src)[NI], const f32x2 (&wk)[7]) {
+    f32x2 xin[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      // columns left of the image (segment 0, loaded from column 0: shifted by 3) / right of it
+      // (last segment): zero padding
+      uint32_t v;
+      if (j < 3) v = left ? 0u : src[j];
+      else if (j >= S + 3) v = left ? src[j - 3] : right ? 0u : src[j];
+      else v = left ? src[j - 3] : src[j];
+      xin[j] = f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
+    }
+#pragma unroll
+    for (int kw = 0; kw < 7; ++kw)
+#pragma unroll
+      for (int p = 0; p < S; ++p) acc[p] = xin[p + kw] * wk[kw] + acc[p];
+  };
+  uint32_t rb[2][NI];
+  f32x2 wb[2][7];
+  load_row(0, rb[0]);
+  load_w(0, wb[0]);
+#pragma unroll 1
+  for (int kh = 0; kh < 6; kh += 2) {
+    load_row(kh + 1, rb[1]);
+    load_w(kh + 1, wb[1]);
+    row_fma(rb[0], wb[0]);
+    load_row(kh + 2, rb[0]);
+    load_w(kh + 2, wb[0]);
+    row_fma(rb[1], wb[1]);
+  }
+  row_fma(rb[0], wb[0]);
+  const long o0 = (row * W + sg * S) * (long)C + c;
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    f32x2 o = acc[p];
+    if (res) {
+      const uint32_t v = *(const uint32_t*)(res + o0 + (long)p * C);
+      o += f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
+    }
+    *(bf16x2*)(y + o0 + (long)p * C) = bf16x2{(bf16)o[0], (bf16)o[1]};
+  }
+}
+
+// Opt-in (IMGCAP_DW_SEG=1).  Measured slower than the channel-tiled kernel at every wide-stage
+// shape (tools/dw_wide_bench.py, us, segment vs tiled: Tiny s1 B64 58.8 vs 49.5, Tiny s2 B64 34.0
+// vs 26.3, Base s1 B32 40.7 vs 34.1, Base s2 B32 23.5 vs 16.9, Large s1 B64 109.7 vs 81.9; C4
+// 8.17k vs 8.23-8.24k img/s): S + 6 loads per S outputs and a lane's own weight loads per kernel
+// row put it on the load-issue rate, where the tiled kernel's LDS patch serves 7 rows per load.
+bool dw_seg_fits(int W, int C) {
+  const char* e = getenv("IMGCAP_DW_SEG");
+  return e && *e == '1' && (W == 56 || W == 28) && C % 2 == 0;
+}
+
+int dwconv7_seg_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
+                       const void* res, int flip, hipStream_t st) {
+  const int S = W == 56 ? 8 : 7;
+  const long total = (long)B * H * (W / S) * (C / 2);
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  if (S == 8)
+    hipLaunchKernelGGL((dwconv7_seg_kernel<8>), grid, block, 0, st, B, H, W, C, (const bf16*)x, w, bias, (bf16*)y,
+                       (const bf16*)res, flip);
+  else
+    hipLaunchKernelGGL((dwconv7_seg_kernel<7>), grid, block, 0, st, B, H, W, C, (const bf16*)x, w, bias, (bf16*)y,
+                       (const bf16*)res, flip);
+  IMGCAP_CHECK_LAUNCH("imgcap_dwconv7 (column segments)");
+  return 0;
+}
+
 template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
                    hipStream_t st, const void* res = nullptr, int flip = 0) {
   if (sizeof(T) == 2 && dw_cp_fits(W, C))
     return dwconv7_cp_launch(B, H, W, C, x, w, bias, nullptr, nullptr, y, res, flip, st);
+  if (sizeof(T) == 2 && dw_seg_fits(W, C)) return dwconv7_seg_launch(B, H, W, C, x, w, bias, y, res, flip, st);
   // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups.
   // Narrow mode (dw_narrow): the 28 / 14 / 7-wide stages with 4 / 2 / 1 pixels per lane -- 7
   // lanes per image row, so 2-4x the lanes and blocks of the late stages' small grids
