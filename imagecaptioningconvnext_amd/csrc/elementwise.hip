@@ -219,10 +219,79 @@ __global__ void mean_mid_kernel(int B, int P, int E, const TI* __restrict__ x, T
 // decoder.py:64,79-81 in one launch: sort the batch by caption length (descending, stable --
 // the order the engine has always used), gather encoder_out and the captions into that order,
 // decode lengths (len - 1, int32) and the pixel mean of each gathered row (decoder.py:64, the
-// same p-order fp32 sum as mean_mid_kernel).  Block r = destination row r: every block ranks the
-// (<= 256) lengths itself, so no second launch is needed for the gather.
+// same p-order fp32 sum as mean_mid_kernel).  Block (r, chunk) = destination row r, 32 16-byte
+// column vectors: every block ranks the (<= 256) lengths itself, so no second launch is needed
+// for the gather.  The 8 waves' lanes split the pixels (all of a block's loads in flight at
+// once, 256 threads busy instead of the 96 of one thread per vector), stage them in LDS, and
+// the first 32 threads sum each vector's pixels in p order from there.
 template <typename T>
 __global__ __launch_bounds__(256) void sort_gather_kernel(int B, int P, int E, int L, const int64_t* __restrict__ lens,
+                                                          const T* __restrict__ enc, const int64_t* __restrict__ caps,
+                                                          T* __restrict__ enc_out, T* __restrict__ mean_out,
+                                                          int64_t* __restrict__ caps_out, int64_t* __restrict__ sort_ind,
+                                                          int32_t* __restrict__ dl) {
+  extern __shared__ uint4 stage[];  // [P][32] 16-byte vectors
+  __shared__ int64_t ls[256];
+  __shared__ int src_s;
+  const int r = blockIdx.x, tid = threadIdx.x;
+  if (tid < B) ls[tid] = lens[tid];
+  __syncthreads();
+  if (tid < B) {
+    const int64_t li = ls[tid];
+    int rank = 0;
+    for (int j = 0; j < B; ++j) rank += (ls[j] > li) || (ls[j] == li && j < tid);
+    if (rank == r) src_s = tid;
+  }
+  __syncthreads();
+  const int src = src_s;
+  if (blockIdx.y == 0) {
+    if (tid == 0) {
+      sort_ind[r] = src;
+      dl[r] = (int32_t)(ls[src] - 1);
+    }
+    for (int i = tid; i < L; i += 256) caps_out[(long)r * L + i] = caps[(long)src * L + i];
+  }
+  constexpr int VEC = 16 / sizeof(T);
+  const int vl = tid & 31, ps = tid >> 5;
+  const int v = blockIdx.y * 32 + vl;
+  const bool ok = v < E / VEC;
+  const T* in = enc + (long)src * P * E;
+  T* out = enc_out + (long)r * P * E;
+  if (ok) {
+    constexpr int PB = 8;  // pixels ps, ps + 8, .. : up to PB loads in flight per thread
+    for (int p0 = ps; p0 < P; p0 += 8 * PB) {
+      uint4 u[PB];
+#pragma unroll
+      for (int i = 0; i < PB; ++i)
+        if (p0 + 8 * i < P) u[i] = *(const uint4*)(in + (long)(p0 + 8 * i) * E + v * VEC);
+#pragma unroll
+      for (int i = 0; i < PB; ++i)
+        if (p0 + 8 * i < P) {
+          *(uint4*)(out + (long)(p0 + 8 * i) * E + v * VEC) = u[i];
+          stage[(p0 + 8 * i) * 32 + vl] = u[i];
+        }
+    }
+  }
+  __syncthreads();
+  if (ps == 0 && ok) {
+    float acc[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    for (int p = 0; p < P; ++p) {
+      const uint4 u = stage[p * 32 + vl];
+      const T* x = (const T*)&u;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] += to_f(x[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) mean_out[(long)r * E + v * VEC + k] = from_f<T>(acc[k] / P);
+  }
+}
+
+// The one-block-per-row form (96 threads busy per block at E = 768): kept for B > 32, where it
+// measured faster in the C3 step (17.33-17.35k vs 17.23k img/s, tools/gpu/r3_sortg.sh).
+template <typename T>
+__global__ __launch_bounds__(256) void sort_gather_row_kernel(int B, int P, int E, int L, const int64_t* __restrict__ lens,
                                                           const T* __restrict__ enc, const int64_t* __restrict__ caps,
                                                           T* __restrict__ enc_out, T* __restrict__ mean_out,
                                                           int64_t* __restrict__ caps_out, int64_t* __restrict__ sort_ind,
@@ -413,11 +482,25 @@ extern "C" int imgcap_sort_gather_rows(int dtype, int B, int P, int E, int L, co
   const int vec = dtype == IMGCAP_BF16 ? 8 : 4;
   IMGCAP_REQUIRE(E % vec == 0 && ((uintptr_t)enc & 15) == 0 && ((uintptr_t)enc_out & 15) == 0,
                  "imgcap_sort_gather_rows: 16-byte aligned rows of E elements");
+  IMGCAP_REQUIRE(P >= 1 && P <= 256, "imgcap_sort_gather_rows: 1 <= P <= 256 pixels (LDS stage)");
+  if (B > 32) {  // measured: the row form is faster in the B = 64 step (see sort_gather_row_kernel)
+    if (dtype == IMGCAP_BF16)
+      hipLaunchKernelGGL((sort_gather_row_kernel<bf16>), dim3(B), dim3(256), 0, (hipStream_t)stream, B, P, E, L,
+                         lens, (const bf16*)enc, caps, (bf16*)enc_out, (bf16*)mean_out, caps_out, sort_ind, dl);
+    else
+      hipLaunchKernelGGL((sort_gather_row_kernel<float>), dim3(B), dim3(256), 0, (hipStream_t)stream, B, P, E, L,
+                         lens, (const float*)enc, caps, (float*)enc_out, (float*)mean_out, caps_out, sort_ind, dl);
+    IMGCAP_CHECK_LAUNCH("imgcap_sort_gather_rows");
+    return 0;
+  }
+  // B <= 32: column chunks (C2 step 12.77-12.83k -> 13.04-13.06k img/s, tools/gpu/r3_sortg.sh)
+  const dim3 grid((unsigned)B, (unsigned)((E / vec + 31) / 32));
+  const size_t smem = (size_t)P * 32 * 16;
   if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL((sort_gather_kernel<bf16>), dim3(B), dim3(256), 0, (hipStream_t)stream, B, P, E, L, lens,
+    hipLaunchKernelGGL((sort_gather_kernel<bf16>), grid, dim3(256), smem, (hipStream_t)stream, B, P, E, L, lens,
                        (const bf16*)enc, caps, (bf16*)enc_out, (bf16*)mean_out, caps_out, sort_ind, dl);
   else
-    hipLaunchKernelGGL((sort_gather_kernel<float>), dim3(B), dim3(256), 0, (hipStream_t)stream, B, P, E, L, lens,
+    hipLaunchKernelGGL((sort_gather_kernel<float>), grid, dim3(256), smem, (hipStream_t)stream, B, P, E, L, lens,
                        (const float*)enc, caps, (float*)enc_out, (float*)mean_out, caps_out, sort_ind, dl);
   IMGCAP_CHECK_LAUNCH("imgcap_sort_gather_rows");
   return 0;

@@ -506,12 +506,14 @@ def test_gemm_grouped_weight_gradients(hip_device):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("B", [1, 5, 32, 256])
-def test_sort_gather_rows(hip_device, dtype, B):
+@pytest.mark.parametrize("B,P,E", [(1, 49, 768), (5, 49, 768), (32, 49, 768), (256, 49, 768), (3, 64, 1000),
+                                   (2, 1, 1024)])
+def test_sort_gather_rows(hip_device, dtype, B, P, E):
     """decoder.py:64,79-81 fused: stable descending length sort (ties keep batch order), the
-    gathered encoder rows / captions bit-exact, decode lengths, and the pixel mean."""
+    gathered encoder rows / captions bit-exact, decode lengths, and the pixel mean (column chunks
+    of 32 vectors: a ragged last chunk at E = 1000)."""
     g = torch.Generator(device="cpu").manual_seed(B)
-    P, E, L = 49, 768, 52
+    L = 52
     lens = torch.randint(8, 14, (B, 1), generator=g)  # many ties
     enc = torch.randn(B, P, E, generator=g).to(dtype)
     caps = torch.randint(0, 9490, (B, L), generator=g)
