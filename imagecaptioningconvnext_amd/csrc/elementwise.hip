@@ -119,11 +119,33 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(int n, int dim, const i
                                                          uint32_t stream_id, float* __restrict__ dtable) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= n) return;
+  // the neighbours' ids and this index's position in one round trip
   const int id = sid[i];
-  if (i > 0 && sid[i - 1] == id) return;  // not the first index of its run
+  const int prev = i > 0 ? sid[i - 1] : -1, next = i + 1 < n ? sid[i + 1] : -1;
+  const int pos0 = spos[i];
+  if (prev == id) return;  // not the first index of its run
   const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
   const bool vec = (dim % 8) == 0;
   constexpr int NC = EMB_MAXDIM / 512;
+  if (next != id && vec) {
+    // a one-position run (most ids of a batch): its row and the table row requested together,
+    // the same single addition as the general loop (0 + x * scale, then table += that)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int c0 = c * 512 + lane * 8;
+      if (c0 >= dim) continue;
+      float x[8], t[8];
+      ld_g<T, 8>(dout + (long)pos0 * dim + c0, x);
+      float* tp = dtable + (long)id * dim + c0;
+      *(f32x4*)t = *(const f32x4*)tp;
+      *(f32x4*)(t + 4) = *(const f32x4*)(tp + 4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[k] += 0.f + x[k] * dropout_scale(seed, stream_id, (long)pos0 * dim + c0 + k, p);
+      *(f32x4*)tp = *(const f32x4*)t;
+      *(f32x4*)(tp + 4) = *(const f32x4*)(t + 4);
+    }
+    return;
+  }
   float acc[NC][8];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
