@@ -64,6 +64,38 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(int n, int dim, cons
   }
 }
 
+// dim % 8 == 0: one thread per 8 columns of a position -- the id read once, the table / pe rows
+// as 16-byte loads, 32-bit index math (the element form divides a 64-bit index per element);
+// the same per-element arithmetic (table * dropout scale of element e, then + pe)
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_fwd8_kernel(int n, int dim, const int64_t* __restrict__ ids,
+                                                             const float* __restrict__ table,
+                                                             const float* __restrict__ pe, int L, float p,
+                                                             uint64_t seed0, const uint64_t* seed_ctr, uint32_t sid,
+                                                             T* __restrict__ out) {
+  const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
+  const unsigned d8 = (unsigned)dim >> 3, total = (unsigned)n * d8;
+  for (unsigned g = blockIdx.x * 256u + threadIdx.x; g < total; g += gridDim.x * 256u) {
+    const unsigned r = g / d8, c = (g - r * d8) * 8;
+    const float* tp = table + ids[r] * (long)dim + c;
+    const f32x4 a = *(const f32x4*)tp, b = *(const f32x4*)(tp + 4);
+    float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    const long e0 = (long)r * dim + c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= dropout_scale(seed, sid, e0 + k, p);
+    if (pe) {
+      const float* pp = pe + (long)(r % (unsigned)L) * dim + c;
+      const f32x4 pa = *(const f32x4*)pp, pb = *(const f32x4*)(pp + 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k] += pa[k];
+        v[k + 4] += pb[k];
+      }
+    }
+    st_g<T, 8>(out + e0, v);
+  }
+}
+
 // Deterministic embedding backward (nn.Embedding, decoder.py:84 / transformerDecoder.py:94):
 // dtable[id] += sum over the positions r with ids[r] == id, IN POSITION ORDER, of dout[r]
 // (times the dropout mask of the Transformer path).  No float atomics, so the result is
@@ -427,6 +459,18 @@ extern "C" int imgcap_embedding_fwd(int dtype, int n, int dim, const int64_t* id
   if (n == 0) return 0;
   IMGCAP_REQUIRE(pe == nullptr || L > 0, "imgcap_embedding_fwd: L");
   const long total = (long)n * dim;
+  const bool v8 = dim % 8 == 0 && total < (1L << 31) && ((uintptr_t)table & 15) == 0 && (!pe || ((uintptr_t)pe & 15) == 0) &&
+                  ((uintptr_t)out & 15) == 0;
+  if (v8) {
+    if (dtype == IMGCAP_BF16)
+      hipLaunchKernelGGL(embedding_fwd8_kernel<bf16>, grid_for(total / 8), dim3(256), 0, (hipStream_t)stream, n, dim,
+                         ids, table, pe, L, drop_p, seed, g_seed_ctr, drop_stream, (bf16*)out);
+    else
+      hipLaunchKernelGGL(embedding_fwd8_kernel<float>, grid_for(total / 8), dim3(256), 0, (hipStream_t)stream, n, dim,
+                         ids, table, pe, L, drop_p, seed, g_seed_ctr, drop_stream, (float*)out);
+    IMGCAP_CHECK_LAUNCH("imgcap_embedding_fwd");
+    return 0;
+  }
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(embedding_fwd_kernel<bf16>, grid_for(total), dim3(256), 0, (hipStream_t)stream, n, dim, ids,
                        table, pe, L, drop_p, seed, g_seed_ctr, drop_stream, (bf16*)out);

@@ -304,6 +304,27 @@ def test_embedding_fwd_bwd(hip_device):
     assert _rel(dt_.cpu(), refd) < 1e-5
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("with_pe", [False, True])
+def test_embedding_fwd_vector_form_bitwise(hip_device, dtype, with_pe):
+    """The 8-column form (dim % 8 == 0, 16-byte aligned rows) against the element form (forced by
+    a misaligned output view): bitwise equal, dropout mask included."""
+    g = torch.Generator().manual_seed(3)
+    V, dim, n, L = 9490, 512, 1632, 51
+    table = torch.randn(V, dim, generator=g).to(hip_device)
+    ids = torch.randint(0, V, (n,), generator=g).to(hip_device)
+    pe = torch.randn(L, dim, generator=g).to(hip_device) if with_pe else None
+    out = torch.empty(n, dim, device=hip_device, dtype=dtype)
+    K.embedding_fwd(ids, table, out, pe=pe, L=L, drop_p=0.3, seed=11, drop_stream=4)
+    base = torch.empty(n * dim + 1, device=hip_device, dtype=dtype)
+    out2 = base[1:].view(n, dim)  # 2 / 4 bytes off 16-byte alignment: the element form
+    K.embedding_fwd(ids, table, out2, pe=pe, L=L, drop_p=0.3, seed=11, drop_stream=4)
+    assert torch.equal(out, out2)
+    if not with_pe:
+        kept = (out != 0).float().mean().item()
+        assert 0.6 < kept < 0.8
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
 @pytest.mark.parametrize("H,C", [(56, 96), (28, 192), (14, 384), (7, 768), (8, 256), (16, 128)])
 def test_dwconv7_ln(hip_device, dtype, tol, H, C):
