@@ -950,8 +950,10 @@ bool dw_cp_enabled() {  // IMGCAP_DW_CP=0: the channel-tiled kernels at W = 14 /
 // LN (imgcap_dwconv7_ln): the LayerNorm in the epilogue (a first form with 2 x W wave sums per
 // lane measured 1.1-2.4x slower than this kernel + add_layernorm; the LDS form above reduces each
 // pixel once per block).
-bool dw_cp_fits(int W, int C) {
-  return dw_cp_enabled() && (W == 7 || W == 14) && C % 128 == 0 && C <= 1024;
+// C <= 1024 with the LayerNorm (one block holds every channel of a pixel: at most 8 waves);
+// without it any C % 128 == 0 (channel-group blocks), e.g. ConvNeXt-Large stage 4, C = 1536
+bool dw_cp_fits(int W, int C, bool ln) {
+  return dw_cp_enabled() && (W == 7 || W == 14) && C % 128 == 0 && (!ln || C <= 1024);
 }
 
 // Output rows per block.  Measured (tools/dw_ln_bench.py, us, one vs two rows): without LN Large
@@ -1110,7 +1112,7 @@ int dwconv7_seg_launch(int B, int H, int W, int C, const void* x, const float* w
 template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
                    hipStream_t st, const void* res = nullptr, int flip = 0) {
-  if (sizeof(T) == 2 && dw_cp_fits(W, C))
+  if (sizeof(T) == 2 && dw_cp_fits(W, C, false))
     return dwconv7_cp_launch(B, H, W, C, x, w, bias, nullptr, nullptr, y, res, flip, st);
   if (sizeof(T) == 2 && dw_seg_fits(W, C)) return dwconv7_seg_launch(B, H, W, C, x, w, bias, y, res, flip, st);
   // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups.
@@ -1302,7 +1304,7 @@ extern "C" int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const vo
   IMGCAP_REQUIRE(x != out, "imgcap_dwconv7_ln: in-place not supported");
   if ((long)B * H * W == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == IMGCAP_BF16 && dw_cp_fits(W, C))
+  if (dtype == IMGCAP_BF16 && dw_cp_fits(W, C, true))
     return dwconv7_cp_launch(B, H, W, C, x, w, bias, ln_w, ln_b, out, nullptr, 0, st);
   if (dtype == IMGCAP_BF16) {
     if (W % 7 == 0) return launch_dw<bf16, 7>(B, H, W, C, x, w, bias, ln_w, ln_b, out, st);

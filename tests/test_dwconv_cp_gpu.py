@@ -1,5 +1,6 @@
 """Depthwise 7x7 for the narrow late stages (the channel-pair kernel of convnext.hip: W = 7 and 14,
-C <= 1024, bf16; one or two output rows per block, IMGCAP_DW_CP_R) against torch fp32 conv2d(groups=C) on the bf16-rounded input and against
+C <= 1024 with the fused LayerNorm, any C % 128 == 0 without; bf16; one or two output rows per
+block, IMGCAP_DW_CP_R) against torch fp32 conv2d(groups=C) on the bf16-rounded input and against
 the channel-tiled kernel (IMGCAP_DW_CP=0), plain and in the backward data-gradient form (flipped
 taps + residual, odd H with two rows per block); C = 768 runs 2-wave channel-group blocks, and imgcap_dwconv7_ln
 (row kernel) against torch LayerNorm of the same conv."""
@@ -28,7 +29,8 @@ def _ref(x, w49, bias, flip=False):
 
 
 @pytest.mark.parametrize("rows", ["1", "2"])
-@pytest.mark.parametrize("B,H,C", [(3, 14, 384), (2, 14, 512), (2, 7, 768), (3, 7, 1024), (1, 14, 1024), (2, 14, 768)])
+@pytest.mark.parametrize("B,H,C", [(3, 14, 384), (2, 14, 512), (2, 7, 768), (3, 7, 1024), (1, 14, 1024), (2, 14, 768),
+                                   (2, 7, 1536)])
 def test_dwconv_cp_matches_torch(hip_device, monkeypatch, rows, B, H, C):
     monkeypatch.setenv("IMGCAP_DW_CP_R", rows)
     g = torch.Generator(device="cpu").manual_seed(B * H + C)
@@ -56,7 +58,7 @@ def test_dwconv_cp_matches_torch(hip_device, monkeypatch, rows, B, H, C):
 
 
 @pytest.mark.parametrize("rows", ["1", "2"])
-@pytest.mark.parametrize("H,C", [(14, 384), (7, 768)])
+@pytest.mark.parametrize("H,C", [(14, 384), (7, 768), (7, 1536)])
 def test_dwconv_cp_backward_data_form(hip_device, monkeypatch, rows, H, C):
     """Flipped taps + residual (imgcap_dwconv7_bwd_data's use of the forward kernel)."""
     monkeypatch.setenv("IMGCAP_DW_CP_R", rows)
