@@ -109,6 +109,79 @@ __global__ __launch_bounds__(256) void dwconv7_wgrad_kernel(int B, int H, int W,
   }
 }
 
+// W = 7 (the last stage): a wave's image row is 7 pixels, so the sliding window above spends
+// its time waiting on one dependent load pair per output pixel (C5's fine-tuned stage 4: ~107 us
+// per call).  Here the row's 7 gradient pixels and the 7 x 7 input window are requested at once
+// (fully unrolled: 56 loads in flight per lane) and the 49 taps accumulate from registers; the
+// per-tap sums keep the sliding form's order (output pixels w = 0..6 per kernel row, kernel rows
+// in order, image rows in order), and the block reduction is the same.
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv7_wgrad_w7_kernel(int B, int H, int C, const T* __restrict__ dz,
+                                                               const T* __restrict__ x, float* __restrict__ ws,
+                                                               int rows_per_wave) {
+  constexpr int W = 7;
+  __shared__ float red[4][WG_CH][51];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * WG_CH + 2 * lane;
+  const int cc = c < C ? c : 0;
+  float acc[49][2], accb[2] = {0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 49; ++t) acc[t][0] = acc[t][1] = 0.f;
+  const long R = (long)B * H;
+  const long r0 = ((long)blockIdx.y * 4 + wv) * rows_per_wave;
+  const long r1 = std::min<long>(R, r0 + rows_per_wave);
+  for (long r = r0; r < r1; ++r) {
+    const int h = (int)(r % H);
+    float g[W][2], xw[7][W][2];
+    const T* drow = dz + r * W * C + cc;
+#pragma unroll
+    for (int w = 0; w < W; ++w) ld2<T>(drow + (long)w * C, g[w][0], g[w][1]);
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      const int ih = h + kh - 3;
+      const bool ok = ih >= 0 && ih < H;
+      const T* xrow = x + (ok ? r + kh - 3 : r) * W * C + cc;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        ld2<T>(xrow + (long)w * C, xw[kh][w][0], xw[kh][w][1]);
+        if (!ok) xw[kh][w][0] = xw[kh][w][1] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      accb[0] += g[w][0];
+      accb[1] += g[w][1];
+    }
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      if (h + kh - 3 < 0 || h + kh - 3 >= H) continue;  // the sliding form skips these rows too
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+#pragma unroll
+        for (int kw = 0; kw < 7; ++kw) {
+          const int iw = w + kw - 3;
+          const float x0 = (iw >= 0 && iw < W) ? xw[kh][iw][0] : 0.f, x1 = (iw >= 0 && iw < W) ? xw[kh][iw][1] : 0.f;
+          acc[kh * 7 + kw][0] += g[w][0] * x0;
+          acc[kh * 7 + kw][1] += g[w][1] * x1;
+        }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 49; ++t) {
+    red[wv][2 * lane][t] = acc[t][0];
+    red[wv][2 * lane + 1][t] = acc[t][1];
+  }
+  red[wv][2 * lane][49] = accb[0];
+  red[wv][2 * lane + 1][49] = accb[1];
+  __syncthreads();
+  for (int e = threadIdx.x; e < WG_CH * 50; e += 256) {
+    const int cl = e / 50, t = e % 50;
+    const int ch = blockIdx.x * WG_CH + cl;
+    if (ch < C)
+      ws[((long)blockIdx.y * C + ch) * 50 + t] = ((red[0][cl][t] + red[1][cl][t]) + red[2][cl][t]) + red[3][cl][t];
+  }
+}
+
 // t_i = sum_s ws[s * ld + i] for i < n (fixed slice order), stored as
 //   split == 0 : out0[i] = beta*out0[i] + t_i
 //   split > 0  : i < split -> out0[i], else out1[i - split]   (both with beta)
@@ -306,7 +379,15 @@ extern "C" int imgcap_dwconv7_wgrad(int dtype, int B, int H, int W, int C, const
   if (!ws) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_dwconv7_wgrad: ") + last_error());
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid(cblocks, slices);
-  if (dtype == IMGCAP_BF16)
+  const char* we = getenv("IMGCAP_DW_WGRAD_W7");  // 0: the sliding-window kernel at W = 7 too (A/B)
+  const bool w7 = W == 7 && !(we && *we == '0');
+  if (w7 && dtype == IMGCAP_BF16)
+    hipLaunchKernelGGL(dwconv7_wgrad_w7_kernel<bf16>, grid, dim3(256), 0, st, B, H, C, (const bf16*)dz,
+                       (const bf16*)x, ws, rpw);
+  else if (w7)
+    hipLaunchKernelGGL(dwconv7_wgrad_w7_kernel<float>, grid, dim3(256), 0, st, B, H, C, (const float*)dz,
+                       (const float*)x, ws, rpw);
+  else if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(dwconv7_wgrad_kernel<bf16>, grid, dim3(256), 0, st, B, H, W, C, (const bf16*)dz,
                        (const bf16*)x, ws, rpw);
   else

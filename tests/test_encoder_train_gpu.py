@@ -22,7 +22,7 @@ def _g(seed):
 
 
 # ---- kernels ------------------------------------------------------------------------------
-@pytest.mark.parametrize("H,C", [(7, 96), (14, 64), (56, 96)])
+@pytest.mark.parametrize("H,C", [(7, 96), (14, 64), (56, 96), (7, 1536), (7, 160)])  # W = 7: the unrolled wgrad
 def test_dwconv7_backward(hip_device, H, C):
     from imagecaptioningconvnext_amd import kernels as K
     B = 2
