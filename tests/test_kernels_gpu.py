@@ -408,15 +408,15 @@ def test_cnblock_mlp_with_layernorm(hip_device, C, M):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
-@pytest.mark.parametrize("C0,HW", [(96, 224), (128, 224), (192, 256)])
-def test_stem(hip_device, dtype, tol, C0, HW):
+@pytest.mark.parametrize("C0,HW,B", [(96, 224, 2), (128, 224, 2), (192, 256, 2), (192, 224, 24)])  # last: > 1024 groups
+def test_stem(hip_device, dtype, tol, C0, HW, B):
     torch.manual_seed(C0)
-    img = torch.randn(2, 3, HW, HW)
+    img = torch.randn(B, 3, HW, HW)
     w = torch.randn(C0, 3, 4, 4) * 0.1
     b, lw, lb = torch.randn(C0), torch.randn(C0), torch.randn(C0)
     ref = F.conv2d(img, w, b, stride=4).permute(0, 2, 3, 1)
     ref = F.layer_norm(ref, (C0,), lw, lb, 1e-6)
-    out = torch.empty(2, HW // 4, HW // 4, C0, dtype=dtype, device=hip_device)
+    out = torch.empty(B, HW // 4, HW // 4, C0, dtype=dtype, device=hip_device)
     K.convnext_stem(img.to(hip_device), w.view(C0, 48).contiguous().to(hip_device), b.to(hip_device),
                     lw.to(hip_device), lb.to(hip_device), out)
     assert _rel(out.cpu(), ref) < tol
