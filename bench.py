@@ -6,9 +6,10 @@
 ``--gpus N`` without a launcher (no WORLD_SIZE in the environment) starts the N rank processes
 itself, before anything touches the GPU, and exits with their status.
 
-Default workload = BASELINE.json configs[1] (C2): ConvNeXt-Tiny encoder (frozen, train mode)
-+ LSTM-attention decoder, teacher forced, 32 images per GPU, 224x224x3, captions of length
-52 (decode length 51), vocab 9490, bf16 compute / fp32 master weights + Adam.  One step =
+Default workload = BASELINE.json configs[2] (C3), the largest single-GPU configuration (the
+metric names no config): ConvNeXt-Tiny encoder (frozen, train mode) + Transformer decoder,
+teacher forced, 64 images per GPU, 224x224x3, captions of length 52, vocab 9490, bf16 compute /
+fp32 master weights + Adam.  --config C2 (Tiny + LSTM, B=32), C4, C5 select the others.  One step =
 the full train.py:251-299 body (encoder fwd, decoder fwd, CE + alpha reg, backward, RCCL grad
 all-reduce when N > 1, clip + Adam, metrics).  Synthetic data, pre-generated in HBM; weights
 randomly initialised (no network).  Per-GPU work is fixed as N grows ("scaling": "weak").
@@ -46,7 +47,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -190,10 +191,44 @@ def cpu_model():
     return platform.processor() or None
 
 
+def physical_cores():
+    """Physical cores this process may run on: distinct (package, core) pairs of the CPUs in its
+    affinity mask (/proc/cpuinfo), capped by the cgroup CPU quota (cpu.max) when one is set --
+    the GPU box grants each GPU a share of a larger host.  Returns (cores, detail)."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    pairs, cur = {}, {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ":" not in ln:
+                    if "processor" in cur:
+                        pairs[cur["processor"]] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+                    cur = {}
+                    continue
+                k, v = (s.strip() for s in ln.split(":", 1))
+                cur[k] = v
+        if "processor" in cur:
+            pairs[cur["processor"]] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+    except OSError:
+        pass
+    phys = len({pairs.get(str(c), (None, c)) for c in cpus}) or len(cpus)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    cores = min(phys, quota) if quota else phys
+    return cores, f"{phys} physical cores in the affinity mask ({len(cpus)} logical)" + (
+        f", cgroup quota {quota} CPUs" if quota else "")
+
+
 def cpu_baseline(seconds):
     """Oracle (plain PyTorch CPU restatement) of the C1 train step: Tiny + LSTM, B=4, fp32."""
     from oracle import convnext, decoders, shapes, train_step
-    nthreads = min(16, os.cpu_count() or 1)
+    nthreads, core_detail = physical_cores()
     torch.set_num_threads(nthreads)
     B, E = 4, 768
     sd = convnext.init_params("tiny")
@@ -220,7 +255,8 @@ def cpu_baseline(seconds):
             n += 1
         if (t_steps >= seconds and n >= 2) or step >= 50:
             break
-    return dict(value=round(B * n / t_steps, 3), unit="images/s", cores=nthreads, kind="port", cpu=cpu_model(),
+    return dict(value=round(B * n / t_steps, 3), unit="images/s", cores=nthreads, cores_detail=core_detail,
+                kind="port", cpu=cpu_model(),
                 sample=f"oracle C1 train step (ConvNeXt-Tiny + LSTM-attention, B=4, fp32, 224x224, L=52, "
                        f"V={V}), {n} timed steps after 1 warm-up, {t_steps:.1f} s")
 

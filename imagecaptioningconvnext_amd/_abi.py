@@ -99,9 +99,7 @@ _SIGS = {
     "imgcap_ce_fused": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                         c_void_p, c_int64, c_void_p],
     "imgcap_clamp_adam": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
-                          c_float, c_int, c_float, c_float, c_void_p],
-    "imgcap_clamp_adam_dev": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
-                              c_void_p, c_float, c_float, c_void_p],
+                          c_float, c_int, c_float, c_float, c_void_p, c_void_p],
     "imgcap_lstm_tf_fwd": [ctypes.POINTER(LstmDesc), c_void_p],
     "imgcap_lstm_tf_bwd": [ctypes.POINTER(LstmDesc), c_void_p],
     "imgcap_lstm_sync_words": [ctypes.POINTER(LstmDesc)],

@@ -13,11 +13,10 @@ __global__ __launch_bounds__(256) void clamp_adam_kernel(long n, float* __restri
                                                          float* __restrict__ m, float* __restrict__ v,
                                                          bf16* __restrict__ shadow, float lr, float b1, float b2,
                                                          float eps, float step_size, float bc2_sqrt, float clip,
-                                                         float inv_div, const float* __restrict__ scal) {
-  if (scal) {  // imgcap_clamp_adam_dev: the step's bias-corrected scalars from device memory
-    step_size = scal[0];
-    bc2_sqrt = scal[1];
-  }
+                                                         float inv_div, const float* __restrict__ skip) {
+  // a step whose persistent LSTM hand-off timed out (its metrics' error word) leaves the
+  // parameters and moments untouched: its gradients are invalid
+  if (skip && *skip != 0.f) return;
   const long n4 = n / 4;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     f32x4 gg = ((const f32x4*)g)[i], mm = ((f32x4*)m)[i], vv = ((f32x4*)v)[i], pp = ((f32x4*)p)[i];
@@ -422,7 +421,7 @@ using namespace imgcap;
 
 extern "C" int imgcap_clamp_adam(int64_t n, float* param, const float* grad, float* m, float* v, void* shadow_bf16,
                                  float lr, float beta1, float beta2, float eps, int step, float clip, float grad_div,
-                                 void* stream) {
+                                 const float* skip, void* stream) {
   if (n == 0) return 0;
   IMGCAP_REQUIRE(step >= 1, "imgcap_clamp_adam: step must be >= 1");
   IMGCAP_REQUIRE(aligned16(param) && aligned16(grad) && aligned16(m) && aligned16(v),
@@ -432,25 +431,8 @@ extern "C" int imgcap_clamp_adam(int64_t n, float* param, const float* grad, flo
   const double bc2 = 1.0 - std::pow((double)beta2, step);
   hipLaunchKernelGGL(clamp_adam_kernel, grid_for(n / 4 + 1), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad,
                      m, v, (bf16*)shadow_bf16, lr, beta1, beta2, eps, (float)(lr / bc1), (float)std::sqrt(bc2), clip,
-                     1.0f / grad_div, nullptr);
+                     1.0f / grad_div, skip);
   IMGCAP_CHECK_LAUNCH("imgcap_clamp_adam");
-  return 0;
-}
-
-// The same update with the step's scalars read from device memory at run time (scal[0] = the
-// float of lr / (1 - beta1^t), scal[1] = the float of sqrt(1 - beta2^t), computed as above by the
-// caller), so a captured graph can carry the optimizer step while the step count advances.
-extern "C" int imgcap_clamp_adam_dev(int64_t n, float* param, const float* grad, float* m, float* v, void* shadow_bf16,
-                                     float beta1, float beta2, float eps, const float* scal, float clip,
-                                     float grad_div, void* stream) {
-  if (n == 0) return 0;
-  IMGCAP_REQUIRE(scal != nullptr, "imgcap_clamp_adam_dev: scal");
-  IMGCAP_REQUIRE(aligned16(param) && aligned16(grad) && aligned16(m) && aligned16(v),
-                 "imgcap_clamp_adam_dev: buffers must be 16-byte aligned");
-  IMGCAP_REQUIRE(shadow_bf16 == nullptr || (((uintptr_t)shadow_bf16) & 7) == 0, "imgcap_clamp_adam_dev: shadow align");
-  hipLaunchKernelGGL(clamp_adam_kernel, grid_for(n / 4 + 1), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad,
-                     m, v, (bf16*)shadow_bf16, 0.f, beta1, beta2, eps, 0.f, 1.f, clip, 1.0f / grad_div, scal);
-  IMGCAP_CHECK_LAUNCH("imgcap_clamp_adam_dev");
   return 0;
 }
 

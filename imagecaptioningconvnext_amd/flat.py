@@ -51,8 +51,6 @@ class FlatParams:
                 p.data = self.flat[o:o + n].view(shp)
                 p.grad = self.grad[o:o + n].view(shp)
         self.step_count = 0
-        self._scal = torch.zeros(2, **f32)  # the step's Adam scalars for adam_dev (adam_scalars)
-        self._scal_host = None
         self._shadow_version = None
         self.refresh_shadow()
 
@@ -115,43 +113,12 @@ class FlatParams:
     def zero_grad(self):
         self.grad.zero_()
 
-    def adam_scalars(self, lr, betas=(0.9, 0.999)):
-        """Advance the step count and write that step's bias-corrected Adam scalars to the device
-        (an H2D copy on the current stream, before the kernels that read them: adam_dev, whose
-        launches a captured graph can hold).  The same float values imgcap_clamp_adam derives on
-        the host: (float)(lr / (1 - b1^t)), (float)sqrt(1 - b2^t), with lr, b1, b2 as floats."""
-        self.step_count += 1
-        t = self.step_count
-        lr32, b1, b2 = (float(np.float32(x)) for x in (lr, betas[0], betas[1]))
-        bc1, bc2 = 1.0 - b1 ** t, 1.0 - b2 ** t
-        # a pageable host tensor made this copy wait for the device (the host could not run ahead:
-        # C2 12.8k -> 11.8k img/s); pinned slots, each reused only once its last copy has run
-        if self._scal_host is None:
-            self._scal_host = torch.zeros(4, 2, dtype=torch.float32).pin_memory()
-            self._scal_ev = [None] * 4
-        i = t % 4
-        if self._scal_ev[i] is not None:
-            self._scal_ev[i].synchronize()
-        self._scal_host[i, 0] = float(np.float32(lr32 / bc1))
-        self._scal_host[i, 1] = float(np.float32(math.sqrt(bc2)))
-        self._scal.copy_(self._scal_host[i], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self._scal_ev[i] = ev
-
-    def adam_dev(self, lo, hi, clip, grad_div=1.0, betas=(0.9, 0.999), eps=1e-8):
-        """clip + Adam over flat[lo:hi] with the scalars adam_scalars wrote (the whole-buffer
-        update split into ranges whose gradients are final at different points of the backward;
-        every element's update is the one adam_step makes)."""
-        sh = None if self.shadow is None else self.shadow[lo:hi]
-        K.clamp_adam_dev(self.flat[lo:hi], self.grad[lo:hi], self.m[lo:hi], self.v[lo:hi], sh, self._scal, clip,
-                         grad_div=grad_div, betas=betas, eps=eps)
-        self._shadow_version = self.flat._version  # kernel wrote flat + shadow through raw pointers
-
-    def adam_step(self, lr, clip, grad_div=1.0, betas=(0.9, 0.999), eps=1e-8):
-        """clip_gradient (clamp +-clip) then Adam, fused; refreshes the bf16 shadow."""
+    def adam_step(self, lr, clip, grad_div=1.0, betas=(0.9, 0.999), eps=1e-8, skip=None):
+        """clip_gradient (clamp +-clip) then Adam, fused; refreshes the bf16 shadow.  ``skip``: a
+        device fp32 word (the step's hand-off error count); nonzero at run time leaves the
+        parameters, moments and shadow unchanged (the step count still advances)."""
         self.sync_shadow()
         self.step_count += 1
         K.clamp_adam(self.flat, self.grad, self.m, self.v, self.shadow, lr, self.step_count, clip,
-                     grad_div=grad_div, betas=betas, eps=eps)
+                     grad_div=grad_div, betas=betas, eps=eps, skip=skip)
         self._shadow_version = self.flat._version  # kernel wrote flat + shadow through raw pointers

@@ -356,18 +356,11 @@ def loss_finalize(loss_rows, hit5, targets, extra, out):
               ptr(extra), out.data_ptr(), stream())
 
 
-def clamp_adam(param, grad, m, v, shadow, lr, step, clip, grad_div=1.0, betas=(0.9, 0.999), eps=1e-8):
+def clamp_adam(param, grad, m, v, shadow, lr, step, clip, grad_div=1.0, betas=(0.9, 0.999), eps=1e-8, skip=None):
+    """skip: optional device fp32 word; a nonzero value at run time leaves every buffer as it was."""
     _abi.call("imgcap_clamp_adam", param.numel(), param.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(),
               ptr(shadow), lr, betas[0], betas[1], eps, step, clip if clip is not None else 3.4e38, grad_div,
-              stream())
-
-
-def clamp_adam_dev(param, grad, m, v, shadow, scal, clip, grad_div=1.0, betas=(0.9, 0.999), eps=1e-8):
-    """clamp_adam with the step's bias-corrected scalars read from ``scal`` (device, [2]) at run
-    time (FlatParams.adam_scalars writes them): capturable in a graph."""
-    _abi.call("imgcap_clamp_adam_dev", param.numel(), param.data_ptr(), grad.data_ptr(), m.data_ptr(), v.data_ptr(),
-              ptr(shadow), betas[0], betas[1], eps, scal.data_ptr(), clip if clip is not None else 3.4e38, grad_div,
-              stream())
+              ptr(skip), stream())
 
 
 def greedy_select(logits, V, t, end_id, finished, next_ids, sequences, predictions, alpha=None, alphas=None):

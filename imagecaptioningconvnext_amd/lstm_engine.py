@@ -413,15 +413,12 @@ class LstmEngine:
         GEMMs of the rest still run (DDP-style bucketed all-reduce)."""
         return self.fp.span(["embedding.weight", "fc.weight", "fc.bias"])
 
-    def backward(self, s, dlogits=None, dalpha=None, gbuf=None, want_denc=False, bucket_hook=None, adam=None):
+    def backward(self, s, dlogits=None, dalpha=None, gbuf=None, want_denc=False, bucket_hook=None):
         """Writes dL/dparams into ``gbuf`` (default: the flat grad buffer).  Default upstream:
         the fused loss of forward(loss=True); otherwise ``dlogits`` [B*T, V(pad)] (compute
         dtype) and ``dalpha`` [B, T, P] (f32).  want_denc: also dL/d encoder_out (fp32, the
         caller's batch order) into s["denc"] -- encoder fine-tuning.  ``bucket_hook`` is called
-        (on the current stream's timeline) once the early_bucket() gradients are final.
-        ``adam`` (dict: clip, grad_div): also apply clip + Adam (FlatParams.adam_dev, the scalars
-        of FlatParams.adam_scalars) -- the fc and embedding ranges on the side stream as soon as
-        their gradients are final (fc beside the backward recurrence), the rest at the end."""
+        (on the current stream's timeline) once the early_bucket() gradients are final."""
         fp, ct = self.fp, self.ct
         gbuf = fp.grad if gbuf is None else gbuf
 
@@ -457,11 +454,6 @@ class LstmEngine:
             ev_fc = torch.cuda.Event()  # gbuf cleared, fc dW / db written
             ev_fc.record(side)
         par_tail = bucket_hook is None and not want_denc and ct == torch.bfloat16
-        if adam is not None and gbuf is not fp.grad:
-            raise ValueError("backward(adam=...) updates the flat parameters from their own grad buffer")
-        if adam is not None and par_tail:
-            with torch.cuda.stream(side):  # fc.weight / fc.bias: final; not read again this step
-                fp.adam_dev(*fp.span(["fc.weight", "fc.bias"]), **adam)
         f32 = dict(device=dev, dtype=torch.float32)
         dcat = torch.empty(B, T, W3, device=dev, dtype=ct)
         xs, ys = self.X_SLICES, self.Y_SLICES
@@ -511,8 +503,6 @@ class LstmEngine:
                     self._fold_status(s["metrics"][4:5])  # the backward recurrence's error word
                 demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
                 K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
-                if adam is not None:
-                    fp.adam_dev(*fp.span(["embedding.weight"]), **adam)
             main.wait_event(ev_fc)
         elif "metrics" in s:
             self._fold_status(s["metrics"][4:5])
@@ -544,10 +534,6 @@ class LstmEngine:
         cb.run()
         if par_tail:
             main.wait_stream(side)  # the embedding gradient and the metrics' error word
-        if adam is not None:
-            # every other parameter (whose gradients the grouped GEMMs / column sums just wrote);
-            # without the side-stream tail, the whole buffer here
-            fp.adam_dev(0, fp.span(["embedding.weight"])[0] if par_tail else fp.numel, **adam)
         s["denc"] = None
         if want_denc:
             # decoder.py:26 (att1 = enc W_ea), :64-66 (mean -> init_h/c), :102-103 (context)

@@ -134,6 +134,10 @@ class Encoder(nn.Module):
         # (train_step drops them when it re-captures)
         self._retired_packs = []
         self._engine = None
+        # bumped by weights_updated() after every fine-tuned optimizer step: the engine's Adam
+        # writes the trainable children through raw pointers, which bumps no tensor version
+        self._weights_epoch = 0
+        self._packed_epoch = 0
         self.fine_tune()
 
     def fine_tune(self, fine_tune=True, startingLayer=7):
@@ -165,29 +169,60 @@ class Encoder(nn.Module):
                            stem_ln.bias.float().contiguous())}
             stages = []
             for st in range(4):
-                blocks = []
-                for blk in f[1 + 2 * st]:
-                    dw, ln, l1, l2 = blk.block[0], blk.block[2], blk.block[3], blk.block[5]
-                    C = dw.out_channels
-                    blocks.append(dict(
-                        w49=dw.weight.reshape(C, 49).t().float().contiguous(), dwb=dw.bias.float().contiguous(),
-                        lnw=ln.weight.float().contiguous(), lnb=ln.bias.float().contiguous(),
-                        w1=l1.weight.to(ct).contiguous(), b1=l1.bias.float().contiguous(),
-                        w2=l2.weight.to(ct).contiguous(), b2=l2.bias.float().contiguous(),
-                        gamma=blk.layer_scale.reshape(C).float().contiguous(), sd=blk.sd_prob))
-                    if self._mx_stage(C):  # fp8 copies of the frozen Linear weights (rows = outputs)
-                        blocks[-1].update(w1mx=K.mx_quant_rows(l1.weight.float().contiguous()),
-                                          w2mx=K.mx_quant_rows(l2.weight.float().contiguous()))
-                down = None
-                if st < 3:
-                    ln, cv = f[2 + 2 * st][0], f[2 + 2 * st][1]
-                    down = dict(lnw=ln.weight.float().contiguous(), lnb=ln.bias.float().contiguous(),
-                                w=cv.weight.permute(0, 2, 3, 1).reshape(cv.out_channels, -1).to(ct).contiguous(),
-                                b=cv.bias.float().contiguous())
+                blocks = [self._pack_block(blk) for blk in f[1 + 2 * st]]
+                down = self._pack_down(f[2 + 2 * st]) if st < 3 else None
                 stages.append((blocks, down))
             pk["stages"] = stages
         self._packed, self._packed_key = pk, key
+        self._packed_epoch = self._weights_epoch
         return pk
+
+    def _pack_block(self, blk):
+        ct = self.compute_dtype
+        dw, ln, l1, l2 = blk.block[0], blk.block[2], blk.block[3], blk.block[5]
+        C = dw.out_channels
+        d = dict(w49=dw.weight.reshape(C, 49).t().float().contiguous(), dwb=dw.bias.float().contiguous(),
+                 lnw=ln.weight.float().contiguous(), lnb=ln.bias.float().contiguous(),
+                 w1=l1.weight.to(ct).contiguous(), b1=l1.bias.float().contiguous(),
+                 w2=l2.weight.to(ct).contiguous(), b2=l2.bias.float().contiguous(),
+                 gamma=blk.layer_scale.reshape(C).float().contiguous(), sd=blk.sd_prob)
+        if self._mx_stage(C):  # fp8 copies of the frozen Linear weights (rows = outputs)
+            d.update(w1mx=K.mx_quant_rows(l1.weight.float().contiguous()),
+                     w2mx=K.mx_quant_rows(l2.weight.float().contiguous()))
+        return d
+
+    def _pack_down(self, seq):
+        ln, cv = seq[0], seq[1]
+        return dict(lnw=ln.weight.float().contiguous(), lnb=ln.bias.float().contiguous(),
+                    w=cv.weight.permute(0, 2, 3, 1).reshape(cv.out_channels, -1).to(self.compute_dtype).contiguous(),
+                    b=cv.bias.float().contiguous())
+
+    def weights_updated(self):
+        """The fine-tuned children's weights changed behind torch's back (EncoderEngine's Adam
+        writes its flat buffer through raw pointers): the packed copies the frozen fast path reads
+        for those children are refreshed before their next use (_run_frozen over them, e.g.
+        validation under no_grad)."""
+        self._weights_epoch += 1
+
+    def _refresh_trainable(self, pk, upto):
+        """Re-derive, in place, the packed entries of trainable children below ``upto`` (captured
+        graphs keep their pointers; the frozen prefix is untouched)."""
+        f = self.convnext
+        with torch.no_grad():
+            for st, (blocks, down) in enumerate(pk["stages"]):
+                ci = 1 + 2 * st
+                if ci < upto and any(p.requires_grad for p in f[ci].parameters()):
+                    for d, blk in zip(blocks, f[ci]):
+                        for k, v in self._pack_block(blk).items():
+                            if torch.is_tensor(v):
+                                d[k].copy_(v)
+                            elif isinstance(v, tuple):
+                                for a, b in zip(d[k], v):
+                                    a.copy_(b)
+                if down is not None and ci + 1 < upto and any(p.requires_grad for p in f[ci + 1].parameters()):
+                    for k, v in self._pack_down(f[ci + 1]).items():
+                        down[k].copy_(v)
+        self._packed_epoch = self._weights_epoch
 
     def _mx_stage(self, C):
         return (self.frozen_fp8 and self.compute_dtype == torch.bfloat16 and C not in K.CNBLOCK_MLP_CHANNELS
@@ -210,6 +245,8 @@ class Encoder(nn.Module):
         """Stem + children [1, upto) of the trunk on the frozen fast path (no saved state).
         Returns (x NHWC in the compute dtype, index of the next CNBlock for the SD scales)."""
         pk = self._pack()
+        if self._packed_epoch != self._weights_epoch:
+            self._refresh_trainable(pk, upto)
         ct = self.compute_dtype
         B, _, H, W = images.shape
         dev = images.device

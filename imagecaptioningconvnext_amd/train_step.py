@@ -42,11 +42,6 @@ PIPE_SPLIT = int(os.environ.get("IMGCAP_PIPE_SPLIT", "0"))
 # Measured (bench, 1x MI355X, two runs each): C2 8,254 vs 8,366 img/s (within spread), C3 16,605
 # vs 15,108, C4 7,007 vs 6,117 -- "start" stays the default.
 PIPE_FORK = os.environ.get("IMGCAP_PIPE_FORK", "start")
-# the decoder's clip + Adam inside its backward (TeacherForcedTrainer._inline_adam; 1) or after it
-# (0, default).  Same-box A/B at C2 (tools/gpu/ab_adam.sh, three rounds): inside 12.80-12.89k,
-# after 12.89-12.94k img/s -- the fc range's update (147 MB of HBM traffic) beside the backward
-# recurrence costs it more than the ~25 us it takes off the step's tail
-INLINE_ADAM = os.environ.get("IMGCAP_INLINE_ADAM", "0") == "1"
 
 
 def _trainable(encoder):
@@ -181,27 +176,12 @@ class TeacherForcedTrainer:
             return self.enc_eng.forward(imgs)
         return self._encode(imgs), None
 
-    def _fwd_bwd(self, imgs, caps, caplens, adam=False):
+    def _fwd_bwd(self, imgs, caps, caplens):
         feats, es = self._enc_part(imgs)
         self._feat_meta = (tuple(feats.shape), feats.dtype)
-        return self._dec(feats, caps, caplens, es, adam=adam)
+        return self._dec(feats, caps, caplens, es)
 
-    # ---- clip + Adam inside the decoder's backward (one rank, LSTM, bf16, frozen encoder) --------
-    def _inline_adam(self):
-        """The decoder's clip + Adam runs inside its backward (LstmEngine.backward(adam=...): the
-        fc / embedding ranges on the side stream as soon as their gradients are final, the rest
-        at the end; captured in the step's graph) instead of after it: one rank (with DDP the
-        update waits for the all-reduce), LSTM, bf16, frozen encoder."""
-        return (INLINE_ADAM and self.world == 1 and self.lstm and self.enc_eng is None
-                and getattr(self.eng, "ct", None) == torch.bfloat16)
-
-    def _prep_adam(self):
-        """Before a decoder pass that applies the update itself (eager or a graph replay): this
-        step's Adam scalars (FlatParams.adam_scalars; _update then skips adam_step)."""
-        if self._inline_adam():
-            self.eng.fp.adam_scalars(self.decoder_lr)
-
-    def _dec(self, feats, caps, caplens, es=None, mid=None, adam=False):
+    def _dec(self, feats, caps, caplens, es=None, mid=None):
         self.decoder.train()
         if self.lstm:
             s = self.eng.forward(feats, caps, caplens, fixed_T=self._cur_T if self._cur_T else True, alphaC=self.alphaC)
@@ -221,8 +201,6 @@ class TeacherForcedTrainer:
             self.enc_eng.backward(es, s["denc"].reshape(feats.shape))
         else:
             kw = {"bucket_hook": self._bucket_hook} if hook else {}
-            if adam and self._inline_adam():
-                kw["adam"] = dict(clip=self.grad_clip, grad_div=float(self.world))
             self.eng.backward(s, **kw)
         return s["metrics"]
 
@@ -317,7 +295,7 @@ class TeacherForcedTrainer:
             return
         gd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gd):
-            self._metrics = self._dec(self._feat_slot, self._inputs[1], self._inputs[2], es, adam=True)
+            self._metrics = self._dec(self._feat_slot, self._inputs[1], self._inputs[2], es)
         self._graph = _SeqGraphs(ge, gd)
 
     # ---- encoder / decoder pipeline ------------------------------------------------------------
@@ -366,7 +344,7 @@ class TeacherForcedTrainer:
                 pool_e = ge.pool()
                 gd = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gd, pool=pool_d):
-                    m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k], adam=True)
+                    m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k])
                 pool_d = gd.pool()
                 S["genc"].append(ge)
                 S["gdec"].append(gd)
@@ -394,7 +372,7 @@ class TeacherForcedTrainer:
                 if PIPE_FORK != "bwd":
                     fork()
                 m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k],
-                              mid=fork if PIPE_FORK == "bwd" else None, adam=True)
+                              mid=fork if PIPE_FORK == "bwd" else None)
                 cur.wait_stream(side)
                 if split:
                     self._end_split_capture(g2)
@@ -421,8 +399,7 @@ class TeacherForcedTrainer:
             m = None
             if P["pending"] is not None:
                 self._cur_T = P["pending"][3]
-                self._prep_adam()
-                m = self._dec(*P["pending"][:3], adam=True)
+                m = self._dec(*P["pending"][:3])
             self._hook_mode = None
             main.wait_stream(P["side"])
             feats.record_stream(main)
@@ -451,7 +428,6 @@ class TeacherForcedTrainer:
             P["feats"][k].copy_(f)
         else:
             S = P["sets"][P["T"][1 - k]]
-            self._prep_adam()
             if "genc" in S:
                 main = torch.cuda.current_stream()
                 self._seed_ctr.add_(1)  # before both branches read it (masks drawn at kernel run time)
@@ -478,8 +454,7 @@ class TeacherForcedTrainer:
                 self._hook_mode = None
                 return None
             self._cur_T = P["pending"][3]
-            self._prep_adam()
-            m = self._dec(*P["pending"][:3], adam=True)
+            m = self._dec(*P["pending"][:3])
             P["pending"] = None
         else:
             if P["i"] == 0:
@@ -487,8 +462,7 @@ class TeacherForcedTrainer:
                 return None
             j = (P["i"] - 1) % 2
             self._cur_T = P["T"][j]
-            self._prep_adam()
-            m = self._dec(P["feats"][j], P["caps"][j], P["lens"][j], adam=True)
+            m = self._dec(P["feats"][j], P["caps"][j], P["lens"][j])
             P["i"] = 0
         self._hook_mode = None
         return self._update(m)
@@ -513,7 +487,6 @@ class TeacherForcedTrainer:
             for dst, src in zip(self._inputs, (imgs, caps, caplens)):
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src, non_blocking=True)
-            self._prep_adam()
             self._replay(self._graph)
             m = self._metrics
         return self._update(m)
@@ -521,14 +494,30 @@ class TeacherForcedTrainer:
     def _eager(self, imgs, caps, caplens):
         self._hook_mode = "eager"
         try:
-            self._prep_adam()
-            return self._fwd_bwd(imgs, caps, caplens, adam=True)
+            return self._fwd_bwd(imgs, caps, caplens)
         finally:
             self._hook_mode = None
 
     def _update(self, m):
-        """DDP gradient average, clip + Adam, metric reduction (trainMultiGPU.py:384-403)."""
+        """DDP gradient average, clip + Adam, metric reduction (trainMultiGPU.py:384-403).
+
+        m = [loss, tokens, top-5 hits, 1/tokens, hand-off errors]; m[4] counts the persistent LSTM
+        recurrences' timed-out hand-offs.  Such a step's gradients are invalid: the Adam kernels
+        read the (rank-summed) error word on the device and leave every parameter and moment as
+        it was, the step's loss reads NaN and drain_metrics() raises (decoder.py:100-111 must
+        never degrade silently).  One rank: the step's metric vector is logged as is (one copy,
+        reduced on the host at drain time); DDP: the reduceLossAndTokens / accuracy sums across
+        ranks (trainMultiGPU.py:96-108, 398-403), reduced before the update so every rank skips
+        the same steps."""
         fp = self.eng.fp
+        if self.world == 1:
+            red = m.clone()
+        else:
+            zero = torch.zeros((), device=m.device, dtype=m.dtype)
+            red = torch.stack([m[0] * m[1], m[1], m[2], zero, m[4] if m.numel() > 4 else zero])
+            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)
+            red[0] = red[0] / red[1]  # global token-weighted mean loss, back in m's layout
+        skip = red[4:5] if red.numel() > 4 else None
         if self.world > 1:
             if self._early_issued:  # the early bucket is in flight on the comm stream: the rest
                 lo, hi = self._bucket
@@ -540,26 +529,15 @@ class TeacherForcedTrainer:
                 self._early_issued = False
             else:
                 dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
-        if not self._inline_adam():  # (inline: applied inside the decoder's backward, _dec)
-            fp.adam_step(self.decoder_lr, self.grad_clip, grad_div=float(self.world))
+        fp.adam_step(self.decoder_lr, self.grad_clip, grad_div=float(self.world), skip=skip)
         if self.enc_eng is not None:
             efp = self.enc_eng.fp
             if self.world > 1:
                 dist.all_reduce(efp.grad, op=dist.ReduceOp.SUM, group=self.pg)
-            efp.adam_step(self.encoder_lr, self.grad_clip, grad_div=float(self.world))
-        # m = [loss, tokens, top-5 hits, 1/tokens, hand-off errors]; m[4] counts the persistent
-        # LSTM recurrences' timed-out hand-offs: such a step's loss reads NaN and drain_metrics()
-        # raises (decoder.py:100-111 must never degrade silently).  One rank: the step's metric
-        # vector is logged as is (one copy, reduced on the host at drain time); DDP: the
-        # reduceLossAndTokens / accuracy sums across ranks (trainMultiGPU.py:96-108, 398-403).
-        if self.world == 1:
-            red = m.clone()
-            self._metric_log.append(red)
-            return red
-        zero = torch.zeros((), device=m.device, dtype=m.dtype)
-        red = torch.stack([m[0] * m[1], m[1], m[2], zero, m[4] if m.numel() > 4 else zero])
-        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)
-        red[0] = red[0] / red[1]  # global token-weighted mean loss, back in m's layout
+            efp.adam_step(self.encoder_lr, self.grad_clip, grad_div=float(self.world), skip=skip)
+            upd = getattr(self.encoder, "weights_updated", None)
+            if upd is not None:  # packed copies of the fine-tuned children go stale
+                upd()
         self._metric_log.append(red)
         return red
 

@@ -317,17 +317,13 @@ int imgcap_ce_fused(int dtype, int n, int V, const void* logits, int64_t ld, con
  * clip_gradient (utils.py:183-192, clamp to +-clip) + torch.optim.Adam step
  * (train.py:110,289-291) over a flat fp32 parameter buffer; optionally refreshes a bf16
  * shadow copy of the weights used by the bf16 kernels.  grad is divided by grad_div first
- * (DDP mean over ranks, trainMultiGPU.py:233,384).
+ * (DDP mean over ranks, trainMultiGPU.py:233,384).  skip (device, may be NULL): when *skip != 0
+ * at run time the update is not applied (the step's error word: a timed-out persistent LSTM
+ * hand-off made its gradients invalid; the step is reported failed by the metrics).
  * -------------------------------------------------------------------------------------- */
 int imgcap_clamp_adam(int64_t n, float* param, const float* grad, float* m, float* v,
                       void* shadow_bf16, float lr, float beta1, float beta2, float eps,
-                      int step, float clip, float grad_div, void* stream);
-/* The same with the step's scalars in device memory: scal[0] = (float)(lr / (1 - beta1^t)),
- * scal[1] = (float)sqrt(1 - beta2^t) (beta1/beta2 as floats promoted to double, as above) -- a
- * captured graph then carries the update of each replay's step. */
-int imgcap_clamp_adam_dev(int64_t n, float* param, const float* grad, float* m, float* v,
-                          void* shadow_bf16, float beta1, float beta2, float eps, const float* scal,
-                          float clip, float grad_div, void* stream);
+                      int step, float clip, float grad_div, const float* skip, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * LSTM + soft-attention decoder, teacher forced (decoder.py:69-113, Attention 25-31,

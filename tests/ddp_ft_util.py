@@ -72,9 +72,11 @@ class _OracleFlat:
     def refresh_shadow(self):
         pass
 
-    def adam_step(self, lr, clip, grad_div=1.0):
+    def adam_step(self, lr, clip, grad_div=1.0, skip=None):
         from oracle import train_step
         self.t += 1
+        if skip is not None and float(skip.reshape(-1)[0]) != 0.0:  # FlatParams.adam_step's gate
+            return
         g = {n: v / grad_div for n, v in self.views(self.grad).items()}
         p = {n: v.clone() for n, v in self.views(self.flat).items()}
         new = train_step.adam_step(p, train_step.clip_gradient(g, clip), self.state, lr, self.t)

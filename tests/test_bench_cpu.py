@@ -23,4 +23,4 @@ def test_bench_defaults_are_one_gpu():
     sys.path.insert(0, ROOT)
     import bench
     a = bench.parse([])
-    assert a.gpus == 1 and a.config == "C2" and a.steps >= 100
+    assert a.gpus == 1 and a.config == "C3" and a.steps >= 100

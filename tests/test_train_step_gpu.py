@@ -201,11 +201,17 @@ def test_persistent_lstm_handoff_timeout_raises(hip_device, monkeypatch, directi
     tr.step(*_batch(hip_device, 0))  # healthy step first
     assert tr.eng._sync is not None  # the persistent recurrences ran
     assert len(tr.drain_metrics()) == 1
+    fp = tr.eng.fp
+    before = (fp.flat.clone(), fp.m.clone(), fp.v.clone(), fp.shadow)
     monkeypatch.setenv(f"IMGCAP_LSTM_FAULT_{direction}", "2")
     tr.step(*_batch(hip_device, 1))
     monkeypatch.delenv(f"IMGCAP_LSTM_FAULT_{direction}")
     red = tr._metric_log[-1].cpu()  # [loss, tokens, top-5 hits, 1/tokens, hand-off errors]
     assert red[4] > 0
+    # the Adam kernel read the error word on the device: the failed step's (invalid) gradients
+    # reached neither the parameters nor the moments
+    for x, y in zip(before[:3], (fp.flat, fp.m, fp.v)):
+        assert torch.equal(x, y)
     with pytest.raises(RuntimeError, match="hand-off timed out"):
         tr.drain_metrics()
     tr.step(*_batch(hip_device, 1))  # the knob is read per launch: clean again
@@ -305,3 +311,37 @@ def test_lstm_length_buckets_match_full_steps(hip_device, pipeline):
     for a, b in zip(m0, m1):
         assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]) and a[1] == b[1] and abs(a[2] - b[2]) < 1e-6
     assert ((p0 - p1).norm() / p0.norm()).item() < 2e-5  # Adam sign flips at round-off-level grads
+
+
+def test_eval_after_finetune_step_sees_updated_encoder(hip_device):
+    """After a fine-tuned step (EncoderEngine's Adam writes the trainable children through raw
+    pointers), the no_grad encoder forward used by validation runs the UPDATED weights: it equals
+    a fresh encoder loaded with the updated state_dict (fp32)."""
+    from imagecaptioningconvnext_amd import kernels as K
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    enc, dec = _models(hip_device, "transformer", dropout=0.0, sd_off=True, starting_layer=5)
+    imgs = _batch(hip_device, 3, B=2, hw=224)[0]
+    enc.eval()
+    with torch.no_grad():
+        f0 = enc(imgs).clone()  # packs the weights before fine-tuning
+    tr = TeacherForcedTrainer(enc, dec, lstm=False, graph=False, encoder_lr=1e-2)
+    for i in range(2):
+        tr.step(*_batch(hip_device, i, B=2, hw=224))
+    torch.cuda.synchronize()
+    tr.drain_metrics()
+    enc.eval()
+    with torch.no_grad():
+        f1 = enc(imgs)
+    ref = Encoder(variant="tiny", compute_dtype=torch.float32)
+    ref.load_state_dict({k: v.detach().clone() for k, v in enc.state_dict().items()})
+    ref = ref.to(hip_device).eval()
+    ref.fine_tune(False)
+    for m in ref.modules():
+        if hasattr(m, "sd_prob"):
+            m.sd_prob = 0.0
+    with torch.no_grad():
+        f2 = ref(imgs)
+    assert (f1 - f0).abs().max() > 1e-4  # the update is visible
+    torch.testing.assert_close(f1, f2, rtol=1e-5, atol=1e-5)
+    K.set_seed_counter(None)
