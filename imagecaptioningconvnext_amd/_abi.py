@@ -67,6 +67,8 @@ _SIGS = {
     "imgcap_version": [],
     "imgcap_set_seed_counter": [c_void_p],
     "imgcap_gemm_plan": [c_int] * 6 + [c_int64, c_int64, c_int, c_int, c_void_p],
+    "imgcap_gemm_plan_ep": [c_int] * 6 + [c_int64, c_int64, c_int, c_void_p, c_void_p],
+    "imgcap_gemm_set_pt": [c_int],
     "imgcap_dwconv7": [c_int] * 5 + [c_void_p] * 5,
     "imgcap_cnblock_mlp": [c_int, c_int] + [c_void_p] * 9 + [c_int, c_void_p, c_void_p],
     "imgcap_cnblock_mlp_wide_pack": [c_int, c_void_p, c_void_p, c_void_p, c_void_p],

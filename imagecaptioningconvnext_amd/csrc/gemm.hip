@@ -405,6 +405,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 #include "gemm_glds.h"
 #include "gemm256.h"
 #include "gemm_mx.h"
+#include "gemm_pt.h"
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
@@ -529,10 +530,140 @@ static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, lon
   return {tiles128 < 512 ? IMGCAP_GEMM_TILED64 : IMGCAP_GEMM_TILED128, 1};
 }
 
+// ---- persistent-tile kernel (gemm_pt.h): selection and launch ------------------------------
+// IMGCAP_GEMM_PT / imgcap_gemm_set_pt: -1 by shape, 0 never (default until it wins: the first
+// measurements, tools/gpu/r4_pt.sh, had it slower than the LDS-staged plan on the step's shapes),
+// 1 wherever eligible (tile by the cost model), 2..4 wherever eligible with tile config 2..4 forced
+static int g_gemm_pt_mode = [] {
+  const char* e = getenv("IMGCAP_GEMM_PT");
+  return e ? atoi(e) : 0;
+}();
+
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    hipDeviceProp_t pr;
+    cus[dev] = hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0 ? pr.multiProcessorCount : 256;
+  }
+  return cus[dev];
+}
+
+// tile configs: 1 = 128x256 (8 waves 2x4, 3 stages), 2 = 256x128 (8 waves 4x2, 3 stages),
+// 3 = 128x128 (8 waves 2x4, 4 stages)
+struct PtCfg { int bm, bn; };
+static PtCfg pt_cfg(int c) { return c == 1 ? PtCfg{128, 256} : c == 2 ? PtCfg{256, 128} : PtCfg{128, 128}; }
+
+// cycles of one tile on a CU: per 64-deep k-step max(MFMA, operand delivery at ~48 B/cycle),
+// plus a fixed per-tile cost (epilogue, pipeline turn-around); rounds = tiles over the CUs
+static double pt_estimate(int c, int M, int N, int K, int cus) {
+  const PtCfg t = pt_cfg(c);
+  const long tiles = (long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
+  const long rounds = (tiles + cus - 1) / cus;
+  const double nk = (K + 63) / 64;
+  const double step = std::max((double)t.bm * t.bn / 32.0, (t.bm + t.bn) * 128.0 / 48.0);
+  const double epi = t.bm * t.bn / 64.0;  // ~ stores + epilogue math
+  return rounds * (nk * step + epi);
+}
+
+static int pt_choose(int M, int N, int K) {
+  const int cus = device_cus();
+  int best = 0;
+  double bt = 0;
+  for (int c = 1; c <= 3; ++c) {
+    const double t = pt_estimate(c, M, N, K, cus);
+    if (!best || t < bt) { best = c; bt = t; }
+  }
+  return best;
+}
+
+// which PT config serves this call (0: none) -- the epilogue forms the kernel implements
+static int pt_plan(int ak, int bk, int M, int N, int K, long lda, long ldb, int batch, int split,
+                   const imgcap_epilogue* ep, bool vec_ok) {
+  const int mode = g_gemm_pt_mode;
+  if (mode == 0 || batch != 1 || split != 1 || lda % 8 || ldb % 8 || N % 4) return 0;
+  if (ep) {
+    if (!vec_ok || ep->c_dtype != IMGCAP_BF16) return 0;
+    if (ep->aux && ep->act != IMGCAP_ACT_GELU && ep->act != IMGCAP_ACT_DGELU) return 0;  // relu-mask aux
+    if (ep->rowscale && ep->rows_per_scale <= 0) return 0;
+  }
+  // the general epilogue (dGELU's saved pre-activation, beta) only on the 128x128 tile (registers)
+  const bool general = ep && ((ep->aux && ep->act == IMGCAP_ACT_DGELU) || ep->beta != 0.f);
+  if (general) return mode < 0 && ((long)M * N < 1000000L || K < 256) ? 0 : 3;
+  if (mode >= 2 && mode <= 4) return mode - 1;
+  if (mode < 0) {
+    // by shape: big enough grids only (measured crossover: tools/gpu/r4_pt.sh)
+    if ((long)M * N < 1000000L || K < 256) return 0;
+  }
+  return pt_choose(M, N, K);
+}
+
+static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb,
+                     void* C, long ldc, const imgcap_epilogue& ep, hipStream_t st) {
+  const PtCfg t = pt_cfg(cfg);
+  PtArgs a;
+  a.A = A;
+  a.B = B;
+  a.C = C;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  const int tm = (M + t.bm - 1) / t.bm;
+  a.tiles_n = (N + t.bn - 1) / t.bn;
+  a.ntiles = tm * a.tiles_n;
+  const int cus = device_cus();
+  int G = a.ntiles < cus ? a.ntiles : cus;
+  if (G >= 64) G -= G % 8;
+  // each XCD's concurrent tiles (G / 8 of them) as a rectangle of grp tile rows balancing its
+  // A and B bytes: rows ~ sqrt(run * BN / BM)
+  const double run = std::max(1.0, G / 8.0);
+  a.grp = std::max(1, std::min(tm, (int)(std::sqrt(run * t.bn / t.bm) + 0.5)));
+  a.ep = ep;
+  a.seed_ctr = g_seed_ctr;
+  a.c_bytes = ((uint64_t)(M - 1) * ldc + N) * 2;
+  a.res_bytes = ep.res ? ((uint64_t)(M - 1) * ep.ldr + N) * 2 : 0;
+  a.aux_bytes = ep.aux ? ((uint64_t)(M - 1) * ep.ldaux + N) * 2 : 0;
+  if (a.c_bytes > 0x7fffffffull || a.res_bytes > 0x7fffffffull || a.aux_bytes > 0x7fffffffull)
+    return fail(IMGCAP_EUNSUPPORTED, "imgcap_gemm(pt): operand over 2 GiB");
+  const bool general = (ep.aux && ep.act == IMGCAP_ACT_DGELU) || ep.beta != 0.f;
+  if (general && cfg != 3) return fail(IMGCAP_EINVAL, "imgcap_gemm(pt): general epilogue needs the 128x128 tile");
+  const int ek = general ? 2 : ep.res ? 1 : 0;
+#define PT_L(BM_, BN_, WM_, WN_, S_, AKV, BKV, EK_)                                                               \
+  hipLaunchKernelGGL((gemm_pt_kernel<BM_, BN_, WM_, WN_, S_, AKV, BKV, EK_>), dim3(G), dim3(WM_ * WN_ * 64), 0, st, \
+                     a)
+#define PT_C(AKV, BKV)                                              \
+  do {                                                              \
+    if (ek == 2) PT_L(128, 128, 2, 4, 4, AKV, BKV, 2);              \
+    else if (cfg == 1 && ek == 0) PT_L(128, 256, 2, 4, 3, AKV, BKV, 0); \
+    else if (cfg == 1) PT_L(128, 256, 2, 4, 3, AKV, BKV, 1);        \
+    else if (cfg == 2 && ek == 0) PT_L(256, 128, 4, 2, 3, AKV, BKV, 0); \
+    else if (cfg == 2) PT_L(256, 128, 4, 2, 3, AKV, BKV, 1);        \
+    else if (ek == 0) PT_L(128, 128, 2, 4, 4, AKV, BKV, 0);         \
+    else PT_L(128, 128, 2, 4, 4, AKV, BKV, 1);                      \
+  } while (0)
+  if (ak && bk) PT_C(true, true);
+  else if (ak) PT_C(true, false);
+  else if (bk) PT_C(false, true);
+  else PT_C(false, false);
+#undef PT_C
+#undef PT_L
+  IMGCAP_CHECK_LAUNCH("imgcap_gemm(pt)");
+  return 0;
+}
+
 template <typename T>
 static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
                          long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
                          int vec_ok, hipStream_t st, int split) {
+  if constexpr (sizeof(T) == 2) {
+    const int pc = pt_plan(ak, bk, M, N, K, lda, ldb, batch, split, &ep, vec_ok != 0);
+    if (pc) return pt_launch(pc, ak, bk, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, C, ldc, ep, st);
+  }
   const GemmPlan plan = gemm_plan(sizeof(T) == 2, ak, bk, M, N, K, lda, ldb, batch, split);
   if (plan.kind == IMGCAP_GEMM_SKINNY) {
     const int blocks = (N + 15) / 16;
@@ -930,6 +1061,27 @@ extern "C" int imgcap_transpose(int dtype, int rows, int cols, const void* in, i
                        (const float*)in, ldi, (float*)out, ldo);
   IMGCAP_CHECK_LAUNCH("imgcap_transpose");
   return 0;
+}
+
+extern "C" int imgcap_gemm_set_pt(int mode) {
+  IMGCAP_REQUIRE(mode >= -1 && mode <= 4, "imgcap_gemm_set_pt: -1..4");
+  g_gemm_pt_mode = mode;
+  return 0;
+}
+
+extern "C" int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda,
+                                   int64_t ldb, int batch, const imgcap_epilogue* epi, int* splits) {
+  const int split = (epi == nullptr || epi->split_k == 0 || epi->split_k == 1) ? 1 : epi->split_k;
+  if (dtype == IMGCAP_BF16) {
+    const int pc = pt_plan(a_kmajor, b_kmajor, M, N, K, lda, ldb, batch, split, epi, true);
+    if (pc) {
+      if (splits) *splits = 1;
+      return IMGCAP_GEMM_PT + pc - 1;
+    }
+  }
+  const GemmPlan p = gemm_plan(dtype == IMGCAP_BF16, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch, split);
+  if (splits) *splits = p.split;
+  return p.kind;
 }
 
 extern "C" int imgcap_gemm_set_policy(int glds256) {

@@ -71,10 +71,22 @@ def gemm_set_policy(glds256):
     _abi.call("imgcap_gemm_set_policy", int(glds256))
 
 
-def gemm_plan(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch=1, split_k=0):
-    """(kernel kind, K slices) imgcap_gemm picks for these operands (IMGCAP_GEMM_* ids)."""
+def gemm_set_pt(mode):
+    """Persistent-tile GEMM (imgcap_gemm_set_pt): -1 by shape (default), 0 never, 1 wherever
+    eligible, 2..4 wherever eligible with tile 128x256 / 256x128 / 128x128."""
+    _abi.call("imgcap_gemm_set_pt", int(mode))
+
+
+def gemm_plan(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch=1, split_k=0, ep=None):
+    """(kernel kind, K slices) imgcap_gemm picks for these operands (IMGCAP_GEMM_* ids); with the
+    call's Epilogue ``ep`` the persistent-tile kernel's eligibility is known too."""
     sp = ctypes.c_int(1)
-    kind = _abi.lib().imgcap_gemm_plan(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch, split_k, ctypes.byref(sp))
+    if ep is not None:
+        kind = _abi.lib().imgcap_gemm_plan_ep(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch, ctypes.byref(ep),
+                                              ctypes.byref(sp))
+    else:
+        kind = _abi.lib().imgcap_gemm_plan(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch, split_k,
+                                           ctypes.byref(sp))
     return kind, sp.value
 
 

@@ -1,0 +1,152 @@
+"""Persistent-tile GEMM (csrc/gemm_pt.h): every operand layout, tile config and epilogue form
+against a PyTorch fp32 reference on the bf16-rounded operands, and against the LDS-staged kernels
+(imgcap_gemm_set_pt(0)) on the same call.  Ragged M / N (rows and columns past the last tile), K
+tails (K % 64 != 0), grids with more tiles than CUs (persistent rounds, the cross-tile prefetch)
+and fewer."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+bf = torch.bfloat16
+
+
+def _gelu(x):
+    return 0.5 * x * (1.0 + torch.erf(x * 0.7071067811865476))
+
+
+def _gelu_grad(x):
+    return 0.5 * (1.0 + torch.erf(x * 0.7071067811865476)) + x * 0.3989422804014327 * torch.exp(-0.5 * x * x)
+
+
+def _operands(dev, M, N, Kd, ta, tb, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    r8 = lambda x: (x + 7) // 8 * 8  # noqa: E731
+    # 16-byte row pitches (the engines' allocations), sliced on the device
+    af = (torch.randn(Kd, r8(M), generator=g) if ta else torch.randn(M, r8(Kd), generator=g)).to(bf)
+    bfull = (torch.randn(N, r8(Kd), generator=g) if tb else torch.randn(Kd, r8(N), generator=g)).to(bf)
+    a = af[:, :M] if ta else af[:, :Kd]
+    b = bfull[:, :Kd] if tb else bfull[:, :N]
+    A = (a.t() if ta else a).float()
+    Bm = (b.t() if tb else b).float()
+    ad, bd = af.to(dev), bfull.to(dev)
+    ad = ad[:, :M] if ta else ad[:, :Kd]
+    bd = bd[:, :Kd] if tb else bd[:, :N]
+    return ad, bd, A @ Bm  # fp32 product of the bf16 operands [M, N]
+
+
+SHAPES = [(300, 264, 200), (1000, 512, 384), (389, 264, 336), (2100, 1032, 640)]
+LAYOUTS = [(False, True), (False, False), (True, True), (True, False)]
+
+
+@pytest.mark.parametrize("M,N,Kd", SHAPES)
+@pytest.mark.parametrize("ta,tb", LAYOUTS)
+@pytest.mark.parametrize("cfg", [2, 3, 4])
+def test_pt_plain_matches_fp32(hip_device, M, N, Kd, ta, tb, cfg):
+    from imagecaptioningconvnext_amd import kernels as K
+    a, b, ref = _operands(hip_device, M, N, Kd, ta, tb, 1)
+    try:
+        K.gemm_set_pt(cfg)
+        out = K.gemm(a, b, trans_a=ta, trans_b=tb)
+        torch.cuda.synchronize()
+    finally:
+        K.gemm_set_pt(0)
+    err = (out.float().cpu() - ref).abs().max() / ref.abs().max()
+    assert err < 8e-3, err
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("form", ["gelu_aux", "res_scales", "dgelu_beta", "relu_alpha", "dropout"])
+def test_pt_epilogues_match_fp32_and_lds_kernels(hip_device, cfg, form):
+    from imagecaptioningconvnext_amd import kernels as K
+    dev = hip_device
+    M, N, Kd = 1500, 776, 384
+    a, b, prod = _operands(dev, M, N, Kd, False, True, 7)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    bias = torch.randn(N, generator=g)
+    cs = torch.rand(N, generator=g) + 0.5
+    rps = 49
+    rs = (torch.rand((M + rps - 1) // rps, generator=g) > 0.3).float() * 1.25
+    res = torch.randn(M, N, generator=g).to(bf)
+    old = torch.randn(M, N, generator=g).to(bf)
+    aux_in = torch.randn(M, N, generator=g).to(bf)
+
+    def run(mode):
+        K.gemm_set_pt(mode)
+        try:
+            out = old.clone().to(dev)
+            aux = None
+            kw = {}
+            if form == "gelu_aux":
+                aux = torch.zeros(M, N, dtype=bf, device=dev)
+                kw = dict(bias=bias.to(dev), act=K.ACT_GELU, aux=aux)
+            elif form == "res_scales":
+                kw = dict(bias=bias.to(dev), colscale=cs.to(dev), rowscale=rs.to(dev), rows_per_scale=rps,
+                          res=res.to(dev))
+            elif form == "dgelu_beta":
+                kw = dict(act=K.ACT_DGELU, aux=aux_in.to(dev), beta=0.5)
+            elif form == "relu_alpha":
+                kw = dict(bias=bias.to(dev), act=K.ACT_RELU, alpha=0.75)
+            else:
+                kw = dict(bias=bias.to(dev), drop_p=0.3, seed=1234, drop_stream=5)
+            K.gemm(a, b, trans_b=True, out=out, **kw)
+            torch.cuda.synchronize()
+            return out.float().cpu(), None if aux is None else aux.float().cpu()
+        finally:
+            K.gemm_set_pt(0)
+
+    got, got_aux = run(cfg)
+    base, base_aux = run(0)
+    # fp32 reference of the epilogue (imgcap_epilogue order)
+    x = prod.clone()
+    if form == "gelu_aux":
+        pre = x + bias
+        ref = _gelu(pre)
+        torch.testing.assert_close(got_aux, pre.to(bf).float(), rtol=1e-2, atol=1e-2)
+    elif form == "res_scales":
+        ref = (x + bias) * (cs * rs.repeat_interleave(rps)[:M, None]) + res.float()
+    elif form == "dgelu_beta":
+        ref = x * _gelu_grad(aux_in.float()) + 0.5 * old.float()
+    elif form == "relu_alpha":
+        ref = torch.relu(0.75 * x + bias)
+    else:
+        ref = None  # the mask: compared with the LDS-staged kernel (same counter-based draw)
+    if ref is not None:
+        err = (got - ref).abs().max() / ref.abs().max()
+        assert err < 1e-2, err
+    # the LDS-staged kernels compute the same epilogue: equal up to one bf16 rounding
+    diff = (got - base).abs()
+    tol = 1e-2 * base.abs() + 1e-2
+    assert bool((diff <= tol).all()), float(diff.max())
+    if form == "dropout":
+        assert torch.equal((got == 0), (base == 0))
+
+
+def test_pt_persistent_rounds_and_xcd_slots(hip_device):
+    """More tiles than CUs (several tiles per block, the next tile's k-steps prefetched under the
+    epilogue), a K of one k-step, and a K tail inside the prefetch window."""
+    from imagecaptioningconvnext_amd import kernels as K
+    for (M, N, Kd) in [(12544, 384, 1536), (6272, 1536, 64), (3328, 2048, 72), (7000, 600, 136)]:
+        a, b, ref = _operands(hip_device, M, N, Kd, False, True, 11)
+        for cfg in (2, 3, 4):
+            K.gemm_set_pt(cfg)
+            try:
+                out = K.gemm(a, b, trans_b=True)
+                torch.cuda.synchronize()
+            finally:
+                K.gemm_set_pt(0)
+            err = (out.float().cpu() - ref).abs().max() / ref.abs().max()
+            assert err < 8e-3, (M, N, Kd, cfg, float(err))
+
+
+def test_pt_bitwise_repeatable(hip_device):
+    from imagecaptioningconvnext_amd import kernels as K
+    a, b, _ = _operands(hip_device, 5000, 1536, 384, False, True, 5)
+    K.gemm_set_pt(1)
+    try:
+        o1 = K.gemm(a, b, trans_b=True, act=K.ACT_GELU)
+        o2 = K.gemm(a, b, trans_b=True, act=K.ACT_GELU)
+        torch.cuda.synchronize()
+    finally:
+        K.gemm_set_pt(0)
+    assert torch.equal(o1, o2)
