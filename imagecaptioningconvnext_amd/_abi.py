@@ -71,9 +71,6 @@ _SIGS = {
     "imgcap_gemm_set_pt": [c_int],
     "imgcap_dwconv7": [c_int] * 5 + [c_void_p] * 5,
     "imgcap_cnblock_mlp": [c_int, c_int] + [c_void_p] * 9 + [c_int, c_void_p, c_void_p],
-    "imgcap_cnblock_mlp_wide_pack": [c_int, c_void_p, c_void_p, c_void_p, c_void_p],
-    "imgcap_cnblock_mlp_wide_scratch": [c_int, c_int, ctypes.POINTER(c_uint64), ctypes.POINTER(c_uint64)],
-    "imgcap_cnblock_mlp_wide": [c_int, c_int] + [c_void_p] * 8 + [c_int] + [c_void_p] * 4,
     "imgcap_stochastic_depth_scales": [c_int, c_int, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p],
     "imgcap_gemm": [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int64, c_void_p, c_int64,
                     c_int64, c_void_p, c_int64, c_int64, c_int, ctypes.POINTER(Epilogue), c_void_p],

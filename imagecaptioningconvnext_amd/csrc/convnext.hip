@@ -487,35 +487,30 @@ __host__ __device__ constexpr int dw_roll_row_slots(int W, int PW, int sppx) {
 }
 
 // ---------------------------------------------------------------------------------------
-// The same depthwise conv over NTL consecutive row tiles per block (compile-time width): the
-// block keeps a ring of 2*TR + 6 input rows in LDS, so the 6 halo rows are fetched once per
-// NTL*TR rows instead of once per TR (stage 1 at W = 56: 1.75x -> 1.25x the input at NTL = 3),
-// and the TR new rows of tile k+1 are loaded into registers before tile k is computed and
-// written to the ring after it -- their latency hides behind tile k's arithmetic.  Ring row of
-// input row i (counted from the block's first output row - 3) = i mod (2*TR + 6): tile k reads
-// rows [k*TR, k*TR + TR + 6), its prefetch lands in rows [k*TR + TR + 6, k*TR + 2*TR + 6),
-// the slots of rows k*TR - TR .. k*TR - 1 that tile k-1 finished with before the barrier.
-template <typename T, int PW, int WC, int NC, int NTL, bool F32L>
+// The same depthwise conv with a compile-time width (the encoder's 56 / 28 / 14 / 7, and 64 / 32
+// / 16 / 8): one tile of TR output rows per block, its TR + 6 input rows staged in LDS through
+// buffer loads whose range check supplies the zero halo.  Variants measured and removed (round 3,
+// tools/microbench.py dw): 2-4 row tiles per block with a ring (halo fetched once; one block per
+// CU, 1.2-3x slower) and bf16 staged as fp32 (1.2x slower).
+template <typename T, int PW, int WC, int NC>
 __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, int H, int C, const T* __restrict__ x,
                                                            const float* __restrict__ w,
                                                            const float* __restrict__ bias, T* __restrict__ y,
                                                            const T* res, int flip) {
   extern __shared__ __attribute__((aligned(16))) char dsm[];
-  static_assert(WC > 0 && NTL >= 1, "compile-time width");
-  // LDS element type: the input's, or fp32 (F32L: the bf16 -> fp32 unpack done once per staged
-  // element instead of once per window read, 7 kernel rows x 7 lanes later)
-  using LT = typename std::conditional<F32L, float, T>::type;
+  static_assert(WC > 0, "compile-time width");
+  using LT = T;  // LDS element type
   constexpr int VE = 16 / sizeof(T);
   constexpr int NV = DW_CT / VE;
   constexpr int SPPX = DW_CT * (int)sizeof(LT) / 16;  // 16-byte slots per pixel
   constexpr int NT = 64 * DW_CT / NC;
   constexpr int W = WC, GW = W / PW, TR = 64 / GW, WP = W + 6;
   constexpr int RS = dw_roll_row_slots(WC, PW, SPPX);
-  constexpr int RING = NTL > 1 ? 2 * TR + 6 : TR + 6;
+  constexpr int RING = TR + 6;
   constexpr int PSTEP = NT / NV;                      // pixels per load instruction of the block
   constexpr int NPF = (TR * WP + PSTEP - 1) / PSTEP;  // loads per thread for TR new rows
   const long R = (long)B * H;
-  const long rb = (long)blockIdx.x * (NTL * TR);      // the block's first output row
+  const long rb = (long)blockIdx.x * TR;              // the block's first output row
   const int cb = blockIdx.y * DW_CT;
   uint4* img = (uint4*)dsm;
   auto slot = [&](int rr, int px, int s) { return rr * RS + SPPX * px + px / PW + s; };
@@ -574,11 +569,9 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, in
 #pragma unroll
   for (int j = 0; j < NC; ++j) bv[j] = 0.f;
   if (bias) ldc<float, NC>(bias + c0, bv);
-  for (int k = 0; k < NTL; ++k) {
-    uint4 pf[NPF];
-    const bool more = k + 1 < NTL;
-    if (more) load_rows(k * TR + TR + 6, TR, pf);
-    const long orow = rb + (long)k * TR + lr;
+  {
+    constexpr int k = 0;
+    const long orow = rb + lr;
     if (orow < R) {
       const int h = (int)(orow % H);
       f32x2 acc[PW][NP];
@@ -628,8 +621,6 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, in
         stc<T, NC>(out + (long)p * C, o);
       }
     }
-    if (more) store_rows(k * TR + TR + 6, TR, pf);
-    __syncthreads();
   }
 }
 
@@ -722,53 +713,16 @@ __global__ void sd_scales_kernel(int n, int B, const float* __restrict__ probs, 
 using namespace imgcap;
 
 namespace {
-// IMGCAP_DW_NC=4|8 forces the channels per lane of the depthwise kernel (A/B timing)
-int dw_nc_override() {
-  static const int v = [] {
-    const char* e = getenv("IMGCAP_DW_NC");
-    return e ? atoi(e) : 0;
-  }();
-  return v == 4 || v == 8 ? v : 0;
-}
-// IMGCAP_DW_NARROW=0|1 (A/B timing of the late-stage lane mapping)
-bool dw_narrow() {
-  static const int v = [] {
-    const char* e = getenv("IMGCAP_DW_NARROW");
-    return e ? atoi(e) : 0;
-  }();
-  return v == 1;
-}
-// the rolling kernel's ring exceeds the default 64 KB of dynamic LDS: raise the limit once per
-// instantiation (first launch, before any capture)
-template <typename T, int P, int WC, int N, bool FL>
+// the rolling kernel's staged rows can exceed the default 64 KB of dynamic LDS: raise the limit
+// once per instantiation (first launch, before any capture)
+template <typename T, int P, int WC>
 void dw_roll_attr() {
   static const bool done = [] {
-    (void)hipFuncSetAttribute((const void*)dwconv7_roll_kernel<T, P, WC, 8, N, FL>,
+    (void)hipFuncSetAttribute((const void*)dwconv7_roll_kernel<T, P, WC, 8>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)done;
-}
-
-// IMGCAP_DW_NTL=k forces k row tiles per block of the rolling kernel (0: the one-tile kernel)
-// IMGCAP_DW_F32L=1: bf16 input staged as fp32 in LDS (read at every launch)
-bool dw_f32l() {
-  const char* e = getenv("IMGCAP_DW_F32L");
-  return e && *e == '1';
-}
-int dw_ntl_override() {  // read at every launch (tests switch it)
-  const char* e = getenv("IMGCAP_DW_NTL");
-  return e && *e ? atoi(e) : -1;
-}
-// Row tiles per block of the rolling kernel.  Measured (tools/microbench.py dw, B = 64, Tiny and
-// Large stage shapes, gpurun_out/r3dw): one tile per block (two blocks per CU) is the fastest at
-// every shape -- 2-4 tiles per block cut the halo re-fetch but hold one block per CU (the ring
-// exceeds 80 KB) and ran 1.2-3x slower; the kernel is VALU-bound (per tap row: 196 packed FMAs
-// + ~200 bf16 unpack / address operations per lane), not halo-bound.  IMGCAP_DW_NTL overrides.
-int dw_pick_ntl(long, int, size_t, size_t) {
-  const int ov = dw_ntl_override();
-  if (ov >= 0) return ov > 4 ? 4 : ov;
-  return 1;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -992,173 +946,31 @@ int dwconv7_cp_launch(int B, int H, int W, int C, const void* x, const float* w,
   return 0;
 }
 
-// ---------------------------------------------------------------------------------------
-// Depthwise 7x7 for the wide early stages (W = 56 / 28), bf16, any even C: lane = (channel pair,
-// segment of S output columns, output row), lanes flattened channel-pair-fastest (consecutive
-// lanes read consecutive 4-byte pairs of one pixel; C = 96 / 192 need no 128-channel groups).
-// Per kernel row a lane loads its S + 6 input pixels as 4-byte pairs (buffer loads: the
-// segment's row start in a VGPR, the column in an SGPR; rows outside the image read 0 through
-// the range check, the columns left / right of it are masked), unpacks each once and applies the 7 taps with
-// packed FMAs, one kernel row of loads ahead in a rolled loop -- no LDS, no staging barrier.
-template <int S>
-__global__ __launch_bounds__(256) void dwconv7_seg_kernel(int B, int H, int W, int C, const bf16* __restrict__ x,
-                                                          const float* __restrict__ w,
-                                                          const float* __restrict__ bias, bf16* __restrict__ y,
-                                                          const bf16* __restrict__ res, int flip) {
-  constexpr int NI = S + 6;
-  const int P = C >> 1, nseg = W / S;
-  const long L = (long)blockIdx.x * 256 + threadIdx.x;
-  const long total = (long)B * H * nseg * P;
-  if (L >= total) return;
-  const int pr = (int)(L % P);
-  const long rest = L / P;
-  const int sg = (int)(rest % nseg);
-  const long row = rest / nseg;  // b * H + h
-  const int h = (int)(row % H);
-  const int c = 2 * pr;
-  const bool left = sg == 0, right = sg == nseg - 1;
-  const auto wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, 49 * C * 4, 0x00020000);
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)((long)B * H * W * C * 2), 0x00020000);
-  auto load_w = [&](int kh, f32x2 (&dst)[7]) {
-#pragma unroll
-    for (int kw = 0; kw < 7; ++kw) {
-      const int t = kh * 7 + kw;
-      dst[kw] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(wr, c * 4, (flip ? 48 - t : t) * C * 4, 0));
-    }
-  };
-  // input row h + kh - 3, columns sg*S - 3 .. sg*S + S + 2
-  auto load_row = [&](int kh, uint32_t (&dst)[NI]) {
-    const int ih = h + kh - 3;
-    const bool ok = ih >= 0 && ih < H;
-    // segment 0 starts at column 0 (its 3 left columns are padding): no offset below the buffer
-    const uint32_t vo = ok ? (uint32_t)((((row - h + ih) * W + (left ? 0 : sg * S - 3)) * (long)C + c) * 2) : 0x80000000u;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) dst[j] = __builtin_amdgcn_raw_buffer_load_b32(xr, vo, j * C * 2, 0);
-  };
-  f32x2 acc[S];
-  {
-    const f32x2 bb = bias ? *(const f32x2*)(bias + c) : f32x2{0.f, 0.f};
-#pragma unroll
-    for (int p = 0; p < S; ++p) acc[p] = bb;
-  }
-  auto row_fma = [&](const uint32_t (&src)[NI], const f32x2 (&wk)[7]) {
-    f32x2 xin[NI];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      // columns left of the image (segment 0, loaded from column 0: shifted by 3) / right of it
-      // (last segment): zero padding
-      uint32_t v;
-      if (j < 3) v = left ? 0u : src[j];
-      else if (j >= S + 3) v = left ? src[j - 3] : right ? 0u : src[j];
-      else v = left ? src[j - 3] : src[j];
-      xin[j] = f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
-    }
-#pragma unroll
-    for (int kw = 0; kw < 7; ++kw)
-#pragma unroll
-      for (int p = 0; p < S; ++p) acc[p] = xin[p + kw] * wk[kw] + acc[p];
-  };
-  uint32_t rb[2][NI];
-  f32x2 wb[2][7];
-  load_row(0, rb[0]);
-  load_w(0, wb[0]);
-#pragma unroll 1
-  for (int kh = 0; kh < 6; kh += 2) {
-    load_row(kh + 1, rb[1]);
-    load_w(kh + 1, wb[1]);
-    row_fma(rb[0], wb[0]);
-    load_row(kh + 2, rb[0]);
-    load_w(kh + 2, wb[0]);
-    row_fma(rb[1], wb[1]);
-  }
-  row_fma(rb[0], wb[0]);
-  const long o0 = (row * W + sg * S) * (long)C + c;
-#pragma unroll
-  for (int p = 0; p < S; ++p) {
-    f32x2 o = acc[p];
-    if (res) {
-      const uint32_t v = *(const uint32_t*)(res + o0 + (long)p * C);
-      o += f32x2{__uint_as_float(v << 16), __uint_as_float(v & 0xFFFF0000u)};
-    }
-    *(bf16x2*)(y + o0 + (long)p * C) = bf16x2{(bf16)o[0], (bf16)o[1]};
-  }
-}
-
-// Opt-in (IMGCAP_DW_SEG=1).  Measured slower than the channel-tiled kernel at every wide-stage
-// shape (tools/dw_wide_bench.py, us, segment vs tiled: Tiny s1 B64 58.8 vs 49.5, Tiny s2 B64 34.0
-// vs 26.3, Base s1 B32 40.7 vs 34.1, Base s2 B32 23.5 vs 16.9, Large s1 B64 109.7 vs 81.9; C4
-// 8.17k vs 8.23-8.24k img/s): S + 6 loads per S outputs and a lane's own weight loads per kernel
-// row put it on the load-issue rate, where the tiled kernel's LDS patch serves 7 rows per load.
-bool dw_seg_fits(int W, int C) {
-  const char* e = getenv("IMGCAP_DW_SEG");
-  return e && *e == '1' && (W == 56 || W == 28) && C % 2 == 0;
-}
-
-int dwconv7_seg_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
-                       const void* res, int flip, hipStream_t st) {
-  const int S = W == 56 ? 8 : 7;
-  const long total = (long)B * H * (W / S) * (C / 2);
-  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
-  if (S == 8)
-    hipLaunchKernelGGL((dwconv7_seg_kernel<8>), grid, block, 0, st, B, H, W, C, (const bf16*)x, w, bias, (bf16*)y,
-                       (const bf16*)res, flip);
-  else
-    hipLaunchKernelGGL((dwconv7_seg_kernel<7>), grid, block, 0, st, B, H, W, C, (const bf16*)x, w, bias, (bf16*)y,
-                       (const bf16*)res, flip);
-  IMGCAP_CHECK_LAUNCH("imgcap_dwconv7 (column segments)");
-  return 0;
-}
-
 template <typename T>
 int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, void* y,
                    hipStream_t st, const void* res = nullptr, int flip = 0) {
   if (sizeof(T) == 2 && dw_cp_fits(W, C, false))
     return dwconv7_cp_launch(B, H, W, C, x, w, bias, nullptr, nullptr, y, res, flip, st);
-  if (sizeof(T) == 2 && dw_seg_fits(W, C)) return dwconv7_seg_launch(B, H, W, C, x, w, bias, y, res, flip, st);
-  // pixels per lane: the largest of 8, 7, 4, 2, 1 dividing W; rows per block: 64 lanes / groups.
-  // Narrow mode (dw_narrow): the 28 / 14 / 7-wide stages with 4 / 2 / 1 pixels per lane -- 7
-  // lanes per image row, so 2-4x the lanes and blocks of the late stages' small grids
-  const bool narrow = dw_narrow() && (W == 28 || W == 14 || W == 7);
-  const int PW = narrow ? W / 7 : W % 7 == 0 ? 7 : W % 8 == 0 ? 8 : W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 1;
+  // pixels per lane: the largest of 7, 8, 4, 2, 1 dividing W; rows per block: 64 lanes / groups.
+  // Channels per lane: 8 (4 waves per block); 4 (8 waves) and 1-4 pixels per lane at the 28 / 14 /
+  // 7-wide stages measured slower and were removed (round 3, tools/microbench.py dw)
+  const int PW = W % 7 == 0 ? 7 : W % 8 == 0 ? 8 : W % 4 == 0 ? 4 : W % 2 == 0 ? 2 : 1;
   const int GW = W / PW, TR = 64 / GW;
   const long R = (long)B * H;
   const int RS = dw_row_slots(W, PW, (int)sizeof(T));
   const size_t shm = (size_t)(TR + 6) * RS * 16;
   dim3 grid((unsigned)((R + TR - 1) / TR), C / DW_CT);
-  // channels per lane: 8 (4 waves per block).  4 (8 waves, twice the waves of the small
-  // late-stage grids) measured slower at every encoder shape (tools/microbench.py dw): the
-  // b64 reads of the 16-byte slot layout conflict 2-way and the staging is the same per block
-  const int nc = dw_nc_override() ? dw_nc_override() : 8;
   // the rolling kernel (compile-time widths, 8 channels per lane, bf16 / fp32)
   const long tiles = (R + TR - 1) / TR;
-  const bool f32l = sizeof(T) == 2 && dw_f32l();
-  const int sppx = DW_CT * (sizeof(T) == 4 || f32l ? 4 : 2) / 16;
-  const int rsr = dw_roll_row_slots(W, PW, sppx);
-  const size_t shm_r1 = (size_t)(TR + 6) * rsr * 16;
-  const size_t shm_roll = (size_t)(2 * TR + 6) * rsr * 16;
-  int ntl = (nc == 8 && !narrow) ? dw_pick_ntl(tiles, C / DW_CT, shm_r1, shm_roll) : 0;
-  if (ntl > 1 && shm_roll > 160 * 1024) ntl = 1;
-#define DWR1_(P, WC, N, FL)                                                                                   \
-  dw_roll_attr<T, P, WC, N, FL>();                                                                            \
-  hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8, N, FL>), dim3((unsigned)((tiles + N - 1) / N), C / DW_CT), \
-                     dim3(256), N == 1 ? shm_r1 : shm_roll, st, B, H, C, (const T*)x, w, bias, (T*)y,          \
-                     (const T*)res, flip)
-#define DWR_(P, WC, N)          \
-  if (f32l) {                   \
-    DWR1_(P, WC, N, true);      \
-  } else {                      \
-    DWR1_(P, WC, N, false);     \
-  }
-#define DWR_ALL(P, WC)                 \
-  do {                                 \
-    switch (ntl) {                     \
-      case 1: DWR_(P, WC, 1); break;   \
-      case 2: DWR_(P, WC, 2); break;   \
-      case 3: DWR_(P, WC, 3); break;   \
-      default: DWR_(P, WC, 4); break;  \
-    }                                  \
+  const int sppx = DW_CT * (int)sizeof(T) / 16;
+  const size_t shm_r1 = (size_t)(TR + 6) * dw_roll_row_slots(W, PW, sppx) * 16;
+#define DWR_ALL(P, WC)                                                                                      \
+  do {                                                                                                     \
+    dw_roll_attr<T, P, WC>();                                                                              \
+    hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8>), dim3((unsigned)tiles, C / DW_CT), dim3(256), shm_r1, \
+                       st, B, H, C, (const T*)x, w, bias, (T*)y, (const T*)res, flip);                     \
   } while (0)
-  if (ntl > 0 && !narrow && (W == 56 || W == 28 || W == 14 || W == 7 || W == 64 || W == 32 || W == 16 || W == 8)) {
+  if (W == 56 || W == 28 || W == 14 || W == 7 || W == 64 || W == 32 || W == 16 || W == 8) {
     switch (W) {
       case 56: DWR_ALL(7, 56); break;
       case 28: DWR_ALL(7, 28); break;
@@ -1173,34 +985,16 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
     return 0;
   }
 #undef DWR_ALL
-#undef DWR_
-#undef DWR1_
-#define DW_(P, WC)                                                                                              \
-  do {                                                                                                         \
-    if (nc == 4)                                                                                               \
-      hipLaunchKernelGGL((dwconv7_kernel<T, P, WC, 4>), grid, dim3(512), shm, st, B, H, W, C, (const T*)x, w,    \
-                         bias, (T*)y, TR, RS, (const T*)res, flip);                                            \
-    else                                                                                                       \
-      hipLaunchKernelGGL((dwconv7_kernel<T, P, WC, 8>), grid, dim3(256), shm, st, B, H, W, C, (const T*)x, w,    \
-                         bias, (T*)y, TR, RS, (const T*)res, flip);                                            \
-  } while (0)
-  switch (W) {  // the encoder's stage widths at 224 and 256 pixel inputs
-    case 56: DW_(7, 56); break;
-    case 28: if (narrow) DW_(4, 28); else DW_(7, 28); break;
-    case 14: if (narrow) DW_(2, 14); else DW_(7, 14); break;
-    case 7: if (narrow) DW_(1, 7); else DW_(7, 7); break;
-    case 64: DW_(8, 64); break;
-    case 32: DW_(8, 32); break;
-    case 16: DW_(8, 16); break;
-    case 8: DW_(8, 8); break;
-    default:
-      switch (PW) {
-        case 8: DW_(8, 0); break;
-        case 7: DW_(7, 0); break;
-        case 4: DW_(4, 0); break;
-        case 2: DW_(2, 0); break;
-        default: DW_(1, 0); break;
-      }
+  // other widths: the runtime-width channel-tiled kernel
+#define DW_(P)                                                                                                  \
+  hipLaunchKernelGGL((dwconv7_kernel<T, P, 0, 8>), grid, dim3(256), shm, st, B, H, W, C, (const T*)x, w, bias, \
+                     (T*)y, TR, RS, (const T*)res, flip)
+  switch (PW) {
+    case 8: DW_(8); break;
+    case 7: DW_(7); break;
+    case 4: DW_(4); break;
+    case 2: DW_(2); break;
+    default: DW_(1); break;
   }
 #undef DW_
   IMGCAP_CHECK_LAUNCH("imgcap_dwconv7");

@@ -625,6 +625,16 @@ static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A
   a.grp = std::max(1, std::min(tm, (int)(std::sqrt(run * t.bn / t.bm) + 0.5)));
   a.ep = ep;
   a.seed_ctr = g_seed_ctr;
+  static const int dbg = [] {
+    const char* e = getenv("IMGCAP_PT_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  static const int grid_all = [] {  // IMGCAP_PT_GRID=1: one block per tile (not persistent)
+    const char* e = getenv("IMGCAP_PT_GRID");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
+  if (grid_all) G = a.ntiles;
   a.c_bytes = ((uint64_t)(M - 1) * ldc + N) * 2;
   a.res_bytes = ep.res ? ((uint64_t)(M - 1) * ep.ldr + N) * 2 : 0;
   a.aux_bytes = ep.aux ? ((uint64_t)(M - 1) * ep.ldaux + N) * 2 : 0;
@@ -1171,23 +1181,12 @@ extern "C" int imgcap_gemm_mx(int M, int N, int K, const void* A, int64_t lda, c
     IMGCAP_REQUIRE(vec_ok && N % 32 == 0 && ldc % 32 == 0 && ep.c_scale && ep.res == nullptr,
                    "imgcap_gemm_mx: MX-FP8 output needs N, ldc % 32 == 0, 16-byte aligned C, c_scale, no res");
   hipStream_t st = (hipStream_t)stream;
-  // The 256x256 tile is opt-in (IMGCAP_MX_TILE=256).  In isolation it wins where it fills a
-  // round of the 256 CUs with K >= 1024 and at C5's K = 3072 stage-3 Linear (62.3 vs 65.9 us,
-  // tools/microbench.py mx), but in the C5 step the 128 tile everywhere measured 5.11k img/s
-  // against 5.05k with the 256 tile at those shapes (tools/gpu/r3_mx.sh: its one block per CU
-  // overlaps worse with the neighbouring kernels).  More stages for the 128 tile (3 / 4: one
-  // block per CU) measured 1.4-1.6x slower at both stage-3 shapes.
-  const char* fe = getenv("IMGCAP_MX_TILE");
-  const bool big = fe && atoi(fe) == 256;
-  if (big) {
-    dim3 grid((N + 255) / 256, (M + 255) / 256);
-    hipLaunchKernelGGL((gemm_mx256_kernel<2>), grid, dim3(512), 0, st, (const uint8_t*)A, (long)lda, As,
-                       (const uint8_t*)B, (long)ldb, Bs, C, (long)ldc, M, N, K, ep, vec_ok ? 1 : 0);
-  } else {
-    dim3 grid((N + 127) / 128, (M + 127) / 128);
-    hipLaunchKernelGGL((gemm_mx_kernel<2>), grid, dim3(256), 0, st, (const uint8_t*)A, (long)lda, As,
-                       (const uint8_t*)B, (long)ldb, Bs, C, (long)ldc, M, N, K, ep, vec_ok ? 1 : 0);
-  }
+  // 128x128 tile, two blocks per CU.  Measured and removed (round 3, tools/gpu/r3_mx.sh): a
+  // 256x256 tile (one block per CU; C5 5.05k vs 5.11k img/s with the 128 tile everywhere) and
+  // 3 / 4 stages for the 128 tile (1.4-1.6x slower at the stage-3 shapes).
+  dim3 grid((N + 127) / 128, (M + 127) / 128);
+  hipLaunchKernelGGL((gemm_mx_kernel<2>), grid, dim3(256), 0, st, (const uint8_t*)A, (long)lda, As,
+                     (const uint8_t*)B, (long)ldb, Bs, C, (long)ldc, M, N, K, ep, vec_ok ? 1 : 0);
   IMGCAP_CHECK_LAUNCH("imgcap_gemm_mx");
   return 0;
 }

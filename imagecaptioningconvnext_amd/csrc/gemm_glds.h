@@ -92,9 +92,6 @@ DEV bf16x8 glds_frag_op(const char* img, int row0, int kk, int lane) {
   }
 }
 
-#ifndef GLDS_ONE_BARRIER
-#define GLDS_ONE_BARRIER 0
-#endif
 // One BM x BN output tile (rows m0.., columns n0..) over k-tiles of slice kz (split-K when
 // kslice > 0): the body shared by the single-problem and the grouped launch.
 template <int BM, int BN, bool AK, bool BKM, int S>
@@ -131,48 +128,8 @@ DEV void glds_tile(const bf16* __restrict__ A, long lda, const bf16* __restrict_
       glds_issue_op<BN, BKM>(B, ldb, n0, N, (kt0 + i) * 64, K, st + TILE_A, w, lane);
     }
   }
-#if GLDS_ONE_BARRIER
-  // one barrier per k-tile: wait for tile kt, barrier, THEN refill the stage tile kt-1 used (every
-  // wave is past it: it has reached this barrier) with tile kt+S-1, and multiply tile kt
-  for (int kt = kt0; kt < nk; ++kt) {
-    const int r = kt - kt0;
-    char* cur = smem + (r % S) * STAGE;
-    const int newer = min(S - 2, nk - 1 - kt);  // tiles issued after kt that may stay in flight
-    if (newer <= 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if ((kt + 1) * 64 > K) {
-        glds_zero_tail<BM, AK>(kt * 64, K, cur, w, lane);
-        glds_zero_tail<BN, BKM>(kt * 64, K, cur + TILE_A, w, lane);
-      }
-    } else if (newer == 1) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT) : "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + S - 1 < nk) {
-      char* nxt = smem + ((r + S - 1) % S) * STAGE;
-      glds_issue_op<BM, AK>(A, lda, m0, M, (kt + S - 1) * 64, K, nxt, w, lane);
-      glds_issue_op<BN, BKM>(B, ldb, n0, N, (kt + S - 1) * 64, K, nxt + TILE_A, w, lane);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = glds_frag_op<BM, AK>(cur, rb + i * 16, kk, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = glds_frag_op<BN, BKM>(cur + TILE_A, cb + j * 16, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // the last stage is read before the epilogue reuses the LDS
-#else
+  // (a one-barrier-per-k-tile order -- wait, barrier, refill the stage of tile k-1, multiply --
+  // measured slower: C2 GEMM census 687 -> 714 us, C3 17.1k -> 16.6k img/s; removed in round 4)
   for (int kt = kt0; kt < nk; ++kt) {
     const int r = kt - kt0;
     char* cur = smem + (r % S) * STAGE;
@@ -216,7 +173,6 @@ DEV void glds_tile(const bf16* __restrict__ A, long lda, const bf16* __restrict_
     asm volatile("" ::: "memory");
   }
 
-#endif
   float* tile = (float*)smem;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {

@@ -123,106 +123,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-// ---- 256x256x128 tile, 8 waves: the gemm256.h geometry on fp8 bytes ----------------------
-// Operand delivery into LDS bounds these tiles (gemm256.h); a 256x256 tile loads twice the FLOP
-// per byte of the 128x128 one.  Each wave owns 128 x 64 outputs (8 x 4 fragments); the 64-deep
-// bf16 k-step image of gemm256 is byte-for-byte a 128-deep fp8 k-step (row swizzle r & 7), so
-// its issue code stages the operands; scales ride along as one 4-byte LDS-DMA per thread (waves
-// 0-3: A rows, 4-7: B rows).  Two stages (132 KiB of LDS, one block per CU).
-template <int S>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_mx256_kernel(
-    const uint8_t* __restrict__ A, long lda, const uint8_t* __restrict__ As, const uint8_t* __restrict__ B, long ldb,
-    const uint8_t* __restrict__ Bs, void* __restrict__ C, long ldc, int M, int N, int K, imgcap_epilogue ep,
-    int vec_ok) {
-  constexpr int BM = 256, BN = 256;
-  constexpr int TILE = BM * 128, SC = BM * 4;
-  constexpr int STAGE = 2 * TILE + 2 * SC;
-  constexpr int TM = 8, TN = 4;
-  constexpr int LDT = BN + 4, EPI_ROWS = 128;
-  constexpr int LPT = (BM + BN) * 8 / 512 + 1;
-  constexpr int SMEM = S * STAGE > EPI_ROWS * LDT * 4 ? S * STAGE : EPI_ROWS * LDT * 4;
-  static_assert(SMEM <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  int bx, by;
-  xcd_remap(bx, by);
-  const int m0 = by * BM, n0 = bx * BN;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w >> 2, wn = w & 3;
-  const int rb = wm * 128, cb = wn * 64;
-  const int fr = lane & 15, fq = lane >> 4;
-  const long kb = K / 32;
-  auto issue = [&](int kt, char* st) {
-    g8_issue<BM, 64, true>((const bf16*)A, lda / 2, m0, M, kt * 64, K / 2, st, w, lane);
-    g8_issue<BN, 64, true>((const bf16*)B, ldb / 2, n0, N, kt * 64, K / 2, st + TILE, w, lane);
-    if (w < 4) mx_issue_scales<BM>(As, kb, m0 + 64 * w, M, kt, st + 2 * TILE + 256 * w, lane);
-    else mx_issue_scales<BN>(Bs, kb, n0 + 64 * (w - 4), N, kt, st + 2 * TILE + SC + 256 * (w - 4), lane);
-  };
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = K / 128;
-#pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < nk) issue(i, smem + i * STAGE);
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt % S) * STAGE;
-    if (kt + S - 1 < nk) issue(kt + S - 1, smem + ((kt + S - 1) % S) * STAGE);
-    const int newer = min(S - 1, nk - 1 - kt);
-    if (newer == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const uint8_t* sa = (const uint8_t*)(cur + 2 * TILE);
-    const uint8_t* sbp = sa + SC;
-    mx_v8i bfr[TN];
-    int xb[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = cb + j * 16 + fr;
-      bfr[j] = mx_frag(cur + TILE, row, fq);
-      xb[j] = sbp[row * 4 + fq];
-    }
-#pragma unroll
-    for (int ih = 0; ih < TM; ih += 4) {  // two halves of the wave's rows: 4 A fragments live at a time
-      mx_v8i af[4];
-      int xa[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = rb + (ih + i) * 16 + fr;
-        af[i] = mx_frag(cur, row, fq);
-        xa[i] = sa[row * 4 + fq];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[ih + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[ih + i][j], 0, 0, 0,
-                                                                            xa[i], 0, xb[j]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-  float* tile = (float*)smem;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {  // as gemm256: fragment rows [4p, 4p+4) of every wave
-    if (pass) __syncthreads();
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          tile[(wm * 64 + ii * 16 + 4 * fq + q) * LDT + cb + j * 16 + fr] = acc[pass * 4 + ii][j][q];
-    __syncthreads();
-    epilogue_tile<BN, EPI_ROWS, 512, 2, 64>(ep, tile, LDT, m0 + pass * 64, n0, M, N, C, ldc, vec_ok != 0);
-  }
-}
-
 // ---- rows -> MX-FP8 (optionally LayerNorm'd first): one wave per row, 8 columns per lane --
 template <typename T>
 __global__ __launch_bounds__(256) void mx_quant_rows_kernel(int R, int K, const T* __restrict__ x, long ldx,

@@ -175,6 +175,7 @@ struct PtArgs {
   imgcap_epilogue ep;
   const uint64_t* seed_ctr;
   uint64_t c_bytes, res_bytes, aux_bytes;  // extents of C, res, aux (buffer range checks)
+  int dbg;  // diagnostics only (IMGCAP_PT_DBG): bit 0 skips the MFMAs, 1 the operand DMA, 2 the barrier, 3 the wait
 };
 
 DEV float pt_bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
@@ -195,6 +196,20 @@ DEV void pt_tile_coords(int L, int tiles_n, int tiles_m, int grp, int& tm, int& 
 // EK: which row x column operands the epilogue may read -- 0 none (bias / scales / GELU with the
 // pre-activation written are all allowed), 1 the residual, 2 any (residual, saved pre-activation
 // for dGELU, old C for beta); fewer live registers for the common forms
+// diagnostic build only (make diag): per-iteration s_memtime stamps of wave 0, iterations < 64,
+// [block][iteration][phase]: 0 top, 1 waited, 2 past barrier, 3 issued, 4 multiplied, 5 end
+#ifdef IMGCAP_STAMPS
+#define PT_STAMP(k)                                                                                         \
+  do {                                                                                                      \
+    if (threadIdx.x == 0 && g_dev_stamps && g < 64)                                                         \
+      g_dev_stamps[((long)blockIdx.x * 64 + g) * 8 + (k)] = __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+#else
+#define PT_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 template <int BM, int BN, int WM, int WN, int S, bool AK, bool BKM, int EK>
 __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
   constexpr int NW = WM * WN, NT = NW * 64;
@@ -224,19 +239,26 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
   const int nk = (K + 63) / 64;
   const int total = my_tiles * nk;
 
-  auto coords = [&](int it, int& m0, int& n0) {
+  auto coords = [&](int it, int& m0, int& n0) {  // once per tile (divisions)
     int tm, tn;
     pt_tile_coords(slot + it * G, tiles_n, tiles_m, a.grp, tm, tn);
     m0 = tm * BM;
     n0 = tn * BN;
   };
-  auto issue = [&](int h) {
-    const int it = h / nk, kt = h - it * nk;
-    int m0, n0;
-    coords(it, m0, n0);
-    char* st = smem + (h % S) * STAGE;
-    pt_issue<BM, AK, NW>(a.A, a.lda, m0, M, kt * 64, K, st, w, lane);
-    pt_issue<BN, BKM, NW>(a.B, a.ldb, n0, N, kt * 64, K, st + TA, w, lane);
+  // the DMA stream's position (tile, k-step, stage) advanced incrementally: no per-step division
+  int is_kt = 0, is_it = 0, is_m0 = 0, is_n0 = 0, is_st = 0;
+  if (my_tiles > 0) coords(0, is_m0, is_n0);
+  auto issue_next = [&]() {
+    char* st = smem + is_st * STAGE;
+    if (!(a.dbg & 2)) {
+      pt_issue<BM, AK, NW>(a.A, a.lda, is_m0, M, is_kt * 64, K, st, w, lane);
+      pt_issue<BN, BKM, NW>(a.B, a.ldb, is_n0, N, is_kt * 64, K, st + TA, w, lane);
+    }
+    is_st = is_st == S - 1 ? 0 : is_st + 1;
+    if (++is_kt == nk) {
+      is_kt = 0;
+      if (++is_it < my_tiles) coords(is_it, is_m0, is_n0);
+    }
   };
 
   const bool has_bias = ep.bias != nullptr, has_cs = ep.colscale != nullptr, has_rs = ep.rowscale != nullptr;
@@ -258,24 +280,27 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int h = 0; h < S - 1 && h < total; ++h) issue(h);
+  for (int h = 0; h < S - 1 && h < total; ++h) issue_next();
 
   int last_epi = -1000;  // iteration of the latest epilogue
+  int kt = 0, cur_st = 0, it = 0;
   for (int g = 0; g < total; ++g) {
-    const int it = g / nk, kt = g - it * nk;
+    PT_STAMP(0);
     // wait for this thread's DMA of step g (ops issued after it may stay in flight)
     const int newer = min(S - 2, total - 1 - g);
-    if (g > last_epi + S - 2) {  // (after an epilogue's wait, steps <= last_epi + S - 2 have landed)
+    if (g > last_epi + S - 2 && !(a.dbg & 8)) {  // (after an epilogue's wait, steps <= last_epi + S - 2 have landed)
       pt_vmwait(newer * LPT + (g == last_epi + S - 1 ? nst : 0));
     }
-    char* cur = smem + (g % S) * STAGE;
+    PT_STAMP(1);
+    char* cur = smem + cur_st * STAGE;
     if ((kt + 1) * 64 > K) {
       pt_zero_tail<BM, AK, NW>(kt * 64, K, cur, w, lane);
       pt_zero_tail<BN, BKM, NW>(kt * 64, K, cur + TA, w, lane);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // step g in LDS for every wave; every wave is past step g - 1
+    if (!(a.dbg & 4)) __builtin_amdgcn_s_barrier();  // step g in LDS for every wave; every wave is past step g - 1
     asm volatile("" ::: "memory");
+    PT_STAMP(2);
 
     const bool last_k = kt == nk - 1;
     int m0 = 0, n0 = 0;
@@ -315,10 +340,12 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
       }
     }
     const bool more = g + S - 1 < total;
-    if (more) issue(g + S - 1);
+    if (more) issue_next();
+    PT_STAMP(3);
 
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      if (a.dbg & 1) break;
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[i] = glds_frag_op<BM, AK>(cur, rb + i * 16, kk, lane);
@@ -331,6 +358,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
 
+    PT_STAMP(4);
     if (last_k) {
       if (more) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
@@ -397,6 +425,12 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
         }
       }
       last_epi = g;
+    }
+    PT_STAMP(5);
+    cur_st = cur_st == S - 1 ? 0 : cur_st + 1;
+    if (++kt == nk) {
+      kt = 0;
+      ++it;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -522,44 +522,6 @@ def cnblock_mlp(z, w1, b1, w2, b2, gamma, x, sd=None, rows_per_sample=1, ln_w=No
     return x
 
 
-# widths the wide fused CNBlock MLP (csrc/cnblock_mlp_wide.hip) accepts; the encoder keeps the
-# LayerNorm + two-GEMM path there (measured faster)
-CNBLOCK_MLP_WIDE_CHANNELS = (384, 512)
-
-
-def cnblock_mlp_wide_pack(w1, w2):
-    """Chunk-major LDS images of a CNBlock's two Linear weights (w1 [4C, C], w2 [C, 4C], bf16) for
-    cnblock_mlp_wide; packed once per weight version."""
-    _check_dev(w1, w2)
-    C = w1.shape[1]
-    img = torch.empty((C // 8) * 128 * C // 2, device=w1.device, dtype=torch.bfloat16)
-    _abi.call("imgcap_cnblock_mlp_wide_pack", C, w1.data_ptr(), w2.data_ptr(), img.data_ptr(), stream())
-    return img
-
-
-def cnblock_mlp_wide_scratch(M, C, device):
-    """(part, sync) scratch of a wide MLP call over M rows: the split-hidden partial slab and the
-    zeroed ticket / flag words (left zero by every call); (None, None) when M needs no split."""
-    pb, sb = ctypes.c_uint64(0), ctypes.c_uint64(0)
-    _abi.call("imgcap_cnblock_mlp_wide_scratch", M, C, ctypes.byref(pb), ctypes.byref(sb))
-    if pb.value == 0:
-        return None, None
-    part = torch.empty(pb.value // 4, device=device, dtype=torch.float32)
-    sync = torch.zeros(max(1, sb.value // 4), device=device, dtype=torch.int32)
-    return part, sync
-
-
-def cnblock_mlp_wide(z, wimg, b1, b2, gamma, x, scratch, sd=None, rows_per_sample=1, ln_w=None, ln_b=None):
-    """cnblock_mlp for C in CNBLOCK_MLP_WIDE_CHANNELS: x += gamma * sd * (GELU(LN(z) W1^T + b1) W2^T
-    + b2) with the weights as packed by cnblock_mlp_wide_pack; scratch from cnblock_mlp_wide_scratch."""
-    _check_dev(z, wimg, x)
-    M, C = x.shape
-    part, sync = scratch
-    _abi.call("imgcap_cnblock_mlp_wide", M, C, z.data_ptr(), ptr(ln_w), ptr(ln_b), wimg.data_ptr(), b1.data_ptr(),
-              b2.data_ptr(), gamma.data_ptr(), ptr(sd), rows_per_sample, x.data_ptr(), ptr(part), ptr(sync), stream())
-    return x
-
-
 def stochastic_depth_scales(probs, B, seed, drop_stream, out):
     _check_dev(probs, out)
     _abi.call("imgcap_stochastic_depth_scales", probs.numel(), B, probs.data_ptr(), seed, drop_stream,

@@ -32,11 +32,6 @@ import torch.distributed as dist
 from . import kernels as K
 
 
-# pipeline mode: one two-branch graph (0, default) or separate encoder / decoder graphs replayed
-# on two streams (1).  Measured (bench, 1x MI355X): split C2 7,070 vs 8,017 img/s, C3 15,233 vs
-# 14,960, C4 6,221 vs 6,181 -- the two-branch graph wins where it matters (C2), the split is
-# within run-to-run spread elsewhere.
-PIPE_SPLIT = int(os.environ.get("IMGCAP_PIPE_SPLIT", "0"))
 # two-branch graph: where the encoder branch forks off the decoder stream -- at the start of the
 # step ("start") or after the decoder forward ("bwd": the encoder overlaps the backward only).
 # Measured (bench, 1x MI355X, two runs each): C2 8,254 vs 8,366 img/s (within spread), C3 16,605
@@ -328,28 +323,6 @@ class TeacherForcedTrainer:
             P["feats"] = [torch.empty_like(f), torch.empty_like(f)]
         S = dict(graphs=[], metrics=[])
         P["sets"][T] = S
-        if PIPE_SPLIT:
-            # one graph per branch and slot, replayed on their own streams (under rocprofv3 the
-            # second branch of a two-branch graph starts late; unprofiled the single graph is as
-            # fast or faster, see PIPE_SPLIT).  Separate memory pools: the two run concurrently.
-            S["genc"], S["gdec"] = [], []
-            pool_e = pool_d = None
-            for k in (0, 1):  # encode the new batch into slot k / train on slot 1-k
-                ge = torch.cuda.CUDAGraph()
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    with torch.cuda.graph(ge, pool=pool_e, stream=side):
-                        P["feats"][k].copy_(self._encode(P["img"]))
-                main.wait_stream(side)
-                pool_e = ge.pool()
-                gd = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gd, pool=pool_d):
-                    m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k])
-                pool_d = gd.pool()
-                S["genc"].append(ge)
-                S["gdec"].append(gd)
-                S["metrics"].append(m)
-            return
         pool = None
         for k in (0, 1):  # graph k: encode the new batch into slot k, train on slot 1-k
             split = self._bucket is not None
@@ -428,16 +401,7 @@ class TeacherForcedTrainer:
             P["feats"][k].copy_(f)
         else:
             S = P["sets"][P["T"][1 - k]]
-            if "genc" in S:
-                main = torch.cuda.current_stream()
-                self._seed_ctr.add_(1)  # before both branches read it (masks drawn at kernel run time)
-                P["side"].wait_stream(main)
-                S["gdec"][k].replay()
-                with torch.cuda.stream(P["side"]):
-                    S["genc"][k].replay()
-                main.wait_stream(P["side"])
-            else:
-                self._replay(S["graphs"][k])
+            self._replay(S["graphs"][k])
             m = S["metrics"][k]
         P["T"][k] = T
         P["i"] += 1

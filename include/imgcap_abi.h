@@ -231,19 +231,6 @@ int imgcap_adaptive_pool_nhwc(int dtype, int B, int H, int W, int C, int OH, int
 int imgcap_cnblock_mlp(int M, int C, const void* y, const float* ln_w, const float* ln_b, const void* w1,
                        const float* b1, const void* w2, const float* b2, const float* gamma, const float* sd,
                        int rows_per_sample, void* x, void* stream);
-/* The same CNBlock MLP for the wide stages, C in {384, 512} (stage 3 of Tiny / Base, which the
- * encoder runs as LayerNorm + two GEMMs with the 4C hidden in HBM; this fused form measured slower
- * at the benchmark row counts and is an opt-in): 8-wave blocks of 64 rows stream
- * the weights through LDS by LDS-DMA from chunk images packed once by
- * imgcap_cnblock_mlp_wide_pack (w1 [4C, C], w2 [C, 4C] bf16 -> img, (C / 8) * 128 * C bytes).
- * Small M splits the hidden over two blocks per 64-row tile: part / sync are caller-owned scratch
- * of the sizes imgcap_cnblock_mlp_wide_scratch reports (0 when M needs no split); sync must be
- * zero before the first call and every call leaves it zero. */
-int imgcap_cnblock_mlp_wide_pack(int C, const void* w1, const void* w2, void* img, void* stream);
-int imgcap_cnblock_mlp_wide_scratch(int M, int C, uint64_t* part_bytes, uint64_t* sync_bytes);
-int imgcap_cnblock_mlp_wide(int M, int C, const void* y, const float* ln_w, const float* ln_b, const void* wimg,
-                            const float* b1, const float* b2, const float* gamma, const float* sd,
-                            int rows_per_sample, void* x, void* part, int* sync, void* stream);
 /* ---------------------------------------------------------------------------------------
  * Backward of the trainable ConvNeXt children (Encoder.fine_tune, encoder.py:29-34; the
  * encoder half of loss.backward() / encoderOptimizer.step() at train.py:278-290).

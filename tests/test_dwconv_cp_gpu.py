@@ -74,25 +74,3 @@ def test_dwconv_cp_backward_data_form(hip_device, monkeypatch, rows, H, C):
     assert _rel(out.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("B,H,C", [(2, 56, 96), (1, 56, 128), (2, 28, 192), (1, 28, 384), (1, 56, 160)])
-def test_dwconv_seg_matches_torch(hip_device, monkeypatch, B, H, C):
-    """The opt-in column-segment kernel of the 56 / 28-wide stages (IMGCAP_DW_SEG=1; any even C,
-    edge segments masked) against torch, against the channel-tiled kernel (IMGCAP_DW_SEG=0), and
-    in the backward data form (flipped taps + residual)."""
-    monkeypatch.setenv("IMGCAP_DW_SEG", "1")
-    g = torch.Generator(device="cpu").manual_seed(B * H + C)
-    x = torch.randn(B, H, H, C, generator=g).bfloat16()
-    w49 = torch.randn(49, C, generator=g) * 0.1
-    bias, res = torch.randn(C, generator=g), torch.randn(B, H, H, C, generator=g).bfloat16()
-    d = lambda t: t.to(hip_device)  # noqa: E731
-    y = torch.empty(B, H, H, C, device=hip_device, dtype=torch.bfloat16)
-    K.dwconv7(d(x), d(w49), d(bias), y)
-    assert _rel(y.cpu(), _ref(x, w49, bias)) < 1e-2
-    monkeypatch.setenv("IMGCAP_DW_SEG", "0")
-    y0 = torch.empty_like(y)
-    K.dwconv7(d(x), d(w49), d(bias), y0)
-    monkeypatch.setenv("IMGCAP_DW_SEG", "1")
-    assert _rel(y.cpu(), y0.cpu()) < 1e-2
-    out = torch.empty_like(y)
-    K.dwconv7_bwd_data(d(x), d(w49), out, res=d(res))
-    assert _rel(out.cpu(), _ref(x, w49, None, flip=True) + res.float()) < 1e-2

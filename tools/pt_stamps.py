@@ -1,0 +1,53 @@
+"""In-kernel s_memtime stamps of the persistent-tile GEMM's k-loop (diagnostic build, GPU box):
+    make -C imagecaptioningconvnext_amd/csrc diag && python tools/pt_stamps.py [cfg]
+Per iteration of wave 0 (first 64 iterations of every block): wait, barrier, DMA issue, MFMAs,
+epilogue / rest; prints median cycles per phase over blocks and iterations, the iteration total,
+and the same for the first iteration of each tile."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["IMGCAP_LIB"] = os.path.join(ROOT, "build", "libimgcap_hip_diag.so")
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from imagecaptioningconvnext_amd import _abi  # noqa: E402
+from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
+
+L = _abi.lib()
+L.imgcap_debug_stamps.argtypes = [ctypes.c_void_p]
+dev = torch.device("cuda:0")
+bf = torch.bfloat16
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+
+
+def run(M, N, Kd):
+    a = torch.randn(M, Kd, device=dev).to(bf)
+    b = torch.randn(N, Kd, device=dev).to(bf)
+    out = torch.empty(M, N, device=dev, dtype=bf)
+    K.gemm_set_pt(cfg)
+    st = torch.zeros(1024 * 64 * 8, device=dev, dtype=torch.int64)
+    for _ in range(3):
+        K.gemm(a, b, trans_b=True, out=out)
+    torch.cuda.synchronize()
+    L.imgcap_debug_stamps(st.data_ptr())
+    K.gemm(a, b, trans_b=True, out=out)
+    torch.cuda.synchronize()
+    L.imgcap_debug_stamps(None)
+    K.gemm_set_pt(0)
+    s = st.view(1024, 64, 8).cpu().double()
+    used = s[:, :, 0] > 0
+    nk = (Kd + 63) // 64
+    names = ["wait", "zero/bar", "issue", "mfma", "epi/rest"]
+    res = []
+    for k in range(5):
+        d = (s[:, :, k + 1] - s[:, :, k])[used]
+        res.append(d.median().item())
+    nxt = (s[:, 1:, 0] - s[:, :-1, 0])[used[:, 1:]]
+    print(f"cfg {cfg} M={M} N={N} K={Kd}: " + "  ".join(f"{n} {v:.0f}" for n, v in zip(names, res)) +
+          f"  | iteration {nxt.median().item():.0f} cyc (p90 {nxt.quantile(0.9).item():.0f})", flush=True)
+
+
+for shape in ((12544, 1536, 384), (12544, 384, 1536), (3136, 768, 3072), (4096, 4096, 4096)):
+    run(*shape)
