@@ -438,6 +438,18 @@ def dw_ln_fused(W, C, dtype):
             and W in (7, 14))
 
 
+def dwconv7_ln_mx(x, w49, bias, ln_w, ln_b, out):
+    """Depthwise 7x7 + LayerNorm (eps 1e-6) with MX-FP8 output: out = (q [B*H*W, C] uint8, s
+    [B*H*W, C/32] uint8), as mx_quant_rows(LN(dwconv7(x))) would give them (the LayerNorm from
+    the fp32 depthwise sums).  dw_ln_fused(W, C) shapes, bf16 x."""
+    _check_dev(x, w49, bias, ln_w, ln_b)
+    B, H, W, C = x.shape
+    q, sc = out
+    _abi.call("imgcap_dwconv7_ln_mx", B, H, W, C, x.data_ptr(), w49.data_ptr(), bias.data_ptr(), ln_w.data_ptr(),
+              ln_b.data_ptr(), q.data_ptr(), sc.data_ptr(), stream())
+    return out
+
+
 def dwconv7_ln(x, w49, bias, ln_w, ln_b, out):
     B, H, W, C = x.shape
     _abi.call("imgcap_dwconv7_ln", dt(x), B, H, W, C, x.data_ptr(), w49.data_ptr(), bias.data_ptr(),

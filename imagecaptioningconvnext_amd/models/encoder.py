@@ -273,9 +273,14 @@ class Encoder(nn.Module):
                 hid = torch.empty(M, 4 * C, device=dev, dtype=ct)
                 zn = torch.empty(M, C, device=dev, dtype=ct)
             x2 = x.view(M, C)
+            # MX stages at W = 7 / 14: depthwise + LayerNorm write the fp8 rows directly
+            mx_dw = mx and K.dw_ln_fused(w, C, ct)
             for blk in blocks:
                 rs = sd[bid] if (sd is not None and blk["sd"] > 0) else None
-                if w <= 64 and (mx or fused or not K.dw_ln_fused(w, C, ct)):
+                if mx_dw:
+                    K.dwconv7_ln_mx(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], znq)
+                    ln = None
+                elif w <= 64 and (mx or fused or not K.dw_ln_fused(w, C, ct)):
                     # channel-tiled depthwise; LayerNorm applied by the consumer
                     K.dwconv7(x, blk["w49"], blk["dwb"], z)
                     ln = (blk["lnw"], blk["lnb"])
@@ -283,7 +288,9 @@ class Encoder(nn.Module):
                     K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], z)
                     ln = (None, None)
                 if mx:  # LN -> fp8 rows; fp8 Linear + GELU -> fp8 hidden; fp8 Linear + scale + residual
-                    if ln[0] is not None:
+                    if ln is None:
+                        pass  # quantised by the depthwise kernel
+                    elif ln[0] is not None:
                         K.mx_quant_rows(z.view(M, C), ln[0], ln[1], 1e-6, out=znq)
                     else:
                         K.mx_quant_rows(z.view(M, C), out=znq)

@@ -213,6 +213,11 @@ int imgcap_dwconv7(int dtype, int B, int H, int W, int C, const void* x, const f
 int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const void* x, const float* w,
                       const float* bias, const float* ln_w, const float* ln_b, void* out,
                       void* stream);
+/* The same (bf16 x, W = 7 / 14, C % 128 == 0, C <= 1024) with the normalised rows written as
+ * MX-FP8 -- q [B*H*W][C] e4m3fn bytes, s [B*H*W][C/32] E8M0 scales, the block encoding of
+ * imgcap_mx_quant_rows -- for the frozen MX-FP8 CNBlocks (config C5): no bf16 round trip. */
+int imgcap_dwconv7_ln_mx(int B, int H, int W, int C, const void* x, const float* w, const float* bias,
+                         const float* ln_w, const float* ln_b, uint8_t* q, uint8_t* s, void* stream);
 /* features[2,4,6] head: LayerNorm2d(C) then gather 2x2/s2 patches into rows
  * out[B*(H/2)*(W/2)][4C] ordered (kh, kw, c) (weights repacked to match; cmajor = 0) or
  * (c, kh, kw) (cmajor = 1: the torch Conv2d weight [2C][C][2][2] is the GEMM operand as is). */
