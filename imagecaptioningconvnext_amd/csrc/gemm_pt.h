@@ -147,6 +147,42 @@ DEV void pt_issue(const bf16* __restrict__ P, long ld, int r0, int R, int k0, in
   }
 }
 
+// Per-lane source of one operand's LDS-DMA pieces, fixed for a tile: the k-step only adds to it
+// (the 64-bit row address math of pt_issue, ~14 VALU per piece, is paid once per tile)
+template <int ROWS, bool KMAJ, int NW>
+struct PtSrc {
+  static constexpr int PER = ROWS * 8 / (NW * 64);
+  const bf16* base[PER];  // k-major: row start + the slot's k offset; m/n-major: the slot's column
+  int koff[PER];          // k-major: slot k offset (clamped per step); m/n-major: k row in the step
+  DEV void set(const bf16* __restrict__ P, long ld, int r0, int R, int w, int lane) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int p = (j * NW + w) * 64 + lane;
+      if constexpr (KMAJ) {
+        const int r = p >> 3, c = (p & 7) ^ (r & 7);
+        base[j] = P + (long)min(r0 + r, R - 1) * ld;
+        koff[j] = c * 8;
+      } else {
+        constexpr int SL = ROWS / 8;
+        const int kr = p / SL, c = (p % SL) ^ (tr_swz(kr) & (SL - 1));
+        base[j] = P + min(r0 + c * 8, ((R - 1) >> 3) << 3);
+        koff[j] = kr;
+      }
+    }
+  }
+  // piece j of k-step kt into the stage image img (slots lane-linear per wave-instruction)
+  DEV void issue(int j, long ld, int kt, int K, char* img, int w) const {
+    const bf16* src;
+    if constexpr (KMAJ) {
+      src = base[j] + min(kt * 64 + koff[j], ((K - 1) >> 3) << 3);
+    } else {
+      src = base[j] + (long)min(kt * 64 + koff[j], K - 1) * ld;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(img + (j * NW + w) * 64 * 16), 16, 0, 0);
+  }
+};
+
 template <int ROWS, bool KMAJ, int NW>
 DEV void pt_zero_tail(int k0, int K, char* img, int w, int lane) {
   constexpr int PER = ROWS * 8 / (NW * 64);
@@ -246,19 +282,36 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
     n0 = tn * BN;
   };
   // the DMA stream's position (tile, k-step, stage) advanced incrementally: no per-step division
-  int is_kt = 0, is_it = 0, is_m0 = 0, is_n0 = 0, is_st = 0;
-  if (my_tiles > 0) coords(0, is_m0, is_n0);
-  auto issue_next = [&]() {
+  int is_kt = 0, is_it = 0, is_st = 0;
+  PtSrc<BM, AK, NW> srcA;
+  PtSrc<BN, BKM, NW> srcB;
+  auto set_src = [&](int itile) {
+    int m0, n0;
+    coords(itile, m0, n0);
+    srcA.set(a.A, a.lda, m0, M, w, lane);
+    srcB.set(a.B, a.ldb, n0, N, w, lane);
+  };
+  if (my_tiles > 0) set_src(0);
+  constexpr int PA = PtSrc<BM, AK, NW>::PER, PB = PtSrc<BN, BKM, NW>::PER;
+  static_assert(PA + PB == LPT, "pieces");
+  // piece q (0 .. LPT-1) of the pending k-step (A pieces first)
+  auto issue_piece = [&](int q) {
+    if (a.dbg & 2) return;
     char* st = smem + is_st * STAGE;
-    if (!(a.dbg & 2)) {
-      pt_issue<BM, AK, NW>(a.A, a.lda, is_m0, M, is_kt * 64, K, st, w, lane);
-      pt_issue<BN, BKM, NW>(a.B, a.ldb, is_n0, N, is_kt * 64, K, st + TA, w, lane);
-    }
+    if (q < PA) srcA.issue(q, a.lda, is_kt, K, st, w);
+    else srcB.issue(q - PA, a.ldb, is_kt, K, st + TA, w);
+  };
+  auto advance = [&]() {  // the pending k-step has been issued
     is_st = is_st == S - 1 ? 0 : is_st + 1;
     if (++is_kt == nk) {
       is_kt = 0;
-      if (++is_it < my_tiles) coords(is_it, is_m0, is_n0);
+      if (++is_it < my_tiles) set_src(is_it);
     }
+  };
+  auto issue_next = [&]() {
+#pragma unroll
+    for (int q = 0; q < LPT; ++q) issue_piece(q);
+    advance();
   };
 
   const bool has_bias = ep.bias != nullptr, has_cs = ep.colscale != nullptr, has_rs = ep.rowscale != nullptr;
@@ -340,24 +393,34 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
       }
     }
     const bool more = g + S - 1 < total;
-    if (more) issue_next();
     PT_STAMP(3);
-
+    // the k-step: 2 x FM groups of FN MFMAs; the LDS-DMA pieces of step g + S - 1 (into the stage
+    // step g - 1 used, free since the barrier) are issued one per group, so the texture unit
+    // works through them while the matrix pipe runs instead of holding every wave at once
+    constexpr int NG = 2 * FM;
+    static_assert(LPT <= NG, "one DMA piece per MFMA group at most");
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      if (a.dbg & 1) break;
       bf16x8 af[FM], bfr[FN];
+      if (!(a.dbg & 1)) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = glds_frag_op<BM, AK>(cur, rb + i * 16, kk, lane);
+        for (int i = 0; i < FM; ++i) af[i] = glds_frag_op<BM, AK>(cur, rb + i * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = glds_frag_op<BN, BKM>(cur + TA, cb + j * 16, kk, lane);
+        for (int j = 0; j < FN; ++j) bfr[j] = glds_frag_op<BN, BKM>(cur + TA, cb + j * 16, kk, lane);
+      }
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
+        if (!(a.dbg & 1)) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j)  // D^T: rows = output columns (B), columns = output rows (A)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j)  // D^T: rows = output columns (B), columns = output rows (A)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        }
+        const int gi = kk * FM + i;  // compile-time after unrolling
+        // spread the LPT pieces evenly over the NG groups
+        if (more && (gi * LPT) / NG != ((gi + 1) * LPT) / NG) issue_piece((gi * LPT) / NG);
+      }
     }
-
+    if (more) advance();
     PT_STAMP(4);
     if (last_k) {
       if (more) {

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 4: depthwise / MX / PT tests after the variant pruning, then the persistent-tile GEMM
-# skeleton probe + in-kernel stamps (diagnostic build)
+# Round 4: depthwise / MX / PT tests after the variant pruning and the MX depthwise epilogue, then
+# the persistent-tile GEMM skeleton probe + in-kernel stamps (diagnostic build)
 set -o pipefail
 O=gpurun_out/r4ptprobe; mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_dwconv_cp_gpu.py tests/test_mx_gpu.py tests/test_gemm_pt_gpu.py tests/test_kernels_gpu.py -k "dwconv or mx or pt" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }

@@ -3,8 +3,8 @@ rocprofv3 --kernel-trace --stats; the kernel names encode the macro tile / wave 
 import torch
 
 dev = torch.device("cuda:0")
-shapes = [(6272, 1536, 384), (6272, 384, 1536), (1568, 768, 3072), (1568, 3072, 768), (1632, 9490, 512),
-          (12544, 1536, 384), (3328, 1536, 512)]
+shapes = [(12544, 1536, 384), (12544, 384, 1536), (3136, 3072, 768), (3136, 768, 3072), (3328, 1536, 512),
+          (3328, 512, 512), (4096, 4096, 4096)]
 for M, N, K in shapes:
     a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
     b = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
