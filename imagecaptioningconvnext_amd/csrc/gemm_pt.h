@@ -31,39 +31,28 @@ typedef unsigned pt_u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t PT_OOB = 0x80000000u;  // buffer offset past every buffer this kernel addresses
 
-// raw buffer descriptor (stride 0, num_records = bytes) in SGPRs
-DEV pt_i32x4 pt_rsrc(const void* base, uint64_t bytes) {
-  const uint64_t b = (uint64_t)base;
-  pt_i32x4 r;
-  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
-  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(b >> 32) & 0xffffu));
-  r[2] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes));
-  r[3] = 0x00020000;
-  return r;
+// raw buffer descriptor (stride 0, num_records = bytes; offsets past it read 0 / drop the store)
+typedef __amdgpu_buffer_rsrc_t pt_rsrc_t;
+DEV pt_rsrc_t pt_rsrc(const void* base, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes),
+                                           0x00020000);
 }
 
-// loads / stores the compiler does not see (waited for by the kernel's own counted s_waitcnt).
-// Each starts with s_nop 4: hipcc pads no hazard inside an asm statement, and the descriptor
-// SGPRs may have just been written by a VALU instruction (a v_readlane restoring a spilled SGPR),
-// which a VMEM instruction may read only 5 wait states later -- an unpadded read took a stale
-// descriptor and faulted.
-DEV pt_u32x2 pt_ld64(pt_i32x4 rs, uint32_t off) {
-  pt_u32x2 v;
-  asm volatile("s_nop 4\n\tbuffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs));
-  return v;
+// the epilogue's loads / stores as compiler-visible buffer ops.  (Inline-asm loads waited for by
+// the kernel's own counts were tried first: the compiler takes an asm output as ready when the
+// statement ends, and under register pressure it spilled a bias register straight after its
+// load was issued -- the stored value was whatever the register held before the load returned.)
+// The compiler's own vmcnt before a use counts the LDS-DMA pieces issued after the load, so the
+// prefetch stays in flight; the kernel's counted waits below see these ops in the same order.
+DEV pt_u32x2 pt_ld64(pt_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(pt_u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
 }
-DEV pt_u32x4 pt_ld128(pt_i32x4 rs, uint32_t off) {
-  pt_u32x4 v;
-  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs));
-  return v;
+DEV pt_u32x4 pt_ld128(pt_rsrc_t rs, uint32_t off) {
+  return __builtin_bit_cast(pt_u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
 }
-DEV uint32_t pt_ld32(pt_i32x4 rs, uint32_t off) {
-  uint32_t v;
-  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs));
-  return v;
-}
-DEV void pt_st64(pt_i32x4 rs, uint32_t off, pt_u32x2 v) {
-  asm volatile("s_nop 4\n\tbuffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(rs) : "memory");
+DEV uint32_t pt_ld32(pt_rsrc_t rs, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0); }
+DEV void pt_st64(pt_rsrc_t rs, uint32_t off, pt_u32x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, 0);
 }
 
 // s_waitcnt vmcnt(n) for a runtime n (uniform): the immediates this kernel needs
@@ -211,8 +200,18 @@ struct PtArgs {
   imgcap_epilogue ep;
   const uint64_t* seed_ctr;
   uint64_t c_bytes, res_bytes, aux_bytes;  // extents of C, res, aux (buffer range checks)
-  int dbg;  // diagnostics only (IMGCAP_PT_DBG): bit 0 skips the MFMAs, 1 the operand DMA, 2 the barrier, 3 the wait
+  int dbg;  // diagnostic build only (IMGCAP_PT_DBG): bit 0 skips the MFMAs, 1 the operand DMA, 2 the barrier, 3 the wait
 };
+
+// the diagnostic switches exist only in the stamps build: in the product kernel they fold away, so
+// the k-step is one basic block the scheduler can interleave (LDS reads of the next fragment group
+// above the current MFMAs); a runtime test around each MFMA group had split it into ~20 blocks and
+// serialised read -> wait -> MFMA
+#ifdef IMGCAP_STAMPS
+#define PT_DBG(bit) ((a.dbg & (bit)) != 0)
+#else
+#define PT_DBG(bit) false
+#endif
 
 DEV float pt_bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 DEV float pt_bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -296,7 +295,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
   static_assert(PA + PB == LPT, "pieces");
   // piece q (0 .. LPT-1) of the pending k-step (A pieces first)
   auto issue_piece = [&](int q) {
-    if (a.dbg & 2) return;
+    if (PT_DBG(2)) return;
     char* st = smem + is_st * STAGE;
     if (q < PA) srcA.issue(q, a.lda, is_kt, K, st, w);
     else srcB.issue(q - PA, a.ldb, is_kt, K, st + TA, w);
@@ -319,12 +318,12 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
   const bool aux_out = ep.aux != nullptr && ep.act == IMGCAP_ACT_GELU;            // pre-activation written
   const bool aux_in = EK >= 2 && ep.aux != nullptr && ep.act == IMGCAP_ACT_DGELU;  // saved pre-activation read
   const int nst = aux_out ? 2 * NST : NST;
-  const pt_i32x4 rs_c = pt_rsrc(a.C, a.c_bytes);
-  const pt_i32x4 rs_res = pt_rsrc(has_res ? ep.res : a.C, has_res ? a.res_bytes : 0);
-  const pt_i32x4 rs_aux = pt_rsrc(ep.aux ? ep.aux : a.C, ep.aux ? a.aux_bytes : 0);
-  const pt_i32x4 rs_bias = pt_rsrc(has_bias ? (const void*)ep.bias : a.C, has_bias ? (uint64_t)N * 4 : 0);
-  const pt_i32x4 rs_cs = pt_rsrc(has_cs ? (const void*)ep.colscale : a.C, has_cs ? (uint64_t)N * 4 : 0);
-  const pt_i32x4 rs_rs =
+  const pt_rsrc_t rs_c = pt_rsrc(a.C, a.c_bytes);
+  const pt_rsrc_t rs_res = pt_rsrc(has_res ? ep.res : a.C, has_res ? a.res_bytes : 0);
+  const pt_rsrc_t rs_aux = pt_rsrc(ep.aux ? ep.aux : a.C, ep.aux ? a.aux_bytes : 0);
+  const pt_rsrc_t rs_bias = pt_rsrc(has_bias ? (const void*)ep.bias : a.C, has_bias ? (uint64_t)N * 4 : 0);
+  const pt_rsrc_t rs_cs = pt_rsrc(has_cs ? (const void*)ep.colscale : a.C, has_cs ? (uint64_t)N * 4 : 0);
+  const pt_rsrc_t rs_rs =
       pt_rsrc(has_rs ? (const void*)ep.rowscale : a.C, has_rs ? (uint64_t)((M + ep.rows_per_scale - 1) / ep.rows_per_scale) * 4 : 0);
 
   f32x4 acc[FM][FN];
@@ -341,7 +340,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
     PT_STAMP(0);
     // wait for this thread's DMA of step g (ops issued after it may stay in flight)
     const int newer = min(S - 2, total - 1 - g);
-    if (g > last_epi + S - 2 && !(a.dbg & 8)) {  // (after an epilogue's wait, steps <= last_epi + S - 2 have landed)
+    if (g > last_epi + S - 2 && !PT_DBG(8)) {  // (after an epilogue's wait, steps <= last_epi + S - 2 have landed)
       pt_vmwait(newer * LPT + (g == last_epi + S - 1 ? nst : 0));
     }
     PT_STAMP(1);
@@ -351,7 +350,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
       pt_zero_tail<BN, BKM, NW>(kt * 64, K, cur + TA, w, lane);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!(a.dbg & 4)) __builtin_amdgcn_s_barrier();  // step g in LDS for every wave; every wave is past step g - 1
+    if (!PT_DBG(4)) __builtin_amdgcn_s_barrier();  // step g in LDS for every wave; every wave is past step g - 1
     asm volatile("" ::: "memory");
     PT_STAMP(2);
 
@@ -399,27 +398,35 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
     // works through them while the matrix pipe runs instead of holding every wave at once
     constexpr int NG = 2 * FM;
     static_assert(LPT <= NG, "one DMA piece per MFMA group at most");
+    // one straight-line body per case (DMA pieces or none), no runtime test inside
+    auto kstep = [&](auto with_dma) {
+      constexpr bool WD = decltype(with_dma)::value;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[FM], bfr[FN];
-      if (!(a.dbg & 1)) {
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[FM], bfr[FN];
+        if (!PT_DBG(1)) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = glds_frag_op<BM, AK>(cur, rb + i * 16, kk, lane);
+          for (int i = 0; i < FM; ++i) af[i] = glds_frag_op<BM, AK>(cur, rb + i * 16, kk, lane);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = glds_frag_op<BN, BKM>(cur + TA, cb + j * 16, kk, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        if (!(a.dbg & 1)) {
-#pragma unroll
-          for (int j = 0; j < FN; ++j)  // D^T: rows = output columns (B), columns = output rows (A)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) bfr[j] = glds_frag_op<BN, BKM>(cur + TA, cb + j * 16, kk, lane);
         }
-        const int gi = kk * FM + i;  // compile-time after unrolling
-        // spread the LPT pieces evenly over the NG groups
-        if (more && (gi * LPT) / NG != ((gi + 1) * LPT) / NG) issue_piece((gi * LPT) / NG);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          if (!PT_DBG(1)) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j)  // D^T: rows = output columns (B), columns = output rows (A)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          }
+          const int gi = kk * FM + i;  // compile-time after unrolling
+          // spread the LPT pieces evenly over the NG groups
+          if constexpr (WD) {
+            if ((gi * LPT) / NG != ((gi + 1) * LPT) / NG) issue_piece((gi * LPT) / NG);
+          }
+        }
       }
-    }
+    };
+    if (more) kstep(std::true_type{});
+    else kstep(std::false_type{});
     if (more) advance();
     PT_STAMP(4);
     if (last_k) {

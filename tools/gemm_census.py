@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
-from imagecaptioningconvnext_amd.roofline import time_launch  # noqa: E402
+from tools.microbench import time_launch  # noqa: E402
 from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer  # noqa: E402
 
 cfgname = sys.argv[1] if len(sys.argv) > 1 else "C2"
