@@ -517,9 +517,11 @@ static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, lon
     // 64x64 LDS-DMA tile (4 blocks per CU): small grids (the Transformer decoder's d=512
     // projections at B*L rows) and short-K mid-size grids, where the 128 tile's fixed per-tile
     // latency dominates (tools/microbench.py small: 1.2-1.5x at 104-975 128-tiles with K <= 1536;
-    // the 128 tile wins back only on >= ~1000-tile grids)
+    // the 128 tile wins back only on >= ~1000-tile grids with K > 384: at K <= 384 the 64 tile
+    // stays ahead on any grid, tools/gemm_modes.py: 12544x1536x384 38.7 vs 42.0 us, 25088x1024x256
+    // 39.9 vs 48.1)
     if (sk == 1 && (mode == 6 || (mode < 0 && (tiles128 < 128 || (tiles128 < 1024 && K <= 1536) ||
-                                                 (tiles128 < 256 && K <= 4096)))))
+                                                 (tiles128 < 256 && K <= 4096) || K <= 384))))
       return {IMGCAP_GEMM_GLDS64, 1};
     if (sk > 1 || tiles128 >= 128 || mode == 4) return {IMGCAP_GEMM_GLDS, sk};
     if (mode == 7) return {IMGCAP_GEMM_GLDS128X64, 1};

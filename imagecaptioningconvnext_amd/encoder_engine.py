@@ -116,11 +116,53 @@ class EncoderEngine:
                res=x.view(M, C), out=xo.view(M, C))
         return xo, dict(x=x, w49=w49, z=z, zn=zn, mean=mean, rstd=rstd, hpre=hpre, a=a, rs=rs)
 
+    # -- gradient buckets (DDP) ----------------------------------------------------------------
+    BUCKET_BYTES = 25 << 20  # torch DDP's default bucket_cap_mb (trainMultiGPU.py:233)
+
+    def _units(self):
+        """(child, block or None, flat [lo, hi)) of every trainable unit in backward order."""
+        fp = self.fp
+        children = list(self.enc.convnext.children())
+        units = []
+        for ci in range(len(children) - 1, self.s0 - 1, -1):
+            if ci % 2 == 1:
+                for j in range(len(children[ci]) - 1, -1, -1):
+                    pre = f"convnext.{ci}.{j}."
+                    units.append((ci, j, fp.span([n for n in fp.params if n.startswith(pre)])))
+            else:
+                pre = f"convnext.{ci}."
+                units.append((ci, None, fp.span([n for n in fp.params if n.startswith(pre)])))
+        return units
+
+    def grad_buckets(self, cap_bytes=None):
+        """Flat ranges in the order backward() calls ``bucket_hook``: consecutive units (CNBlocks,
+        downsamples) in backward order cut once they reach ``cap_bytes`` of fp32 gradients (25 MiB:
+        DDP's default bucket size, trainMultiGPU.py:233-235); the hook fires when the unit that
+        completes a bucket is done, so its all-reduce overlaps the blocks below.  The last, partial
+        bucket is left to the caller (final when backward() returns).  The flat buffer holds the
+        units in forward order, so each bucket is one contiguous range."""
+        cap = (self.BUCKET_BYTES if cap_bytes is None else cap_bytes) // 4
+        out, fire = [], set()
+        hi = None
+        for ci, j, (lo, uhi) in self._units():
+            hi = uhi if hi is None else hi
+            if hi - lo >= cap:
+                out.append((lo, hi))
+                fire.add((ci, j))
+                hi = None
+        self._fire = fire
+        return out
+
     # -- backward ----------------------------------------------------------------------------
-    def backward(self, saved, dfeat, gbuf=None):
+    def backward(self, saved, dfeat, gbuf=None, bucket_hook=None):
         """dfeat: dL/d(features) [B, s, s, E] (any float dtype).  Writes the trainable
-        parameters' gradients into ``gbuf`` (default ``fp.grad``; overwritten, not accumulated)."""
+        parameters' gradients into ``gbuf`` (default ``fp.grad``; overwritten, not accumulated).
+        ``bucket_hook``: called when the unit completing each grad_buckets() range is done."""
         ct = self.ct
+        fire = getattr(self, "_fire", None) if bucket_hook is not None else None
+        if bucket_hook is not None and fire is None:
+            self.grad_buckets()
+            fire = self._fire
         gbuf = self.fp.grad if gbuf is None else gbuf
         gbuf.zero_()
         x = saved["pre_pool"]
@@ -137,8 +179,12 @@ class EncoderEngine:
             if kind == "stage":
                 for j in range(len(st) - 1, -1, -1):
                     dx = self._block_bwd(dx, self._blk(ci, j, gbuf), st[j], need_dx=need_dx or j > 0)
+                    if fire and (ci, j) in fire:
+                        bucket_hook()
             else:
                 dx = self._down_bwd(dx, self._down(ci, gbuf), st, need_dx=need_dx)
+                if fire and (ci, None) in fire:
+                    bucket_hook()
         return gbuf
 
     def _block_bwd(self, dout, p, st, need_dx):

@@ -413,6 +413,10 @@ class LstmEngine:
         GEMMs of the rest still run (DDP-style bucketed all-reduce)."""
         return self.fp.span(["embedding.weight", "fc.weight", "fc.bias"])
 
+    def grad_buckets(self):
+        """Flat ranges in the order backward() calls ``bucket_hook``: the early bucket."""
+        return [self.early_bucket()]
+
     def backward(self, s, dlogits=None, dalpha=None, gbuf=None, want_denc=False, bucket_hook=None):
         """Writes dL/dparams into ``gbuf`` (default: the flat grad buffer).  Default upstream:
         the fused loss of forward(loss=True); otherwise ``dlogits`` [B*T, V(pad)] (compute

@@ -45,6 +45,18 @@ def _trainable(encoder):
     return bool(fn()) if callable(fn) else False
 
 
+def _complement(ranges, n):
+    """[lo, hi) pieces of [0, n) that no range in ``ranges`` covers (ranges disjoint)."""
+    out, at = [], 0
+    for lo, hi in sorted(ranges):
+        if lo > at:
+            out.append((at, lo))
+        at = max(at, hi)
+    if at < n:
+        out.append((at, n))
+    return out
+
+
 class _SeqGraphs:
     """The sequential-schedule step as two captured graphs (encoder half, decoder half)."""
 
@@ -89,22 +101,20 @@ class TeacherForcedTrainer:
             # split_rows): beside the pipelined encoder branch only the forward is split (the
             # encoder needs the CUs the backward would take); the sequential schedule splits both
             self.eng.row_groups = 4 | (1 if pipeline else 3)
-        # bucketed gradient all-reduce (world > 1): early bucket [lo, hi) of the decoder's flat
-        # grads, reduced on self._comm while the rest of the backward runs
+        # bucketed gradient all-reduce (world > 1): self._buckets = [(FlatParams, [(lo, hi), ..]),
+        # ..] in the order the engines' backward passes call the bucket hook; each is reduced on
+        # self._comm as soon as its gradients are final, while the rest of the backward runs
         self._feat_slot = None   # sequential graph: encoder features between the two graphs
         self._feat_meta = None
         self._enc_saved = None
-        self._bucket = None
+        self._buckets = None
         self._hook_mode = None   # None | "eager" (issue the bucket now) | "split" (capture split)
         self._split = None
-        self._early_issued = False
+        self._next_bucket = 0    # hook calls so far in the step being run / captured
+        self._issued = 0         # buckets already in flight when _update runs
         self._comm = None
-        if self.world > 1 and hasattr(self.eng, "early_bucket"):
-            self._bucket = self.eng.early_bucket()
-            if _trainable(encoder):  # the whole decoder, reduced beside the encoder backward
-                self._bucket = (0, self.eng.fp.grad.numel())
-            if torch.cuda.is_available() and self.eng.fp.grad.is_cuda:
-                self._comm = torch.cuda.Stream(device=self.eng.fp.grad.device)
+        if self.world > 1 and torch.cuda.is_available() and self.eng.fp.grad.is_cuda:
+            self._comm = torch.cuda.Stream(device=self.eng.fp.grad.device)
         if self.world > 1:
             # DDP construction broadcasts rank 0's parameters (trainMultiGPU.py:233); the encoder is
             # broadcast too because its weights are randomly initialised here (SURVEY.md §7 v)
@@ -115,6 +125,25 @@ class TeacherForcedTrainer:
         # fine-tuned encoder children (Encoder.fine_tune, train.py:113-114): their own flat
         # parameter/grad/Adam buffers, trained with encoder_lr after the same all-reduce
         self.enc_eng = encoder.engine() if _trainable(encoder) else None
+        self._plan_buckets()
+
+    def _plan_buckets(self):
+        """DDP gradient buckets (trainMultiGPU.py:233-235,256,384: torch DDP all-reduces ~25 MiB
+        buckets as the backward produces them): the decoder engine's (LSTM: embedding + fc;
+        Transformer: one per layer), then, with a fine-tuned encoder, the rest of the decoder
+        (final before the encoder backward starts) and the encoder's ~25 MiB buckets.  What no
+        bucket covers is reduced in _update.  Every element is summed once either way, so the
+        averaged gradients are the same as one all-reduce of each flat buffer."""
+        self._buckets = None
+        if self.world == 1 or not hasattr(self.eng, "grad_buckets"):
+            return
+        fp = self.eng.fp
+        dec = list(self.eng.grad_buckets())
+        bl = [(fp, [r]) for r in dec]
+        if self.enc_eng is not None:
+            bl.append((fp, _complement(dec, fp.grad.numel())))
+            bl += [(self.enc_eng.fp, [r]) for r in self.enc_eng.grad_buckets()]
+        self._buckets = bl
 
     def enable_encoder_finetune(self, startingLayer):
         """train.py:160-166: from this step on, children[startingLayer:] of the encoder train
@@ -122,8 +151,7 @@ class TeacherForcedTrainer:
         self.encoder.fine_tune(fine_tune=True, startingLayer=startingLayer)
         self.flush()
         self.enc_eng = self.encoder.engine() if _trainable(self.encoder) else None
-        if self._bucket is not None and self.enc_eng is not None:
-            self._bucket = (0, self.eng.fp.grad.numel())
+        self._plan_buckets()
         self._graph = None
         self._pipe = None
         self._seq_store = {}
@@ -184,71 +212,93 @@ class TeacherForcedTrainer:
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
         if mid is not None:
             mid()
-        hook = self._bucket is not None and self._hook_mode is not None
+        hook = self._buckets is not None and self._hook_mode is not None
+        kw = {"bucket_hook": self._bucket_hook} if hook else {}
+        self._next_bucket = 0
         if es is not None:
-            # fine-tuned encoder: the decoder's gradients are all final once its backward is done;
-            # their all-reduce (one bucket, the whole decoder) runs on the comm stream while the
-            # encoder children's backward runs (trainMultiGPU.py:233-235,256,384: DDP's reducer
-            # overlaps the buckets with the rest of the backward)
-            self.eng.backward(s, want_denc=True)
+            # fine-tuned encoder: the decoder's remaining gradients are final once its backward is
+            # done; their all-reduce runs on the comm stream while the encoder children's
+            # backward runs, which in turn hands over its ~25 MiB buckets as its blocks finish
+            # (trainMultiGPU.py:233-235,256,384: DDP's reducer overlaps the buckets with the rest
+            # of the backward)
+            self.eng.backward(s, want_denc=True, **kw)
             if hook:
                 self._bucket_hook()
-            self.enc_eng.backward(es, s["denc"].reshape(feats.shape))
+            self.enc_eng.backward(es, s["denc"].reshape(feats.shape), **kw)
         else:
-            kw = {"bucket_hook": self._bucket_hook} if hook else {}
             self.eng.backward(s, **kw)
+        if hook and self._hook_mode == "eager":
+            self._issued = self._next_bucket
         return s["metrics"]
 
     # ---- bucketed gradient all-reduce --------------------------------------------------------
-    def _reduce_early(self):
-        """All-reduce the early bucket on the communication stream (ordered after the current
-        stream's work so far)."""
-        lo, hi = self._bucket
-        g = self.eng.fp.grad
+    def _reduce_ranges(self, fp, ranges):
+        """All-reduce (sum) fp.grad[lo:hi] for each range on the communication stream, ordered
+        after the current stream's work so far (every collective of the step goes through that
+        one stream, in the same order on every rank)."""
+        g = fp.grad
         if self._comm is None:
-            dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.pg)
-        else:
-            self._comm.wait_stream(torch.cuda.current_stream(g.device))
-            with torch.cuda.stream(self._comm):
-                dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.pg)
-        self._early_issued = True
+            for lo, hi in ranges:
+                if hi > lo:
+                    dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.pg)
+            return
+        self._comm.wait_stream(torch.cuda.current_stream(g.device))
+        with torch.cuda.stream(self._comm):
+            for lo, hi in ranges:
+                if hi > lo:
+                    dist.all_reduce(g[lo:hi], op=dist.ReduceOp.SUM, group=self.pg)
+
+    def _reduce_bucket(self, k):
+        fp, ranges = self._buckets[k]
+        self._reduce_ranges(fp, ranges)
 
     def _bucket_hook(self):
+        k = self._next_bucket
+        self._next_bucket += 1
         if self._hook_mode == "eager":
-            self._reduce_early()
+            self._reduce_bucket(k)
         elif self._hook_mode == "split":
             self._split()
 
     def _begin_split_capture(self, pool=None, join=None):
-        """Capture the step as two graphs split at the bucket hook (world > 1); returns
-        (g1, g2).  ``join``: streams to join before the split (forked branches of graph 1)."""
-        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        """Capture the step as one graph per bucket hook + 1 (world > 1): the hooks end a graph
+        and begin the next in the same pool; returns the list the graphs are appended to.
+        ``join``: streams to join at the first split (forked branches of the first graph)."""
+        graphs = [torch.cuda.CUDAGraph()]
+        joined = []
 
         def split():
             cur = torch.cuda.current_stream()
-            for st in (join or ()):
-                cur.wait_stream(st)
-            g1.capture_end()
-            g2.capture_begin(pool=g1.pool())
+            if not joined:
+                for st in (join or ()):
+                    cur.wait_stream(st)
+                joined.append(True)
+            graphs[-1].capture_end()
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=graphs[0].pool())
+            graphs.append(g)
         self._split = split
         self._hook_mode = "split"
-        g1.capture_begin(pool=pool)
-        return g1, g2
+        graphs[0].capture_begin(pool=pool)
+        return graphs
 
-    def _end_split_capture(self, g2):
+    def _end_split_capture(self, graphs):
         self._hook_mode = None
         self._split = None
-        g2.capture_end()
+        graphs[-1].capture_end()
+        return tuple(graphs)
 
     def _replay(self, g):
         if isinstance(g, _SeqGraphs):  # encoder half, then decoder half
             g.enc.replay()
             self._replay(g.dec)
             return
-        if isinstance(g, tuple):  # split step: early bucket reduced between the two halves
-            g[0].replay()
-            self._reduce_early()
-            g[1].replay()
+        if isinstance(g, tuple):  # split step: bucket i reduced between graphs i and i + 1
+            for i, gi in enumerate(g):
+                gi.replay()
+                if i + 1 < len(g):
+                    self._reduce_bucket(i)
+            self._issued = len(g) - 1
         else:
             g.replay()
 
@@ -277,16 +327,16 @@ class TeacherForcedTrainer:
             feats, es = self._enc_part(self._inputs[0])
             self._feat_slot.copy_(feats)
         self._enc_saved = es  # the fine-tuned children's activations live in ge's pool
-        if self._bucket is not None:  # decoder half split at the early-bucket hook (DDP)
+        if self._buckets is not None:  # decoder half split at the bucket hooks (DDP)
             cap = torch.cuda.Stream(device=dev)
             cap.wait_stream(torch.cuda.current_stream(dev))
             torch.cuda.synchronize(dev)
             with torch.cuda.stream(cap):
-                g1, g2 = self._begin_split_capture()
+                gs = self._begin_split_capture()
                 self._metrics = self._dec(self._feat_slot, self._inputs[1], self._inputs[2], es)
-                self._end_split_capture(g2)
+                gs = self._end_split_capture(gs)
             torch.cuda.current_stream(dev).wait_stream(cap)
-            self._graph = _SeqGraphs(ge, (g1, g2))
+            self._graph = _SeqGraphs(ge, gs)
             return
         gd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gd):
@@ -325,13 +375,13 @@ class TeacherForcedTrainer:
         P["sets"][T] = S
         pool = None
         for k in (0, 1):  # graph k: encode the new batch into slot k, train on slot 1-k
-            split = self._bucket is not None
+            split = self._buckets is not None
             cap = torch.cuda.Stream(device=dev)
             cap.wait_stream(main)
             torch.cuda.synchronize(dev)
             with torch.cuda.stream(cap):
-                if split:  # two graphs; the encoder branch joins graph 1 at the split
-                    g1, g2 = self._begin_split_capture(pool, join=(side,))
+                if split:  # one graph per bucket + 1; the encoder branch joins the first at its end
+                    gs = self._begin_split_capture(pool, join=(side,))
                 else:
                     g = torch.cuda.CUDAGraph()
                     g.capture_begin(pool=pool)
@@ -348,8 +398,7 @@ class TeacherForcedTrainer:
                               mid=fork if PIPE_FORK == "bwd" else None)
                 cur.wait_stream(side)
                 if split:
-                    self._end_split_capture(g2)
-                    g = (g1, g2)
+                    g = self._end_split_capture(gs)
                 else:
                     g.capture_end()
             main.wait_stream(cap)
@@ -483,21 +532,19 @@ class TeacherForcedTrainer:
             red[0] = red[0] / red[1]  # global token-weighted mean loss, back in m's layout
         skip = red[4:5] if red.numel() > 4 else None
         if self.world > 1:
-            if self._early_issued:  # the early bucket is in flight on the comm stream: the rest
-                lo, hi = self._bucket
-                for a, b in ((0, lo), (hi, fp.grad.numel())):
-                    if b > a:
-                        dist.all_reduce(fp.grad[a:b], op=dist.ReduceOp.SUM, group=self.pg)
-                if self._comm is not None:
-                    torch.cuda.current_stream(fp.grad.device).wait_stream(self._comm)
-                self._early_issued = False
-            else:
-                dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
+            # the buckets issued during the backward are in flight on the comm stream; the ranges
+            # none of them covers follow on the same stream, then clip + Adam wait for all of it
+            issued = self._buckets[:self._issued] if self._buckets else []
+            self._issued = 0
+            flats = [fp] + ([self.enc_eng.fp] if self.enc_eng is not None else [])
+            for f in flats:
+                done = [r for bf, rs in issued if bf is f for r in rs]
+                self._reduce_ranges(f, _complement(done, f.grad.numel()))
+            if self._comm is not None:
+                torch.cuda.current_stream(fp.grad.device).wait_stream(self._comm)
         fp.adam_step(self.decoder_lr, self.grad_clip, grad_div=float(self.world), skip=skip)
         if self.enc_eng is not None:
             efp = self.enc_eng.fp
-            if self.world > 1:
-                dist.all_reduce(efp.grad, op=dist.ReduceOp.SUM, group=self.pg)
             efp.adam_step(self.encoder_lr, self.grad_clip, grad_div=float(self.world), skip=skip)
             upd = getattr(self.encoder, "weights_updated", None)
             if upd is not None:  # packed copies of the fine-tuned children go stale

@@ -291,11 +291,27 @@ class TransformerEngine:
 
     # ---------------------------------------------------------------------------------------
     def early_bucket(self):
-        """Flat range whose gradients are final when backward() calls ``bucket_hook``: the
-        token embedding, reduced while the grouped weight-gradient GEMMs run."""
+        """Flat range of the token embedding (final once its backward scatter ran)."""
         return self.fp.span(["embedding.weight"])
 
+    def grad_buckets(self):
+        """Flat ranges in the order backward() calls ``bucket_hook``: one per decoder layer, the
+        last layer first (trainMultiGPU.py:233-235: DDP all-reduces gradient buckets as the
+        backward produces them).  The rest (fc_out, embedding, encoder_proj) is final when
+        backward() returns."""
+        out = []
+        for i in reversed(range(self.layers)):
+            pre = f"{self.layer_prefix}.{i}."
+            out.append(self.fp.span([n for n in self.fp.params if n.startswith(pre)]))
+        return out
+
     def backward(self, s, dlogits=None, gbuf=None, want_denc=False, bucket_hook=None):
+        """Gradients of the step into ``gbuf`` (default fp.grad).  With ``bucket_hook`` (DDP) a
+        layer's deferred weight / bias gradients run as their own grouped launches when its
+        backward is done and the hook is called once per layer (grad_buckets() order), so its
+        all-reduce overlaps the layers below; without it every layer's are deferred to one set of
+        grouped launches at the end.  Each product / column sum is computed by the same kernel
+        either way (per-problem tiles, fixed-order sums): the gradients are bitwise the same."""
         fp, ct = self.fp, self.ct
         gbuf = fp.grad if gbuf is None else gbuf
         G = lambda name, shape=None, count=None: fp.g(name, shape, count, buf=gbuf)  # noqa: E731
@@ -368,6 +384,10 @@ class TransformerEngine:
             cb.add(dqkv, G(lw("self_attn.in_proj_bias")))
             K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
             dx = ds1
+            if bucket_hook is not None:  # layer i's gradients final: its bucket's all-reduce
+                wgb.run()
+                cb.run()
+                bucket_hook()
         # embedding (dropout mask recomputed; PE has no parameters)
         K.embedding_bwd(s["caps"].view(-1), dx, G("embedding.weight"), drop_p=p, seed=seed, drop_stream=_S_EMB)
         denc = None
@@ -379,8 +399,6 @@ class TransformerEngine:
                 denc = K.gemm(dmem_c, fp.w("encoder_proj.weight")).view(B, P, self.E)
         elif want_denc:
             denc = dmem.to(ct).view(B, P, d)
-        if bucket_hook is not None:
-            bucket_hook()
         wgb.run()
         cb.run()
         s["denc"] = denc

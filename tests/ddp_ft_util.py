@@ -6,8 +6,8 @@ mode "oracle" (CPU, gloo): the engines are CPU stand-ins whose forward / backwar
 oracle's (test infrastructure only): the Transformer decoder of oracle/decoders.py and a
 per-channel affine "encoder" (feats = x * w + b: trainable parameters with their own flat
 buffer, Adam at encoder_lr, gradient from the decoder's dL/d encoder_out) -- exercises the
-trainer's broadcasts, the whole-decoder bucket reduced before the encoder backward, the encoder
-all-reduce and grad_div.  ``expected`` is the oracle's single-process averaged step.
+trainer's broadcasts, the per-layer decoder buckets, the decoder's rest reduced before the encoder backward,
+the encoder's bucket reduced inside its backward, the unbucketed rest and grad_div.  ``expected`` is the oracle's single-process averaged step.
 mode "hip" (GPU box): ConvNeXt-Tiny with children[7:] trainable + the HIP Transformer engine,
 both ranks on the one GPU, gloo carrying the all-reduces.
 """
@@ -107,13 +107,26 @@ class _OracleTransformerEngine:
             lo += fp.shapes[n].numel()
         raise KeyError("embedding.weight")
 
+    def grad_buckets(self):  # one per layer, the last first (as the HIP engine's)
+        fp, out = self.fp, []
+        for i in reversed(range(CFG["layers"])):
+            pre, lo, span = f"transformer_decoder.layers.{i}.", 0, []
+            for n in fp.names:
+                k = fp.shapes[n].numel()
+                if n.startswith(pre):
+                    span.append((lo, lo + k))
+                lo += k
+            out.append((span[0][0], span[-1][1]))
+        return out
+
     def backward(self, s, want_denc=False, bucket_hook=None):
         s["loss"].backward()
         for n, v in self.fp.views(self.fp.grad).items():
             v.copy_(s["pr"][n].grad)
         s["denc"] = s["feats"].grad if want_denc else None
         if bucket_hook is not None:
-            bucket_hook()
+            for _ in range(CFG["layers"]):
+                bucket_hook()
 
 
 class _OracleDecoder(torch.nn.Module):
@@ -134,11 +147,17 @@ class _AffineEngine:
         v = self.fp.views(self.fp.flat)
         return x * v["w"] + v["b"], dict(x=x)
 
-    def backward(self, saved, dfeat):
+    def grad_buckets(self):  # "b" (final first); "w" is left to the trainer's update
+        E = self.fp.shapes["w"].numel()
+        return [(E, E + self.fp.shapes["b"].numel())]
+
+    def backward(self, saved, dfeat, bucket_hook=None):
         g = self.fp.views(self.fp.grad)
         x = saved["x"]
-        g["w"].copy_((dfeat * x).reshape(-1, x.shape[-1]).sum(0))
         g["b"].copy_(dfeat.reshape(-1, x.shape[-1]).sum(0))
+        if bucket_hook is not None:
+            bucket_hook()
+        g["w"].copy_((dfeat * x).reshape(-1, x.shape[-1]).sum(0))
 
 
 class _AffineEncoder(torch.nn.Module):
@@ -166,9 +185,10 @@ def worker(rank, world, initfile, outdir, bucketed):
     dp, ep = init_params(rank)
     tr = TeacherForcedTrainer(_AffineEncoder(ep), _OracleDecoder(dp), lstm=False, decoder_lr=LR_DEC,
                               encoder_lr=LR_ENC, grad_clip=CLIP)
-    assert tr._bucket == (0, tr.eng.fp.grad.numel())  # fine-tuning: the whole decoder, one bucket
+    # fine-tuning: one bucket per decoder layer, the decoder's rest, then the encoder's bucket
+    assert [f is tr.eng.fp for f, _ in tr._buckets] == [True] * (CFG["layers"] + 1) + [False]
     if not bucketed:
-        tr._bucket = None
+        tr._buckets = None
     tr.step(*shard(rank))
     (loss, tokens, top5), = tr.drain_metrics()
     out = {"dec." + n: v.clone() for n, v in tr.eng.fp.views(tr.eng.fp.flat).items()}
@@ -228,7 +248,7 @@ def check(results, rtol=1e-5, atol=1e-6):
 HIP_CFG = dict(d=128, ff=128, V=120, layers=2, H=2, L=16, B=2)
 
 
-def hip_models(dev, rank=0):
+def hip_models(dev, rank=0, frozen=False):
     from imagecaptioningconvnext_amd.models.encoder import Encoder
     from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
     c = HIP_CFG
@@ -241,7 +261,8 @@ def hip_models(dev, rank=0):
         for n, p in enc.named_parameters():
             if n.endswith("layer_scale"):
                 p.fill_(0.5)
-    enc.fine_tune(True, startingLayer=7)
+    if not frozen:
+        enc.fine_tune(True, startingLayer=7)
     dec = TransformerDecoder(embed_dim=c["d"], decoder_dim=c["ff"], vocab_size=c["V"], maxLen=c["L"], device=dev,
                              wordMap=None, pretrained_embeddings_path=None, fine_tune_embeddings=True, dropout=0.0,
                              encoder_dim=768, num_heads=c["H"], num_layers=c["layers"], compute_dtype=torch.float32)
@@ -260,7 +281,7 @@ def hip_shard(rank, dev):
     return img.to(dev), caps.to(dev), lens.to(dev)
 
 
-def worker_hip(rank, world, initfile, outdir, graph, bucketed, steps):
+def worker_hip(rank, world, initfile, outdir, graph, bucketed, steps, frozen=False):
     from imagecaptioningconvnext_amd import kernels as K
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
     import faulthandler
@@ -269,16 +290,18 @@ def worker_hip(rank, world, initfile, outdir, graph, bucketed, steps):
     torch.set_num_threads(2)
     dist.init_process_group("gloo", init_method="file://" + initfile, rank=rank, world_size=world)
     dev = torch.device("cuda:0")
-    enc, dec = hip_models(dev, rank)
+    enc, dec = hip_models(dev, rank, frozen)
+    # frozen: the pipelined schedule (the encoder forward of batch i beside the decoder of i - 1)
     tr = TeacherForcedTrainer(enc, dec, lstm=False, decoder_lr=LR_DEC, encoder_lr=LR_ENC, grad_clip=CLIP,
-                              graph=graph)
+                              graph=graph, pipeline=frozen)
     if not bucketed:
-        tr._bucket = None
+        tr._buckets = None
     for _ in range(steps):
         tr.step(*hip_shard(rank, dev))
+    tr.flush()
     torch.cuda.synchronize()
     K.set_seed_counter(None)
-    save_file({"dec": tr.eng.fp.flat.cpu(), "enc": tr.enc_eng.fp.flat.cpu(),
+    save_file({"dec": tr.eng.fp.flat.cpu(), "enc": (tr.enc_eng.fp.flat if tr.enc_eng else tr.eng.fp.m).cpu(),
                "metrics": torch.tensor([m for r in tr.drain_metrics() for m in r], dtype=torch.float64)},
               os.path.join(outdir, f"hip_rank{rank}.safetensors"))
     dist.barrier()
@@ -286,11 +309,12 @@ def worker_hip(rank, world, initfile, outdir, graph, bucketed, steps):
     faulthandler.cancel_dump_traceback_later()
 
 
-def run_hip(tmpdir, graph, bucketed, steps=2, world=2):
+def run_hip(tmpdir, graph, bucketed, steps=2, world=2, frozen=False):
     import torch.multiprocessing as mp
     os.makedirs(str(tmpdir), exist_ok=True)
     initfile = os.path.join(str(tmpdir), "init")
-    mp.spawn(worker_hip, args=(world, initfile, str(tmpdir), graph, bucketed, steps), nprocs=world, join=True)
+    mp.spawn(worker_hip, args=(world, initfile, str(tmpdir), graph, bucketed, steps, frozen), nprocs=world,
+             join=True)
     return [load_file(os.path.join(str(tmpdir), f"hip_rank{r}.safetensors")) for r in range(world)]
 
 

@@ -74,6 +74,9 @@ class _OracleEngine:
         n0 = sum(fp.shapes[n].numel() for n in fp.names[:-2])
         return n0, fp.flat.numel()
 
+    def grad_buckets(self):
+        return [self.early_bucket()]
+
     def backward(self, s, bucket_hook=None):
         s["loss"].backward()
         for n, v in self.fp.views(self.fp.grad).items():
@@ -119,9 +122,9 @@ def worker(rank, world, initfile, mode, outdir, graph=False, bucketed=True):
         dec.load_state_dict({n: v + 0.5 * rank for n, v in params.items()})
         dec = dec.to(dev)
     tr = TeacherForcedTrainer(PassThrough(), dec, lstm=True, decoder_lr=1e-4, grad_clip=5.0, graph=graph)
-    assert tr._bucket is not None  # early bucket (LSTM engine: embedding + fc) reduced in the hook
+    assert tr._buckets is not None and len(tr._buckets) == 1  # early bucket (LSTM engine: embedding + fc)
     if not bucketed:
-        tr._bucket = None
+        tr._buckets = None
     tr.step(t[f"rank{rank}.enc"].to(dev), t[f"rank{rank}.caps"].to(dev), t[f"rank{rank}.caplens"].to(dev))
     (loss, tokens, top5), = tr.drain_metrics()
     fp = tr.eng.fp
@@ -187,7 +190,7 @@ def worker_steps(rank, world, initfile, outdir, pipeline, graph, bucketed, steps
     tr = TeacherForcedTrainer(PassThrough(), dec, lstm=True, decoder_lr=1e-3, grad_clip=5.0, graph=graph,
                               pipeline=pipeline)
     if not bucketed:
-        tr._bucket = None
+        tr._buckets = None
     batch = (t[f"rank{rank}.enc"].to(dev), t[f"rank{rank}.caps"].to(dev), t[f"rank{rank}.caplens"].to(dev))
     for _ in range(steps):
         tr.step(*batch)

@@ -221,10 +221,11 @@ def test_persistent_lstm_handoff_timeout_raises(hip_device, monkeypatch, directi
 @pytest.mark.parametrize("graph", [False, True])
 def test_ddp2_transformer_finetuned_encoder_hip(hip_device, tmp_path, graph):
     """Transformer decoder + ConvNeXt-Tiny children[7:] trainable, 2 gloo ranks on the one GPU
-    (trainMultiGPU.py:233-235, 256, 384-394): the whole decoder reduced as one bucket beside the
-    encoder backward (eager: from the hook on the comm stream; graph: between the decoder-half
-    graph and the encoder-backward graph), the encoder gradients after it; bitwise equal to one
-    collective after the backward, and to a single process summing the two shards' gradients."""
+    (trainMultiGPU.py:233-235, 256, 384-394): one bucket per decoder layer as its backward ends,
+    the decoder's rest beside the encoder backward, the encoder's 25 MiB bucket when its blocks
+    are done, the remainder after (eager: from the hooks on the comm stream; graph: between the
+    graphs the hooks split the step into); bitwise equal to one collective after the backward,
+    and to a single process summing the two shards' gradients."""
     import ddp_ft_util
     a = ddp_ft_util.run_hip(tmp_path / "a", graph, True)
     b = ddp_ft_util.run_hip(tmp_path / "b", graph, False)
@@ -235,6 +236,21 @@ def test_ddp2_transformer_finetuned_encoder_hip(hip_device, tmp_path, graph):
         assert torch.equal(a[0][k], a[1][k]), k
     dec, enc = ddp_ft_util.expected_hip(hip_device)
     assert torch.equal(a[0]["dec"], dec) and torch.equal(a[0]["enc"], enc)
+
+
+def test_ddp2_transformer_pipelined_layer_buckets_hip(hip_device, tmp_path):
+    """Frozen encoder + Transformer decoder, pipelined captured schedule (C3 / C4 under DDP), 2
+    gloo ranks on the one GPU: the per-layer buckets split each step into layers + 1 graphs (the
+    encoder branch joined at the first split); bitwise the parameters, Adam moments and metrics
+    of one collective after the backward, and the ranks agree."""
+    import ddp_ft_util
+    a = ddp_ft_util.run_hip(tmp_path / "a", True, True, steps=3, frozen=True)
+    b = ddp_ft_util.run_hip(tmp_path / "b", True, False, steps=3, frozen=True)
+    for ra, rb in zip(a, b):
+        for k in ra:
+            assert torch.equal(ra[k], rb[k]), k
+    for k in a[0]:
+        assert torch.equal(a[0][k], a[1][k]), k
 
 
 @pytest.mark.parametrize("decoder,pipeline,split", [("lstm", False, False), ("lstm", True, True),
@@ -261,9 +277,9 @@ def test_captured_step_graphs_hold_only_kernel_nodes(hip_device, monkeypatch, de
     monkeypatch.setattr(torch.cuda, "CUDAGraph", Kept)
     enc, dec = _models(hip_device, decoder, 0.1, False)
     tr = TeacherForcedTrainer(enc, dec, lstm=decoder == "lstm", graph=True, pipeline=pipeline)
-    if split:  # the DDP split at the early bucket, reduced over no group (one rank)
-        tr._bucket = tr.eng.early_bucket()
-        tr._reduce_early = lambda: setattr(tr, "_early_issued", False)
+    if split:  # the DDP split at every bucket hook, reduced over no group (one rank)
+        tr._buckets = [(tr.eng.fp, [r]) for r in tr.eng.grad_buckets()]
+        tr._reduce_bucket = lambda k: None
     for i in range(3):
         tr.step(*_batch(hip_device, i))
     torch.cuda.synchronize()
