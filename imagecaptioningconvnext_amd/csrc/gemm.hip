@@ -1204,7 +1204,16 @@ extern "C" int imgcap_mx_quant_rows(int dtype, int R, int K, const void* x, int6
   if (R == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((R + 3) / 4);
-  if (dtype == IMGCAP_BF16)
+  if (dtype == IMGCAP_BF16 && K <= 2048) {  // the row in registers
+#define MXQ_(N)                                                                                                    \
+  hipLaunchKernelGGL((mx_quant_rows_reg_kernel<bf16, N>), grid, dim3(256), 0, st, R, K, (const bf16*)x, (long)ldx, \
+                     ln_w, ln_b, eps, q, s)
+    if (K <= 512) MXQ_(1);
+    else if (K <= 1024) MXQ_(2);
+    else if (K <= 1536) MXQ_(3);
+    else MXQ_(4);
+#undef MXQ_
+  } else if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL((mx_quant_rows_kernel<bf16>), grid, dim3(256), 0, st, R, K, (const bf16*)x, (long)ldx, ln_w,
                        ln_b, eps, q, s);
   else

@@ -172,3 +172,61 @@ __global__ __launch_bounds__(256) void mx_quant_rows_kernel(int R, int K, const 
     mx_store8(v, q + (long)row * K + c, s + (long)row * (K / 32) + c / 32, (lane & 3) == 0, on);
   }
 }
+
+// The same with the row held in registers (K <= 512 * NVL): one read of the row instead of three
+// (sum, squared deviations, quantise), same summation order -- bitwise the outputs of the loop
+// above.  C5's frozen stages quantise 12544 x 768 rows per block: 13.4 us per call before.
+template <typename T, int NVL>
+__global__ __launch_bounds__(256) void mx_quant_rows_reg_kernel(int R, int K, const T* __restrict__ x, long ldx,
+                                                                const float* __restrict__ lnw,
+                                                                const float* __restrict__ lnb, float eps,
+                                                                uint8_t* __restrict__ q, uint8_t* __restrict__ s) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const T* xr = x + (long)row * ldx;
+  float v[NVL][8];
+#pragma unroll
+  for (int i = 0; i < NVL; ++i) {
+    const int c = i * 512 + lane * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    if (c < K) ld_g<T, 8>(xr + c, v[i]);
+  }
+  if (lnw) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < NVL; ++i)
+      if (i * 512 + lane * 8 < K) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum += v[i][j];
+      }
+    const float mean = wave_sum(sum) / K;
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < NVL; ++i)
+      if (i * 512 + lane * 8 < K) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; sq += d * d; }
+      }
+    const float rstd = rsqrtf(wave_sum(sq) / K + eps);
+#pragma unroll
+    for (int i = 0; i < NVL; ++i) {
+      const int c = i * 512 + lane * 8;
+      if (c < K) {
+        float g[8], b[8];
+        ld_g<float, 8>(lnw + c, g);
+        ld_g<float, 8>(lnb + c, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = (v[i][j] - mean) * rstd * g[j] + b[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NVL; ++i) {
+    if (i * 512 >= K) break;  // wave-uniform: the 4-lane groups of mx_store8 stay together
+    const int c = i * 512 + lane * 8;
+    mx_store8(v[i], q + (long)row * K + c, s + (long)row * (K / 32) + c / 32, (lane & 3) == 0, c < K);
+  }
+}
+

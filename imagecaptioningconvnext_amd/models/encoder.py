@@ -15,11 +15,14 @@ suffix runs on encoder_engine.EncoderEngine (saved activations + HIP backward) a
 differentiable; the frozen prefix always takes the fused fast path.
 """
 import math
+import os
 
 import torch
 from torch import nn
 
 from .. import kernels as K
+
+_MX_DW = os.environ.get("IMGCAP_MX_DW", "0") == "1"
 
 VARIANTS = {
     "tiny": ((96, 192, 384, 768), (3, 3, 9, 3), 0.1),
@@ -273,8 +276,12 @@ class Encoder(nn.Module):
                 hid = torch.empty(M, 4 * C, device=dev, dtype=ct)
                 zn = torch.empty(M, C, device=dev, dtype=ct)
             x2 = x.view(M, C)
-            # MX stages at W = 7 / 14: depthwise + LayerNorm write the fp8 rows directly
-            mx_dw = mx and K.dw_ln_fused(w, C, ct)
+            # MX stages: the depthwise writes bf16 rows, the quantiser applies the LayerNorm and
+            # writes the fp8 rows + block scales.  IMGCAP_MX_DW=1: depthwise + LayerNorm + MX
+            # quantisation in one kernel (imgcap_dwconv7_ln_mx) instead -- measured slower at C5
+            # (ConvNeXt-Large, C = 768 / 1536): its LayerNorm epilogue costs the channel-pair
+            # kernel more than the separate quantiser pass (C5 5.21k -> 5.00k img/s)
+            mx_dw = mx and _MX_DW and K.dw_ln_fused(w, C, ct)
             for blk in blocks:
                 rs = sd[bid] if (sd is not None and blk["sd"] > 0) else None
                 if mx_dw:

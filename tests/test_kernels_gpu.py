@@ -593,3 +593,21 @@ def test_caller_workspace_grows_on_demand(hip_device):
     assert need.value >= 8 * 512 * 512 * 4
     ref = a.float() @ b.float()
     assert ((c - ref).norm() / ref.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("C", [96, 192, 768, 1024, 20])
+@pytest.mark.parametrize("cmajor", [False, True])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+def test_ln_patchify2_widths(hip_device, C, cmajor, dtype, tol):
+    """LayerNorm2d + 2x2 patch rows at the ConvNeXt widths (the vectorised patch kernel: thread
+    = 8 channels of a patch's four pixels) and at C % 8 != 0 (the wave-per-pixel kernel), both
+    patch-row layouts, against torch LN + the same permutation."""
+    B, H = 3, 10
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(B, H, H, C, generator=g) * 2 + 0.5
+    lw, lb = 1 + 0.2 * torch.randn(C, generator=g), 0.2 * torch.randn(C, generator=g)
+    y = F.layer_norm(x.to(dtype).float(), (C,), lw, lb, 1e-6).view(B, H // 2, 2, H // 2, 2, C)
+    ref = (y.permute(0, 1, 3, 5, 2, 4) if cmajor else y.permute(0, 1, 3, 2, 4, 5)).reshape(-1, 4 * C)
+    got = torch.empty(ref.shape, dtype=dtype, device=hip_device)
+    K.ln_patchify2(x.to(hip_device, dtype), lw.to(hip_device), lb.to(hip_device), got, cmajor=cmajor)
+    assert _rel(got.cpu(), ref) < tol

@@ -19,11 +19,13 @@ def _mx_ref(v):
     return mx.quant(v)
 
 
+@pytest.mark.parametrize("Kd", [384, 768, 1536, 2080])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_mx_quant_rows_exact(hip_device, dtype):
+def test_mx_quant_rows_exact(hip_device, dtype, Kd):
+    """bf16 rows of K <= 2048 take the register-resident kernel, the rest the row loop."""
     from imagecaptioningconvnext_amd import kernels as K
     g = torch.Generator().manual_seed(3)
-    x = (torch.randn(37, 384, generator=g) * torch.logspace(-3, 2, 384)).to(dtype)
+    x = (torch.randn(37, Kd, generator=g) * torch.logspace(-3, 2, Kd)).to(dtype)
     x[5, :32] = 0.0  # an all-zero block
     q, s = K.mx_quant_rows(x.to(hip_device))
     rq, rs = _mx_ref(x.float())
@@ -32,13 +34,14 @@ def test_mx_quant_rows_exact(hip_device, dtype):
     assert _rel(K.mx_dequant(q, s), x.float()) < 0.04
 
 
-def test_mx_quant_rows_layernorm(hip_device):
+@pytest.mark.parametrize("Kd", [768, 1536])
+def test_mx_quant_rows_layernorm(hip_device, Kd):
     from imagecaptioningconvnext_amd import kernels as K
     g = torch.Generator().manual_seed(4)
-    x = (torch.randn(50, 768, generator=g) * 3 + 1).bfloat16()
-    w, b = 1 + 0.1 * torch.randn(768, generator=g), 0.1 * torch.randn(768, generator=g)
+    x = (torch.randn(50, Kd, generator=g) * 3 + 1).bfloat16()
+    w, b = 1 + 0.1 * torch.randn(Kd, generator=g), 0.1 * torch.randn(Kd, generator=g)
     q, s = K.mx_quant_rows(x.to(hip_device), w.to(hip_device), b.to(hip_device), 1e-6)
-    ref = F.layer_norm(x.float(), (768,), w, b, 1e-6)
+    ref = F.layer_norm(x.float(), (Kd,), w, b, 1e-6)
     assert _rel(K.mx_dequant(q, s), ref) < 0.04
     rq, rs = _mx_ref(ref)
     assert (s.cpu().int() - rs.int()).abs().max().item() <= 1  # block exponents agree (LN round-off)
