@@ -108,6 +108,7 @@ _SIGS = {
     "imgcap_attn_reg": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     "imgcap_dropout": [c_int, c_int64, c_void_p, c_float, c_uint64, c_uint32, c_void_p, c_void_p],
     "imgcap_loss_finalize": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_tf_targets": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "imgcap_mean_mid": [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "imgcap_sort_gather_rows": [c_int] * 5 + [c_void_p] * 9,
     "imgcap_cast": [c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p],

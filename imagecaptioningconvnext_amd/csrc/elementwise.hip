@@ -578,3 +578,32 @@ extern "C" int imgcap_fill(int dtype, int64_t n, float value, void* x, void* str
   IMGCAP_CHECK_LAUNCH("imgcap_fill");
   return 0;
 }
+
+// ---- Transformer loss rows (transformerDecoder.py:88-108 + train.py:262-276) -------------------
+// One launch for what the decoder's loss needs from the captions: tmask[b, l] = l < len[b] - 1 (the
+// decode lengths), targets[b * L + l] = tmask ? caps[b, l + 1] : -1 (position l predicts the next
+// token; the last position's target is never valid), and the step's metric words zeroed.
+__global__ __launch_bounds__(256) void tf_targets_kernel(int B, int L, const int64_t* __restrict__ caps,
+                                                         const int64_t* __restrict__ lens,
+                                                         unsigned char* __restrict__ tmask,
+                                                         int64_t* __restrict__ targets, float* __restrict__ metrics,
+                                                         int n_metrics) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_metrics) metrics[i] = 0.f;
+  if (i >= (long)B * L) return;
+  const int b = (int)(i / L), l = (int)(i % L);
+  const bool ok = (int64_t)l < lens[b] - 1;
+  tmask[i] = ok ? 1 : 0;
+  targets[i] = ok ? caps[(long)b * L + (l + 1 < L ? l + 1 : 0)] : (int64_t)-1;
+}
+
+extern "C" int imgcap_tf_targets(int B, int L, const int64_t* caps, const int64_t* lens, uint8_t* tmask,
+                                 int64_t* targets, float* metrics, int n_metrics, void* stream) {
+  IMGCAP_REQUIRE(B >= 0 && L > 0 && n_metrics >= 0 && n_metrics <= 256, "imgcap_tf_targets: bad sizes");
+  const long n = std::max((long)B * L, (long)n_metrics);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(tf_targets_kernel, grid_for(n), dim3(256), 0, (hipStream_t)stream, B, L, caps, lens, tmask,
+                     targets, metrics, n_metrics);
+  IMGCAP_CHECK_LAUNCH("imgcap_tf_targets");
+  return 0;
+}

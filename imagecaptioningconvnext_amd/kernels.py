@@ -390,6 +390,25 @@ def embedding_fwd(ids, table, out, *, pe=None, L=1, drop_p=0.0, seed=0, drop_str
     return out
 
 
+def tf_targets(caps, lens, n_metrics=5):
+    """(tmask [B, L] bool, targets [B*L] int64, zeroed metrics [n_metrics] fp32) of a caption batch
+    in one launch (imgcap_tf_targets): position l's target is caps[:, l+1] where l < len - 1, else -1."""
+    _check_dev(caps, lens)
+    if caps.dtype != torch.int64 or lens.dtype != torch.int64:
+        raise TypeError("tf_targets: caps and lens must be int64")
+    B, L = caps.shape
+    caps = caps.contiguous()
+    lens = lens.reshape(-1).contiguous()
+    if lens.numel() != B:
+        raise ValueError("tf_targets: one length per caption")
+    tmask = torch.empty(B, L, device=caps.device, dtype=torch.bool)
+    targets = torch.empty(B * L, device=caps.device, dtype=torch.int64)
+    metrics = torch.empty(n_metrics, device=caps.device, dtype=torch.float32)
+    _abi.call("imgcap_tf_targets", B, L, caps.data_ptr(), lens.data_ptr(), tmask.data_ptr(), targets.data_ptr(),
+              metrics.data_ptr(), n_metrics, stream())
+    return tmask, targets, metrics
+
+
 def embedding_bwd(ids, dout, dtable, *, drop_p=0.0, seed=0, drop_stream=0):
     _abi.call("imgcap_embedding_bwd", dt(dout), ids.numel(), dtable.shape[1], ids.data_ptr(), dout.data_ptr(),
               drop_p, seed, drop_stream, dtable.data_ptr(), stream())

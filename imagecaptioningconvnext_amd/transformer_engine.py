@@ -158,18 +158,19 @@ class TransformerEngine:
             x = x3
         s["mem"] = mem
         s["xL"] = x
-        dl = (caption_lengths.reshape(-1) - 1).to(torch.int64)
-        tmask = torch.arange(L, device=dev).view(1, L) < dl.view(B, 1)
+        # the decode mask, position l's target caps[:, l+1] (-1 past the decode length) and the zeroed
+        # metrics (loss, tokens, top5 hits, 1/tokens, hand-off errors: none here) in one launch
+        lens = caption_lengths.reshape(-1)
+        if lens.dtype != torch.int64:
+            lens = lens.to(torch.int64)
+        tmask, targets, metrics = K.tf_targets(caps if caps.dtype == torch.int64 else caps.to(torch.int64), lens)
         s["tmask"] = tmask
         if loss:
             logits = torch.empty(BL, self.Vpad, **ctd)
             K.gemm(x, fp.w("fc_out.weight"), trans_b=True, bias=fp.f32("fc_out.bias"), out=logits, N=V)
-            nxt = torch.cat([caps[:, 1:], caps[:, :1]], dim=1)  # target of position l is caps[:, l+1]
-            targets = torch.where(tmask, nxt, torch.full_like(nxt, -1)).reshape(-1)
             lse = torch.empty(BL, **f32)
             lrow = torch.empty(BL, **f32)
             hit = torch.empty(BL, **f32)
-            metrics = torch.zeros(5, **f32)  # loss, tokens, top5 hits, 1/tokens, hand-off errors (none here)
             # loss, top-5 and the loss gradient in one pass over the logits (train.py:266-276)
             dlogits = torch.empty(BL, self.Vpad, **ctd)
             K.ce_train(logits, targets, V, metrics, lse, lrow, hit, dlogits,

@@ -462,6 +462,12 @@ int imgcap_dropout(int dtype, int64_t n, const void* x, float p, uint64_t seed, 
 int imgcap_loss_finalize(int n, const float* loss_rows, const float* hit5, const int64_t* targets,
                          const float* extra, float* out, void* stream);
 
+/* Transformer loss rows from the captions, one launch (transformerDecoder.py:88-108, train.py:262-276):
+ * tmask[b*L+l] = l < lens[b] - 1 (uint8), targets[b*L+l] = tmask ? caps[b, l+1] : -1, metrics[0..n) = 0
+ * (caps [B, L] int64, lens [B] int64 caption lengths incl. <start>/<end>) */
+int imgcap_tf_targets(int B, int L, const int64_t* caps, const int64_t* lens, uint8_t* tmask, int64_t* targets,
+                      float* metrics, int n_metrics, void* stream);
+
 /* out[b, e] = mean_p x[b, p, e] (decoder.py:64, input of init_h/init_c) */
 int imgcap_mean_mid(int dtype, int B, int P, int E, const void* x, void* out, void* stream);
 /* decoder.py:64,79-81 fused: rows sorted by caption length (descending, stable), enc_out[r] =

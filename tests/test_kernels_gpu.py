@@ -611,3 +611,28 @@ def test_ln_patchify2_widths(hip_device, C, cmajor, dtype, tol):
     got = torch.empty(ref.shape, dtype=dtype, device=hip_device)
     K.ln_patchify2(x.to(hip_device, dtype), lw.to(hip_device), lb.to(hip_device), got, cmajor=cmajor)
     assert _rel(got.cpu(), ref) < tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L", [(1, 1), (3, 7), (64, 52), (5, 300)])
+def test_tf_targets_match_reference_formulas(hip_device, B, L):
+    """imgcap_tf_targets vs the Transformer trainer's torch formulas (transformerDecoder.py:88-108,
+    train.py:262-276): decode mask l < len - 1, target caps[:, l+1] or -1, metrics zeroed.  Lengths
+    cover 1 (nothing decoded), 2, L and values in between; ids are arbitrary int64."""
+    g = torch.Generator().manual_seed(11 + B * L)
+    caps = torch.randint(0, 1 << 40, (B, L), generator=g, dtype=torch.int64)
+    lens = torch.randint(1, L + 1, (B, 1), generator=g, dtype=torch.int64)
+    lens[0, 0] = 1
+    if B > 1:
+        lens[1, 0] = L
+    if B > 2:
+        lens[2, 0] = min(2, L)
+    dl = lens.reshape(-1) - 1
+    tmask = torch.arange(L).view(1, L) < dl.view(B, 1)
+    nxt = torch.cat([caps[:, 1:], caps[:, :1]], dim=1)
+    targets = torch.where(tmask, nxt, torch.full_like(nxt, -1)).reshape(-1)
+    tm, tg, mt = K.tf_targets(caps.to(hip_device), lens.to(hip_device))
+    torch.cuda.synchronize()
+    assert torch.equal(tm.cpu(), tmask)
+    assert torch.equal(tg.cpu(), targets)
+    assert torch.equal(mt.cpu(), torch.zeros(5))

@@ -1,7 +1,7 @@
 """LDS-staged GEMM tile plans at the step's widest-gap shapes (GPU box):
     python tools/gemm_modes.py
-One row per shape: us per launch for the plan by shape (-1), the 256x256 tile (1), 128x128 (4),
-64x64 (6), 128x64 (7), and torch.matmul (hipBLASLt, no epilogue; calibration only)."""
+One row per shape: us per launch for the plan by shape (-1), the 256x256 tile (1: BK 64 x 2
+stages, 2: BK 32 x 4, 3: BK 32 x 3), 128x128 (4), 64x64 (6), 128x64 (7), and torch.matmul (hipBLASLt, no epilogue; calibration only)."""
 import os
 import sys
 
@@ -14,9 +14,10 @@ from tools.microbench import time_launch  # noqa: E402
 dev = torch.device("cuda:0")
 bf = torch.bfloat16
 SHAPES = [(12544, 384, 1536, "res"), (12544, 1536, 384, "gelu"), (3136, 3072, 768, "gelu"), (3136, 768, 3072, "res"),
+          (12544, 384, 768, "bias"), (3136, 768, 1536, "bias"),
           (6272, 2048, 512, "gelu"), (6272, 512, 2048, "res"), (25088, 1024, 256, "gelu"), (3328, 9490, 512, "bias"),
           (3328, 512, 512, "bias"), (3328, 1536, 512, "bias")]
-MODES = (-1, 1, 4, 6, 7)
+MODES = tuple(int(m) for m in os.environ.get("MODES", "-1,1,2,3,4,6,7").split(","))
 print(f"{'M':>6s} {'N':>5s} {'K':>5s} | " + " ".join(f"{m:>7d}" for m in MODES) + " | blaslt  (us)", flush=True)
 for M, N, Kd, form in SHAPES:
     a = torch.randn(M, Kd, device=dev).to(bf)
