@@ -84,7 +84,10 @@ class TeacherForcedTrainer:
         # max_caplen) runs T = the next multiple of 8 >= its longest decode length instead of
         # L - 1 -- the vocab projection, CE, dlogits, weight-gradient GEMMs and every per-step
         # buffer shrink with it.  One captured graph set per bucket; None = L - 1.
-        self.len_buckets = bool(len_buckets) and lstm
+        # Transformer: the same buckets over positions -- L' = the next multiple of 8 >= the longest
+        # caption (positions past every caption are key-padding-masked and carry no loss rows, so
+        # the first L' positions train exactly what L positions do; transformerDecoder.py:88-108)
+        self.len_buckets = bool(len_buckets)
         self._cur_T = None
         self._seq_T = None
         self._seq_store = {}
@@ -164,7 +167,8 @@ class TeacherForcedTrainer:
 
     def bucket_T(self, caps, caplens, max_caplen=None):
         """Steps the LSTM runs for this batch: the next multiple of 8 >= its longest decode length
-        (caplen - 1), or None (= L - 1) when that is not known on the host or length buckets are off."""
+        (caplen - 1); positions the Transformer runs: the next multiple of 8 >= its longest caption.
+        None (= all of L) when that is not known on the host or length buckets are off."""
         if not self.len_buckets:
             return None
         if max_caplen is None:
@@ -172,6 +176,9 @@ class TeacherForcedTrainer:
                 return None
             max_caplen = int(caplens.max())
         L = caps.size(1)
+        if not self.lstm:
+            T = max(8, (int(max_caplen) + 7) // 8 * 8)
+            return None if T >= L else T
         T = max(8, (int(max_caplen) - 1 + 7) // 8 * 8)
         return None if T >= L - 1 else T
 
@@ -209,6 +216,8 @@ class TeacherForcedTrainer:
         if self.lstm:
             s = self.eng.forward(feats, caps, caplens, fixed_T=self._cur_T if self._cur_T else True, alphaC=self.alphaC)
         else:
+            if self._cur_T:  # length bucket: the first _cur_T positions (bucket_T)
+                caps = caps[:, :self._cur_T]
             s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
         if mid is not None:
             mid()

@@ -329,6 +329,33 @@ def test_lstm_length_buckets_match_full_steps(hip_device, pipeline):
     assert ((p0 - p1).norm() / p0.norm()).item() < 2e-5  # Adam sign flips at round-off-level grads
 
 
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_transformer_length_buckets_match_full_steps(hip_device, pipeline):
+    """transformerDecoder.py:88-108: positions past every caption of the batch are key-padding
+    masked and carry no loss rows, so the trainer's Transformer buckets (the first L' = next
+    multiple of 8 >= the longest caption positions) train what all L positions train.  Buckets 8,
+    16, full, 8 (replaying the first's graphs), 16, with graphs (+ pipeline) vs no buckets."""
+    from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
+    seqs = [[7, 5, 3, 8], [12, 9, 16, 2], [20, 4, 11, 6], [6, 6, 6, 6], [10, 15, 3, 9]]
+    out = []
+    for buckets in (False, True):
+        enc, dec = _models(hip_device, "transformer", 0.0, True)
+        tr = TeacherForcedTrainer(enc, dec, lstm=False, graph=True, pipeline=pipeline, len_buckets=buckets)
+        for i, lens in enumerate(seqs):
+            img, caps, caplens, mx = _len_batch(hip_device, i, lens, L=20)
+            want = (mx + 7) // 8 * 8 if buckets else None
+            assert tr.bucket_T(caps, caplens, mx) == (want if want is not None and want < 20 else None)
+            tr.step(img, caps, caplens, max_caplen=mx)
+        tr.flush()
+        torch.cuda.synchronize()
+        out.append((tr.eng.fp.flat.detach().cpu().clone(), tr.drain_metrics()))
+    (p0, m0), (p1, m1) = out
+    assert len(m0) == len(m1) == len(seqs)
+    for a, b in zip(m0, m1):
+        assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]) and a[1] == b[1] and abs(a[2] - b[2]) < 1e-6
+    assert ((p0 - p1).norm() / p0.norm()).item() < 2e-5  # Adam sign flips at round-off-level grads
+
+
 def test_eval_after_finetune_step_sees_updated_encoder(hip_device):
     """After a fine-tuned step (EncoderEngine's Adam writes the trainable children through raw
     pointers), the no_grad encoder forward used by validation runs the UPDATED weights: it equals
