@@ -182,30 +182,48 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(int n, int dim, const i
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[c][k] = 0.f;
-  // the run is sorted indices [i, end): windows of 64; its members are a prefix of each window
+  // the run is sorted indices [i, end): windows of 64; its members are a prefix of each window.
+  // Rows are added in position order, RB at a time: the RB rows' loads are all issued before the
+  // first addition, so a long run (the padding id: thousands of rows) costs one memory round trip
+  // per RB rows instead of one per row; the additions themselves stay sequential (same sums).
+  constexpr int RB = 8;
   for (int base = i;; base += 64) {
     const int j = base + lane;
     const int jid = j < n ? sid[j] : -1;
     const int jpos = j < n ? spos[j] : 0;
     unsigned long long m = __ballot(jid == id);
     const bool more = (m >> 63) & 1ull;
-    while (m) {  // rows in position order
-      const int l = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      const long row = __shfl(jpos, l, 64);
+    while (m) {  // rows in position order, RB per round
+      long rows[RB];
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int l = m ? __ffsll((long long)m) - 1 : 0;
+        if (m) ++cnt;
+        m &= m - 1;
+        rows[u] = __shfl(jpos, l, 64);  // past the run's end: a valid row, loaded and not added
+      }
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int c0 = c * 512 + lane * 8;
         if (c0 >= dim) continue;
-        float x[8];
-        if (vec) {
-          ld_g<T, 8>(dout + row * dim + c0, x);
-        } else {
+        float x[RB][8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) x[k] = c0 + k < dim ? to_f(dout[row * dim + c0 + k]) : 0.f;
+        for (int u = 0; u < RB; ++u) {
+          if (vec) {
+            ld_g<T, 8>(dout + rows[u] * dim + c0, x[u]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[u][k] = c0 + k < dim ? to_f(dout[rows[u] * dim + c0 + k]) : 0.f;
+          }
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[c][k] += x[k] * dropout_scale(seed, stream_id, row * dim + c0 + k, p);
+        for (int u = 0; u < RB; ++u) {
+          if (u >= cnt) break;  // wave-uniform
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            acc[c][k] += x[u][k] * dropout_scale(seed, stream_id, rows[u] * dim + c0 + k, p);
+        }
       }
     }
     if (!more || base + 64 >= n) break;

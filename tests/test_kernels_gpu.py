@@ -636,3 +636,23 @@ def test_tf_targets_match_reference_formulas(hip_device, B, L):
     assert torch.equal(tm.cpu(), tmask)
     assert torch.equal(tg.cpu(), targets)
     assert torch.equal(mt.cpu(), torch.zeros(5))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,V,dim,run", [(3328, 120, 512, 2500), (700, 50, 40, 300), (129, 7, 1000, 100)])
+def test_embedding_bwd_long_runs_sequential_sum(hip_device, dtype, n, V, dim, run):
+    """A padding id occupying thousands of positions (captions padded to L): its rows are still
+    added one at a time in position order, so the table row is bitwise the sequential fp32 sum
+    (the kernel batches the loads of 8 rows, not the additions)."""
+    from imagecaptioningconvnext_amd import kernels as K
+    g = torch.Generator().manual_seed(n + run)
+    ids = torch.randint(0, V, (n,), generator=g)
+    ids[torch.randperm(n, generator=g)[:run]] = 0  # the padding id, spread over the positions
+    dout = torch.randn(n, dim, generator=g).to(dtype)
+    ref = torch.zeros(V, dim, dtype=torch.float32)
+    x = dout.float()
+    for i in range(n):  # position order, fp32
+        ref[ids[i]] += x[i]
+    got = torch.zeros(V, dim, device=hip_device)
+    K.embedding_bwd(ids.to(hip_device), dout.to(hip_device), got)
+    assert torch.equal(got.cpu(), ref)
