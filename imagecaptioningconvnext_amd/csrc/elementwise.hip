@@ -143,22 +143,32 @@ __global__ __launch_bounds__(256) void emb_scatter_kernel(int n, const int64_t* 
 }
 
 constexpr int EMB_MAXDIM = 2048;  // columns: 8 per lane, at most 4 passes of 512
+constexpr int EMB_CH = 64;        // sorted indices per chunk (one wave's share of a long run)
+// The rows of each id summed in position order, in chunks of the sorted index array aligned to
+// EMB_CH: a wave owns a chunk's piece of a run (the run's head, or the chunk's first index when
+// the run started in an earlier chunk).  A run inside one chunk is added to the table directly; a
+// run crossing chunk boundaries leaves its pieces in ws[chunk][0 = continuation, 1 = head] and
+// emb_combine_kernel adds them in chunk order -- a fixed summation order whatever the schedule,
+// and a long run (the padding id of captions padded to L: thousands of positions) is spread over
+// run / EMB_CH waves instead of one.
 template <typename T>
 __global__ __launch_bounds__(256) void emb_segsum_kernel(int n, int dim, const int* __restrict__ spos,
                                                          const int* __restrict__ sid, const T* __restrict__ dout,
                                                          float p, uint64_t seed0, const uint64_t* seed_ctr,
-                                                         uint32_t stream_id, float* __restrict__ dtable) {
+                                                         uint32_t stream_id, float* __restrict__ dtable,
+                                                         float* __restrict__ ws) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= n) return;
   // the neighbours' ids and this index's position in one round trip
   const int id = sid[i];
   const int prev = i > 0 ? sid[i - 1] : -1, next = i + 1 < n ? sid[i + 1] : -1;
   const int pos0 = spos[i];
-  if (prev == id) return;  // not the first index of its run
+  const bool head = prev != id;          // the run starts here
+  if (!head && i % EMB_CH) return;       // inside a chunk piece owned by another wave
   const uint64_t seed = p > 0.f ? eff_seed(seed0, seed_ctr) : seed0;
   const bool vec = (dim % 8) == 0;
   constexpr int NC = EMB_MAXDIM / 512;
-  if (next != id && vec) {
+  if (head && next != id && vec) {
     // a one-position run (most ids of a batch): its row and the table row requested together,
     // the same single addition as the general loop (0 + x * scale, then table += that)
 #pragma unroll
@@ -182,59 +192,93 @@ __global__ __launch_bounds__(256) void emb_segsum_kernel(int n, int dim, const i
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[c][k] = 0.f;
-  // the run is sorted indices [i, end): windows of 64; its members are a prefix of each window.
-  // Rows are added in position order, RB at a time: the RB rows' loads are all issued before the
-  // first addition, so a long run (the padding id: thousands of rows) costs one memory round trip
-  // per RB rows instead of one per row; the additions themselves stay sequential (same sums).
+  // this piece: indices [i, lim) of the run, lim = the chunk's end; its members are a prefix
+  const int chunk = i / EMB_CH;
+  const int lim = min(n, (chunk + 1) * EMB_CH);
+  const int j = i + lane;
+  const int jpos = j < lim ? spos[j] : 0;
+  unsigned long long m = __ballot(j < lim && sid[j] == id);
+  const int cnt_all = __popcll(m);
+  const bool continues = i + cnt_all == lim && lim < n && sid[lim] == id;
+  // rows in position order, RB loads in flight before their (sequential) additions
   constexpr int RB = 8;
-  for (int base = i;; base += 64) {
-    const int j = base + lane;
-    const int jid = j < n ? sid[j] : -1;
-    const int jpos = j < n ? spos[j] : 0;
-    unsigned long long m = __ballot(jid == id);
-    const bool more = (m >> 63) & 1ull;
-    while (m) {  // rows in position order, RB per round
-      long rows[RB];
-      int cnt = 0;
+  while (m) {
+    long rows[RB];
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int l = m ? __ffsll((long long)m) - 1 : 0;
+      if (m) ++cnt;
+      m &= m - 1;
+      rows[u] = __shfl(jpos, l, 64);  // past the piece's end: a valid row, loaded and not added
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int c0 = c * 512 + lane * 8;
+      if (c0 >= dim) continue;
+      float x[RB][8];
 #pragma unroll
       for (int u = 0; u < RB; ++u) {
-        const int l = m ? __ffsll((long long)m) - 1 : 0;
-        if (m) ++cnt;
-        m &= m - 1;
-        rows[u] = __shfl(jpos, l, 64);  // past the run's end: a valid row, loaded and not added
+        if (vec) {
+          ld_g<T, 8>(dout + rows[u] * dim + c0, x[u]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) x[u][k] = c0 + k < dim ? to_f(dout[rows[u] * dim + c0 + k]) : 0.f;
+        }
       }
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int c0 = c * 512 + lane * 8;
-        if (c0 >= dim) continue;
-        float x[RB][8];
+      for (int u = 0; u < RB; ++u) {
+        if (u >= cnt) break;  // wave-uniform
 #pragma unroll
-        for (int u = 0; u < RB; ++u) {
-          if (vec) {
-            ld_g<T, 8>(dout + rows[u] * dim + c0, x[u]);
-          } else {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) x[u][k] = c0 + k < dim ? to_f(dout[rows[u] * dim + c0 + k]) : 0.f;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-          if (u >= cnt) break;  // wave-uniform
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            acc[c][k] += x[u][k] * dropout_scale(seed, stream_id, rows[u] * dim + c0 + k, p);
-        }
+        for (int k = 0; k < 8; ++k)
+          acc[c][k] += x[u][k] * dropout_scale(seed, stream_id, rows[u] * dim + c0 + k, p);
       }
     }
-    if (!more || base + 64 >= n) break;
   }
+  // a whole run: into the table; a piece of a longer one: its chunk slot (0 continuation, 1 head)
+  float* dst = (head && !continues) ? dtable + (long)id * dim
+                                    : ws + ((long)chunk * 2 + (head ? 1 : 0)) * dim;
+  const bool add = head && !continues;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int col = c * 512 + lane * 8 + k;
-      if (col < dim) dtable[(long)id * dim + col] += acc[c][k];
+      if (col < dim) dst[col] = add ? dst[col] + acc[c][k] : acc[c][k];
     }
+}
+
+// The runs that cross chunk boundaries: the wave of chunk k takes the run that starts in chunk k
+// and continues past its end, and adds its head piece and the continuation pieces of the chunks
+// that follow, in chunk order, to the table.
+__global__ __launch_bounds__(256) void emb_combine_kernel(int n, int dim, const int* __restrict__ sid,
+                                                          const float* __restrict__ ws,
+                                                          float* __restrict__ dtable) {
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int last = (k + 1) * EMB_CH - 1;
+  if (last + 1 >= n) return;
+  const int id = sid[last];
+  if (sid[last + 1] != id) return;                     // no run crosses this chunk's end
+  if (k > 0 && sid[k * EMB_CH - 1] == id) return;      // it started in an earlier chunk
+  constexpr int NC = EMB_MAXDIM / 512;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int c0 = c * 512 + lane * 8;
+    if (c0 >= dim) continue;
+    float t[8];
+    const float* h = ws + ((long)k * 2 + 1) * dim + c0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = c0 + e < dim ? h[e] : 0.f;
+    for (int jc = k + 1; jc * EMB_CH < n && sid[jc * EMB_CH] == id; ++jc) {
+      const float* q = ws + (long)jc * 2 * dim + c0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] += c0 + e < dim ? q[e] : 0.f;
+    }
+    float* tp = dtable + (long)id * dim + c0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (c0 + e < dim) tp[e] += t[e];
+  }
 }
 
 template <typename TI, typename TO>
@@ -487,10 +531,13 @@ extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* id
   IMGCAP_REQUIRE(n <= EMB_MAXN && dim <= EMB_MAXDIM, "imgcap_embedding_bwd: n <= 2^20 positions, dim <= 2048");
   hipStream_t st = (hipStream_t)stream;
   const size_t rank_bytes = ((size_t)n * sizeof(int) + 15) / 16 * 16;
-  int* rank = (int*)workspace(rank_bytes + 2 * (size_t)n * sizeof(int), st);
+  const size_t idx_bytes = (2 * (size_t)n * sizeof(int) + 15) / 16 * 16;
+  const int nchunks = (n + EMB_CH - 1) / EMB_CH;
+  int* rank = (int*)workspace(rank_bytes + idx_bytes + (size_t)nchunks * 2 * dim * sizeof(float), st);
   if (!rank) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_embedding_bwd: ") + last_error());
   int* spos = rank + rank_bytes / sizeof(int);
   int* sid = spos + n;
+  float* ws = (float*)((char*)rank + rank_bytes + idx_bytes);  // chunk pieces of boundary-crossing runs
   if (zero_async(rank, rank_bytes, st) != hipSuccess) return fail(IMGCAP_EINVAL, "imgcap_embedding_bwd: zeroing failed");
   const int nb = (n + 255) / 256;
   hipLaunchKernelGGL(emb_rank_kernel, dim3(nb, (n + EMB_CHUNK - 1) / EMB_CHUNK), dim3(256), 0, st, n, ids, rank);
@@ -498,10 +545,12 @@ extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* id
   const dim3 g((n + 3) / 4);
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(emb_segsum_kernel<bf16>, g, dim3(256), 0, st, n, dim, spos, sid, (const bf16*)dout, drop_p,
-                       seed, g_seed_ctr, drop_stream, dtable);
+                       seed, g_seed_ctr, drop_stream, dtable, ws);
   else
     hipLaunchKernelGGL(emb_segsum_kernel<float>, g, dim3(256), 0, st, n, dim, spos, sid, (const float*)dout,
-                       drop_p, seed, g_seed_ctr, drop_stream, dtable);
+                       drop_p, seed, g_seed_ctr, drop_stream, dtable, ws);
+  if (n > EMB_CH)
+    hipLaunchKernelGGL(emb_combine_kernel, dim3((nchunks + 3) / 4), dim3(256), 0, st, n, dim, sid, ws, dtable);
   IMGCAP_CHECK_LAUNCH("imgcap_embedding_bwd");
   return 0;
 }

@@ -639,20 +639,44 @@ def test_tf_targets_match_reference_formulas(hip_device, B, L):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("n,V,dim,run", [(3328, 120, 512, 2500), (700, 50, 40, 300), (129, 7, 1000, 100)])
-def test_embedding_bwd_long_runs_sequential_sum(hip_device, dtype, n, V, dim, run):
-    """A padding id occupying thousands of positions (captions padded to L): its rows are still
-    added one at a time in position order, so the table row is bitwise the sequential fp32 sum
-    (the kernel batches the loads of 8 rows, not the additions)."""
+@pytest.mark.parametrize("n,V,dim,run", [(3328, 120, 512, 2500), (700, 50, 40, 300), (129, 7, 1000, 100),
+                                         (256, 3, 64, 0)])
+def test_embedding_bwd_long_runs_chunked_order(hip_device, dtype, n, V, dim, run):
+    """A padding id occupying thousands of positions (captions padded to L) is summed by many
+    waves: the sorted index array is cut at multiples of 64, each piece of a run is added in
+    position order and the pieces of a run in chunk order.  The table must be bitwise that fp32
+    order (restated here), and within fp32 rounding of the fp64 sum."""
     from imagecaptioningconvnext_amd import kernels as K
     g = torch.Generator().manual_seed(n + run)
     ids = torch.randint(0, V, (n,), generator=g)
-    ids[torch.randperm(n, generator=g)[:run]] = 0  # the padding id, spread over the positions
+    if run:
+        ids[torch.randperm(n, generator=g)[:run]] = 0  # the padding id, spread over the positions
     dout = torch.randn(n, dim, generator=g).to(dtype)
-    ref = torch.zeros(V, dim, dtype=torch.float32)
     x = dout.float()
-    for i in range(n):  # position order, fp32
-        ref[ids[i]] += x[i]
+    order = sorted(range(n), key=lambda i: (int(ids[i]), i))
+    sid = [int(ids[o]) for o in order]
+    ref = torch.zeros(V, dim, dtype=torch.float32)
+    i = 0
+    while i < n:
+        e = i
+        while e < n and sid[e] == sid[i]:
+            e += 1
+        pieces, a = [], i
+        while a < e:
+            b = min(e, (a // 64 + 1) * 64)
+            acc = torch.zeros(dim)
+            for t in range(a, b):
+                acc = acc + x[order[t]]
+            pieces.append(acc)
+            a = b
+        tot = pieces[0]
+        for pc in pieces[1:]:
+            tot = tot + pc
+        ref[sid[i]] = ref[sid[i]] + tot
+        i = e
     got = torch.zeros(V, dim, device=hip_device)
     K.embedding_bwd(ids.to(hip_device), dout.to(hip_device), got)
-    assert torch.equal(got.cpu(), ref)
+    got = got.cpu()
+    assert torch.equal(got, ref)
+    r64 = torch.zeros(V, dim, dtype=torch.float64).index_add_(0, ids, x.double())
+    assert ((got.double() - r64).norm() / r64.norm()).item() < 1e-6
