@@ -32,6 +32,12 @@ template <> struct StemIn<uint8_t> {
   }
 };
 
+// Block = npx output pixels (patches) x C0 channels; a thread computes 8 channels of TWO pixels
+// (q and q + npx/2), so each weight vector it reads from LDS serves two patches (the kernel is
+// LDS-issue bound: per k one patch value per pixel + two 16-byte weight reads).  Patch rows are
+// padded to STEM_PS floats (16-byte rows; the pixels of a wave read distinct banks).  Per pixel
+// the arithmetic is unchanged: bias, then k = 0..47 in order, LayerNorm sums over j then cv.
+constexpr int STEM_PS = 52;
 template <typename T, typename TI = float>
 __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0, const TI* __restrict__ img,
                                                     const float* __restrict__ w, const float* __restrict__ bias,
@@ -40,10 +46,10 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
                                                     const float* __restrict__ nstd) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int CV = C0 / 8;
-  float* ws = sm;                     // [48][C0]
-  float* patch = ws + 48 * C0;        // [npx][48]
-  float* red = patch + npx * 48;      // [npx][CV]
-  float* stat = red + npx * CV;       // [npx][2]
+  float* ws = sm;                       // [48][C0]
+  float* patch = ws + 48 * C0;          // [npx][STEM_PS]
+  float* red = patch + npx * STEM_PS;   // [npx][CV]
+  float* stat = red + npx * CV;         // [npx][2]
   const int HO = H / 4, WO = W / 4;
   const long total = (long)B * HO * WO;
   const long px0 = (long)blockIdx.x * npx;
@@ -59,74 +65,114 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
       const int b = (int)(px / (HO * WO)), rem = (int)(px % (HO * WO)), oh = rem / WO, ow = rem % WO;
       v = StemIn<TI>::load(img + (((long)b * 3 + ci) * H + oh * 4 + kh) * W + ow * 4, ci, nmean, nstd);
     }
-    *(f32x4*)(patch + q * 48 + ci * 16 + kh * 4) = v;
+    *(f32x4*)(patch + q * STEM_PS + ci * 16 + kh * 4) = v;
   }
   __syncthreads();
+  const int half = npx / 2;
   const int q = threadIdx.x / CV, cv = threadIdx.x % CV, c0 = cv * 8;
-  const bool active = q < npx && px0 + q < total;
-  float acc[8];
+  const int qp[2] = {q, q + half};
+  bool active[2];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  if (active) {
+  for (int u = 0; u < 2; ++u) active[u] = q < half && px0 + qp[u] < total;
+  float acc[2][8];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[u][j] = 0.f;
+  if (q < half) {
     const f32x4 b0 = *(const f32x4*)(bias + c0), b1 = *(const f32x4*)(bias + c0 + 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { acc[j] = b0[j]; acc[j + 4] = b1[j]; }
-    const float* pp = patch + q * 48;
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { acc[u][j] = b0[j]; acc[u][j + 4] = b1[j]; }
+    const float* pa = patch + qp[0] * STEM_PS;
+    const float* pb = patch + qp[1] * STEM_PS;
 #pragma unroll 8
     for (int k = 0; k < 48; ++k) {
-      const float x = pp[k];
+      const float xa = pa[k], xb = pb[k];
       const f32x4 w0 = *(const f32x4*)(ws + k * C0 + c0), w1 = *(const f32x4*)(ws + k * C0 + c0 + 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { acc[j] += x * w0[j]; acc[j + 4] += x * w1[j]; }
+      for (int j = 0; j < 4; ++j) {
+        acc[0][j] += xa * w0[j]; acc[0][j + 4] += xa * w1[j];
+        acc[1][j] += xb * w0[j]; acc[1][j + 4] += xb * w1[j];
+      }
     }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!active[u]) continue;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += acc[u][j];
+      red[qp[u] * CV + cv] = s;
+    }
+  }
+  __syncthreads();
+  if (cv == 0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!active[u]) continue;
+      float s = 0.f;
+      for (int i = 0; i < CV; ++i) s += red[qp[u] * CV + i];
+      stat[qp[u] * 2] = s / C0;
+    }
+  }
+  __syncthreads();
+  float mean[2] = {0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!active[u]) continue;
+    mean[u] = stat[qp[u] * 2];
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += acc[j];
-    red[q * CV + cv] = s;
+    for (int j = 0; j < 8; ++j) { const float d = acc[u][j] - mean[u]; s += d * d; }
+    red[qp[u] * CV + cv] = s;
   }
   __syncthreads();
-  if (active && cv == 0) {
-    float s = 0.f;
-    for (int i = 0; i < CV; ++i) s += red[q * CV + i];
-    stat[q * 2] = s / C0;
-  }
-  __syncthreads();
-  float mean = 0.f;
-  if (active) {
-    mean = stat[q * 2];
-    float s = 0.f;
+  if (cv == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { const float d = acc[j] - mean; s += d * d; }
-    red[q * CV + cv] = s;
+    for (int u = 0; u < 2; ++u) {
+      if (!active[u]) continue;
+      float s = 0.f;
+      for (int i = 0; i < CV; ++i) s += red[qp[u] * CV + i];
+      stat[qp[u] * 2 + 1] = rsqrtf(s / C0 + 1e-6f);
+    }
   }
   __syncthreads();
-  if (active && cv == 0) {
-    float s = 0.f;
-    for (int i = 0; i < CV; ++i) s += red[q * CV + i];
-    stat[q * 2 + 1] = rsqrtf(s / C0 + 1e-6f);
-  }
-  __syncthreads();
-  if (active) {
-    const float rstd = stat[q * 2 + 1];
+  if (q < half) {
     const f32x4 g0 = *(const f32x4*)(lw + c0), g1 = *(const f32x4*)(lw + c0 + 4);
     const f32x4 h0 = *(const f32x4*)(lb + c0), h1 = *(const f32x4*)(lb + c0 + 4);
-    float o[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[j] = (acc[j] - mean) * rstd * g0[j] + h0[j];
-      o[j + 4] = (acc[j + 4] - mean) * rstd * g1[j] + h1[j];
-    }
-    T* op = out + (px0 + q) * C0 + c0;
-    if (sizeof(T) == 2) {
-      bf16x8 v;
+    for (int u = 0; u < 2; ++u) {
+      if (!active[u]) continue;
+      const float rstd = stat[qp[u] * 2 + 1];
+      float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (bf16)o[j];
-      *(bf16x8*)op = v;
-    } else {
-      *(f32x4*)op = f32x4{o[0], o[1], o[2], o[3]};
-      *(f32x4*)(op + 4) = f32x4{o[4], o[5], o[6], o[7]};
+      for (int j = 0; j < 4; ++j) {
+        o[j] = (acc[u][j] - mean[u]) * rstd * g0[j] + h0[j];
+        o[j + 4] = (acc[u][j + 4] - mean[u]) * rstd * g1[j] + h1[j];
+      }
+      T* op = out + (px0 + qp[u]) * C0 + c0;
+      if (sizeof(T) == 2) {
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (bf16)o[j];
+        *(bf16x8*)op = v;
+      } else {
+        *(f32x4*)op = f32x4{o[0], o[1], o[2], o[3]};
+        *(f32x4*)(op + 4) = f32x4{o[4], o[5], o[6], o[7]};
+      }
     }
   }
+}
+
+// pixels per stem block (even: two per thread) and its LDS bytes
+static int stem_npx(int C0) {
+  int npx = 2 * (1024 / (C0 / 8));
+  if (npx > 128) npx = 128;
+  return npx & ~1;
+}
+static size_t stem_lds(int C0, int npx) {
+  return (48 * (size_t)C0 + (size_t)npx * STEM_PS + (size_t)npx * (C0 / 8) + (size_t)npx * 2) * sizeof(float);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1172,11 +1218,10 @@ extern "C" int imgcap_convnext_stem(int dtype, int B, int H, int W, int C0, cons
   const long total = (long)B * (H / 4) * (W / 4);
   if (total == 0) return 0;
   const int CV = C0 / 8;
-  int npx = 1024 / CV;
-  if (npx > 64) npx = 64;
-  const int threads = ((npx * CV + 63) / 64) * 64;
+  const int npx = stem_npx(C0);
+  const int threads = ((npx / 2 * CV + 63) / 64) * 64;
   dim3 grid((unsigned)((total + npx - 1) / npx));
-  const size_t shm = (48 * C0 + npx * 48 + npx * CV + npx * 2) * sizeof(float);
+  const size_t shm = stem_lds(C0, npx);
   IMGCAP_REQUIRE(shm <= 160 * 1024, "imgcap_convnext_stem: LDS");
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL((stem_kernel<bf16, float>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, images,
@@ -1198,11 +1243,10 @@ extern "C" int imgcap_convnext_stem_u8(int dtype, int B, int H, int W, int C0, c
   const long total = (long)B * (H / 4) * (W / 4);
   if (total == 0) return 0;
   const int CV = C0 / 8;
-  int npx = 1024 / CV;
-  if (npx > 64) npx = 64;
-  const int threads = ((npx * CV + 63) / 64) * 64;
+  const int npx = stem_npx(C0);
+  const int threads = ((npx / 2 * CV + 63) / 64) * 64;
   dim3 grid((unsigned)((total + npx - 1) / npx));
-  const size_t shm = (48 * C0 + npx * 48 + npx * CV + npx * 2) * sizeof(float);
+  const size_t shm = stem_lds(C0, npx);
   IMGCAP_REQUIRE(shm <= 160 * 1024, "imgcap_convnext_stem_u8: LDS");
   if (dtype == IMGCAP_BF16)
     hipLaunchKernelGGL((stem_kernel<bf16, uint8_t>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0,
