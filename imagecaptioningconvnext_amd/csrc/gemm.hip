@@ -533,10 +533,9 @@ static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, lon
   return {tiles128 < 512 ? IMGCAP_GEMM_TILED64 : IMGCAP_GEMM_TILED128, 1};
 }
 
-// ---- persistent-tile kernel (gemm_pt.h): selection and launch ------------------------------
-// IMGCAP_GEMM_PT / imgcap_gemm_set_pt: -1 by shape, 0 never (default until it wins: the first
-// measurements, tools/gpu/r4_pt.sh, had it slower than the LDS-staged plan on the step's shapes),
-// 1 wherever eligible (tile by the cost model), 2..4 wherever eligible with tile config 2..4 forced
+// ---- stream-tile kernel (gemm_pt.h): selection and launch ---------------------------------
+// IMGCAP_GEMM_PT / imgcap_gemm_set_pt: -1 by shape, 0 never (default), 1 wherever eligible (tile by
+// the cost model), 2..5 wherever eligible with tile config 1..4 forced
 static int g_gemm_pt_mode = [] {
   const char* e = getenv("IMGCAP_GEMM_PT");
   return e ? atoi(e) : 0;
@@ -554,53 +553,128 @@ static int device_cus() {
   return cus[dev];
 }
 
-// tile configs: 1 = 128x256 (8 waves 2x4, 3 stages), 2 = 256x128 (8 waves 4x2, 3 stages),
-// 3 = 128x128 (8 waves 2x4, 4 stages)
+// tile configs (8 waves each): 1 = 256x128 (waves 4x2, 3 stages), 2 = 128x256 (2x4, 3 stages),
+// 3 = 128x128 (2x4, 4 stages), 4 = 128x192 (2x4, 3 stages)
+constexpr int PT_NCFG = 4;
 struct PtCfg { int bm, bn; };
-static PtCfg pt_cfg(int c) { return c == 1 ? PtCfg{128, 256} : c == 2 ? PtCfg{256, 128} : PtCfg{128, 128}; }
+static PtCfg pt_cfg(int c) {
+  return c == 1 ? PtCfg{256, 128} : c == 2 ? PtCfg{128, 256} : c == 3 ? PtCfg{128, 128} : PtCfg{128, 192};
+}
 
-// cycles of one tile on a CU: per 64-deep k-step max(MFMA, operand delivery at ~48 B/cycle),
-// plus a fixed per-tile cost (epilogue, pipeline turn-around); rounds = tiles over the CUs
+// cycles of the busiest block: its tiles (persistent rounds over the CUs) x (k-steps x max(MFMA,
+// operand delivery ~30 B/cycle/CU) + the epilogue's stores at ~8 B/cycle/CU)
 static double pt_estimate(int c, int M, int N, int K, int cus) {
   const PtCfg t = pt_cfg(c);
   const long tiles = (long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
   const long rounds = (tiles + cus - 1) / cus;
   const double nk = (K + 63) / 64;
-  const double step = std::max((double)t.bm * t.bn / 32.0, (t.bm + t.bn) * 128.0 / 48.0);
-  const double epi = t.bm * t.bn / 64.0;  // ~ stores + epilogue math
+  const double step = std::max((double)t.bm * t.bn / 32.0, (t.bm + t.bn) * 128.0 / 30.0);
+  const double epi = t.bm * t.bn * 2.0 / 8.0;
   return rounds * (nk * step + epi);
 }
 
-static int pt_choose(int M, int N, int K) {
+// configs instantiated per (epilogue kind, layout): the 64x64-per-wave tiles hold the general
+// epilogue's operands (and the residual of a transposed layout) only by spilling, so those forms
+// take the 64x32 / 64x48 wave tiles
+static bool pt_allowed(int c, int ek, bool ak, bool bk) {
+  if (ek == 2) return c == 3;
+  if (ek == 1 && !(ak && bk)) return c == 3 || c == 4;
+  return true;
+}
+static int pt_ek(const imgcap_epilogue* ep) {
+  if (!ep) return 0;
+  return ((ep->aux && ep->act != IMGCAP_ACT_GELU) || ep->beta != 0.f) ? 2 : ep->res ? 1 : 0;
+}
+
+static int pt_choose(int M, int N, int K, int ek, bool ak, bool bk) {
   const int cus = device_cus();
   int best = 0;
   double bt = 0;
-  for (int c = 1; c <= 3; ++c) {
+  for (int c = 1; c <= PT_NCFG; ++c) {
+    if (!pt_allowed(c, ek, ak, bk)) continue;
     const double t = pt_estimate(c, M, N, K, cus);
     if (!best || t < bt) { best = c; bt = t; }
   }
   return best;
 }
 
-// which PT config serves this call (0: none) -- the epilogue forms the kernel implements
+static int64_t pt_extent(bool kmaj, int rows, int K, long ld) {  // bytes from the base to the last element + 1
+  return kmaj ? ((int64_t)(rows - 1) * ld + K) * 2 : ((int64_t)(K - 1) * ld + rows) * 2;
+}
+
+// which stream-tile config serves this call (0: none) -- the epilogue forms the kernel implements
 static int pt_plan(int ak, int bk, int M, int N, int K, long lda, long ldb, int batch, int split,
                    const imgcap_epilogue* ep, bool vec_ok) {
   const int mode = g_gemm_pt_mode;
-  if (mode == 0 || batch != 1 || split != 1 || lda % 8 || ldb % 8 || N % 4) return 0;
+  if (mode == 0 || batch != 1 || split != 1 || lda % 8 || ldb % 8 || N % 4 || K < 64) return 0;
+  if (pt_extent(ak, M, K, lda) > 0x7fffffffLL || pt_extent(bk, N, K, ldb) > 0x7fffffffLL) return 0;
   if (ep) {
     if (!vec_ok || ep->c_dtype != IMGCAP_BF16) return 0;
-    if (ep->aux && ep->act != IMGCAP_ACT_GELU && ep->act != IMGCAP_ACT_DGELU) return 0;  // relu-mask aux
     if (ep->rowscale && ep->rows_per_scale <= 0) return 0;
   }
-  // the general epilogue (dGELU's saved pre-activation, beta) only on the 128x128 tile (registers)
-  const bool general = ep && ((ep->aux && ep->act == IMGCAP_ACT_DGELU) || ep->beta != 0.f);
-  if (general) return mode < 0 && ((long)M * N < 1000000L || K < 256) ? 0 : 3;
-  if (mode >= 2 && mode <= 4) return mode - 1;
+  const int ek = pt_ek(ep);
+  if (mode >= 2 && mode <= PT_NCFG + 1) return pt_allowed(mode - 1, ek, ak, bk) ? mode - 1 : pt_choose(M, N, K, ek, ak, bk);
   if (mode < 0) {
-    // by shape: big enough grids only (measured crossover: tools/gpu/r4_pt.sh)
-    if ((long)M * N < 1000000L || K < 256) return 0;
+    // by shape: grids of at least ~a round of the 128x128 tile (the small decoder products stay
+    // on the 64x64 LDS-DMA tile's four blocks per CU)
+    if ((long)M * N < 2000000L || K < 256) return 0;
   }
-  return pt_choose(M, N, K);
+  return pt_choose(M, N, K, ek, ak, bk);
+}
+
+// explicit instantiations of the stream-tile kernels pt_allowed admits (the host stubs of kernel
+// templates first named inside the launcher template were otherwise left undefined)
+template __global__ void gemm_pt_kernel<256, 128, 4, 2, 3, true, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<256, 128, 4, 2, 3, true, true, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<256, 128, 4, 2, 3, true, false, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<256, 128, 4, 2, 3, false, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<256, 128, 4, 2, 3, false, false, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, true, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, true, true, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, true, false, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, false, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, false, false, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, true, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, true, 2>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, false, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, false, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, false, 2>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, false, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, false, true, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, false, true, 2>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, false, false, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, false, false, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, false, false, 2>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, true, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, true, true, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, true, false, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, true, false, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, true, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, false, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, false, 1>(PtArgs);
+
+// only the (config, epilogue kind, layout) combinations pt_allowed admits are instantiated
+template <bool AKV, bool BKV>
+void pt_launch_t(int cfg, int ek, int G, const PtArgs& a, hipStream_t st) {
+#define PT_L(BM_, BN_, WM_, WN_, S_, EK_) \
+  hipLaunchKernelGGL((gemm_pt_kernel<BM_, BN_, WM_, WN_, S_, AKV, BKV, EK_>), dim3(G), dim3(WM_ * WN_ * 64), 0, st, a)
+  if (cfg == 3) {
+    if (ek == 0) PT_L(128, 128, 2, 4, 4, 0);
+    else if (ek == 1) PT_L(128, 128, 2, 4, 4, 1);
+    else PT_L(128, 128, 2, 4, 4, 2);
+  } else if (cfg == 4) {
+    if (ek == 0) PT_L(128, 192, 2, 4, 3, 0);
+    else PT_L(128, 192, 2, 4, 3, 1);
+  } else if (cfg == 1) {
+    if (ek == 0) PT_L(256, 128, 4, 2, 3, 0);
+    else if constexpr (AKV && BKV) PT_L(256, 128, 4, 2, 3, 1);
+  } else {
+    if (ek == 0) PT_L(128, 256, 2, 4, 3, 0);
+    else if constexpr (AKV && BKV) PT_L(128, 256, 2, 4, 3, 1);
+  }
+#undef PT_L
 }
 
 static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb,
@@ -628,44 +702,20 @@ static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A
   a.grp = std::max(1, std::min(tm, (int)(std::sqrt(run * t.bn / t.bm) + 0.5)));
   a.ep = ep;
   a.seed_ctr = g_seed_ctr;
-  static const int dbg = [] {
-    const char* e = getenv("IMGCAP_PT_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  static const int grid_all = [] {  // IMGCAP_PT_GRID=1: one block per tile (not persistent)
-    const char* e = getenv("IMGCAP_PT_GRID");
-    return e ? atoi(e) : 0;
-  }();
-  a.dbg = dbg;
-  if (grid_all) G = a.ntiles;
+  a.a_bytes = pt_extent(ak, M, K, lda);
+  a.b_bytes = pt_extent(bk, N, K, ldb);
   a.c_bytes = ((uint64_t)(M - 1) * ldc + N) * 2;
   a.res_bytes = ep.res ? ((uint64_t)(M - 1) * ep.ldr + N) * 2 : 0;
   a.aux_bytes = ep.aux ? ((uint64_t)(M - 1) * ep.ldaux + N) * 2 : 0;
   if (a.c_bytes > 0x7fffffffull || a.res_bytes > 0x7fffffffull || a.aux_bytes > 0x7fffffffull)
-    return fail(IMGCAP_EUNSUPPORTED, "imgcap_gemm(pt): operand over 2 GiB");
-  const bool general = (ep.aux && ep.act == IMGCAP_ACT_DGELU) || ep.beta != 0.f;
-  if (general && cfg != 3) return fail(IMGCAP_EINVAL, "imgcap_gemm(pt): general epilogue needs the 128x128 tile");
-  const int ek = general ? 2 : ep.res ? 1 : 0;
-#define PT_L(BM_, BN_, WM_, WN_, S_, AKV, BKV, EK_)                                                               \
-  hipLaunchKernelGGL((gemm_pt_kernel<BM_, BN_, WM_, WN_, S_, AKV, BKV, EK_>), dim3(G), dim3(WM_ * WN_ * 64), 0, st, \
-                     a)
-#define PT_C(AKV, BKV)                                              \
-  do {                                                              \
-    if (ek == 2) PT_L(128, 128, 2, 4, 4, AKV, BKV, 2);              \
-    else if (cfg == 1 && ek == 0) PT_L(128, 256, 2, 4, 3, AKV, BKV, 0); \
-    else if (cfg == 1) PT_L(128, 256, 2, 4, 3, AKV, BKV, 1);        \
-    else if (cfg == 2 && ek == 0) PT_L(256, 128, 4, 2, 3, AKV, BKV, 0); \
-    else if (cfg == 2) PT_L(256, 128, 4, 2, 3, AKV, BKV, 1);        \
-    else if (ek == 0) PT_L(128, 128, 2, 4, 4, AKV, BKV, 0);         \
-    else PT_L(128, 128, 2, 4, 4, AKV, BKV, 1);                      \
-  } while (0)
-  if (ak && bk) PT_C(true, true);
-  else if (ak) PT_C(true, false);
-  else if (bk) PT_C(false, true);
-  else PT_C(false, false);
-#undef PT_C
-#undef PT_L
-  IMGCAP_CHECK_LAUNCH("imgcap_gemm(pt)");
+    return fail(IMGCAP_EUNSUPPORTED, "imgcap_gemm(stream tile): operand over 2 GiB");
+  const int ek = pt_ek(&ep);
+  if (!pt_allowed(cfg, ek, ak, bk)) return fail(IMGCAP_EINVAL, "imgcap_gemm(stream tile): config not built for this epilogue");
+  if (ak && bk) pt_launch_t<true, true>(cfg, ek, G, a, st);
+  else if (ak) pt_launch_t<true, false>(cfg, ek, G, a, st);
+  else if (bk) pt_launch_t<false, true>(cfg, ek, G, a, st);
+  else pt_launch_t<false, false>(cfg, ek, G, a, st);
+  IMGCAP_CHECK_LAUNCH("imgcap_gemm(stream tile)");
   return 0;
 }
 
@@ -1077,7 +1127,7 @@ extern "C" int imgcap_transpose(int dtype, int rows, int cols, const void* in, i
 }
 
 extern "C" int imgcap_gemm_set_pt(int mode) {
-  IMGCAP_REQUIRE(mode >= -1 && mode <= 4, "imgcap_gemm_set_pt: -1..4");
+  IMGCAP_REQUIRE(mode >= -1 && mode <= PT_NCFG + 1, "imgcap_gemm_set_pt: -1..5");
   g_gemm_pt_mode = mode;
   return 0;
 }

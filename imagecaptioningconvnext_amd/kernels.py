@@ -72,8 +72,9 @@ def gemm_set_policy(glds256):
 
 
 def gemm_set_pt(mode):
-    """Persistent-tile GEMM (imgcap_gemm_set_pt): -1 by shape (default), 0 never, 1 wherever
-    eligible, 2..4 wherever eligible with tile 128x256 / 256x128 / 128x128."""
+    """Stream-tile GEMM (imgcap_gemm_set_pt): -1 by shape (the library default), 0 never, 1
+    wherever eligible (cost-model tile), 2..5 wherever eligible with tile 256x128 / 128x256 /
+    128x128 / 128x192."""
     _abi.call("imgcap_gemm_set_pt", int(mode))
 
 

@@ -4,7 +4,7 @@ Per step, exactly the reference's work:
   encoder(imgs) in train mode (frozen weights, stochastic depth active)      train.py:242,261
   decoder teacher-forced forward + packed CE (+ alpha reg for LSTM)          :262-276
   zero_grad + backward (into the fine-tuned encoder children too, if any)     :278-281
-  DDP gradient averaging (one RCCL all-reduce over the flat grad buffer)      trainMultiGPU.py:233,384
+  DDP gradient averaging (bucketed RCCL all-reduces of the flat grad buffer)  trainMultiGPU.py:233,384
   clip_gradient (clamp +-5) + Adam step (one fused kernel per optimizer)      :284-291 / :387-394
   loss/token/top-5 metrics (reduceLossAndTokens + accuracy all-reduces,
   fused into one 3-float all-reduce; read back lazily, no per-step host sync) :396-403
@@ -13,13 +13,14 @@ With ``graph=True`` the encoder + decoder forward/backward (several hundred kern
 most of them small on the LSTM recurrence) is captured once into a HIP graph and replayed
 per step; the batch is copied into the graph's static input buffers first.
 
-Data parallel (world > 1): the gradient all-reduce is bucketed like DDP's.  The decoder engine
-names an early bucket (LSTM: embedding + fc, 64 % of its parameters; Transformer: the
-embedding) whose gradients are final before the weight-gradient GEMMs of the rest; its RCCL
-all-reduce runs on a communication stream while those GEMMs run (eager: issued from the
-backward's hook; graph mode: the step is captured as two graphs split at that point and the
-bucket is reduced between the two replays).  The rest is reduced after the backward, then
-clip + Adam (trainMultiGPU.py:384-394).  Dropout and
+Data parallel (world > 1): the gradient all-reduce is bucketed like DDP's.  The engines name
+their buckets in backward order (LSTM: embedding + fc, 64 % of its parameters, final before the
+weight-gradient GEMMs of the rest; Transformer: one per decoder layer, last layer first, or one
+for all layers in the pipelined schedule; fine-tuned encoder: the decoder rest, then ~25 MiB
+encoder buckets).  Each bucket's RCCL all-reduce runs on a communication stream while the rest of
+the backward runs (eager: issued from the backward's hook; graph mode: the step is captured as
+one graph per hook + 1 and each bucket is reduced between two replays).  What no bucket covers
+is reduced after the backward, then clip + Adam (trainMultiGPU.py:384-394).  Dropout and
 stochastic-depth masks stay fresh per replay through the device step counter
 (imgcap_set_seed_counter) bumped inside the graph.  The all-reduce and the Adam step (whose
 bias correction depends on the host step count) run eagerly after the replay.
@@ -140,6 +141,12 @@ class TeacherForcedTrainer:
         self._buckets = None
         if self.world == 1 or not hasattr(self.eng, "grad_buckets"):
             return
+        if hasattr(self.eng, "merged_layer_bucket"):
+            # pipelined frozen-encoder schedule: the next batch's encoder branch joins the captured
+            # step at its first split, so per-layer buckets (the first right after the last layer's
+            # backward) would put the encoder in series with most of the decoder backward; one
+            # bucket for all layers keeps the first split at the end of the layer loop
+            self.eng.merged_layer_bucket = bool(self.pipeline and self.enc_eng is None)
         fp = self.eng.fp
         dec = list(self.eng.grad_buckets())
         bl = [(fp, [r]) for r in dec]

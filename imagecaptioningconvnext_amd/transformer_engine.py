@@ -60,6 +60,10 @@ class TransformerEngine:
             raise NotImplementedError("the HIP attention kernel needs head dim 64 (embed_dim = 64 * num_heads)")
         self.seed = 4321
         self.step_id = 0
+        # one gradient bucket for all layers instead of one per layer (set by the trainer for the
+        # pipelined DDP schedule: the captured step is split at each bucket hook and the encoder
+        # branch of the next batch joins at the first split, so the hook must come late)
+        self.merged_layer_bucket = False
 
     def _lw(self, i, name):
         # nn.TransformerDecoder layers (transformerDecoder.py) or the attention-visualisation
@@ -298,8 +302,11 @@ class TransformerEngine:
     def grad_buckets(self):
         """Flat ranges in the order backward() calls ``bucket_hook``: one per decoder layer, the
         last layer first (trainMultiGPU.py:233-235: DDP all-reduces gradient buckets as the
-        backward produces them).  The rest (fc_out, embedding, encoder_proj) is final when
-        backward() returns."""
+        backward produces them), or one for all layers with ``merged_layer_bucket``.  The rest
+        (fc_out, embedding, encoder_proj) is final when backward() returns."""
+        if self.merged_layer_bucket:
+            pre = f"{self.layer_prefix}."
+            return [self.fp.span([n for n in self.fp.params if n.startswith(pre)])]
         out = []
         for i in reversed(range(self.layers)):
             pre = f"{self.layer_prefix}.{i}."
@@ -385,7 +392,8 @@ class TransformerEngine:
             cb.add(dqkv, G(lw("self_attn.in_proj_bias")))
             K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
             dx = ds1
-            if bucket_hook is not None:  # layer i's gradients final: its bucket's all-reduce
+            if bucket_hook is not None and (i == 0 or not self.merged_layer_bucket):
+                # layer i's gradients final (merged: every layer's): that bucket's all-reduce
                 wgb.run()
                 cb.run()
                 bucket_hook()

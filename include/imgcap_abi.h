@@ -136,15 +136,17 @@ int imgcap_mx_quant_rows(int dtype, int R, int K, const void* x, int64_t ldx, co
  * returns one of IMGCAP_GEMM_*; *splits (if not NULL) = K slices (1 = none). */
 enum { IMGCAP_GEMM_SKINNY = 1, IMGCAP_GEMM_TILED64 = 2, IMGCAP_GEMM_TILED128 = 3, IMGCAP_GEMM_GLDS = 4,
        IMGCAP_GEMM_GLDS256 = 5, IMGCAP_GEMM_GLDS64 = 6, IMGCAP_GEMM_GLDS128X64 = 7,
-       /* persistent-tile kernel with the epilogue from registers (bf16 C): 128x256, 256x128, 128x128 */
-       IMGCAP_GEMM_PT = 8, IMGCAP_GEMM_PT256X128 = 9, IMGCAP_GEMM_PT128 = 10 };
+       /* stream-tile kernel (persistent, epilogue from registers, bf16 C): 256x128, 128x256, 128x128,
+        * 128x192 tiles of 8 waves */
+       IMGCAP_GEMM_PT = 8, IMGCAP_GEMM_PT128X256 = 9, IMGCAP_GEMM_PT128 = 10, IMGCAP_GEMM_PT128X192 = 11 };
 int imgcap_gemm_plan(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda, int64_t ldb,
                      int batch, int split_k, int* splits);
 /* The same, knowing the call's epilogue (the persistent-tile kernel serves bf16 outputs only). */
 int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda, int64_t ldb,
                         int batch, const imgcap_epilogue* epi, int* splits);
-/* Persistent-tile GEMM policy: -1 by shape (default), 0 never, 1 wherever eligible (tile by the
- * cost model), 2..4 wherever eligible with tile 128x256 / 256x128 / 128x128 (A/B measurements). */
+/* Stream-tile GEMM policy: -1 by shape (the library default), 0 never, 1 wherever eligible (tile by
+ * the cost model), 2..5 wherever eligible with tile 256x128 / 128x256 / 128x128 / 128x192 (A/B
+ * measurements; a tile not built for the call's epilogue form falls back to the cost model). */
 int imgcap_gemm_set_pt(int mode);
 /* Kernel-selection policy for A/B tests and benchmarks: glds256 >= 1 serves every eligible
  * GEMM (bf16, unsplit, 16-byte operand pitches) with the 256x256 tile (1: 64-deep k-steps x 2

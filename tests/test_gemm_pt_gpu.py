@@ -1,4 +1,4 @@
-"""Persistent-tile GEMM (csrc/gemm_pt.h): every operand layout, tile config and epilogue form
+"""Stream-tile GEMM (csrc/gemm_pt.h): every operand layout, tile config and epilogue form
 against a PyTorch fp32 reference on the bf16-rounded operands, and against the LDS-staged kernels
 (imgcap_gemm_set_pt(0)) on the same call.  Ragged M / N (rows and columns past the last tile), K
 tails (K % 64 != 0), grids with more tiles than CUs (persistent rounds, the cross-tile prefetch)
@@ -41,7 +41,7 @@ LAYOUTS = [(False, True), (False, False), (True, True), (True, False)]
 
 @pytest.mark.parametrize("M,N,Kd", SHAPES)
 @pytest.mark.parametrize("ta,tb", LAYOUTS)
-@pytest.mark.parametrize("cfg", [2, 3, 4])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_pt_plain_matches_fp32(hip_device, M, N, Kd, ta, tb, cfg):
     from imagecaptioningconvnext_amd import kernels as K
     a, b, ref = _operands(hip_device, M, N, Kd, ta, tb, 1)
@@ -55,7 +55,7 @@ def test_pt_plain_matches_fp32(hip_device, M, N, Kd, ta, tb, cfg):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("form", ["gelu_aux", "res_scales", "dgelu_beta", "relu_alpha", "dropout"])
 def test_pt_epilogues_match_fp32_and_lds_kernels(hip_device, cfg, form):
     from imagecaptioningconvnext_amd import kernels as K
@@ -128,7 +128,7 @@ def test_pt_persistent_rounds_and_xcd_slots(hip_device):
     from imagecaptioningconvnext_amd import kernels as K
     for (M, N, Kd) in [(12544, 384, 1536), (6272, 1536, 64), (3328, 2048, 72), (7000, 600, 136)]:
         a, b, ref = _operands(hip_device, M, N, Kd, False, True, 11)
-        for cfg in (2, 3, 4):
+        for cfg in (2, 3, 4, 5):
             K.gemm_set_pt(cfg)
             try:
                 out = K.gemm(a, b, trans_b=True)

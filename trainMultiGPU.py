@@ -1,7 +1,8 @@
 """Multi-GPU (one process per GPU) teacher-forced training entry point, trainMultiGPU.py's
 counterpart: SLURM variables (trainMultiGPU.py:144-146) or torchrun's RANK / WORLD_SIZE /
 LOCAL_RANK, backend "nccl" (= RCCL over xGMI), DDP-equivalent gradient averaging inside
-``TeacherForcedTrainer`` (one all-reduce of the flat gradient buffer per step) and the
+``TeacherForcedTrainer`` (bucketed all-reduces of the flat gradient buffer as the backward produces
+the buckets, like DDP's reducer) and the
 ``reduceLossAndTokens`` metric reduction (:96-108).
 
     srun python3 trainMultiGPU.py --port 29500 --teacherForcing        (the reference's launch line)
