@@ -553,12 +553,14 @@ static int device_cus() {
   return cus[dev];
 }
 
-// tile configs (8 waves each): 1 = 256x128 (waves 4x2, 3 stages), 2 = 128x256 (2x4, 3 stages),
-// 3 = 128x128 (2x4, 4 stages), 4 = 128x192 (2x4, 3 stages)
-constexpr int PT_NCFG = 4;
-struct PtCfg { int bm, bn; };
+// tile configs: 1 = 256x128 (8 waves 4x2, 3 stages), 2 = 128x256 (2x4, 3 stages), 3 = 128x128 (2x4, 4
+// stages), 4 = 128x192 (2x4, 3 stages) -- one block per CU; 5 = 128x128 (4 waves 2x2, 2 stages), two
+// blocks per CU
+constexpr int PT_NCFG = 5;
+struct PtCfg { int bm, bn, bpc; };
 static PtCfg pt_cfg(int c) {
-  return c == 1 ? PtCfg{256, 128} : c == 2 ? PtCfg{128, 256} : c == 3 ? PtCfg{128, 128} : PtCfg{128, 192};
+  return c == 1 ? PtCfg{256, 128, 1} : c == 2 ? PtCfg{128, 256, 1} : c == 3 ? PtCfg{128, 128, 1}
+       : c == 4 ? PtCfg{128, 192, 1} : PtCfg{128, 128, 2};
 }
 
 // cycles of the busiest block: its tiles (persistent rounds over the CUs) x (k-steps x max(MFMA,
@@ -566,7 +568,7 @@ static PtCfg pt_cfg(int c) {
 static double pt_estimate(int c, int M, int N, int K, int cus) {
   const PtCfg t = pt_cfg(c);
   const long tiles = (long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
-  const long rounds = (tiles + cus - 1) / cus;
+  const long rounds = (tiles + cus * t.bpc - 1) / (cus * t.bpc);
   const double nk = (K + 63) / 64;
   const double step = std::max((double)t.bm * t.bn / 32.0, (t.bm + t.bn) * 128.0 / 30.0);
   const double epi = t.bm * t.bn * 2.0 / 8.0;
@@ -579,6 +581,7 @@ static double pt_estimate(int c, int M, int N, int K, int cus) {
 static bool pt_allowed(int c, int ek, bool ak, bool bk) {
   if (ek == 2) return c == 3;
   if (ek == 1 && !(ak && bk)) return c == 3 || c == 4;
+  if (c == 5) return ek <= 1 && ak && bk;
   return true;
 }
 static int pt_ek(const imgcap_epilogue* ep) {
@@ -598,8 +601,12 @@ static int pt_choose(int M, int N, int K, int ek, bool ak, bool bk) {
   return best;
 }
 
-static int64_t pt_extent(bool kmaj, int rows, int K, long ld) {  // bytes from the base to the last element + 1
-  return kmaj ? ((int64_t)(rows - 1) * ld + K) * 2 : ((int64_t)(K - 1) * ld + rows) * 2;
+// bytes from an operand's base to the end of its last 16-byte slot: the descriptor's range check is
+// per dword, so an extent ending inside a slot would zero the valid elements of a partial dword
+// (the pitch is a multiple of 8 elements >= the row, so the rounded extent stays inside the rows)
+static int64_t pt_extent(bool kmaj, int rows, int K, long ld) {
+  const auto r8 = [](int64_t x) { return (x + 7) / 8 * 8; };
+  return kmaj ? ((int64_t)(rows - 1) * ld + r8(K)) * 2 : ((int64_t)(K - 1) * ld + r8(rows)) * 2;
 }
 
 // which stream-tile config serves this call (0: none) -- the epilogue forms the kernel implements
@@ -654,6 +661,8 @@ template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, true, 0>(PtArg
 template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, true, 1>(PtArgs);
 template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, false, 0>(PtArgs);
 template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, false, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 2, 2, true, true, 0>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 2, 2, true, true, 1>(PtArgs);
 
 // only the (config, epilogue kind, layout) combinations pt_allowed admits are instantiated
 template <bool AKV, bool BKV>
@@ -667,6 +676,11 @@ void pt_launch_t(int cfg, int ek, int G, const PtArgs& a, hipStream_t st) {
   } else if (cfg == 4) {
     if (ek == 0) PT_L(128, 192, 2, 4, 3, 0);
     else PT_L(128, 192, 2, 4, 3, 1);
+  } else if (cfg == 5) {
+    if constexpr (AKV && BKV) {
+      if (ek == 0) PT_L(128, 128, 2, 2, 2, 0);
+      else PT_L(128, 128, 2, 2, 2, 1);
+    }
   } else if (cfg == 1) {
     if (ek == 0) PT_L(256, 128, 4, 2, 3, 0);
     else if constexpr (AKV && BKV) PT_L(256, 128, 4, 2, 3, 1);
@@ -694,7 +708,7 @@ static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A
   a.tiles_n = (N + t.bn - 1) / t.bn;
   a.ntiles = tm * a.tiles_n;
   const int cus = device_cus();
-  int G = a.ntiles < cus ? a.ntiles : cus;
+  int G = a.ntiles < cus * t.bpc ? a.ntiles : cus * t.bpc;
   if (G >= 64) G -= G % 8;
   // each XCD's concurrent tiles (G / 8 of them) as a rectangle of grp tile rows balancing its
   // A and B bytes: rows ~ sqrt(run * BN / BM)
@@ -707,6 +721,11 @@ static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A
   a.c_bytes = ((uint64_t)(M - 1) * ldc + N) * 2;
   a.res_bytes = ep.res ? ((uint64_t)(M - 1) * ep.ldr + N) * 2 : 0;
   a.aux_bytes = ep.aux ? ((uint64_t)(M - 1) * ep.ldaux + N) * 2 : 0;
+  static const int dbg = [] {  // diagnostic build switches (gemm_pt.h PT_DBG)
+    const char* e = getenv("IMGCAP_PT_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
   if (a.c_bytes > 0x7fffffffull || a.res_bytes > 0x7fffffffull || a.aux_bytes > 0x7fffffffull)
     return fail(IMGCAP_EUNSUPPORTED, "imgcap_gemm(stream tile): operand over 2 GiB");
   const int ek = pt_ek(&ep);
@@ -1127,7 +1146,7 @@ extern "C" int imgcap_transpose(int dtype, int rows, int cols, const void* in, i
 }
 
 extern "C" int imgcap_gemm_set_pt(int mode) {
-  IMGCAP_REQUIRE(mode >= -1 && mode <= PT_NCFG + 1, "imgcap_gemm_set_pt: -1..5");
+  IMGCAP_REQUIRE(mode >= -1 && mode <= PT_NCFG + 1, "imgcap_gemm_set_pt: -1..6");
   g_gemm_pt_mode = mode;
   return 0;
 }

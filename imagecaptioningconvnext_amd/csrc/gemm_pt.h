@@ -31,6 +31,12 @@ typedef unsigned pt_u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t PT_OOB = 0x80000000u;  // buffer offset past every buffer this kernel addresses
 
 typedef __amdgpu_buffer_rsrc_t pt_rsrc_t;
+
+// s_waitcnt lgkmcnt(0) as the builtin (vmcnt / expcnt fields at their maxima), so that the
+// compiler's own wait bookkeeping sees the fragment reads complete: after an inline-asm wait it
+// still counted them pending and, once the next half-step's reads were issued, made the MFMAs
+// wait for those as well (s_waitcnt lgkmcnt(3..0) ahead of every second MFMA group)
+DEV void pt_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 // raw buffer descriptor (stride 0, num_records = bytes: offsets at or past it read 0 / drop)
 DEV pt_rsrc_t pt_rsrc(const void* base, int64_t bytes) {
   const int n = bytes <= 0 ? 0 : bytes > 0x7fffffffLL ? 0x7fffffff : (int)bytes;
@@ -97,13 +103,6 @@ struct PtSrc {
   }
 };
 
-// k-step kt's descriptor of an operand P (pitch ld, `bytes` from P to its last element + 1)
-template <bool KMAJ>
-DEV pt_rsrc_t pt_step_rsrc(const bf16* P, long ld, int64_t bytes, int kt) {
-  const int64_t d = KMAJ ? (int64_t)kt * 128 : (int64_t)kt * 128 * ld;
-  return pt_rsrc((const char*)P + d, bytes - d);
-}
-
 // zero what this thread's DMA put at k >= K into a k-step's image (the K tail: slots past K of a
 // k-major row hold the next row's elements; k-rows past K of m/n-major images read as zeros
 // through the range check and are cleared here as well)
@@ -136,7 +135,14 @@ struct PtArgs {
   const uint64_t* seed_ctr;
   int64_t a_bytes, b_bytes;                // operand extents (descriptor range checks)
   uint64_t c_bytes, res_bytes, aux_bytes;  // extents of C, res, aux
+  int dbg;  // diagnostic build only (IMGCAP_PT_DBG): bit 1 no MFMAs, bit 2 no DMA after the prologue,
+            // bit 3 phase stamps
 };
+#ifdef IMGCAP_STAMPS
+#define PT_DBG(bit) ((a.dbg & (bit)) != 0)
+#else
+#define PT_DBG(bit) false
+#endif
 
 DEV float pt_bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 DEV float pt_bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -191,8 +197,9 @@ DEV imgcap_epilogue pt_load_ep(pt_kptr ka) {
 // EK: which row x column operands the epilogue may read -- 0 none (bias / scales / GELU with the
 // pre-activation written are all allowed), 1 the residual, 2 any (residual, saved operand for
 // dGELU / the ReLU mask, old C for beta); fewer live registers for the common forms
+// 8-wave blocks run one per CU; 4-wave blocks two per CU (both: two waves per SIMD)
 template <int BM, int BN, int WM, int WN, int S, bool AK, bool BKM, int EK>
-__global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
+__global__ __launch_bounds__(WM* WN * 64, 2) void gemm_pt_kernel(PtArgs a) {
   constexpr int NW = WM * WN;
   constexpr int TA = BM * 64 * 2, TB = BN * 64 * 2, STAGE = TA + TB;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -201,8 +208,26 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
   constexpr int PA = SrcA::PER, PB = SrcB::PER, LPT = PA + PB;  // DMA pieces per thread per k-step
   constexpr int NST = FM * FN;                                   // 8-byte stores per thread per epilogue
   static_assert(FM >= 1 && FN >= 1 && FM * 16 * WM == BM && FN * 16 * WN == BN, "wave tiles");
-  static_assert(S >= 3 && S * STAGE <= 160 * 1024, "stages");
-  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
+  static_assert(S >= 2 && S * STAGE * (NW == 4 ? 2 : 1) <= 160 * 1024, "stages");
+#ifdef IMGCAP_STAMPS
+  // diagnostic build: wave 0's s_memtime per iteration phase (first 64 iterations) kept in LDS
+  // behind the stages and copied out at the end (a global store would enter the counted waits)
+  constexpr int STAMP_BYTES = 64 * 8 * 8;
+#else
+  constexpr int STAMP_BYTES = 0;
+#endif
+  __shared__ __attribute__((aligned(16))) char smem[S * STAGE + STAMP_BYTES];
+#ifdef IMGCAP_STAMPS
+#define PT_STAMP(k)                                                                                     \
+  do {                                                                                                  \
+    if ((a.dbg & 8) && threadIdx.x == 0 && g < 64)                                                  \
+      ((uint64_t*)(smem + S * STAGE))[g * 8 + (k)] = __builtin_amdgcn_s_memtime();                     \
+  } while (0)
+#else
+#define PT_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
   const int K = a.K;
   const int lane = threadIdx.x & 63;
@@ -227,8 +252,10 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
     m0 = tm * BM;
     n0 = tn * BN;
   };
-  // the DMA stream's position (tile, k-step, stage), advanced incrementally
-  int is_kt = 0, is_it = 0, is_st = 0;
+  // the DMA stream: the next k-step to issue (tile is_it, k-step is_kt) as its descriptor words --
+  // base address and range in bytes, advanced by one k-step's stride with scalar adds (a step
+  // past the block's last tile gets range 0: its pieces read zeros into a stage no step reads)
+  int is_kt = 0, is_it = 0;
   SrcA srcA;
   SrcB srcB;
   auto set_src = [&](int itile) {
@@ -239,23 +266,42 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
     srcB.set(ka->ldb, n0, ka->N, w, lane);
   };
   set_src(0);
-  const bf16* const Ap = a.A;
-  const bf16* const Bp = a.B;
-  const long lda = a.lda, ldb = a.ldb;
-  const int64_t a_bytes = a.a_bytes, b_bytes = a.b_bytes;
-  auto issue_next = [&]() {  // every piece of the pending k-step, then advance the stream
-    char* st = smem + is_st * STAGE;
-    const pt_rsrc_t ra = pt_step_rsrc<AK>(Ap, lda, a_bytes, is_kt);
-    const pt_rsrc_t rb_ = pt_step_rsrc<BKM>(Bp, ldb, b_bytes, is_kt);
-#pragma unroll
-    for (int j = 0; j < PA; ++j) srcA.issue(j, ra, st, w);
-#pragma unroll
-    for (int j = 0; j < PB; ++j) srcB.issue(j, rb_, st + TA, w);
-    is_st = is_st == S - 1 ? 0 : is_st + 1;
+  const uint64_t a_base = (uint64_t)a.A, b_base = (uint64_t)a.B;
+  const int a_ext = (int)a.a_bytes, b_ext = (int)a.b_bytes;  // host-checked < 2^31
+  const int sa = AK ? 128 : 128 * (int)a.lda, sb = BKM ? 128 : 128 * (int)a.ldb;
+  uint64_t da = a_base, db = b_base;
+  int na = a_ext, nb = b_ext;
+  // piece q (A pieces first) of the pending k-step into the stage image st
+  auto issue_piece = [&](int q, pt_rsrc_t ra, pt_rsrc_t rb_, char* st) {
+    if (q < PA) srcA.issue(q, ra, st, w);
+    else srcB.issue(q - PA, rb_, st + TA, w);
+  };
+  auto advance = [&]() {  // the pending k-step has been issued
     if (++is_kt == nk) {
       is_kt = 0;
-      if (++is_it < my_tiles) set_src(is_it);
+      da = a_base;
+      db = b_base;
+      const bool live = ++is_it < my_tiles;
+      na = live ? a_ext : 0;
+      nb = live ? b_ext : 0;
+      if (live) set_src(is_it);
+    } else {
+      da += (uint32_t)sa;
+      db += (uint32_t)sb;
+      na = max(na - sa, 0);
+      nb = max(nb - sb, 0);
     }
+  };
+  auto step_rsrcs = [&](pt_rsrc_t& ra, pt_rsrc_t& rb_) {
+    ra = __builtin_amdgcn_make_buffer_rsrc((void*)da, 0, na, 0x00020000);
+    rb_ = __builtin_amdgcn_make_buffer_rsrc((void*)db, 0, nb, 0x00020000);
+  };
+  auto issue_next = [&](char* st) {  // every piece of the pending k-step at once (the prologue)
+    pt_rsrc_t ra, rb_;
+    step_rsrcs(ra, rb_);
+#pragma unroll
+    for (int q = 0; q < LPT; ++q) issue_piece(q, ra, rb_, st);
+    advance();
   };
   // the dropout seed mixed with the device step counter once, before any DMA is in flight (its
   // load would otherwise be waited for with everything else at the first epilogue)
@@ -286,58 +332,84 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
     for (int i = 0; i < FM; ++i) fa[i] = glds_frag_op<BM, AK>(img, rb + i * 16, kk, lane);
   };
   auto mfmas = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN]) {
+    if (PT_DBG(2)) return;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)  // D^T: rows = output columns (B), columns = output rows (A)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
   };
+  // the same MFMAs with the LPT DMA pieces of the pending k-step spread evenly between them (one
+  // piece after every FM*FN/LPT MFMAs, order pinned): the texture unit works through the pieces
+  // while the matrix pipe runs, instead of every wave stalling on its pieces at once after the
+  // barrier (in-kernel stamps: 620 of a 2,640-cycle 256x128 k-step)
+  auto mfmas_dma = [&](const bf16x8 (&fa)[FM], const bf16x8 (&fb)[FN], char* st) {
+    pt_rsrc_t ra, rb_;
+    step_rsrcs(ra, rb_);
+    constexpr int NM = FM * FN;
+    if (!PT_DBG(4)) {
+#pragma unroll
+      for (int q = 0; q < LPT; ++q) issue_piece(q, ra, rb_, st);
+    }
+    mfmas(fa, fb);
+    // scheduling groups: (NM / LPT MFMAs, one DMA piece) x LPT, then the remaining MFMAs
+#pragma unroll
+    for (int q = 0; q < LPT; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, NM / LPT, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         // VMEM read (the LDS-DMA piece)
+    }
+    if constexpr (NM % LPT) __builtin_amdgcn_sched_group_barrier(0x008, NM % LPT, 0);
+    advance();
+  };
 
-  const int pre = min(S, total);
-  for (int h = 0; h < pre; ++h) issue_next();
+  // steps 0 .. S - 1 (an iteration g then always refills with step g + S)
+#pragma unroll
+  for (int h = 0; h < S; ++h) issue_next(smem + h * STAGE);
   // step 0 in LDS for every wave, its first half-step's fragments in registers
-  pt_vmwait((pre - 1) * LPT);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * LPT) : "memory");
   if (ktail && nk == 1) {
     pt_zero_tail<BM, AK, NW>(0, K, smem, w, lane);
     pt_zero_tail<BN, BKM, NW>(0, K, smem + TA, w, lane);
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pt_lgkm0();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   read_frags(smem, 0, fa0, fb0);
 
   int e1 = -1000, e2 = -1000;  // the iterations of the two latest epilogues
-  int kt = 0, cur_st = 0, it = 0;
+  int kt = 0, it = 0;
+  int cur_off = 0;  // byte offset of step g's stage (the refill target too)
   for (int g = 0; g < total; ++g) {
-    const char* cur = smem + cur_st * STAGE;
-    const int nxt_st = cur_st == S - 1 ? 0 : cur_st + 1;
+    char* cur = smem + cur_off;
+    const int nxt_off = cur_off == (S - 1) * STAGE ? 0 : cur_off + STAGE;
     const bool last_k = kt == nk - 1;
+    PT_STAMP(0);
     // second half of step g from LDS while the first half's MFMAs run
     read_frags(cur, 1, fa1, fb1);
     __builtin_amdgcn_s_setprio(1);
     mfmas(fa0, fb0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    PT_STAMP(1);
     if (g + 1 < total) {
       // this thread's DMA of step g + 1 has landed once at most N younger ops are outstanding:
       // the pieces of steps g + 2 .. (issued so far) and the stores of epilogues after it
-      if (e1 < g + 1 - S && g + S <= total) {  // steady state: S - 2 younger steps, no stores
+      if (e1 < g + 1 - S) {  // steady state: the S - 2 younger steps, no epilogue stores
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * (S - 2)) : "memory");
       } else {
-        int n = LPT * max(0, min(total, g + S) - g - 2);
-        if (e1 >= g + 1 - S) n += nst;
-        if (e2 >= g + 1 - S) n += nst;
-        pt_vmwait(n);
+        pt_vmwait(LPT * (S - 2) + nst * ((e1 >= g + 1 - S) + (e2 >= g + 1 - S)));
       }
       if (ktail && (kt == nk - 2 || nk == 1)) {  // step g + 1 is a tile's last (K tail) step
-        pt_zero_tail<BM, AK, NW>((nk - 1) * 64, K, smem + nxt_st * STAGE, w, lane);
-        pt_zero_tail<BN, BKM, NW>((nk - 1) * 64, K, smem + nxt_st * STAGE + TA, w, lane);
+        pt_zero_tail<BM, AK, NW>((nk - 1) * 64, K, smem + nxt_off, w, lane);
+        pt_zero_tail<BN, BKM, NW>((nk - 1) * 64, K, smem + nxt_off + TA, w, lane);
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PT_STAMP(2);
+    pt_lgkm0();
     __builtin_amdgcn_s_barrier();  // step g + 1 in LDS for every wave; every wave is done reading step g
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    PT_STAMP(3);
 
     // the tile's last step: its epilogue operands are requested before the DMA of step g + S (the
     // compiler's wait for them then leaves that DMA in flight)
@@ -345,7 +417,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
     int M = 0, N = 0, m0 = 0, n0 = 0;
     bool has_bias = false, has_cs = false, has_rs = false, has_res = false, has_beta = false, aux_out = false,
          aux_in = false;
-    pt_rsrc_t rs_c = pt_rsrc(Ap, 0), rs_res = rs_c, rs_aux = rs_c, rs_bias = rs_c, rs_cs = rs_c, rs_rs = rs_c;
+    pt_rsrc_t rs_c = pt_rsrc(a.A, 0), rs_res = rs_c, rs_aux = rs_c, rs_bias = rs_c, rs_cs = rs_c, rs_rs = rs_c;
     pt_u32x4 bias_v[FN], cs_v[FN];
     pt_u32x2 res_v[EK >= 1 ? FM : 1][FN], aux_v[EK >= 2 ? FM : 1][FN], old_v[EK >= 2 ? FM : 1][FN];
     uint32_t rsc_v[FM];
@@ -399,14 +471,19 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
           }
         }
       }
+      // the scalar reads of the argument block done here (s_waitcnt lgkmcnt(0), vm/exp untouched):
+      // left pending, the compiler's wait at the join below also held the next fragment reads
+      // before the second half-step's MFMAs on every iteration
+      __builtin_amdgcn_s_waitcnt(0xC07F);
     }
     // refill the stage step g was read from with step g + S; the first half of step g + 1 from
     // LDS while the second half of step g is multiplied
-    if (g + S < total) issue_next();
-    if (g + 1 < total) read_frags(smem + nxt_st * STAGE, 0, fa0, fb0);
+    PT_STAMP(4);
+    if (g + 1 < total) read_frags(smem + nxt_off, 0, fa0, fb0);
     __builtin_amdgcn_s_setprio(1);
-    mfmas(fa1, fb1);
+    mfmas_dma(fa1, fb1, cur);  // with the pieces of step g + S (into the stage step g was read from)
     __builtin_amdgcn_s_setprio(0);
+    PT_STAMP(5);
 
     if (last_k) {
       __builtin_amdgcn_sched_barrier(0);
@@ -479,11 +556,19 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void gemm_pt_kernel(PtArgs a) {
       e2 = e1;
       e1 = g;
     }
-    cur_st = nxt_st;
+    PT_STAMP(6);
+    cur_off = nxt_off;
     if (++kt == nk) {
       kt = 0;
       ++it;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef IMGCAP_STAMPS
+  if ((a.dbg & 8) && threadIdx.x == 0 && g_dev_stamps) {
+    const uint64_t* st = (const uint64_t*)(smem + S * STAGE);
+    for (int i = 0; i < 64 * 8; ++i) g_dev_stamps[(long)blockIdx.x * 64 * 8 + i] = st[i];
+  }
+#endif
+#undef PT_STAMP
 }

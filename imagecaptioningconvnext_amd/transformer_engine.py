@@ -12,6 +12,7 @@ add+dropout+LN -> q GEMM / kv GEMM on the memory -> MHA -> out-proj -> add+LN ->
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -22,6 +23,10 @@ from .flat import FlatParams
 # weight gradients: long-K fp32 products into the gradient buffer, K sliced over the
 # grid (imgcap_epilogue.split_k)
 DW = dict(split_k=-1)
+
+# backward tail: bias-gradient column sums on a side stream beside the grouped weight-gradient
+# GEMMs (IMGCAP_TF_TAIL_FORK=0: one stream)
+TAIL_FORK = os.environ.get("IMGCAP_TF_TAIL_FORK", "1") != "0"
 
 # dropout stream ids (each site gets its own counter-based mask stream)
 _S_EMB = 1
@@ -408,7 +413,24 @@ class TransformerEngine:
                 denc = K.gemm(dmem_c, fp.w("encoder_proj.weight")).view(B, P, self.E)
         elif want_denc:
             denc = dmem.to(ct).view(B, P, d)
-        wgb.run()
-        cb.run()
+        if bucket_hook is None and TAIL_FORK and cb.items:
+            # the bias-gradient column sums (one launch, ~120 us at C3, reading every dY of the
+            # backward) beside the grouped weight-gradient GEMMs that read the same dY: the two
+            # are independent, and the step ends with them alone on the chip
+            main = torch.cuda.current_stream(dev)
+            side = self._side_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                cb.run()
+            wgb.run()
+            main.wait_stream(side)
+        else:
+            wgb.run()
+            cb.run()
         s["denc"] = denc
         return gbuf
+
+    def _side_stream(self, dev):
+        if getattr(self, "_side", None) is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(device=dev)
+        return self._side

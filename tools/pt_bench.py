@@ -58,7 +58,7 @@ def case(name, M, N, Kd, form):
     elif form == "bias":
         kw = dict(bias=bias)
     row = []
-    for mode in (0, 2, 3, 4, 5, 1):
+    for mode in (0, 2, 3, 4, 5, 6, 1):
         K.gemm_set_pt(mode)
         try:
             t = time_launch(lambda: K.gemm(a, b, trans_b=True, out=out, **kw), reps=reps)
@@ -68,13 +68,13 @@ def case(name, M, N, Kd, form):
     tt = time_launch(lambda: torch.matmul(a, b.t()), reps=reps)
     f = 2.0 * M * N * Kd
     cells = " ".join(f"{t * 1e6:7.1f}" for t in row)
-    best = min(row[1:5])
+    best = min(row[1:6])
     print(f"{name:18s} {M:6d} {N:5d} {Kd:5d} | {cells} | blaslt {tt * 1e6:7.1f} | "
-          f"old {f / row[0] / 1e12:6.0f} TF  st-best {f / best / 1e12:6.0f} TF  st-auto {f / row[5] / 1e12:6.0f} TF "
-          f"({row[0] / row[5]:.2f}x)", flush=True)
+          f"old {f / row[0] / 1e12:6.0f} TF  st-best {f / best / 1e12:6.0f} TF  st-auto {f / row[6] / 1e12:6.0f} TF "
+          f"({row[0] / row[6]:.2f}x)", flush=True)
 
 
 print(f"{'shape':18s} {'M':>6s} {'N':>5s} {'K':>5s} | {'old':>7s} {'256x128':>7s} {'128x256':>7s} {'128x128':>7s} "
-      f"{'128x192':>7s} {'auto':>7s} | us", flush=True)
+      f"{'128x192':>7s} {'128x128x2':>9s} {'auto':>7s} | us", flush=True)
 for s in SHAPES:
     case(*s)

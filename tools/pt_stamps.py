@@ -1,4 +1,4 @@
-"""In-kernel s_memtime stamps of the persistent-tile GEMM's k-loop (diagnostic build, GPU box):
+"""In-kernel s_memtime stamps of the stream-tile GEMM's k-loop (diagnostic build, GPU box):
     make -C imagecaptioningconvnext_amd/csrc diag && python tools/pt_stamps.py [cfg]
 Per iteration of wave 0 (first 64 iterations of every block): wait, barrier, DMA issue, MFMAs,
 epilogue / rest; prints median cycles per phase over blocks and iterations, the iteration total,
@@ -27,7 +27,7 @@ def run(M, N, Kd):
     b = torch.randn(N, Kd, device=dev).to(bf)
     out = torch.empty(M, N, device=dev, dtype=bf)
     K.gemm_set_pt(cfg)
-    st = torch.zeros(1024 * 64 * 8, device=dev, dtype=torch.int64)
+    st = torch.zeros(1024 * 64 * 8, device=dev, dtype=torch.int64)  # [block][iteration][phase]
     for _ in range(3):
         K.gemm(a, b, trans_b=True, out=out)
     torch.cuda.synchronize()
@@ -38,16 +38,20 @@ def run(M, N, Kd):
     K.gemm_set_pt(0)
     s = st.view(1024, 64, 8).cpu().double()
     used = s[:, :, 0] > 0
-    nk = (Kd + 63) // 64
-    names = ["wait", "zero/bar", "issue", "mfma", "epi/rest"]
+    names = ["mfma0+reads", "wait", "barrier", "issue/eload", "reads+mfma1", "epi"]
     res = []
-    for k in range(5):
+    for k in range(6):
         d = (s[:, :, k + 1] - s[:, :, k])[used]
         res.append(d.median().item())
     nxt = (s[:, 1:, 0] - s[:, :-1, 0])[used[:, 1:]]
     print(f"cfg {cfg} M={M} N={N} K={Kd}: " + "  ".join(f"{n} {v:.0f}" for n, v in zip(names, res)) +
-          f"  | iteration {nxt.median().item():.0f} cyc (p90 {nxt.quantile(0.9).item():.0f})", flush=True)
+          f"  | iteration {nxt.median().item():.0f} cyc (p10 {nxt.quantile(0.1).item():.0f} p90 {nxt.quantile(0.9).item():.0f})",
+          flush=True)
 
 
-for shape in ((12544, 1536, 384), (12544, 384, 1536), (3136, 768, 3072), (4096, 4096, 4096)):
+shapes = ((12544, 1536, 384), (12544, 384, 1536), (3136, 768, 3072), (4096, 4096, 4096), (3328, 512, 512))
+if os.environ.get("IMGCAP_PT_DBG"):
+    print(f"IMGCAP_PT_DBG={os.environ['IMGCAP_PT_DBG']} (1: DMA of k-step 0 only, 2: no MFMA, 4: no DMA)")
+    shapes = shapes[1:2] + shapes[3:4]
+for shape in shapes:
     run(*shape)
