@@ -83,7 +83,6 @@ _SIGS = {
     "imgcap_convnext_stem": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p],
     "imgcap_convnext_stem_u8": [c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 9,
-    "imgcap_dwconv7_ln_mx": [c_int, c_int, c_int, c_int] + [c_void_p] * 7 + [c_void_p],
     "imgcap_dwconv7_ln": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p],
     "imgcap_ln_patchify2": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,

@@ -870,16 +870,11 @@ void dw_roll_attr() {
 // 4-byte bf16 pairs (64 lanes = 256 contiguous bytes, the next row requested before the current
 // one is used), unpacks it once and applies all 7 taps of that kernel row with packed FMAs
 // (≈ 0.7 VALU per MAC), and the grid is B*H rows x C/128 waves.  flip / res: the backward data gradient (taps mirrored, residual added), as dwconv7_kernel.
-// MXQ (with LN): the normalised rows leave as MX-FP8 -- e4m3 bytes in y, one E8M0 scale per 32
-// channels in qs -- the A operand of the frozen stages' fp8 Linear (imgcap_gemm_mx), with the
-// block encoding of imgcap_mx_quant_rows (e = floor(log2 amax) - 8, values clamped to +-448);
-// the separate quantiser pass and the bf16 round trip of the normalised rows are gone.
-template <int W, bool LN, int R, bool MXQ = false>
+template <int W, bool LN, int R>
 __global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf16* __restrict__ x,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
                                                          const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                         bf16* __restrict__ y, const bf16* __restrict__ res, int flip,
-                                                         uint8_t* __restrict__ qs = nullptr) {
+                                                         bf16* __restrict__ y, const bf16* __restrict__ res, int flip) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int HB = (H + R - 1) / R;  // R output rows per block (R = 2: each weight row loaded once for both)
   const long r = blockIdx.x;       // b * HB + row block
@@ -1017,24 +1012,7 @@ __global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf1
       const f32x2 a = acc[p / W][p % W];
       const float rstd = rsqrtf(stat[1][p] + 1e-6f);
       const float v0 = (a[0] - mean[p]) * rstd * g2[0] + b2[0], v1 = (a[1] - mean[p]) * rstd * g2[1] + b2[1];
-      if constexpr (MXQ) {
-        // 32 channels = 16 lanes: block amax over lanes l ^ 1, 2, 4, 8
-        float amax = fmaxf(fabsf(v0), fabsf(v1));
-        amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
-        amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
-        amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
-        amax = fmaxf(amax, __shfl_xor(amax, 8, 64));
-        const int ex = (int)((__float_as_uint(amax) >> 23) & 0xff);
-        const int sb = ex == 0 ? 127 : max(ex - 8, 1);
-        const float inv = __uint_as_float((uint32_t)(254 - sb) << 23);
-        const float q0 = fminf(fmaxf(v0 * inv, -448.f), 448.f), q1 = fminf(fmaxf(v1 * inv, -448.f), 448.f);
-        const uint32_t pk = __builtin_amdgcn_cvt_pk_fp8_f32(q0, q1, 0, false);
-        uint8_t* qb = (uint8_t*)y;
-        *(uint16_t*)(qb + o0 + (long)p * C) = (uint16_t)(pk & 0xffffu);
-        if ((lane & 15) == 0) qs[(o0 + (long)p * C) / 32] = (uint8_t)sb;
-      } else {
-        *(bf16x2*)(y + o0 + (long)p * C) = bf16x2{(bf16)v0, (bf16)v1};
-      }
+      *(bf16x2*)(y + o0 + (long)p * C) = bf16x2{(bf16)v0, (bf16)v1};
     }
   } else {
 #pragma unroll
@@ -1078,7 +1056,7 @@ int dw_cp_rows(int W, int C, bool ln) {
 }
 
 int dwconv7_cp_launch(int B, int H, int W, int C, const void* x, const float* w, const float* bias, const float* lnw,
-                      const float* lnb, void* y, const void* res, int flip, hipStream_t st, uint8_t* qs = nullptr) {
+                      const float* lnb, void* y, const void* res, int flip, hipStream_t st) {
   // the LayerNorm form needs every channel of a pixel in one block; without it a block takes 4, 2
   // or 1 waves of 128 channels (blockIdx.y: channel group) so blocks pack a CU's wave slots
   const int nw = C / 128, wpb = lnw ? nw : (nw % 4 == 0 ? 4 : nw % 2 == 0 ? 2 : 1);
@@ -1086,23 +1064,10 @@ int dwconv7_cp_launch(int B, int H, int W, int C, const void* x, const float* w,
   const dim3 grid((unsigned)((long)B * ((H + R - 1) / R)), (unsigned)(nw / wpb)), block((unsigned)(wpb * 64));
 #define CP_(WW, L, RR)                                                                                          \
   hipLaunchKernelGGL((dwconv7_cp_kernel<WW, L, RR>), grid, block, 0, st, H, C, (const bf16*)x, w, bias, lnw, lnb, \
-                     (bf16*)y, (const bf16*)res, flip, nullptr)
+                     (bf16*)y, (const bf16*)res, flip)
 #define CP_R(WW, L) \
   if (R == 2) CP_(WW, L, 2); \
   else CP_(WW, L, 1)
-#define CPQ_(WW, RR)                                                                                            \
-  hipLaunchKernelGGL((dwconv7_cp_kernel<WW, true, RR, true>), grid, block, 0, st, H, C, (const bf16*)x, w, bias,  \
-                     lnw, lnb, (bf16*)y, nullptr, 0, qs)
-  if (qs) {  // MX-FP8 output (LayerNorm form)
-    if (W == 14) {
-      if (R == 2) CPQ_(14, 2); else CPQ_(14, 1);
-    } else {
-      if (R == 2) CPQ_(7, 2); else CPQ_(7, 1);
-    }
-    IMGCAP_CHECK_LAUNCH("imgcap_dwconv7_ln_mx");
-    return 0;
-  }
-#undef CPQ_
   if (W == 14) {
     if (lnw) CP_R(14, true);
     else CP_R(14, false);
@@ -1256,14 +1221,6 @@ extern "C" int imgcap_convnext_stem_u8(int dtype, int B, int H, int W, int C0, c
                        images, w, bias, ln_w, ln_b, (float*)out, npx, mean3, std3);
   IMGCAP_CHECK_LAUNCH("imgcap_convnext_stem_u8");
   return 0;
-}
-
-extern "C" int imgcap_dwconv7_ln_mx(int B, int H, int W, int C, const void* x, const float* w, const float* bias,
-                                    const float* ln_w, const float* ln_b, uint8_t* q, uint8_t* s, void* stream) {
-  IMGCAP_REQUIRE(dw_cp_fits(W, C, true), "imgcap_dwconv7_ln_mx: W must be 7 or 14, C % 128 == 0, C <= 1024");
-  IMGCAP_REQUIRE(x && w && ln_w && ln_b && q && s, "imgcap_dwconv7_ln_mx: null operand");
-  IMGCAP_REQUIRE(aligned16(x) && ((uintptr_t)q & 1) == 0, "imgcap_dwconv7_ln_mx: alignment");
-  return dwconv7_cp_launch(B, H, W, C, x, w, bias, ln_w, ln_b, q, nullptr, 0, (hipStream_t)stream, s);
 }
 
 extern "C" int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const void* x, const float* w,

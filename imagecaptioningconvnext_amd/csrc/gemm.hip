@@ -534,11 +534,11 @@ static GemmPlan gemm_plan(bool bf16_op, int ak, int bk, int M, int N, int K, lon
 }
 
 // ---- stream-tile kernel (gemm_pt.h): selection and launch ---------------------------------
-// IMGCAP_GEMM_PT / imgcap_gemm_set_pt: -1 by shape, 0 never (default), 1 wherever eligible (tile by
-// the cost model), 2..5 wherever eligible with tile config 1..4 forced
+// IMGCAP_GEMM_PT / imgcap_gemm_set_pt: -1 by shape (default, pt_by_shape), 0 never, 1 wherever
+// eligible (tile by the cost model), 2..7 wherever eligible with tile config 1..6 forced
 static int g_gemm_pt_mode = [] {
   const char* e = getenv("IMGCAP_GEMM_PT");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : -1;
 }();
 
 static int device_cus() {
@@ -555,12 +555,19 @@ static int device_cus() {
 
 // tile configs: 1 = 256x128 (8 waves 4x2, 3 stages), 2 = 128x256 (2x4, 3 stages), 3 = 128x128 (2x4, 4
 // stages), 4 = 128x192 (2x4, 3 stages) -- one block per CU; 5 = 128x128 (4 waves 2x2, 2 stages), two
-// blocks per CU
-constexpr int PT_NCFG = 5;
-struct PtCfg { int bm, bn, bpc; };
+// blocks per CU; 6 = 128x128 (2x4, 2 stages of 128-deep k-steps).  (4-wave blocks with 128-row wave
+// tiles at one wave per SIMD -- 256x128 / 256x256 / 128x256 -- spilled and ran 1.5-20x slower.)
+constexpr int PT_NCFG = 6;
+struct PtCfg { int bm, bn, bpc, ks; };
 static PtCfg pt_cfg(int c) {
-  return c == 1 ? PtCfg{256, 128, 1} : c == 2 ? PtCfg{128, 256, 1} : c == 3 ? PtCfg{128, 128, 1}
-       : c == 4 ? PtCfg{128, 192, 1} : PtCfg{128, 128, 2};
+  switch (c) {
+    case 1: return {256, 128, 1, 1};
+    case 2: return {128, 256, 1, 1};
+    case 3: return {128, 128, 1, 1};
+    case 4: return {128, 192, 1, 1};
+    case 5: return {128, 128, 2, 1};
+    default: return {128, 128, 1, 2};
+  }
 }
 
 // cycles of the busiest block: its tiles (persistent rounds over the CUs) x (k-steps x max(MFMA,
@@ -569,8 +576,8 @@ static double pt_estimate(int c, int M, int N, int K, int cus) {
   const PtCfg t = pt_cfg(c);
   const long tiles = (long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
   const long rounds = (tiles + cus * t.bpc - 1) / (cus * t.bpc);
-  const double nk = (K + 63) / 64;
-  const double step = std::max((double)t.bm * t.bn / 32.0, (t.bm + t.bn) * 128.0 / 30.0);
+  const double nk = (K + 64 * t.ks - 1) / (64 * t.ks);
+  const double step = t.ks * std::max((double)t.bm * t.bn / 32.0, (t.bm + t.bn) * 128.0 / 30.0);
   const double epi = t.bm * t.bn * 2.0 / 8.0;
   return rounds * (nk * step + epi);
 }
@@ -578,7 +585,9 @@ static double pt_estimate(int c, int M, int N, int K, int cus) {
 // configs instantiated per (epilogue kind, layout): the 64x64-per-wave tiles hold the general
 // epilogue's operands (and the residual of a transposed layout) only by spilling, so those forms
 // take the 64x32 / 64x48 wave tiles
-static bool pt_allowed(int c, int ek, bool ak, bool bk) {
+static bool pt_allowed(int c, int ek, bool ak, bool bk, int K) {
+  if (K % (64 * pt_cfg(c).ks)) return false;  // 128-deep k-steps: no K tail
+  if (c == 6) return ek == 0 || (ek == 1 && ak && bk);
   if (ek == 2) return c == 3;
   if (ek == 1 && !(ak && bk)) return c == 3 || c == 4;
   if (c == 5) return ek <= 1 && ak && bk;
@@ -594,11 +603,33 @@ static int pt_choose(int M, int N, int K, int ek, bool ak, bool bk) {
   int best = 0;
   double bt = 0;
   for (int c = 1; c <= PT_NCFG; ++c) {
-    if (!pt_allowed(c, ek, ak, bk)) continue;
+    if (!pt_allowed(c, ek, ak, bk, K)) continue;
     const double t = pt_estimate(c, M, N, K, cus);
     if (!best || t < bt) { best = c; bt = t; }
   }
   return best;
+}
+
+// the default plan: the stream tile only where a step census (tools/gemm_census.py, C3 / C4 steps,
+// every call timed under each config) measured it ahead of the LDS-staged 64x64 plan -- the
+// forward pointwise / downsample products of the encoder (A, B both k-major, no saved-operand
+// epilogue):
+//   N = 384 (128x192: two column tiles, no N tail), M >= 8192:         12544x384x1536 28.2 vs 31.7 us
+//   N = 256 (128x128, two blocks a CU), M >= 8192:                     25088x256x1024 26.2 vs 29.0
+//   N = 512, K >= 1024, M >= 4096 (128x128, 128-deep k-steps):         6272x512x2048  25.4 vs 29.9
+//   N >= 1024 and M >= 20000, or N >= 4096 and K >= 1024 (128x128 x2):  25088x1024x256 37.6 vs 43.4,
+//                                                                     1568x4096x1024 24.2 vs 27.9
+// everything else (decoder products, grids under a round of 128x128 tiles, the deep-K stage-4
+// second Linear, the backward's transposed layouts) stays on the 64x64 plan, which was as fast or
+// faster there
+static int pt_by_shape(int M, int N, int K, int ek, bool ak, bool bk) {
+  if (!(ak && bk) || ek > 1) return 0;
+  int c = 0;
+  if (N == 384 && M >= 8192) c = 4;
+  else if (N == 256 && M >= 8192) c = 5;
+  else if (N == 512 && K >= 1024 && M >= 4096) c = 6;
+  else if ((N >= 1024 && M >= 20000) || (N >= 4096 && K >= 1024)) c = 5;
+  return c && pt_allowed(c, ek, ak, bk, K) ? c : 0;
 }
 
 // bytes from an operand's base to the end of its last 16-byte slot: the descriptor's range check is
@@ -620,12 +651,8 @@ static int pt_plan(int ak, int bk, int M, int N, int K, long lda, long ldb, int 
     if (ep->rowscale && ep->rows_per_scale <= 0) return 0;
   }
   const int ek = pt_ek(ep);
-  if (mode >= 2 && mode <= PT_NCFG + 1) return pt_allowed(mode - 1, ek, ak, bk) ? mode - 1 : pt_choose(M, N, K, ek, ak, bk);
-  if (mode < 0) {
-    // by shape: grids of at least ~a round of the 128x128 tile (the small decoder products stay
-    // on the 64x64 LDS-DMA tile's four blocks per CU)
-    if ((long)M * N < 2000000L || K < 256) return 0;
-  }
+  if (mode >= 2 && mode <= PT_NCFG + 1) return pt_allowed(mode - 1, ek, ak, bk, K) ? mode - 1 : pt_choose(M, N, K, ek, ak, bk);
+  if (mode < 0) return pt_by_shape(M, N, K, ek, ak, bk);
   return pt_choose(M, N, K, ek, ak, bk);
 }
 
@@ -663,6 +690,11 @@ template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, false, 0>(PtAr
 template __global__ void gemm_pt_kernel<128, 192, 2, 4, 3, false, false, 1>(PtArgs);
 template __global__ void gemm_pt_kernel<128, 128, 2, 2, 2, true, true, 0>(PtArgs);
 template __global__ void gemm_pt_kernel<128, 128, 2, 2, 2, true, true, 1>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 2, true, true, 0, 2>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 2, true, true, 1, 2>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 2, true, false, 0, 2>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 2, false, true, 0, 2>(PtArgs);
+template __global__ void gemm_pt_kernel<128, 128, 2, 4, 2, false, false, 0, 2>(PtArgs);
 
 // only the (config, epilogue kind, layout) combinations pt_allowed admits are instantiated
 template <bool AKV, bool BKV>
@@ -676,6 +708,10 @@ void pt_launch_t(int cfg, int ek, int G, const PtArgs& a, hipStream_t st) {
   } else if (cfg == 4) {
     if (ek == 0) PT_L(128, 192, 2, 4, 3, 0);
     else PT_L(128, 192, 2, 4, 3, 1);
+  } else if (cfg == 6) {
+    if (ek == 0) hipLaunchKernelGGL((gemm_pt_kernel<128, 128, 2, 4, 2, AKV, BKV, 0, 2>), dim3(G), dim3(512), 0, st, a);
+    else if constexpr (AKV && BKV)
+      hipLaunchKernelGGL((gemm_pt_kernel<128, 128, 2, 4, 2, AKV, BKV, 1, 2>), dim3(G), dim3(512), 0, st, a);
   } else if (cfg == 5) {
     if constexpr (AKV && BKV) {
       if (ek == 0) PT_L(128, 128, 2, 2, 2, 0);
@@ -708,8 +744,7 @@ static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A
   a.tiles_n = (N + t.bn - 1) / t.bn;
   a.ntiles = tm * a.tiles_n;
   const int cus = device_cus();
-  int G = a.ntiles < cus * t.bpc ? a.ntiles : cus * t.bpc;
-  if (G >= 64) G -= G % 8;
+  const int G = a.ntiles < cus * t.bpc ? a.ntiles : cus * t.bpc;
   // each XCD's concurrent tiles (G / 8 of them) as a rectangle of grp tile rows balancing its
   // A and B bytes: rows ~ sqrt(run * BN / BM)
   const double run = std::max(1.0, G / 8.0);
@@ -729,7 +764,7 @@ static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A
   if (a.c_bytes > 0x7fffffffull || a.res_bytes > 0x7fffffffull || a.aux_bytes > 0x7fffffffull)
     return fail(IMGCAP_EUNSUPPORTED, "imgcap_gemm(stream tile): operand over 2 GiB");
   const int ek = pt_ek(&ep);
-  if (!pt_allowed(cfg, ek, ak, bk)) return fail(IMGCAP_EINVAL, "imgcap_gemm(stream tile): config not built for this epilogue");
+  if (!pt_allowed(cfg, ek, ak, bk, K)) return fail(IMGCAP_EINVAL, "imgcap_gemm(stream tile): config not built for this epilogue");
   if (ak && bk) pt_launch_t<true, true>(cfg, ek, G, a, st);
   else if (ak) pt_launch_t<true, false>(cfg, ek, G, a, st);
   else if (bk) pt_launch_t<false, true>(cfg, ek, G, a, st);
@@ -1146,7 +1181,7 @@ extern "C" int imgcap_transpose(int dtype, int rows, int cols, const void* in, i
 }
 
 extern "C" int imgcap_gemm_set_pt(int mode) {
-  IMGCAP_REQUIRE(mode >= -1 && mode <= PT_NCFG + 1, "imgcap_gemm_set_pt: -1..6");
+  IMGCAP_REQUIRE(mode >= -1 && mode <= PT_NCFG + 1, "imgcap_gemm_set_pt: -1..7");
   g_gemm_pt_mode = mode;
   return 0;
 }

@@ -96,10 +96,11 @@ struct PtSrc {
       }
     }
   }
-  // piece j of the k-step whose descriptor is rs into the stage image img
-  DEV void issue(int j, pt_rsrc_t rs, char* img, int w) const {
+  // piece j of the k-step whose descriptor is rs into the stage image img (soff: the sub-image's
+  // byte offset from the descriptor base, a scalar)
+  DEV void issue(int j, pt_rsrc_t rs, char* img, int w, int soff = 0) const {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + (j * NW + w) * 1024),
-                                             16, voff[j], 0, 0, 0);
+                                             16, voff[j], soff, 0, 0);
   }
 };
 
@@ -198,17 +199,22 @@ DEV imgcap_epilogue pt_load_ep(pt_kptr ka) {
 // pre-activation written are all allowed), 1 the residual, 2 any (residual, saved operand for
 // dGELU / the ReLU mask, old C for beta); fewer live registers for the common forms
 // 8-wave blocks run one per CU; 4-wave blocks two per CU (both: two waves per SIMD)
-template <int BM, int BN, int WM, int WN, int S, bool AK, bool BKM, int EK>
-__global__ __launch_bounds__(WM* WN * 64, 2) void gemm_pt_kernel(PtArgs a) {
+// KS: 64-deep sub-images per stage (a k-step of 64 KS: one barrier and one round of bookkeeping
+// per 2 KS half-steps of MFMAs; KS = 2 needs K % 128 == 0)
+// WPE: waves per SIMD the registers are sized for -- 2 (<= 256 VGPRs + AGPRs a lane), or 1 for
+// the 4-wave blocks with 128-row wave tiles (up to 512, the accumulators in AGPRs)
+template <int BM, int BN, int WM, int WN, int S, bool AK, bool BKM, int EK, int KS = 1, int WPE = 2>
+__global__ __launch_bounds__(WM* WN * 64, WPE) void gemm_pt_kernel(PtArgs a) {
   constexpr int NW = WM * WN;
-  constexpr int TA = BM * 64 * 2, TB = BN * 64 * 2, STAGE = TA + TB;
+  constexpr int TA = BM * 64 * 2, TB = BN * 64 * 2, SUB = TA + TB, STAGE = KS * SUB;
+  constexpr int H = 2 * KS;  // 32-deep half-steps per k-step
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
   using SrcA = PtSrc<BM, AK, NW>;
   using SrcB = PtSrc<BN, BKM, NW>;
-  constexpr int PA = SrcA::PER, PB = SrcB::PER, LPT = PA + PB;  // DMA pieces per thread per k-step
+  constexpr int PA = SrcA::PER, PB = SrcB::PER, LPT = KS * (PA + PB);  // DMA pieces per thread per k-step
   constexpr int NST = FM * FN;                                   // 8-byte stores per thread per epilogue
   static_assert(FM >= 1 && FN >= 1 && FM * 16 * WM == BM && FN * 16 * WN == BN, "wave tiles");
-  static_assert(S >= 2 && S * STAGE * (NW == 4 ? 2 : 1) <= 160 * 1024, "stages");
+  static_assert(S >= 2 && S * STAGE * (NW == 4 && WPE == 2 ? 2 : 1) <= 160 * 1024, "stages");
 #ifdef IMGCAP_STAMPS
   // diagnostic build: wave 0's s_memtime per iteration phase (first 64 iterations) kept in LDS
   // behind the stages and copied out at the end (a global store would enter the counted waits)
@@ -239,9 +245,11 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_pt_kernel(PtArgs a) {
   // this block's tiles: slot, slot + G, ...; the blocks sharing an XCD (b % 8) own consecutive
   // slots, i.e. one rectangle of the output per round
   const int G = gridDim.x, b = blockIdx.x;
-  const int slot = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;
+  // (XCD x = b % 8 holds G / 8 + (x < G % 8) blocks: a bijection onto 0 .. G - 1 for any G)
+  const int xq = G / 8, xr = G % 8, xb = b % 8;
+  const int slot = xb * xq + min(xb, xr) + b / 8;
   const int my_tiles = slot < a.ntiles ? (a.ntiles - 1 - slot) / G + 1 : 0;
-  const int nk = (K + 63) / 64;
+  const int nk = (K + 64 * KS - 1) / (64 * KS);
   const int total = my_tiles * nk;
   const bool ktail = (K & 63) != 0;
   if (total == 0) return;
@@ -268,13 +276,17 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_pt_kernel(PtArgs a) {
   set_src(0);
   const uint64_t a_base = (uint64_t)a.A, b_base = (uint64_t)a.B;
   const int a_ext = (int)a.a_bytes, b_ext = (int)a.b_bytes;  // host-checked < 2^31
-  const int sa = AK ? 128 : 128 * (int)a.lda, sb = BKM ? 128 : 128 * (int)a.ldb;
+  // bytes between two 64-deep sub-images; a k-step advances KS of them
+  const int sa1 = AK ? 128 : 128 * (int)a.lda, sb1 = BKM ? 128 : 128 * (int)a.ldb;
+  const int sa = KS * sa1, sb = KS * sb1;
   uint64_t da = a_base, db = b_base;
   int na = a_ext, nb = b_ext;
-  // piece q (A pieces first) of the pending k-step into the stage image st
+  // piece q of the pending k-step into the stage image st: sub-image q / (PA + PB), A pieces first
   auto issue_piece = [&](int q, pt_rsrc_t ra, pt_rsrc_t rb_, char* st) {
-    if (q < PA) srcA.issue(q, ra, st, w);
-    else srcB.issue(q - PA, rb_, st + TA, w);
+    constexpr int PU = PA + PB;
+    const int u = q / PU, r = q % PU;
+    if (r < PA) srcA.issue(r, ra, st + u * SUB, w, u * sa1);
+    else srcB.issue(r - PA, rb_, st + u * SUB + TA, w, u * sb1);
   };
   auto advance = [&]() {  // the pending k-step has been issued
     if (++is_kt == nk) {
@@ -367,7 +379,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_pt_kernel(PtArgs a) {
   for (int h = 0; h < S; ++h) issue_next(smem + h * STAGE);
   // step 0 in LDS for every wave, its first half-step's fragments in registers
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * LPT) : "memory");
-  if (ktail && nk == 1) {
+  if (KS == 1 && ktail && nk == 1) {  // (KS > 1: the host guarantees K % (64 KS) == 0)
     pt_zero_tail<BM, AK, NW>(0, K, smem, w, lane);
     pt_zero_tail<BN, BKM, NW>(0, K, smem + TA, w, lane);
   }
@@ -384,10 +396,19 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_pt_kernel(PtArgs a) {
     const int nxt_off = cur_off == (S - 1) * STAGE ? 0 : cur_off + STAGE;
     const bool last_k = kt == nk - 1;
     PT_STAMP(0);
-    // second half of step g from LDS while the first half's MFMAs run
-    read_frags(cur, 1, fa1, fb1);
+    // half-step h + 1 of step g from LDS while half-step h's MFMAs run (h = 0 .. H - 2; even
+    // half-steps in set 0, odd in set 1)
     __builtin_amdgcn_s_setprio(1);
-    mfmas(fa0, fb0);
+#pragma unroll
+    for (int h = 0; h < H - 1; ++h) {
+      if (h & 1) {
+        read_frags(cur + (h + 1) / 2 * SUB, (h + 1) & 1, fa0, fb0);
+        mfmas(fa1, fb1);
+      } else {
+        read_frags(cur + (h + 1) / 2 * SUB, (h + 1) & 1, fa1, fb1);
+        mfmas(fa0, fb0);
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     PT_STAMP(1);
@@ -399,7 +420,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_pt_kernel(PtArgs a) {
       } else {
         pt_vmwait(LPT * (S - 2) + nst * ((e1 >= g + 1 - S) + (e2 >= g + 1 - S)));
       }
-      if (ktail && (kt == nk - 2 || nk == 1)) {  // step g + 1 is a tile's last (K tail) step
+      if (KS == 1 && ktail && (kt == nk - 2 || nk == 1)) {  // step g + 1 is a tile's last (K tail) step
         pt_zero_tail<BM, AK, NW>((nk - 1) * 64, K, smem + nxt_off, w, lane);
         pt_zero_tail<BN, BKM, NW>((nk - 1) * 64, K, smem + nxt_off + TA, w, lane);
       }
@@ -481,7 +502,7 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void gemm_pt_kernel(PtArgs a) {
     PT_STAMP(4);
     if (g + 1 < total) read_frags(smem + nxt_off, 0, fa0, fb0);
     __builtin_amdgcn_s_setprio(1);
-    mfmas_dma(fa1, fb1, cur);  // with the pieces of step g + S (into the stage step g was read from)
+    mfmas_dma(fa1, fb1, cur);  // half-step H - 1 with the pieces of step g + S (into the stage step g was read from)
     __builtin_amdgcn_s_setprio(0);
     PT_STAMP(5);
 

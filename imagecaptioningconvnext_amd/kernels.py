@@ -73,8 +73,8 @@ def gemm_set_policy(glds256):
 
 def gemm_set_pt(mode):
     """Stream-tile GEMM (imgcap_gemm_set_pt): -1 by shape (the library default), 0 never, 1
-    wherever eligible (cost-model tile), 2..5 wherever eligible with tile 256x128 / 128x256 /
-    128x128 / 128x192."""
+    wherever eligible (cost-model tile), 2..7 wherever eligible with tile 256x128 / 128x256 /
+    128x128 / 128x192 / 128x128 (4 waves, two blocks a CU) / 128x128 (128-deep k-steps)."""
     _abi.call("imgcap_gemm_set_pt", int(mode))
 
 
@@ -456,18 +456,6 @@ def dw_ln_fused(W, C, dtype):
     the encoder then skips the separate add_layernorm pass."""
     return (os.environ.get("IMGCAP_DW_CP", "1") != "0" and dtype == torch.bfloat16 and C % 128 == 0 and C <= 1024
             and W in (7, 14))
-
-
-def dwconv7_ln_mx(x, w49, bias, ln_w, ln_b, out):
-    """Depthwise 7x7 + LayerNorm (eps 1e-6) with MX-FP8 output: out = (q [B*H*W, C] uint8, s
-    [B*H*W, C/32] uint8), as mx_quant_rows(LN(dwconv7(x))) would give them (the LayerNorm from
-    the fp32 depthwise sums).  dw_ln_fused(W, C) shapes, bf16 x."""
-    _check_dev(x, w49, bias, ln_w, ln_b)
-    B, H, W, C = x.shape
-    q, sc = out
-    _abi.call("imgcap_dwconv7_ln_mx", B, H, W, C, x.data_ptr(), w49.data_ptr(), bias.data_ptr(), ln_w.data_ptr(),
-              ln_b.data_ptr(), q.data_ptr(), sc.data_ptr(), stream())
-    return out
 
 
 def dwconv7_ln(x, w49, bias, ln_w, ln_b, out):

@@ -15,14 +15,12 @@ suffix runs on encoder_engine.EncoderEngine (saved activations + HIP backward) a
 differentiable; the frozen prefix always takes the fused fast path.
 """
 import math
-import os
 
 import torch
 from torch import nn
 
 from .. import kernels as K
 
-_MX_DW = os.environ.get("IMGCAP_MX_DW", "0") == "1"
 
 VARIANTS = {
     "tiny": ((96, 192, 384, 768), (3, 3, 9, 3), 0.1),
@@ -277,17 +275,11 @@ class Encoder(nn.Module):
                 zn = torch.empty(M, C, device=dev, dtype=ct)
             x2 = x.view(M, C)
             # MX stages: the depthwise writes bf16 rows, the quantiser applies the LayerNorm and
-            # writes the fp8 rows + block scales.  IMGCAP_MX_DW=1: depthwise + LayerNorm + MX
-            # quantisation in one kernel (imgcap_dwconv7_ln_mx) instead -- measured slower at C5
-            # (ConvNeXt-Large, C = 768 / 1536): its LayerNorm epilogue costs the channel-pair
-            # kernel more than the separate quantiser pass (C5 5.21k -> 5.00k img/s)
-            mx_dw = mx and _MX_DW and K.dw_ln_fused(w, C, ct)
+            # writes the fp8 rows + block scales (a depthwise + LayerNorm + MX quantisation kernel
+            # measured slower at C5 in round 4 and was removed)
             for blk in blocks:
                 rs = sd[bid] if (sd is not None and blk["sd"] > 0) else None
-                if mx_dw:
-                    K.dwconv7_ln_mx(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], znq)
-                    ln = None
-                elif w <= 64 and (mx or fused or not K.dw_ln_fused(w, C, ct)):
+                if w <= 64 and (mx or fused or not K.dw_ln_fused(w, C, ct)):
                     # channel-tiled depthwise; LayerNorm applied by the consumer
                     K.dwconv7(x, blk["w49"], blk["dwb"], z)
                     ln = (blk["lnw"], blk["lnb"])
@@ -295,9 +287,7 @@ class Encoder(nn.Module):
                     K.dwconv7_ln(x, blk["w49"], blk["dwb"], blk["lnw"], blk["lnb"], z)
                     ln = (None, None)
                 if mx:  # LN -> fp8 rows; fp8 Linear + GELU -> fp8 hidden; fp8 Linear + scale + residual
-                    if ln is None:
-                        pass  # quantised by the depthwise kernel
-                    elif ln[0] is not None:
+                    if ln[0] is not None:
                         K.mx_quant_rows(z.view(M, C), ln[0], ln[1], 1e-6, out=znq)
                     else:
                         K.mx_quant_rows(z.view(M, C), out=znq)

@@ -33,7 +33,8 @@ SLEEP_CYCLES = 400_000    # device sleep in front of each timed call (> the host
 _KIND_NAME = {1: "gemm_skinny_kernel", 2: "gemm_kernel<64,64,64>", 3: "gemm_kernel<128,128,64>",
               4: "gemm_glds_kernel<128,128>", 5: "gemm256_kernel<256,256>", 6: "gemm_glds_kernel<64,64>",
               7: "gemm_glds_kernel<128,64>", 8: "gemm_pt_kernel<256,128>", 9: "gemm_pt_kernel<128,256>",
-              10: "gemm_pt_kernel<128,128>", 11: "gemm_pt_kernel<128,192>"}
+              10: "gemm_pt_kernel<128,128>", 11: "gemm_pt_kernel<128,192>", 12: "gemm_pt_kernel<128,128,4w>",
+              13: "gemm_pt_kernel<128,128,k128>"}
 
 # calls that launch nothing
 _NO_KERNEL = {"imgcap_workspace_slot", "imgcap_set_seed_counter", "imgcap_gemm_set_policy", "imgcap_workspace_attach",
@@ -75,7 +76,7 @@ def _gemm_group(a):
     lda, ldb, ep = a[7], a[10], a[16]._obj
     kind, splits = K.gemm_plan(dtype, ak, bk, M, N, K_, lda, ldb, a[15], ep.split_k, ep=ep)
     name = _KIND_NAME.get(kind, f"gemm kind {kind}")
-    if kind in (2, 3, 4, 5, 6, 7, 8, 9, 10, 11):
+    if kind in (2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13):
         name += f"<ak={ak},bk={bk}>" + (" (split-K)" if splits > 1 else "")
     tf = lambda v: "true" if v else "false"  # noqa: E731
     sym = {4: f"gemm_glds_kernel<128, 128, {tf(ak)}, {tf(bk)}, ",  # any stage count
@@ -85,7 +86,9 @@ def _gemm_group(a):
            8: "gemm_pt_kernel<256, 128, 4, 2, 3, " + f"{tf(ak)}, {tf(bk)}, ",
            9: "gemm_pt_kernel<128, 256, 2, 4, 3, " + f"{tf(ak)}, {tf(bk)}, ",
            10: "gemm_pt_kernel<128, 128, 2, 4, 4, " + f"{tf(ak)}, {tf(bk)}, ",
-           11: "gemm_pt_kernel<128, 192, 2, 4, 3, " + f"{tf(ak)}, {tf(bk)}, "}.get(kind, _KIND_NAME.get(kind, ""))
+           11: "gemm_pt_kernel<128, 192, 2, 4, 3, " + f"{tf(ak)}, {tf(bk)}, ",
+           12: "gemm_pt_kernel<128, 128, 2, 2, 2, " + f"{tf(ak)}, {tf(bk)}, ",
+           13: "gemm_pt_kernel<128, 128, 2, 4, 2, " + f"{tf(ak)}, {tf(bk)}, "}.get(kind, _KIND_NAME.get(kind, ""))
     return name, sym
 
 

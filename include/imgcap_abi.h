@@ -137,16 +137,20 @@ int imgcap_mx_quant_rows(int dtype, int R, int K, const void* x, int64_t ldx, co
 enum { IMGCAP_GEMM_SKINNY = 1, IMGCAP_GEMM_TILED64 = 2, IMGCAP_GEMM_TILED128 = 3, IMGCAP_GEMM_GLDS = 4,
        IMGCAP_GEMM_GLDS256 = 5, IMGCAP_GEMM_GLDS64 = 6, IMGCAP_GEMM_GLDS128X64 = 7,
        /* stream-tile kernel (persistent, epilogue from registers, bf16 C): 256x128, 128x256, 128x128,
-        * 128x192 tiles of 8 waves */
-       IMGCAP_GEMM_PT = 8, IMGCAP_GEMM_PT128X256 = 9, IMGCAP_GEMM_PT128 = 10, IMGCAP_GEMM_PT128X192 = 11 };
+        * 128x192 tiles of 8 waves; 128x128 of 4 waves, two blocks a CU; 128x128 of 8 waves with
+        * 128-deep k-steps */
+       IMGCAP_GEMM_PT = 8, IMGCAP_GEMM_PT128X256 = 9, IMGCAP_GEMM_PT128 = 10, IMGCAP_GEMM_PT128X192 = 11,
+       IMGCAP_GEMM_PT128X2 = 12, IMGCAP_GEMM_PT128K = 13 };
 int imgcap_gemm_plan(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda, int64_t ldb,
                      int batch, int split_k, int* splits);
 /* The same, knowing the call's epilogue (the persistent-tile kernel serves bf16 outputs only). */
 int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda, int64_t ldb,
                         int batch, const imgcap_epilogue* epi, int* splits);
-/* Stream-tile GEMM policy: -1 by shape (the library default), 0 never, 1 wherever eligible (tile by
- * the cost model), 2..5 wherever eligible with tile 256x128 / 128x256 / 128x128 / 128x192 (A/B
- * measurements; a tile not built for the call's epilogue form falls back to the cost model). */
+/* Stream-tile GEMM policy: -1 by shape (the library default: the encoder's large forward pointwise
+ * products, where a step census measured it ahead of the LDS-staged tiles), 0 never, 1 wherever
+ * eligible (tile by the cost model), 2..7 wherever eligible with config 1..6 (IMGCAP_GEMM_PT ..
+ * IMGCAP_GEMM_PT128K; a config not built for the call's epilogue form or K falls back to the cost
+ * model). */
 int imgcap_gemm_set_pt(int mode);
 /* Kernel-selection policy for A/B tests and benchmarks: glds256 >= 1 serves every eligible
  * GEMM (bf16, unsplit, 16-byte operand pitches) with the 256x256 tile (1: 64-deep k-steps x 2
@@ -215,11 +219,6 @@ int imgcap_dwconv7(int dtype, int B, int H, int W, int C, const void* x, const f
 int imgcap_dwconv7_ln(int dtype, int B, int H, int W, int C, const void* x, const float* w,
                       const float* bias, const float* ln_w, const float* ln_b, void* out,
                       void* stream);
-/* The same (bf16 x, W = 7 / 14, C % 128 == 0, C <= 1024) with the normalised rows written as
- * MX-FP8 -- q [B*H*W][C] e4m3fn bytes, s [B*H*W][C/32] E8M0 scales, the block encoding of
- * imgcap_mx_quant_rows -- for the frozen MX-FP8 CNBlocks (config C5): no bf16 round trip. */
-int imgcap_dwconv7_ln_mx(int B, int H, int W, int C, const void* x, const float* w, const float* bias,
-                         const float* ln_w, const float* ln_b, uint8_t* q, uint8_t* s, void* stream);
 /* features[2,4,6] head: LayerNorm2d(C) then gather 2x2/s2 patches into rows
  * out[B*(H/2)*(W/2)][4C] ordered (kh, kw, c) (weights repacked to match; cmajor = 0) or
  * (c, kh, kw) (cmajor = 1: the torch Conv2d weight [2C][C][2][2] is the GEMM operand as is). */

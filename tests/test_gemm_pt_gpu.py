@@ -1,7 +1,7 @@
 """Stream-tile GEMM (csrc/gemm_pt.h): every operand layout, tile config and epilogue form
 against a PyTorch fp32 reference on the bf16-rounded operands, and against the LDS-staged kernels
 (imgcap_gemm_set_pt(0)) on the same call.  Ragged M / N (rows and columns past the last tile), K
-tails (K % 64 != 0), grids with more tiles than CUs (persistent rounds, the cross-tile prefetch)
+tails (K % 64 != 0; the 128-deep k-step config takes only K % 128 == 0 and passes the rest on), grids with more tiles than CUs (persistent rounds, the cross-tile prefetch)
 and fewer."""
 import pytest
 import torch
@@ -41,7 +41,7 @@ LAYOUTS = [(False, True), (False, False), (True, True), (True, False)]
 
 @pytest.mark.parametrize("M,N,Kd", SHAPES)
 @pytest.mark.parametrize("ta,tb", LAYOUTS)
-@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5, 6, 7])
 def test_pt_plain_matches_fp32(hip_device, M, N, Kd, ta, tb, cfg):
     from imagecaptioningconvnext_amd import kernels as K
     a, b, ref = _operands(hip_device, M, N, Kd, ta, tb, 1)
@@ -55,7 +55,7 @@ def test_pt_plain_matches_fp32(hip_device, M, N, Kd, ta, tb, cfg):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("form", ["gelu_aux", "res_scales", "dgelu_beta", "relu_alpha", "dropout"])
 def test_pt_epilogues_match_fp32_and_lds_kernels(hip_device, cfg, form):
     from imagecaptioningconvnext_amd import kernels as K
@@ -126,9 +126,10 @@ def test_pt_persistent_rounds_and_xcd_slots(hip_device):
     """More tiles than CUs (several tiles per block, the next tile's k-steps prefetched under the
     epilogue), a K of one k-step, and a K tail inside the prefetch window."""
     from imagecaptioningconvnext_amd import kernels as K
-    for (M, N, Kd) in [(12544, 384, 1536), (6272, 1536, 64), (3328, 2048, 72), (7000, 600, 136)]:
+    # (3136, 520, 768): 100 - 125 tiles, a grid that is no multiple of the 8 XCDs
+    for (M, N, Kd) in [(12544, 384, 1536), (6272, 1536, 64), (3328, 2048, 72), (7000, 600, 136), (3136, 520, 768)]:
         a, b, ref = _operands(hip_device, M, N, Kd, False, True, 11)
-        for cfg in (2, 3, 4, 5):
+        for cfg in (2, 3, 4, 5, 6, 7):
             K.gemm_set_pt(cfg)
             try:
                 out = K.gemm(a, b, trans_b=True)

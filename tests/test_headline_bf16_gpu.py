@@ -7,10 +7,16 @@ batch 2 is encoded beside it).  The reference's step (train.py:262-291: packed C
 clamp +-5, Adam) is the oracle's fp32 restatement on the same weights and batch.  Dropout is 0
 here (the oracle cannot draw the HIP kernels' counter-based masks; dropout has its own tests).
 
-Tolerances (bf16 activations and weights against fp32): loss 1e-2 relative, top-5 within 0.5
-points, every gradient tensor within 3e-2 relative (norm), and Adam's first step (which moves an
-entry by ~lr * sign(g)) in the oracle's direction wherever the two gradients agree in sign with
-margin.  The encoder is a pass-through (the batch is encoder features), as in
+Tolerances (bf16 activations against fp32; the oracle multiplies the engine's bf16 weight copies):
+loss 1e-2 relative, top-5 within 0.5 points, every gradient tensor within 3e-2 relative (norm) --
+except the FFN's first Linear (linear1.weight / .bias), 8e-2: its gradient passes the ReLU mask of
+a hidden pre-activation the engine computes in bf16, and the ~0.3 % of hidden units that lie within
+bf16 rounding of zero flip; each flipped unit contributes a full-size term, so the relative error
+is ~sqrt(0.003) = 5-6 % (measured 0.055-0.061, layers 2-4) with everything else under 3e-2.  The
+same step in fp32 (third case) holds every tensor, linear1 included, to 1e-2: the engine's
+arithmetic is exact, the bf16 gap is rounding.  Adam's first step (which moves an entry by
+~lr * sign(g)) is in the oracle's direction wherever the two gradients agree in sign with margin.
+The encoder is a pass-through (the batch is encoder features), as in
 tests/test_trainer_fullsize_gpu.py."""
 import pytest
 import torch
@@ -40,8 +46,8 @@ def _lengths(B, seed):
     return pool[torch.randint(0, len(pool), (B,), generator=g)].tolist()
 
 
-@pytest.mark.parametrize("B,E", [(64, 768), (32, 1024)])
-def test_bf16_pipelined_graph_step_vs_oracle(hip_device, B, E):
+@pytest.mark.parametrize("B,E,dt", [(64, 768, "bf16"), (32, 1024, "bf16"), (64, 768, "fp32")])
+def test_bf16_pipelined_graph_step_vs_oracle(hip_device, B, E, dt):
     from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder
     from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer
     dev = hip_device
@@ -52,13 +58,18 @@ def test_bf16_pipelined_graph_step_vs_oracle(hip_device, B, E):
     caps2, lens2 = make_captions(B, L, _lengths(B, 76), V, 77)
     dec = TransformerDecoder(embed_dim=D, decoder_dim=D, vocab_size=V, maxLen=L, device=dev, wordMap=None,
                              pretrained_embeddings_path=None, fine_tune_embeddings=True, dropout=0.0, encoder_dim=E,
-                             num_heads=H, num_layers=LAYERS, compute_dtype=torch.bfloat16)
+                             num_heads=H, num_layers=LAYERS,
+                             compute_dtype=torch.bfloat16 if dt == "bf16" else torch.float32)
     p["pos_encoding.pe"] = dec.pos_encoding.pe.clone()
     dec.load_state_dict(p)
     dec = dec.to(dev)
 
-    # oracle: the reference's step on batch 1 in fp32
-    pr = {k: v.clone().requires_grad_(k != "pos_encoding.pe") for k, v in p.items()}
+    # oracle: the reference's step on batch 1 in fp32, on the operands the bf16 engine multiplies
+    # (its bf16 weight copies and features; the fp32 masters are what Adam updates, below)
+    rb = lambda t: t.to(torch.bfloat16).float() if dt == "bf16" and t.is_floating_point() else t  # noqa: E731
+    pr = {k: (v if k == "pos_encoding.pe" else rb(v)).clone().requires_grad_(k != "pos_encoding.pe")
+          for k, v in p.items()}
+    feats1 = rb(feats1)
     pad = caps1 == 0
     preds, cs, dls = decoders.transformer_tf_forward(pr, feats1, caps1, lens1, pad, H, LAYERS)
     loss, scores, targets = train_step.transformer_loss(preds, cs, dls)
@@ -77,8 +88,14 @@ def test_bf16_pipelined_graph_step_vs_oracle(hip_device, B, E):
     assert abs(g_top5 - top5) <= 0.5, (g_top5, top5)
 
     # the batch-1 gradients the replay left in the flat buffer, per tensor
-    worst = max((_rel(tr.eng.fp.g(k), grads[k]), k) for k in grads)
-    assert worst[0] <= 3e-2, worst
+    errs = sorted(((_rel(tr.eng.fp.g(k), grads[k]), k) for k in grads), reverse=True)
+    if dt == "fp32":
+        assert errs[0][0] <= 1e-2, errs[:6]
+    else:
+        relu_gated = [e for e in errs if ".linear1." in e[1]]
+        assert max(e[0] for e in relu_gated) <= 8e-2, relu_gated[:4]
+        others = [e for e in errs if ".linear1." not in e[1]]
+        assert others[0][0] <= 3e-2, others[:6]
 
     # post-Adam parameters: Adam's first step moves an entry by lr * g / (|g| + eps)
     clip = train_step.clip_gradient(grads, 5.0)

@@ -1,70 +1,88 @@
-"""Every GEMM of one train step at a bench config, timed in isolation (GPU box):
-    python tools/gemm_census.py [C2|C3|C4|C5]
-Prints one line per call (shape, operand layout, epilogue, plan, us, TFLOP/s) sorted by time."""
+"""Every GEMM one training step issues, timed under each imgcap_gemm_set_pt mode (GPU box):
+    python tools/gemm_census.py [C3|C4|C2|C5] [reps]
+Runs one eager (ungraphed, unpipelined) step of the bench's configuration with kernels.gemm
+wrapped to record each call (operands, layout, epilogue), then replays every distinct call
+back-to-back in a HIP graph under each mode (PT_MODES env, default the LDS-staged plan 0, the
+stream-tile configs 4..7 and the by-shape plan -1).  Prints per call: count per step, layout,
+epilogue kind, µs per mode; and per mode the step's GEMM total (count-weighted) -- the number a
+plan change moves."""
 import os
 import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
 from tools.microbench import time_launch  # noqa: E402
-from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer  # noqa: E402
 
-cfgname = sys.argv[1] if len(sys.argv) > 1 else "C2"
-cfg = bench.CONFIGS[cfgname]
+cfg_name = sys.argv[1] if len(sys.argv) > 1 else "C3"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+MODES = [int(m) for m in os.environ.get("PT_MODES", "0 4 5 6 7 -1").split()]
 dev = torch.device("cuda:0")
+
+cfg = dict(bench.CONFIGS[cfg_name])
+torch.manual_seed(42)
 enc, dec = bench.build(cfg, dev)
-tr = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm", graph=False)
-batch = bench.synthetic_batch(cfg["batch"], 0, 0, dev)[:3]
-tr.step(*batch)
-rec = []
-K.record_gemms(rec)
-tr._fwd_bwd(*batch)
-K.record_gemms(None)
+from imagecaptioningconvnext_amd.train_step import TeacherForcedTrainer  # noqa: E402
+tr = TeacherForcedTrainer(enc, dec, lstm=cfg["decoder"] == "lstm", graph=False, pipeline=False)
+B = cfg["batch"]
+batch = bench.synthetic_batch(B, 0, 0, dev)
+tr.step(*batch[:3], max_caplen=batch[3])  # warm: workspaces, packs
 torch.cuda.synchronize()
-def torch_time(c, reps=20):
-    """hipBLASLt (torch.matmul) on the same shape / operand layout, bf16 out, no epilogue:
-    a calibration column only (the product never calls it)."""
-    M, N, Kd = c["M"], c["N"], c["K"]
-    a = torch.randn((M, Kd) if c["ak"] else (Kd, M), device=dev, dtype=torch.bfloat16)
-    b = torch.randn((N, Kd) if c["bk"] else (Kd, N), device=dev, dtype=torch.bfloat16)
-    aa = a if c["ak"] else a.t()
-    bb = b.t() if c["bk"] else b
-    out = torch.matmul(aa, bb)
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):  # warm hipBLASLt's heuristics / workspace outside the capture
-        for _ in range(3):
-            torch.matmul(aa, bb, out=out)
-    torch.cuda.current_stream().wait_stream(side)
-    g = torch.cuda.CUDAGraph()  # replayed, so the host launch cost (~18 us per eager call) is out
-    with torch.cuda.graph(g):
-        for _ in range(reps):
-            torch.matmul(aa, bb, out=out)
-    g.replay()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    g.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps * 1e-3
+
+orig = K.gemm
+calls = {}
 
 
-rows = []
-for c in rec:
-    kind, sp = K.gemm_plan(c["dtype"], c["ak"], c["bk"], c["M"], c["N"], c["K"], c["lda"], c["ldb"], 1, c["split_k"])
-    ep = c["keep"][-1]
-    t = time_launch(c["call"], reps=20, warm=2)
-    rows.append((t, c, kind, sp, ep, torch_time(c)))
-tot = sum(r[0] for r in rows)
-print(f"{cfgname}: {len(rows)} GEMM calls, {tot * 1e6:.1f} us in isolation")
-print(f"hipBLASLt (torch.matmul, same shapes, no epilogue): {sum(r[5] for r in rows) * 1e6:.1f} us")
-for t, c, kind, sp, ep, tt in sorted(rows, key=lambda r: -r[0]):
-    f = 2.0 * c["M"] * c["N"] * c["K"]
-    print(f"{t * 1e6:8.1f} us {f / t / 1e12:7.1f} TF  M={c['M']:6d} N={c['N']:5d} K={c['K']:5d} "
-          f"ak={c['ak']} bk={c['bk']} act={ep.act} c={'f32' if ep.c_dtype == 0 else 'bf16'} "
-          f"bias={int(bool(ep.bias))} res={int(bool(ep.res))} beta={ep.beta:g} kind={kind} split={sp} "
-          f"| blaslt {tt * 1e6:6.1f} us {f / tt / 1e12:6.1f} TF")
+def _key(a, b, kw):
+    ep = "+".join(sorted(k for k, v in kw.items() if v is not None and k not in ("out", "out_dtype")
+                         and not (k == "act" and v == K.ACT_NONE)))
+    return (tuple(a.shape), tuple(a.stride()), tuple(b.shape), tuple(b.stride()), kw.get("trans_a", False),
+            kw.get("trans_b", False), ep, kw.get("K"), kw.get("N"))
+
+
+def rec(a, b, **kw):
+    k = _key(a, b, kw)
+    if k in calls:
+        calls[k][2] += 1
+    else:
+        calls[k] = [a, b, 1, dict(kw)]
+    return orig(a, b, **kw)
+
+
+K.gemm = rec
+tr.step(*batch[:3], max_caplen=batch[3])
+torch.cuda.synchronize()
+K.gemm = orig
+tr.flush() if hasattr(tr, "flush") else None
+
+tot = {m: 0.0 for m in MODES}
+best_tot = 0.0
+print(f"{cfg_name}: {len(calls)} distinct GEMM calls, {sum(c[2] for c in calls.values())} per step", flush=True)
+print(f"{'M':>6s} {'N':>5s} {'K':>5s} {'ta':>2s}{'tb':>3s} {'n':>3s} {'epilogue':24s} | "
+      + " ".join(f"{m:>7d}" for m in MODES) + " | us", flush=True)
+for k, (a, b, n, kw) in sorted(calls.items(), key=lambda kv: -kv[1][2] * kv[1][0].numel() * kv[1][1].shape[0]):
+    ta, tb = kw.get("trans_a", False), kw.get("trans_b", False)
+    M = a.shape[1] if ta else a.shape[0]
+    Kd = a.shape[0] if ta else a.shape[1]
+    N = b.shape[0] if tb else b.shape[1]
+    if kw.get("N") is not None:
+        N = kw["N"]
+    kw2 = dict(kw)
+    if kw2.get("out") is None:  # one output for all replays (no allocation per launch)
+        kw2["out"] = orig(a, b, **kw)
+    row = []
+    for m in MODES:
+        K.gemm_set_pt(m)
+        try:
+            row.append(time_launch(lambda: orig(a, b, **kw2), reps=reps))
+        finally:
+            K.gemm_set_pt(0)
+    for m, t in zip(MODES, row):
+        tot[m] += n * t
+    best_tot += n * min(row)
+    print(f"{M:6d} {N:5d} {Kd:5d} {int(ta):2d}{int(tb):3d} {n:3d} {k[6][:24]:24s} | "
+          + " ".join(f"{t * 1e6:7.1f}" for t in row), flush=True)
+print("step GEMM total (us): " + "  ".join(f"mode {m}: {tot[m] * 1e6:.0f}" for m in MODES)
+      + f"  best-of: {best_tot * 1e6:.0f}", flush=True)

@@ -2,7 +2,7 @@
     python tools/pt_bench.py [reps]
 Each row: one shape (forward nn.Linear form unless marked), µs per launch (graph replay of
 back-to-back launches, random bf16 operands) for the LDS-staged plan (pt=0), the persistent
-kernel with each tile config (2: 256x128, 3: 128x256, 4: 128x128, 5: 128x192), its cost-model pick (1), and
+kernel with each tile config (2: 256x128, 3: 128x256, 4: 128x128, 5: 128x192), its cost-model pick (1) and 7: 128x128 with 128-deep k-steps, and
 torch.matmul (hipBLASLt, no epilogue: a calibration column only)."""
 import os
 import sys
@@ -16,6 +16,10 @@ from tools.microbench import time_launch  # noqa: E402
 dev = torch.device("cuda:0")
 bf = torch.bfloat16
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+# IMGCAP_GEMM_PT modes: 0 the LDS-staged plan, c + 1 stream-tile config c, 1 the cost-model pick (last)
+NAMES = {0: "old", 2: "256x128", 3: "128x256", 4: "128x128", 5: "128x192", 6: "128x128b2", 7: "128x128k",
+         8: "256x128w", 9: "256x256w", 10: "128x256w", 1: "auto"}
+MODES = [int(m) for m in os.environ.get("PT_MODES", "0 2 3 4 5 6 7 8 9 10 1").split()]
 
 SHAPES = [
     # C3 (Tiny, B=64) encoder
@@ -58,7 +62,7 @@ def case(name, M, N, Kd, form):
     elif form == "bias":
         kw = dict(bias=bias)
     row = []
-    for mode in (0, 2, 3, 4, 5, 6, 1):
+    for mode in MODES:
         K.gemm_set_pt(mode)
         try:
             t = time_launch(lambda: K.gemm(a, b, trans_b=True, out=out, **kw), reps=reps)
@@ -68,13 +72,13 @@ def case(name, M, N, Kd, form):
     tt = time_launch(lambda: torch.matmul(a, b.t()), reps=reps)
     f = 2.0 * M * N * Kd
     cells = " ".join(f"{t * 1e6:7.1f}" for t in row)
-    best = min(row[1:6])
+    best = min(row[1:-1])
     print(f"{name:18s} {M:6d} {N:5d} {Kd:5d} | {cells} | blaslt {tt * 1e6:7.1f} | "
           f"old {f / row[0] / 1e12:6.0f} TF  st-best {f / best / 1e12:6.0f} TF  st-auto {f / row[6] / 1e12:6.0f} TF "
           f"({row[0] / row[6]:.2f}x)", flush=True)
 
 
-print(f"{'shape':18s} {'M':>6s} {'N':>5s} {'K':>5s} | {'old':>7s} {'256x128':>7s} {'128x256':>7s} {'128x128':>7s} "
-      f"{'128x192':>7s} {'128x128x2':>9s} {'auto':>7s} | us", flush=True)
+print(f"{'shape':18s} {'M':>6s} {'N':>5s} {'K':>5s} | " + " ".join(f"{NAMES[m]:>7s}" for m in MODES) + " | us",
+      flush=True)
 for s in SHAPES:
     case(*s)
