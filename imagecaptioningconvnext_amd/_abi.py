@@ -80,6 +80,7 @@ _SIGS = {
                                  c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "imgcap_add_layernorm_bwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                  c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "imgcap_add_layernorm_bwd_blocks": [c_int],
     "imgcap_convnext_stem": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p],
     "imgcap_convnext_stem_u8": [c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 9,
@@ -124,6 +125,7 @@ _SIGS = {
     "imgcap_workspace_attach": [c_int, c_void_p, c_uint64],
     "imgcap_workspace_needed": [c_int, ctypes.POINTER(c_uint64)],
     "imgcap_colsum_multi": [c_int, c_void_p, c_void_p],
+    "imgcap_colsum_multi_part": [c_int, c_void_p, c_void_p, c_int64, c_void_p],
     "imgcap_gemm_grouped": [c_int, c_int, c_int, c_void_p, c_void_p],
     "imgcap_gemm_mx": [c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                        c_int64, ctypes.POINTER(Epilogue), c_void_p],

@@ -985,20 +985,20 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(int cols, int slices
 }
 
 // ---- many column sums in one launch (the bias gradients of a whole backward pass) ----------
-// Block = (item, 64-column group): 8 column vectors x 128 row lanes walk ALL rows of the item
-// (8 rows in flight per lane: 128 KB per block -- with 32 row lanes the grid of a 9490-wide
-// dlogits sum, 149 blocks, held too few bytes in flight to reach HBM rate), fixed-order LDS
-// reduction, out = beta*out + sum.
-constexpr int COLSUM_MAX_ITEMS = 64;
+// A block = (item, 64-column group), 256 threads = 32 row lanes x 8 column vectors: each lane
+// walks its rows with 8 rows' 16-byte loads in flight per trip, then a fixed-order LDS sum over
+// the row lanes: out = beta*out + sum (deterministic, no library scratch -- the LSTM engine runs
+// these sums on a side stream beside scratch users).  The round-4 kernel (1024-thread blocks,
+// 128 row lanes) spilled its fp32 path to scratch memory and took ~250 us for C3's bias sums.
+constexpr int COLSUM_MAX_ITEMS = 48;
 struct ColsumBatch {
   int n;
   int first_block[COLSUM_MAX_ITEMS + 1];
   imgcap_colsum_item it[COLSUM_MAX_ITEMS];
 };
 
-constexpr int COLSUM_RL = 128;  // row lanes per block
-__global__ __launch_bounds__(1024) void colsum_multi_kernel(ColsumBatch b) {
-  __shared__ float red[COLSUM_RL][65];
+__global__ __launch_bounds__(256) void colsum_multi_kernel(ColsumBatch b) {
+  __shared__ float red[32][65];
   int k = 0;
   while (k + 1 < b.n && (int)blockIdx.x >= b.first_block[k + 1]) ++k;
   const imgcap_colsum_item& item = b.it[k];
@@ -1006,6 +1006,8 @@ __global__ __launch_bounds__(1024) void colsum_multi_kernel(ColsumBatch b) {
   const int cv = threadIdx.x & 7, rl = threadIdx.x >> 3;
   const int c0 = cg * 64 + cv * 8;
   const bool vec = item.vec_ok && c0 + 8 <= item.cols;
+  const int rows = item.rows;
+  const long ld = item.ld;
   float s[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = 0.f;
@@ -1013,51 +1015,53 @@ __global__ __launch_bounds__(1024) void colsum_multi_kernel(ColsumBatch b) {
     constexpr int U = 8;  // rows in flight per lane
     int r = rl;
     if (item.dtype == IMGCAP_BF16) {
-      const bf16* x = (const bf16*)item.x;
-      for (; vec && r + COLSUM_RL * (U - 1) < item.rows; r += COLSUM_RL * U) {
-        bf16x8 v[U];
+      const bf16* x = (const bf16*)item.x + c0;
+      if (vec) {
+        for (; r + 32 * (U - 1) < rows; r += 32 * U) {
+          bf16x8 v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = *(const bf16x8*)(x + (long)(r + COLSUM_RL * u) * item.ld + c0);
+          for (int u = 0; u < U; ++u) v[u] = *(const bf16x8*)(x + (long)(r + 32 * u) * ld);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+          for (int u = 0; u < U; ++u)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) s[j] += (float)v[u][j];
-      }
-      for (; r < item.rows; r += COLSUM_RL) {  // tail rows: one vector per lane and row
-        if (vec) {
-          const bf16x8 v = *(const bf16x8*)(x + (long)r * item.ld + c0);
+            for (int j = 0; j < 8; ++j) s[j] += (float)v[u][j];
+        }
+        for (; r < rows; r += 32) {
+          const bf16x8 v = *(const bf16x8*)(x + (long)r * ld);
 #pragma unroll
           for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
-        } else {
+        }
+      } else {
+        for (; r < rows; r += 32)
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (c0 + j < item.cols) s[j] += (float)x[(long)r * item.ld + c0 + j];
-        }
+            if (c0 + j < item.cols) s[j] += (float)x[(long)r * ld + j];
       }
     } else {
-      const float* x = (const float*)item.x;
-      for (; vec && r + COLSUM_RL * (U - 1) < item.rows; r += COLSUM_RL * U) {
-        f32x4 v[U][2];
+      const float* x = (const float*)item.x + c0;
+      if (vec) {
+        for (; r + 32 * (U - 1) < rows; r += 32 * U) {
+          f32x4 v[U][2];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          v[u][0] = *(const f32x4*)(x + (long)(r + COLSUM_RL * u) * item.ld + c0);
-          v[u][1] = *(const f32x4*)(x + (long)(r + COLSUM_RL * u) * item.ld + c0 + 4);
+          for (int u = 0; u < U; ++u) {
+            v[u][0] = *(const f32x4*)(x + (long)(r + 32 * u) * ld);
+            v[u][1] = *(const f32x4*)(x + (long)(r + 32 * u) * ld + 4);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { s[j] += v[u][0][j]; s[j + 4] += v[u][1][j]; }
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { s[j] += v[u][0][j]; s[j + 4] += v[u][1][j]; }
-      }
-      for (; r < item.rows; r += COLSUM_RL) {
-        if (vec) {
-          const f32x4 v0 = *(const f32x4*)(x + (long)r * item.ld + c0), v1 = *(const f32x4*)(x + (long)r * item.ld + c0 + 4);
+        for (; r < rows; r += 32) {
+          const f32x4 v0 = *(const f32x4*)(x + (long)r * ld), v1 = *(const f32x4*)(x + (long)r * ld + 4);
 #pragma unroll
           for (int j = 0; j < 4; ++j) { s[j] += v0[j]; s[j + 4] += v1[j]; }
-        } else {
+        }
+      } else {
+        for (; r < rows; r += 32)
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (c0 + j < item.cols) s[j] += x[(long)r * item.ld + c0 + j];
-        }
+            if (c0 + j < item.cols) s[j] += x[(long)r * ld + j];
       }
     }
   }
@@ -1067,9 +1071,110 @@ __global__ __launch_bounds__(1024) void colsum_multi_kernel(ColsumBatch b) {
   if (threadIdx.x < 64) {
     const int c = cg * 64 + threadIdx.x;
     float t = 0.f;
-    for (int i = 0; i < COLSUM_RL; ++i) t += red[i][threadIdx.x];
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) t += red[i][threadIdx.x];
     if (c < item.cols) item.out[c] = (item.beta != 0.f ? item.beta * item.out[c] : 0.f) + t;
   }
+}
+
+// Two-pass form with caller-owned scratch (imgcap_colsum_multi_part): phase 1 blocks = (item,
+// 64-column group, 256-row chunk), every load of a block in flight at once, partial sums to
+// part[chunk][cols]; phase 2 adds an item's chunk partials in order.  Thousands of one-trip
+// blocks instead of ~900 blocks walking up to 3,328 rows each.
+constexpr int COLSUM_RC = 256;
+struct ColsumBatch2 {
+  int n;
+  int first_block[COLSUM_MAX_ITEMS + 1];
+  int first_col[COLSUM_MAX_ITEMS + 1];
+  long part_off[COLSUM_MAX_ITEMS];
+  imgcap_colsum_item it[COLSUM_MAX_ITEMS];
+  float* part;
+};
+
+__global__ __launch_bounds__(256) void colsum_part_kernel(ColsumBatch2 b) {
+  __shared__ float red[32][65];
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.first_block[k + 1]) ++k;
+  const imgcap_colsum_item& item = b.it[k];
+  const int ngrp = (item.cols + 63) / 64;
+  const int lb = blockIdx.x - b.first_block[k];
+  const int cg = lb % ngrp, ch = lb / ngrp;
+  const int cv = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = cg * 64 + cv * 8;
+  const int r0 = ch * COLSUM_RC + rl;
+  const int rend = min(item.rows, (ch + 1) * COLSUM_RC);
+  const bool vec = item.vec_ok && c0 + 8 <= item.cols;
+  const long ld = item.ld;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (c0 < item.cols) {
+    constexpr int U = COLSUM_RC / 32;  // rows per lane, all in flight
+    if (item.dtype == IMGCAP_BF16) {
+      const bf16* x = (const bf16*)item.x + c0;
+      if (vec) {
+        bf16x8 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int r = r0 + 32 * u;
+          v[u] = r < rend ? *(const bf16x8*)(x + (long)r * ld) : bf16x8{};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += (float)v[u][j];
+      } else {
+        for (int r = r0; r < rend; r += 32)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (c0 + j < item.cols) s[j] += (float)x[(long)r * ld + j];
+      }
+    } else {
+      const float* x = (const float*)item.x + c0;
+      if (vec) {
+        f32x4 v[U][2];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int r = r0 + 32 * u;
+          v[u][0] = r < rend ? *(const f32x4*)(x + (long)r * ld) : f32x4{};
+          v[u][1] = r < rend ? *(const f32x4*)(x + (long)r * ld + 4) : f32x4{};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { s[j] += v[u][0][j]; s[j + 4] += v[u][1][j]; }
+      } else {
+        for (int r = r0; r < rend; r += 32)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (c0 + j < item.cols) s[j] += x[(long)r * ld + j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cv * 8 + j] = s[j];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = cg * 64 + threadIdx.x;
+    float t = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) t += red[i][threadIdx.x];
+    if (c < item.cols) b.part[b.part_off[k] + (long)ch * item.cols + c] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_fin_kernel(ColsumBatch2 b) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= b.first_col[b.n]) return;
+  int k = 0;
+  while (k + 1 < b.n && g >= b.first_col[k + 1]) ++k;
+  const imgcap_colsum_item& item = b.it[k];
+  const int c = g - b.first_col[k];
+  const int nch = (item.rows + COLSUM_RC - 1) / COLSUM_RC;
+  const float* p = b.part + b.part_off[k] + c;
+  float t = 0.f;
+  for (int i = 0; i < nch; ++i) t += p[(long)i * item.cols];
+  item.out[c] = (item.beta != 0.f ? item.beta * item.out[c] : 0.f) + t;
 }
 
 // out[c][r] = in[r][c] (2-D transpose through an LDS tile; weights -> k-major copies)
@@ -1215,12 +1320,13 @@ extern "C" int imgcap_debug_stamps(void* p) {
 #endif
 
 extern "C" int imgcap_colsum_multi(int n, const imgcap_colsum_item* items, void* stream) {
-  IMGCAP_REQUIRE(n >= 0 && n <= COLSUM_MAX_ITEMS, "imgcap_colsum_multi: at most 64 items per call");
+  IMGCAP_REQUIRE(n >= 0 && n <= COLSUM_MAX_ITEMS, "imgcap_colsum_multi: at most 48 items per call");
   if (n == 0) return 0;
   ColsumBatch b{};
   b.n = n;
   int blocks = 0;
   for (int i = 0; i < n; ++i) {
+    IMGCAP_REQUIRE(items[i].rows >= 0 && items[i].cols >= 0, "imgcap_colsum_multi: negative extent");
     b.it[i] = items[i];
     b.it[i].vec_ok = aligned16(items[i].x) && (items[i].dtype == IMGCAP_BF16 ? items[i].ld % 8 == 0
                                                                                : items[i].ld % 4 == 0);
@@ -1229,8 +1335,41 @@ extern "C" int imgcap_colsum_multi(int n, const imgcap_colsum_item* items, void*
   }
   b.first_block[n] = blocks;
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL(colsum_multi_kernel, dim3(blocks), dim3(COLSUM_RL * 8), 0, (hipStream_t)stream, b);
+  hipLaunchKernelGGL(colsum_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
   IMGCAP_CHECK_LAUNCH("imgcap_colsum_multi");
+  return 0;
+}
+
+extern "C" int imgcap_colsum_multi_part(int n, const imgcap_colsum_item* items, float* part, int64_t part_floats,
+                                        void* stream) {
+  IMGCAP_REQUIRE(n >= 0 && n <= COLSUM_MAX_ITEMS, "imgcap_colsum_multi_part: at most 48 items per call");
+  if (n == 0) return 0;
+  ColsumBatch2 b{};
+  b.n = n;
+  int blocks = 0, cols = 0;
+  long off = 0;
+  for (int i = 0; i < n; ++i) {
+    IMGCAP_REQUIRE(items[i].rows >= 0 && items[i].cols >= 0, "imgcap_colsum_multi_part: negative extent");
+    b.it[i] = items[i];
+    b.it[i].vec_ok = aligned16(items[i].x) && (items[i].dtype == IMGCAP_BF16 ? items[i].ld % 8 == 0
+                                                                               : items[i].ld % 4 == 0);
+    b.first_block[i] = blocks;
+    b.first_col[i] = cols;
+    b.part_off[i] = off;
+    const int nch = (items[i].rows + COLSUM_RC - 1) / COLSUM_RC;
+    blocks += ((items[i].cols + 63) / 64) * nch;
+    cols += items[i].cols;
+    off += (long)nch * items[i].cols;
+  }
+  b.first_block[n] = blocks;
+  b.first_col[n] = cols;
+  IMGCAP_REQUIRE(off <= part_floats && (off == 0 || part), "imgcap_colsum_multi_part: partials buffer too small");
+  if (cols == 0) return 0;
+  b.part = part;
+  hipStream_t st = (hipStream_t)stream;
+  if (blocks > 0) hipLaunchKernelGGL(colsum_part_kernel, dim3(blocks), dim3(256), 0, st, b);
+  hipLaunchKernelGGL(colsum_fin_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, b);
+  IMGCAP_CHECK_LAUNCH("imgcap_colsum_multi_part");
   return 0;
 }
 

@@ -351,6 +351,271 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(imgcap_mha_desc d, const u
   }
 }
 
+// ---- bf16: natural row images, transposed operands read by ds_read_b64_tr_b16 ----------------
+// Every head slice sits in LDS as it is in memory, [64 rows][64 columns] (128-byte rows), its
+// 16-byte slots XOR-swizzled by row bits 1 and 3: both operand reads are then conflict-free
+// (k-contiguous fragments by ds_read_b128: 4 LDS cycles a wave-instruction; fragments whose k
+// runs down the image by ds_read_b64_tr_b16: 2).  No transposed copies (the round-4 kernels
+// built 1 (fwd) / 3 (bwd) by 2-byte element moves at 2.4-3 conflict cycles per LDS instruction)
+// and one (fwd) / two (bwd) barriers.  MFMAs run as D^T = B^T A^T, so a lane ends with one row
+// and 4 consecutive columns: softmax row sums over 4 lanes, 8-byte stores of P / dS / outputs.
+typedef short mi_v4s16 __attribute__((ext_vector_type(4)));
+typedef short mi_v8s16 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) mi_v4s16 mi_lds_v4s16;
+constexpr int MI_IMG = LP * HD * 2;  // bytes of one image
+
+DEV int mi_swz(int r) { return (((r >> 1) & 1) * 2) ^ (((r >> 3) & 1) * 4); }
+DEV int mi_off(int r, int c) { return r * 128 + (((c >> 3) ^ mi_swz(r)) << 4) + ((c & 7) << 1); }
+
+// operand rows row0 + (lane & 15), k = 32 kk + 8 (lane >> 4) + 0..7, from an image whose rows are
+// the operand's rows
+DEV bf16x8 mi_frag_k(const char* img, int row0, int kk, int lane) {
+  const int r = row0 + (lane & 15);
+  return *(const bf16x8*)(img + r * 128 + (((4 * kk + (lane >> 4)) ^ mi_swz(r)) << 4));
+}
+// the same fragment from an image whose COLUMNS are the operand's rows (k down the image): lane
+// 4q+p of a 16-lane group reads 4 columns of image row 8g+q (+4), the hardware transpose hands
+// lane i column col0 + i
+DEV bf16x8 mi_frag_t(const char* img, int col0, int kk, int lane) {
+  const int fr = lane & 15, g = lane >> 4;
+  const int kr = kk * 32 + 8 * g + (fr >> 2), col = col0 + 4 * (fr & 3);
+  const mi_v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mi_lds_v4s16*)(img + mi_off(kr, col)));
+  const mi_v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mi_lds_v4s16*)(img + mi_off(kr + 4, col)));
+  const mi_v8s16 all = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, all);
+}
+DEV void mi_store(char* img, const RowVecs<bf16>& rv) {
+#pragma unroll
+  for (int i = 0; i < RowVecs<bf16>::PER; ++i) {
+    const int e = threadIdx.x + i * 256, r = e >> 3;
+    *(uint4*)(img + r * 128 + (((e & 7) ^ mi_swz(r)) << 4)) = rv.v[i];
+  }
+}
+// D^T[xrows][yrows] over k = 0..63: acc[cb] = sum_k X[16 cb + ..][k] Y[y0 + ..][k] for the 4
+// 16-row blocks of X (both given as fragment readers)
+#define MI_MM(acc, XFRAG, YFRAG)                                                   \
+  do {                                                                             \
+    _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) acc[j_] = f32x4{0.f, 0.f, 0.f, 0.f}; \
+    _Pragma("unroll") for (int kk_ = 0; kk_ < 2; ++kk_) {                          \
+      const bf16x8 y_ = YFRAG(kk_);                                                \
+      _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_)                             \
+        acc[j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(XFRAG(j_, kk_), y_, acc[j_], 0, 0, 0); \
+    }                                                                              \
+  } while (0)
+DEV uint2 mi_pack4(float a, float b, float c, float e) {
+  const bf16x2 lo = {(bf16)a, (bf16)b}, hi = {(bf16)c, (bf16)e};
+  return make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+}
+DEV float mi_row_max(float v) { return fmaxf(fmaxf(v, __shfl_xor(v, 16, 64)), fmaxf(__shfl_xor(v, 32, 64), __shfl_xor(v, 48, 64))); }
+DEV float mi_row_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+__global__ __launch_bounds__(256) void mha_fwd_bf16_kernel(imgcap_mha_desc d, const uint64_t* seed_ctr) {
+  if (d.drop_p > 0.f) d.seed = eff_seed(d.seed, seed_ctr);
+  __shared__ __attribute__((aligned(16))) char sm[4 * MI_IMG];
+  __shared__ unsigned char kpad[LP];
+  char* Qs = sm;
+  char* Ks = sm + MI_IMG;
+  char* Vs = sm + 2 * MI_IMG;
+  char* Ps = sm + 3 * MI_IMG;
+  const int bh = blockIdx.x, b = bh / d.H, h = bh % d.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  const long kvr = d.kv_rows ? d.kv_rows : d.Lk;
+  const bf16* q = (const bf16*)d.q + (long)b * d.Lq * d.ldq + h * HD;
+  const bf16* k = (const bf16*)d.k + (long)b * kvr * d.ldk + h * HD;
+  const bf16* v = (const bf16*)d.v + (long)b * kvr * d.ldv + h * HD;
+  {
+    RowVecs<bf16> qv, kv, vv;
+    load_rows<bf16>(qv, q, d.ldq, d.Lq);
+    load_rows<bf16>(kv, k, d.ldk, d.Lk);
+    load_rows<bf16>(vv, v, d.ldv, d.Lk);
+    const unsigned char kp = threadIdx.x < LP ? key_pad_flag(d, b, threadIdx.x) : 0;
+    mi_store(Qs, qv);
+    mi_store(Ks, kv);
+    mi_store(Vs, vv);
+    if (threadIdx.x < LP) kpad[threadIdx.x] = kp;
+  }
+  __syncthreads();
+  const int row0 = 16 * w, i = row0 + fr;  // this lane's query row; keys j = 16 jb + 4 fq + r
+  f32x4 s[4];
+#define XK(jb, kk) mi_frag_k(Ks, 16 * (jb), kk, lane)
+#define YQ(kk) mi_frag_k(Qs, row0, kk, lane)
+  MI_MM(s, XK, YQ);
+#undef XK
+#undef YQ
+  float m = -INFINITY;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jb + 4 * fq + r;
+      const float x = key_masked(d, kpad, i, j) ? -INFINITY : s[jb][r] * d.scale;
+      s[jb][r] = x;
+      m = fmaxf(m, x);
+    }
+  m = mi_row_max(m);
+  if (m == -INFINITY) m = 0.f;
+  float sum = 0.f;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = __expf(s[jb][r] - m);
+      s[jb][r] = e;
+      sum += e;
+    }
+  sum = mi_row_sum(sum);
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;
+  const float lse = m + logf(sum > 0.f ? sum : 1.f);
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jb + 4 * fq + r;
+      float pv = s[jb][r] * inv;
+      if (d.drop_p > 0.f && i < d.Lq && j < d.Lk)
+        pv *= dropout_scale(d.seed, d.drop_stream, (((uint64_t)bh * d.Lq + i) * d.Lk + j), d.drop_p);
+      s[jb][r] = pv;
+      if (d.probs && i < d.Lq && j < d.Lk) d.probs[((long)bh * d.Lq + i) * d.Lk + j] = pv;
+    }
+    *(uint2*)(Ps + mi_off(i, 16 * jb + 4 * fq)) = mi_pack4(s[jb][0], s[jb][1], s[jb][2], s[jb][3]);
+  }
+  // a wave reads back only its own 16 rows of P~: LDS operations of one wave complete in order
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  f32x4 o[4];
+#define XV(cb, kk) mi_frag_t(Vs, 16 * (cb), kk, lane)
+#define YP(kk) mi_frag_k(Ps, row0, kk, lane)
+  MI_MM(o, XV, YP);
+#undef XV
+#undef YP
+  if (i < d.Lq) {
+    bf16* out = (bf16*)d.o + ((long)b * d.Lq + i) * d.ldo + h * HD;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) *(uint2*)(out + 16 * cb + 4 * fq) = mi_pack4(o[cb][0], o[cb][1], o[cb][2], o[cb][3]);
+    if (fq == 0) d.lse[(long)bh * d.Lq + i] = lse;
+  }
+}
+
+__global__ __launch_bounds__(256) void mha_bwd_bf16_kernel(imgcap_mha_desc d, const uint64_t* seed_ctr) {
+  if (d.drop_p > 0.f) d.seed = eff_seed(d.seed, seed_ctr);
+  __shared__ __attribute__((aligned(16))) char sm[6 * MI_IMG];
+  __shared__ unsigned char kpad[LP];
+  char* Qs = sm;
+  char* Ks = sm + MI_IMG;
+  char* Vs = sm + 2 * MI_IMG;
+  char* dOs = sm + 3 * MI_IMG;
+  char* Pt = sm + 4 * MI_IMG;   // P~ (dropped-out probabilities)
+  char* dSs = sm + 5 * MI_IMG;  // dS (unscaled)
+  const int bh = blockIdx.x, b = bh / d.H, h = bh % d.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  const bf16* q = (const bf16*)d.q + (long)b * d.Lq * d.ldq + h * HD;
+  const bf16* k = (const bf16*)d.k + (long)b * d.Lk * d.ldk + h * HD;
+  const bf16* v = (const bf16*)d.v + (long)b * d.Lk * d.ldv + h * HD;
+  const bf16* dO = (const bf16*)d.dout + (long)b * d.Lq * d.lddo + h * HD;
+  const int row0 = 16 * w, i = row0 + fr;  // query row of the S / dP phase
+  float lse;
+  {
+    RowVecs<bf16> qv, kv, vv, ov;
+    load_rows<bf16>(qv, q, d.ldq, d.Lq);
+    load_rows<bf16>(kv, k, d.ldk, d.Lk);
+    load_rows<bf16>(vv, v, d.ldv, d.Lk);
+    load_rows<bf16>(ov, dO, d.lddo, d.Lq);
+    const unsigned char kp = threadIdx.x < LP ? key_pad_flag(d, b, threadIdx.x) : 0;
+    lse = i < d.Lq ? d.lse[(long)bh * d.Lq + i] : 0.f;
+    mi_store(Qs, qv);
+    mi_store(Ks, kv);
+    mi_store(Vs, vv);
+    mi_store(dOs, ov);
+    if (threadIdx.x < LP) kpad[threadIdx.x] = kp;
+  }
+  __syncthreads();
+  f32x4 p[4], dp[4];
+#define XK(jb, kk) mi_frag_k(Ks, 16 * (jb), kk, lane)
+#define XV(jb, kk) mi_frag_k(Vs, 16 * (jb), kk, lane)
+#define YQ(kk) mi_frag_k(Qs, row0, kk, lane)
+#define YO(kk) mi_frag_k(dOs, row0, kk, lane)
+  MI_MM(p, XK, YQ);   // S
+  MI_MM(dp, XV, YO);  // dP~ = dO V^T
+#undef XK
+#undef XV
+#undef YQ
+#undef YO
+  // P from the saved lse; P~ = P * mask; dP = dP~ * mask; dS = P (dP - rowsum(P dP))
+  float ms[4][4];
+  float dot = 0.f;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jb + 4 * fq + r;
+      const bool masked = i >= d.Lq || key_masked(d, kpad, i, j);
+      const float pr = masked ? 0.f : __expf(p[jb][r] * d.scale - lse);
+      ms[jb][r] = (d.drop_p > 0.f && !masked)
+                      ? dropout_scale(d.seed, d.drop_stream, (((uint64_t)bh * d.Lq + i) * d.Lk + j), d.drop_p)
+                      : 1.f;
+      const float dpv = dp[jb][r] * ms[jb][r];
+      dot += pr * dpv;
+      p[jb][r] = pr;
+      dp[jb][r] = dpv;
+    }
+  dot = mi_row_sum(dot);
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+    float ds[4], pt[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ds[r] = p[jb][r] * (dp[jb][r] - dot);
+      pt[r] = p[jb][r] * ms[jb][r];
+    }
+    *(uint2*)(Pt + mi_off(i, 16 * jb + 4 * fq)) = mi_pack4(pt[0], pt[1], pt[2], pt[3]);
+    *(uint2*)(dSs + mi_off(i, 16 * jb + 4 * fq)) = mi_pack4(ds[0], ds[1], ds[2], ds[3]);
+  }
+  __syncthreads();  // dV / dK sum over every wave's query rows
+  const int j = row0 + fr;  // key row of the dV / dK phase
+  f32x4 acc[4];
+  // dV[j][c] = sum_i P~[i][j] dO[i][c]
+#define XO(cb, kk) mi_frag_t(dOs, 16 * (cb), kk, lane)
+#define YP(kk) mi_frag_t(Pt, row0, kk, lane)
+  MI_MM(acc, XO, YP);
+#undef XO
+#undef YP
+  if (j < d.Lk) {
+    bf16* dv = (bf16*)d.dv + ((long)b * d.Lk + j) * d.lddv + h * HD;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) *(uint2*)(dv + 16 * cb + 4 * fq) = mi_pack4(acc[cb][0], acc[cb][1], acc[cb][2], acc[cb][3]);
+  }
+  // dK[j][c] = scale sum_i dS[i][j] Q[i][c]
+#define XQ(cb, kk) mi_frag_t(Qs, 16 * (cb), kk, lane)
+#define YS(kk) mi_frag_t(dSs, row0, kk, lane)
+  MI_MM(acc, XQ, YS);
+#undef XQ
+#undef YS
+  if (j < d.Lk) {
+    bf16* dk = (bf16*)d.dk + ((long)b * d.Lk + j) * d.lddk + h * HD;
+    const float sc = d.scale;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      *(uint2*)(dk + 16 * cb + 4 * fq) = mi_pack4(acc[cb][0] * sc, acc[cb][1] * sc, acc[cb][2] * sc, acc[cb][3] * sc);
+  }
+  // dQ[i][c] = scale sum_j dS[i][j] K[j][c]
+#define XKT(cb, kk) mi_frag_t(Ks, 16 * (cb), kk, lane)
+#define YS(kk) mi_frag_k(dSs, row0, kk, lane)
+  MI_MM(acc, XKT, YS);
+#undef XKT
+#undef YS
+  if (i < d.Lq) {
+    bf16* dq = (bf16*)d.dq + ((long)b * d.Lq + i) * d.lddq + h * HD;
+    const float sc = d.scale;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+      *(uint2*)(dq + 16 * cb + 4 * fq) = mi_pack4(acc[cb][0] * sc, acc[cb][1] * sc, acc[cb][2] * sc, acc[cb][3] * sc);
+  }
+}
+#undef MI_MM
+
 static int check(const imgcap_mha_desc* d) {
   IMGCAP_REQUIRE(d != nullptr, "mha desc NULL");
   IMGCAP_REQUIRE(d->dh == HD, "mha: head dim must be 64");
@@ -371,8 +636,7 @@ extern "C" int imgcap_mha_fwd(const imgcap_mha_desc* d, void* stream) {
   if (int rc = check(d)) return rc;
   const dim3 grid(d->B * d->H);
   if (d->dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(mha_fwd_kernel<bf16>, grid, dim3(256), 3 * Img<bf16>::ELEMS * sizeof(bf16),
-                       (hipStream_t)stream, *d, g_seed_ctr);
+    hipLaunchKernelGGL(mha_fwd_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, *d, g_seed_ctr);
   else
     hipLaunchKernelGGL(mha_fwd_kernel<float>, grid, dim3(256), 3 * Img<float>::ELEMS * sizeof(float),
                        (hipStream_t)stream, *d, g_seed_ctr);
@@ -394,8 +658,7 @@ extern "C" int imgcap_mha_bwd(const imgcap_mha_desc* d, void* stream) {
     attr_set = true;
   }
   if (d->dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL(mha_bwd_kernel<bf16>, grid, dim3(256), 6 * Img<bf16>::ELEMS * sizeof(bf16),
-                       (hipStream_t)stream, *d, g_seed_ctr);
+    hipLaunchKernelGGL(mha_bwd_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, *d, g_seed_ctr);
   else
     hipLaunchKernelGGL(mha_bwd_kernel<float>, grid, dim3(256), 6 * Img<float>::ELEMS * sizeof(float),
                        (hipStream_t)stream, *d, g_seed_ctr);

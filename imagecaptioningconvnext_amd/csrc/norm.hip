@@ -80,8 +80,7 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, con
                                                          const float* __restrict__ rstd_i, const float* __restrict__ g,
                                                          float p, uint64_t seed0, const uint64_t* seed_ctr,
                                                          uint32_t stream_id, T* __restrict__ dx, T* __restrict__ dr,
-                                                         float* __restrict__ ws, float* __restrict__ dyx,
-                                                         int rows_per_wave) {
+                                                         float* __restrict__ ws, int rows_per_wave) {
   constexpr int MAXJ = MAXC / (64 * G);
   __shared__ float part[2][4][MAXC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -115,12 +114,6 @@ __global__ __launch_bounds__(256) void add_ln_bwd_kernel(int rows, int cols, con
           lb[j][e] += dv[e];
           s1 += gdy[j][e];
           s2 += gdy[j][e] * xh[j][e];
-        }
-        if (dyx) {  // dy * xhat for a deferred dgamma column sum (imgcap_colsum_multi)
-          float q[G];
-#pragma unroll
-          for (int e = 0; e < G; ++e) q[e] = dv[e] * xh[j][e];
-          st_g<float, G>(dyx + idx, q);
         }
       }
     }
@@ -199,18 +192,26 @@ extern "C" int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const voi
   return 0;
 }
 
+// rows per wave and blocks of the LN backward: ~512 blocks of 4 waves
+static int lnb_rpw(int rows) { return std::max(1, (rows + 4 * 512 - 1) / (4 * 512)); }
+extern "C" int imgcap_add_layernorm_bwd_blocks(int rows) {
+  if (rows <= 0) return 0;
+  const int rpw = lnb_rpw(rows);
+  return (rows + 4 * rpw - 1) / (4 * rpw);
+}
+
 extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const void* dy, const void* s,
                                         const float* mean, const float* rstd, const float* gamma, float drop_p,
                                         uint64_t seed, uint32_t drop_stream, void* dx, void* dr, float* dgamma,
-                                        float* dbeta, float* dyx, void* stream) {
-  IMGCAP_REQUIRE(!dyx || (!dgamma && !dbeta), "imgcap_add_layernorm_bwd: dyx replaces dgamma/dbeta");
+                                        float* dbeta, float* part, void* stream) {
+  IMGCAP_REQUIRE(!part || (!dgamma && !dbeta), "imgcap_add_layernorm_bwd: part replaces dgamma/dbeta");
   IMGCAP_REQUIRE(cols > 0 && cols <= LN_MAXC, "imgcap_add_layernorm_bwd: cols must be in (0, 2048]");
   if (rows == 0) return 0;
-  const int rpw = std::max(1, (rows + 4 * 512 - 1) / (4 * 512));  // ~512 blocks of 4 waves
-  const int nblk = (rows + 4 * rpw - 1) / (4 * rpw);
+  const int rpw = lnb_rpw(rows);
+  const int nblk = imgcap_add_layernorm_bwd_blocks(rows);
   dim3 grid(nblk);
   hipStream_t st = (hipStream_t)stream;
-  float* ws = nullptr;
+  float* ws = part;  // the caller's [nblk][2][cols] partials (its deferred column sums), or ours
   if (dgamma || dbeta) {
     ws = (float*)workspace((size_t)nblk * 2 * cols * sizeof(float), st);
     if (!ws) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_add_layernorm_bwd: ") + last_error());
@@ -221,7 +222,7 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
   } while (0)
 #define LNB2_(T, G, MC)                                                                                         \
   hipLaunchKernelGGL((add_ln_bwd_kernel<T, G, MC>), grid, dim3(256), 0, st, rows, cols, (const T*)dy, (const T*)s,   \
-                     mean, rstd, gamma, drop_p, seed, g_seed_ctr, drop_stream, (T*)dx, (T*)dr, ws, dyx, rpw)
+                     mean, rstd, gamma, drop_p, seed, g_seed_ctr, drop_stream, (T*)dx, (T*)dr, ws, rpw)
   if (dtype == IMGCAP_BF16) {
     if (vec_rows<bf16>(cols, {dy, s, dx, dr})) LNB_(bf16, 8); else LNB_(bf16, 1);
   } else {
@@ -232,6 +233,7 @@ extern "C" int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const voi
   IMGCAP_CHECK_LAUNCH("imgcap_add_layernorm_bwd");
   // the [nblk][2][cols] partials are column-summed by the multi-colsum kernel (rows in
   // parallel; a per-column serial walk over ~500 slices cost ~30 us)
+  if (part) return 0;
   imgcap_colsum_item it[2];
   int n = 0;
   if (dgamma) it[n++] = imgcap_colsum_item{ws, dgamma, 2L * cols, nblk, cols, IMGCAP_F32, 0, 1.f};

@@ -239,7 +239,7 @@ def colsum(x, out, beta=0.0, rows=None, cols=None, ld=None):
 
 class ColsumBatch:
     """Deferred bias gradients: ``add`` records colsum(x) -> out (x kept alive), ``run`` issues
-    them as ONE imgcap_colsum_multi launch per 64 items (instead of 1-2 launches each)."""
+    them as ONE imgcap_colsum_multi call per 48 items (instead of 1-2 launches each)."""
 
     def __init__(self):
         self.items = []
@@ -249,14 +249,22 @@ class ColsumBatch:
         self.items.append((x, out, x.shape[0] if rows is None else rows, x.shape[1] if cols is None else cols,
                            x.stride(0) if ld is None else ld, beta))
 
+    TWO_PASS = os.environ.get("IMGCAP_COLSUM", "1") == "2"
+
     def run(self):
-        for i0 in range(0, len(self.items), 64):
-            chunk = self.items[i0:i0 + 64]
+        for i0 in range(0, len(self.items), 48):
+            chunk = self.items[i0:i0 + 48]
             arr = (_abi.ColsumItem * len(chunk))()
             for a, (x, out, rows, cols, ld, beta) in zip(arr, chunk):
                 a.x, a.out, a.ld, a.rows, a.cols, a.dtype, a.beta = x.data_ptr(), out.data_ptr(), ld, rows, cols, \
                     dt(x), beta
-            _abi.call("imgcap_colsum_multi", len(chunk), ctypes.cast(arr, ctypes.c_void_p), stream())
+            if self.TWO_PASS:
+                n = sum((rows + 255) // 256 * cols for (_, _, rows, cols, _, _) in chunk)
+                part = torch.empty(max(n, 1), device=chunk[0][1].device, dtype=torch.float32)
+                _abi.call("imgcap_colsum_multi_part", len(chunk), ctypes.cast(arr, ctypes.c_void_p), part.data_ptr(),
+                          n, stream())
+            else:
+                _abi.call("imgcap_colsum_multi", len(chunk), ctypes.cast(arr, ctypes.c_void_p), stream())
         self.items = []
 
 
@@ -307,18 +315,20 @@ def add_layernorm(x, r, gamma, beta, eps, *, drop_p=0.0, seed=0, drop_stream=0, 
 def add_layernorm_bwd(dy, s, mean, rstd, gamma, dgamma, dbeta, *, drop_p=0.0, seed=0, drop_stream=0, dx=None,
                       dr=None, cb=None):
     """LN backward; dgamma/dbeta accumulate (+=).  With a ColsumBatch ``cb`` their column sums
-    are deferred to cb.run() (dy * xhat materialised in fp32) instead of reduced here."""
+    are deferred to cb.run(): the kernel leaves its per-block partials [nblk, 2, cols] (fp32,
+    ~1/8 of the rows at C3) and cb sums them."""
     rows, cols = dy.shape
     dx = torch.empty_like(dy) if dx is None else dx
-    dyx = None
+    part = None
     if cb is not None:
-        dyx = torch.empty(rows, cols, device=dy.device, dtype=torch.float32)
-        cb.add(dyx, dgamma, beta=1.0)
-        cb.add(dy, dbeta, beta=1.0)
+        nblk = _abi.lib().imgcap_add_layernorm_bwd_blocks(rows)
+        part = torch.empty(nblk, 2, cols, device=dy.device, dtype=torch.float32)
+        cb.add(part[:, 0], dgamma, beta=1.0)
+        cb.add(part[:, 1], dbeta, beta=1.0)
         dgamma = dbeta = None
     _abi.call("imgcap_add_layernorm_bwd", dt(dy), rows, cols, dy.data_ptr(), s.data_ptr(), mean.data_ptr(),
               rstd.data_ptr(), gamma.data_ptr(), drop_p, seed, drop_stream, dx.data_ptr(), ptr(dr), ptr(dgamma),
-              ptr(dbeta), ptr(dyx), stream())
+              ptr(dbeta), ptr(part), stream())
     return dx
 
 

@@ -126,6 +126,16 @@ class TransformerEngine:
         K.embedding_fwd(caps.view(-1), fp.f32("embedding.weight"), x, pe=self.dec.pos_encoding.pe.view(-1, d)[:L]
                         .contiguous().float(), L=L, drop_p=p, seed=seed, drop_stream=_S_EMB)
         s["x0"] = x
+        # the cross-attention K/V projections of all layers depend on the memory alone (:81-82,
+        # nn.MultiheadAttention in_proj rows d..3d): one GEMM [B*P, 2d*layers] against the layers'
+        # stacked W_kv / b_kv (copied from the bf16 weights: 2 copy launches for 6 GEMMs).  Layer i
+        # reads its K/V as the column slice i of kv_all; the backward's dK/dV go to the matching
+        # slices of one buffer and the memory gradient is one GEMM against the same stack.
+        nkv = 2 * d * self.layers
+        wkv = torch.cat([fp.w(self._lw(i, "multihead_attn.in_proj_weight"))[d:] for i in range(self.layers)])
+        bkv = torch.cat([fp.f32(self._lw(i, "multihead_attn.in_proj_bias"))[d:] for i in range(self.layers)])
+        kv_all = K.gemm(mem, wkv, trans_b=True, bias=bkv)
+        s.update(wkv=wkv, kv_all=kv_all)
         for i in range(self.layers):
             lw = lambda n: self._lw(i, n)  # noqa: E731
             st = {"x": x}
@@ -141,14 +151,14 @@ class TransformerEngine:
             wq = fp.w(lw("multihead_attn.in_proj_weight"))
             bq = fp.f32(lw("multihead_attn.in_proj_bias"))
             q2 = K.gemm(x1, wq[:d], trans_b=True, bias=bq[:d])
-            kv2 = K.gemm(mem, wq[d:], trans_b=True, bias=bq[d:])
+            kv2 = kv_all[:, 2 * d * i:2 * d * (i + 1)]
             o2 = torch.empty(BL, d, **ctd)
             lse2 = torch.empty(B, self.H, L, **f32)
             pr = None
             if self.cross_probs is not None:
                 pr = torch.empty(B, self.H, L, P, **f32)
                 self.cross_probs.append(pr)
-            self._mha(B=B, Lq=L, Lk=P, q=q2, ldq=d, k=kv2, ldk=2 * d, v=kv2[:, d:], ldv=2 * d, o=o2, ldo=d, lse=lse2,
+            self._mha(B=B, Lq=L, Lk=P, q=q2, ldq=d, k=kv2, ldk=nkv, v=kv2[:, d:], ldv=nkv, o=o2, ldo=d, lse=lse2,
                       causal=False, key_ids=None, pad_id=0, p=p, seed=seed, sid=_s(i, 2), probs=pr)
             y2 = K.gemm(o2, fp.w(lw("multihead_attn.out_proj.weight")), trans_b=True,
                         bias=fp.f32(lw("multihead_attn.out_proj.bias")))
@@ -340,7 +350,8 @@ class TransformerEngine:
         wgb.add(dlogits, s["xL"], out=G("fc_out.weight"), M=V, trans_a=True)
         cb.add(dlogits, G("fc_out.bias"), cols=V)
         dx = K.gemm(dlogits, fp.w("fc_out.weight"), K=V)                    # [BL, d]
-        dmem = torch.zeros(BP, d, device=dev, dtype=torch.float32)
+        nkv = 2 * d * self.layers
+        dkv_all = torch.empty(BP, nkv, device=dev, dtype=ct)  # every layer's dK | dV (forward's kv_all layout)
         for i in reversed(range(self.layers)):
             lw = lambda n: self._lw(i, n)  # noqa: E731
             st = s["layers"][i]
@@ -365,11 +376,11 @@ class TransformerEngine:
             cb.add(dy2, G(lw("multihead_attn.out_proj.bias")))
             do2 = K.gemm(dy2, fp.w(lw("multihead_attn.out_proj.weight")))
             dq2 = torch.empty(BL, d, device=dev, dtype=ct)
-            dkv2 = torch.empty(BP, 2 * d, device=dev, dtype=ct)
-            self._mha(B=B, Lq=L, Lk=P, q=st["q2"], ldq=d, k=st["kv2"], ldk=2 * d, v=st["kv2"][:, d:], ldv=2 * d,
+            dkv2 = dkv_all[:, 2 * d * i:2 * d * (i + 1)]
+            self._mha(B=B, Lq=L, Lk=P, q=st["q2"], ldq=d, k=st["kv2"], ldk=nkv, v=st["kv2"][:, d:], ldv=nkv,
                       o=None, ldo=d, lse=st["lse2"], causal=False, key_ids=None, pad_id=0, p=p, seed=seed,
-                      sid=_s(i, 2), dout=do2, lddo=d, dq=dq2, lddq=d, dk=dkv2, lddk=2 * d, dv=dkv2[:, d:],
-                      lddv=2 * d, bwd=True)
+                      sid=_s(i, 2), dout=do2, lddo=d, dq=dq2, lddq=d, dk=dkv2, lddk=nkv, dv=dkv2[:, d:],
+                      lddv=nkv, bwd=True)
             gw = G(lw("multihead_attn.in_proj_weight"))
             gb = G(lw("multihead_attn.in_proj_bias"))
             wq = fp.w(lw("multihead_attn.in_proj_weight"))
@@ -377,7 +388,6 @@ class TransformerEngine:
             cb.add(dq2, gb[:d])
             wgb.add(dkv2, s["mem"], out=gw[d:], trans_a=True)
             cb.add(dkv2, gb[d:])
-            K.gemm(dkv2, wq[d:], out=dmem, beta=1.0)                          # dmem += dkv2 W_kv
             K.gemm(dq2, wq[:d], out=ds2, beta=1.0)                            # dx1 = ds2 + dq2 W_q
             # x1 = LN1(x + drop(y))
             dy = torch.empty_like(dx)
@@ -402,6 +412,9 @@ class TransformerEngine:
                 wgb.run()
                 cb.run()
                 bucket_hook()
+        # dmem = sum over layers of dK|dV_i W_kv_i: one GEMM over the stacked K = 2d * layers
+        dmem = torch.empty(BP, d, device=dev, dtype=torch.float32)
+        K.gemm(dkv_all, s["wkv"], out=dmem, split_k=-1)
         # embedding (dropout mask recomputed; PE has no parameters)
         K.embedding_bwd(s["caps"].view(-1), dx, G("embedding.weight"), drop_p=p, seed=seed, drop_stream=_S_EMB)
         denc = None

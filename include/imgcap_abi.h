@@ -164,7 +164,8 @@ int imgcap_transpose(int dtype, int rows, int cols, const void* in, int64_t ldi,
                      void* stream);
 
 /* Many column sums in one launch: out_i = beta_i*out_i + colsum(x_i)  (the bias gradients of a
- * whole backward pass, deferred to its end; <= 64 items per call; vec_ok is set by the library) */
+ * whole backward pass, deferred to its end; <= 48 items per call; vec_ok is set by the library;
+ * deterministic fixed-order sums; no library scratch) */
 typedef struct imgcap_colsum_item {
   const void* x;      /* [rows, ld] of dtype */
   float* out;         /* [cols] fp32 */
@@ -173,6 +174,11 @@ typedef struct imgcap_colsum_item {
   float beta;
 } imgcap_colsum_item;
 int imgcap_colsum_multi(int n, const imgcap_colsum_item* items, void* stream);
+/* The same in two launches with caller-owned fp32 scratch part[sum_i ceil(rows_i / 256) * cols_i]:
+ * per-(256-row chunk, 64 columns) partial sums, then each column's chunk partials added in order
+ * -- deterministic, the same sums in a different association than imgcap_colsum_multi. */
+int imgcap_colsum_multi_part(int n, const imgcap_colsum_item* items, float* part, int64_t part_floats,
+                             void* stream);
 
 /* column sums of a [rows, cols] matrix into fp32 out[cols] (bias gradients); beta=1 accumulates */
 int imgcap_colsum(int dtype, int rows, int cols, const void* x, int64_t ldx, float* out, float beta,
@@ -188,13 +194,16 @@ int imgcap_add_layernorm_fwd(int dtype, int rows, int cols, const void* x, const
                              const float* gamma, const float* beta, float eps,
                              void* s_out, void* y, float* mean, float* rstd, void* stream);
 /* dS = LN backward of dy;  dx = dS;  dr = dS * dropmask  (dr may be NULL);
- * dgamma/dbeta accumulated (+=) in fp32 -- or, with dyx != NULL (and dgamma = dbeta = NULL),
- * dyx[rows, cols] = dy * xhat (fp32) is written for the caller's deferred column sums
- * (dgamma = colsum(dyx), dbeta = colsum(dy): imgcap_colsum_multi). */
+ * dgamma/dbeta accumulated (+=) in fp32 -- or, with part != NULL (and dgamma = dbeta = NULL),
+ * the per-block partial sums are written to part[nblk][2][cols] (nblk =
+ * imgcap_add_layernorm_bwd_blocks(rows); [b][0] of dy * xhat, [b][1] of dy) for the caller's
+ * deferred column sums (dgamma = colsum(part[:, 0]), dbeta = colsum(part[:, 1]):
+ * imgcap_colsum_multi). */
 int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const void* dy, const void* s,
                              const float* mean, const float* rstd, const float* gamma,
                              float drop_p, uint64_t seed, uint32_t drop_stream,
-                             void* dx, void* dr, float* dgamma, float* dbeta, float* dyx, void* stream);
+                             void* dx, void* dr, float* dgamma, float* dbeta, float* part, void* stream);
+int imgcap_add_layernorm_bwd_blocks(int rows);
 
 /* ---------------------------------------------------------------------------------------
  * ConvNeXt trunk (torchvision features reached via encoder.py:24), NHWC activations.

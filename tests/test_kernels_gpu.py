@@ -147,22 +147,30 @@ def test_colsum(hip_device, rows, cols):
 
 
 def test_colsum_multi(hip_device):
-    """The batched bias-gradient column sums (imgcap_colsum_multi: 128 row lanes x 8 column
-    vectors per block): bf16 and fp32 items, ragged widths (non-vector tails), row counts below,
-    at and past the 1024-row vector stride, beta accumulation, a row pitch wider than the item."""
+    """The batched bias-gradient column sums (imgcap_colsum_multi: a block of 32 row lanes x 8
+    column vectors per 64-column group): bf16 and fp32 items, ragged widths
+    (non-vector tails), row counts of 0, below, at and past a row-lane trip, beta accumulation, a row
+    pitch wider than the item, an item not 16-byte aligned (scalar path); the same sums twice are
+    bitwise equal."""
     g = torch.Generator().manual_seed(5)
-    cases = [(1632, 9490, torch.bfloat16, 0.0), (3264, 512, torch.bfloat16, 0.5), (1023, 77, torch.float32, 0.0),
-             (1025, 2048, torch.float32, 1.0), (32, 1024, torch.bfloat16, 0.0), (5000, 100, torch.bfloat16, 0.0)]
-    cb, refs = K.ColsumBatch(), []
-    for rows, cols, dtype, beta in cases:
-        x = torch.randn(rows, cols + 8, generator=g).to(dtype)
-        out0 = torch.randn(cols, generator=g)
-        out = out0.to(hip_device)
-        cb.add(x.to(hip_device)[:, :cols], out, beta=beta)
-        refs.append((out, x[:, :cols].float().sum(0) + beta * out0))
-    cb.run()
-    for out, ref in refs:
-        assert _rel(out.cpu(), ref) < 1e-5
+    cases = [(1632, 9490, torch.bfloat16, 0.0, 0), (3264, 512, torch.bfloat16, 0.5, 0),
+             (1023, 77, torch.float32, 0.0, 0), (1025, 2048, torch.float32, 1.0, 0), (32, 1024, torch.bfloat16, 0.0, 0),
+             (5000, 100, torch.bfloat16, 0.0, 0), (0, 64, torch.bfloat16, 0.5, 0), (255, 65, torch.float32, 0.0, 0),
+             (256, 512, torch.bfloat16, 0.0, 0), (257, 512, torch.bfloat16, 0.0, 1), (3328, 1536, torch.float32, 0.0, 3)]
+    outs = []
+    for rep in range(2):
+        cb, refs = K.ColsumBatch(), []
+        for rows, cols, dtype, beta, off in cases:
+            x = torch.randn(rows, cols + 8, generator=torch.Generator().manual_seed(rows * 7 + cols)).to(dtype)
+            out0 = torch.randn(cols, generator=torch.Generator().manual_seed(cols))
+            out = out0.to(hip_device)
+            cb.add(x.to(hip_device)[:, off:off + cols], out, beta=beta)
+            refs.append((out, x[:, off:off + cols].float().sum(0) + beta * out0))
+        cb.run()
+        for out, ref in refs:
+            assert _rel(out.cpu(), ref) < 1e-5
+        outs.append([o.cpu() for o, _ in refs])
+    assert all(torch.equal(a, b) for a, b in zip(*outs))
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
@@ -186,7 +194,7 @@ def test_add_layernorm_fwd_bwd(hip_device, dtype, tol):
     dx = K.add_layernorm_bwd(dy.to(hip_device, dtype), s, mean, rstd, g.to(hip_device), dg, db, dr=dr)
     assert _rel(dx.cpu(), xs.grad) < tol and _rel(dr.cpu(), xs.grad) < tol
     assert _rel(dg.cpu(), gg.grad) < tol and _rel(db.cpu(), bb.grad) < tol
-    # deferred parameter sums: dy*xhat materialised, reduced with the backward's other column sums
+    # deferred parameter sums: the kernel's per-block partials, reduced with the backward's other column sums
     cb = K.ColsumBatch()
     dg2 = torch.full((cols,), 0.5, device=hip_device)
     db2 = torch.full((cols,), -0.5, device=hip_device)

@@ -1,0 +1,79 @@
+"""The Transformer decoder chain's non-GEMM kernels at C3 shapes, one at a time (GPU box):
+    python tools/chain_bench.py [reps]
+µs per launch (graph replay of back-to-back launches) of the post-norm add+LayerNorm forward /
+backward (dropout 0 and 0.1), the batched cross-attention K/V projection and the stacked dmem
+GEMM against the six per-layer launches they replace."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
+from tools.microbench import time_launch  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+dev = torch.device("cuda:0")
+bf = torch.bfloat16
+BL, BP, d, layers = 3328, 3136, 512, 6
+
+
+def us(fn):
+    return time_launch(fn, reps=reps) * 1e6
+
+
+x = torch.randn(BL, d, device=dev).to(bf)
+r = torch.randn(BL, d, device=dev).to(bf)
+g = torch.randn(d, device=dev)
+b = torch.randn(d, device=dev)
+s_out = torch.empty_like(x)
+y = torch.empty_like(x)
+for p in (0.0, 0.1):
+    print(f"add_ln_fwd p={p}: {us(lambda: K.add_layernorm(x, r, g, b, 1e-5, drop_p=p, seed=3, s_out=s_out, y=y)):.2f} us",
+          flush=True)
+_, mean, rstd = K.add_layernorm(x, r, g, b, 1e-5, s_out=s_out, y=y)
+dg = torch.zeros(d, device=dev)
+db = torch.zeros(d, device=dev)
+dx = torch.empty_like(x)
+dr = torch.empty_like(x)
+for p in (0.0, 0.1):
+    print(f"add_ln_bwd p={p}: {us(lambda: K.add_layernorm_bwd(x, s_out, mean, rstd, g, dg, db, drop_p=p, seed=3, dx=dx, dr=dr)):.2f} us"
+          f"  (deferred sums: {us(lambda: K.add_layernorm_bwd(x, s_out, mean, rstd, g, dg, db, drop_p=p, seed=3, dx=dx, dr=dr, cb=K.ColsumBatch())):.2f})",
+          flush=True)
+
+mem = torch.randn(BP, d, device=dev).to(bf)
+ws = [torch.randn(3 * d, d, device=dev).to(bf) for _ in range(layers)]
+bs = [torch.randn(3 * d, device=dev) for _ in range(layers)]
+kv = [torch.empty(BP, 2 * d, device=dev, dtype=bf) for _ in range(layers)]
+
+
+def per_layer():
+    for i in range(layers):
+        K.gemm(mem, ws[i][d:], trans_b=True, bias=bs[i][d:], out=kv[i])
+
+
+wkv = torch.empty(layers * 2 * d, d, device=dev, dtype=bf)
+bkv = torch.empty(layers * 2 * d, device=dev)
+kv_all = torch.empty(BP, layers * 2 * d, device=dev, dtype=bf)
+
+
+def batched():
+    torch.cat([w[d:] for w in ws], out=wkv)
+    torch.cat([c[d:] for c in bs], out=bkv)
+    K.gemm(mem, wkv, trans_b=True, bias=bkv, out=kv_all)
+
+
+print(f"cross K/V projections: 6 GEMMs {us(per_layer):.1f} us, cat + one GEMM {us(batched):.1f} us", flush=True)
+dkv = [torch.randn(BP, 2 * d, device=dev).to(bf) for _ in range(layers)]
+dmem = torch.zeros(BP, d, device=dev)
+
+
+def dmem_per_layer():
+    for i in range(layers):
+        K.gemm(dkv[i], ws[i][d:], out=dmem, beta=1.0)
+
+
+dkv_all = torch.randn(BP, layers * 2 * d, device=dev).to(bf)
+print(f"dmem: 6 accumulating GEMMs {us(dmem_per_layer):.1f} us, one stacked-K GEMM "
+      f"{us(lambda: K.gemm(dkv_all, wkv, out=dmem, split_k=-1)):.1f} us "
+      f"(no split {us(lambda: K.gemm(dkv_all, wkv, out=dmem)):.1f})", flush=True)
