@@ -249,7 +249,10 @@ class ColsumBatch:
         self.items.append((x, out, x.shape[0] if rows is None else rows, x.shape[1] if cols is None else cols,
                            x.stride(0) if ld is None else ld, beta))
 
-    TWO_PASS = os.environ.get("IMGCAP_COLSUM", "1") == "2"
+    # two launches over 256-row chunks with the partials in a torch-allocated buffer (the
+    # default: C3's 80 bias sums, 302 MB, in 76 us vs 95 us single-pass); IMGCAP_COLSUM=1 runs the
+    # single-pass kernel.  Neither takes library scratch (tests/test_stream_hazards_gpu.py).
+    TWO_PASS = os.environ.get("IMGCAP_COLSUM", "2") == "2"
 
     def run(self):
         for i0 in range(0, len(self.items), 48):

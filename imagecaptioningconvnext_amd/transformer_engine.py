@@ -433,10 +433,15 @@ class TransformerEngine:
             main = torch.cuda.current_stream(dev)
             side = self._side_stream(dev)
             side.wait_stream(main)
+            # the operands the side stream reads were allocated on the main stream: held until the
+            # join, so the caching allocator cannot hand their blocks to a main-stream allocation
+            # while the column sums still read them (the round-4 side-stream drift)
+            held = [it[0] for it in cb.items]
             with torch.cuda.stream(side):
                 cb.run()
             wgb.run()
             main.wait_stream(side)
+            del held
         else:
             wgb.run()
             cb.run()

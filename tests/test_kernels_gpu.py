@@ -158,7 +158,8 @@ def test_colsum_multi(hip_device):
              (5000, 100, torch.bfloat16, 0.0, 0), (0, 64, torch.bfloat16, 0.5, 0), (255, 65, torch.float32, 0.0, 0),
              (256, 512, torch.bfloat16, 0.0, 0), (257, 512, torch.bfloat16, 0.0, 1), (3328, 1536, torch.float32, 0.0, 3)]
     outs = []
-    for rep in range(2):
+    for rep in range(4):  # single-pass twice, two-pass twice
+        K.ColsumBatch.TWO_PASS = rep >= 2
         cb, refs = K.ColsumBatch(), []
         for rows, cols, dtype, beta, off in cases:
             x = torch.randn(rows, cols + 8, generator=torch.Generator().manual_seed(rows * 7 + cols)).to(dtype)
@@ -170,7 +171,9 @@ def test_colsum_multi(hip_device):
         for out, ref in refs:
             assert _rel(out.cpu(), ref) < 1e-5
         outs.append([o.cpu() for o, _ in refs])
-    assert all(torch.equal(a, b) for a, b in zip(*outs))
+    K.ColsumBatch.TWO_PASS = True
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
+    assert all(torch.equal(a, b) for a, b in zip(outs[2], outs[3]))
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])

@@ -1,0 +1,62 @@
+"""Cross-stream hazards of the captured schedules ("round 4 side-stream drift and the
+round 5 scratch race").
+
+The library's split-reduction scratch is one buffer per workspace slot, and a slot is shared by
+every stream of a schedule branch.  The LSTM backward runs the embedding gradient -- a scratch
+user -- on a side stream beside the main stream's grouped weight-gradient GEMMs and bias column
+sums, so those two entry points must never request scratch: a round-5 two-pass column sum that
+did faulted the LSTM checkpoint test with an illegal address.  The check: attach a 16-byte caller
+workspace to the slot and call the entry points directly -- any scratch request returns
+IMGCAP_EWORKSPACE (-3) instead of enqueuing (a split-K GEMM is the positive control)."""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_side_stream_entry_points_take_no_library_scratch(hip_device):
+    from imagecaptioningconvnext_amd import _abi
+    from imagecaptioningconvnext_amd import kernels as K
+    dev = hip_device
+    K.colsum(torch.zeros(1, 8, device=dev), torch.zeros(8, device=dev))  # workspaces attached
+    L = _abi.lib()
+    tiny = torch.empty(16, dtype=torch.uint8, device=dev)
+    x = torch.randn(3328, 1536, device=dev).to(torch.bfloat16)
+    xf = torch.randn(416, 1024, device=dev)
+    outs = [torch.zeros(1536, device=dev), torch.zeros(512, device=dev)]
+    items = (_abi.ColsumItem * 2)()
+    for it, (t, o, cols, ld) in zip(items, ((x, outs[0], 1536, 1536), (xf, outs[1], 512, 1024))):
+        it.x, it.out, it.ld, it.rows, it.cols, it.dtype, it.beta = t.data_ptr(), o.data_ptr(), ld, t.shape[0], cols, \
+            K.dt(t), 0.0
+    a = torch.randn(3328, 512, device=dev).to(torch.bfloat16)
+    b = torch.randn(3328, 512, device=dev).to(torch.bfloat16)
+    g = torch.zeros(512, 512, device=dev)
+    probs = (_abi.GemmProblem * 1)()
+    p = probs[0]
+    p.A, p.B, p.C = a.data_ptr(), b.data_ptr(), g.data_ptr()
+    p.lda, p.ldb, p.ldc = 512, 512, 512
+    p.M, p.N, p.K, p.alpha, p.beta = 512, 512, 3328, 1.0, 0.0
+    st = K.stream()
+    old = _abi._ws[(dev.index or 0, 0)]
+    assert L.imgcap_workspace_slot(0) == 0
+    assert L.imgcap_workspace_attach(0, tiny.data_ptr(), 16) == 0
+    try:
+        rc_cs = L.imgcap_colsum_multi(2, ctypes.cast(items, ctypes.c_void_p), st)
+        part = torch.empty(13 * 1536 + 2 * 512, device=dev)  # the two-pass form: caller-owned partials
+        rc_cs2 = L.imgcap_colsum_multi_part(2, ctypes.cast(items, ctypes.c_void_p), part.data_ptr(), part.numel(), st)
+        rc_gg = L.imgcap_gemm_grouped(0, 0, 1, ctypes.cast(probs, ctypes.c_void_p), st)
+        # positive control: a split-K product needs scratch and is refused
+        ep = _abi.Epilogue()
+        ep.alpha, ep.c_dtype, ep.split_k, ep.rows_per_scale, ep.drop_ld = 1.0, _abi.F32, 4, 1, 512
+        rc_split = L.imgcap_gemm(K.dt(a), 0, 0, 512, 512, 3328, a.data_ptr(), 512, 0, b.data_ptr(), 512, 0,
+                                 g.data_ptr(), 512, 0, 1, ctypes.byref(ep), st)
+    finally:
+        assert L.imgcap_workspace_attach(0, old.data_ptr(), old.numel()) == 0
+    torch.cuda.synchronize()
+    assert rc_split == _abi.IMGCAP_EWORKSPACE
+    assert rc_cs == 0 and rc_cs2 == 0 and rc_gg == 0
+    torch.testing.assert_close(outs[0], x.float().sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(outs[1], xf[:, :512].sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(g, a.float().t() @ b.float(), rtol=2e-2, atol=2e-1)
