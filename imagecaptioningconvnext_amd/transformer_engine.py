@@ -144,10 +144,8 @@ class TransformerEngine:
             lse1 = torch.empty(B, self.H, L, **f32)
             self._mha(B=B, Lq=L, Lk=L, q=qkv, ldq=3 * d, k=qkv[:, d:], ldk=3 * d, v=qkv[:, 2 * d:], ldv=3 * d, o=o,
                       ldo=d, lse=lse1, causal=True, key_ids=key_ids, pad_id=pad_id, p=p, seed=seed, sid=_s(i, 0))
-            y = K.gemm(o, fp.w(lw("self_attn.out_proj.weight")), trans_b=True, bias=fp.f32(lw("self_attn.out_proj.bias")))
             s1 = torch.empty(BL, d, **ctd)
-            x1, mu1, rs1 = K.add_layernorm(x, y, fp.f32(lw("norm1.weight")), fp.f32(lw("norm1.bias")), 1e-5,
-                                           drop_p=p, seed=seed, drop_stream=_s(i, 1), s_out=s1)
+            x1, mu1, rs1 = self._linear_add_ln(o, "self_attn.out_proj", x, "norm1", i, p, seed, _s(i, 1), s1)
             wq = fp.w(lw("multihead_attn.in_proj_weight"))
             bq = fp.f32(lw("multihead_attn.in_proj_bias"))
             q2 = K.gemm(x1, wq[:d], trans_b=True, bias=bq[:d])
@@ -160,17 +158,12 @@ class TransformerEngine:
                 self.cross_probs.append(pr)
             self._mha(B=B, Lq=L, Lk=P, q=q2, ldq=d, k=kv2, ldk=nkv, v=kv2[:, d:], ldv=nkv, o=o2, ldo=d, lse=lse2,
                       causal=False, key_ids=None, pad_id=0, p=p, seed=seed, sid=_s(i, 2), probs=pr)
-            y2 = K.gemm(o2, fp.w(lw("multihead_attn.out_proj.weight")), trans_b=True,
-                        bias=fp.f32(lw("multihead_attn.out_proj.bias")))
             s2 = torch.empty(BL, d, **ctd)
-            x2, mu2, rs2 = K.add_layernorm(x1, y2, fp.f32(lw("norm2.weight")), fp.f32(lw("norm2.bias")), 1e-5,
-                                           drop_p=p, seed=seed, drop_stream=_s(i, 3), s_out=s2)
+            x2, mu2, rs2 = self._linear_add_ln(o2, "multihead_attn.out_proj", x1, "norm2", i, p, seed, _s(i, 3), s2)
             hdn = K.gemm(x2, fp.w(lw("linear1.weight")), trans_b=True, bias=fp.f32(lw("linear1.bias")),
                          act=K.ACT_RELU, drop_p=p, seed=seed, drop_stream=_s(i, 4))
-            y3 = K.gemm(hdn, fp.w(lw("linear2.weight")), trans_b=True, bias=fp.f32(lw("linear2.bias")))
             s3 = torch.empty(BL, d, **ctd)
-            x3, mu3, rs3 = K.add_layernorm(x2, y3, fp.f32(lw("norm3.weight")), fp.f32(lw("norm3.bias")), 1e-5,
-                                           drop_p=p, seed=seed, drop_stream=_s(i, 5), s_out=s3)
+            x3, mu3, rs3 = self._linear_add_ln(hdn, "linear2", x2, "norm3", i, p, seed, _s(i, 5), s3)
             st.update(qkv=qkv, o=o, lse1=lse1, s1=s1, mu1=mu1, rs1=rs1, x1=x1, q2=q2, kv2=kv2, o2=o2, lse2=lse2,
                       s2=s2, mu2=mu2, rs2=rs2, x2=x2, hdn=hdn, s3=s3, mu3=mu3, rs3=rs3)
             s["layers"].append(st)
@@ -196,6 +189,38 @@ class TransformerEngine:
                        lambda: K.loss_finalize(lrow, hit, targets, None, metrics))
             s.update(logits=logits, targets=targets, lse=lse, metrics=metrics, dlogits=dlogits)
         return s
+
+    def _fused_ln(self):
+        # the row-complete GEMM + LayerNorm kernels: bf16, d_model = 512 (one block row), K % 64
+        return self.ct == torch.bfloat16 and self.d == 512 and self.ff % 64 == 0
+
+    def _linear_add_ln(self, a, linear, x, norm, i, p, seed, sid, s_out):
+        """x' = LN(x + dropout(a W^T + b)) (transformerDecoder.py:82,104, post-norm): one launch
+        (imgcap_gemm_add_ln_fwd) or the GEMM + imgcap_add_layernorm_fwd pair."""
+        fp = self.fp
+        w, b = fp.w(self._lw(i, f"{linear}.weight")), fp.f32(self._lw(i, f"{linear}.bias"))
+        g, be = fp.f32(self._lw(i, f"{norm}.weight")), fp.f32(self._lw(i, f"{norm}.bias"))
+        if self._fused_ln():
+            return K.gemm_add_ln(a, w, b, x, g, be, 1e-5, drop_p=p, seed=seed, drop_stream=sid, s_out=s_out)
+        y = K.gemm(a, w, trans_b=True, bias=b)
+        return K.add_layernorm(x, y, g, be, 1e-5, drop_p=p, seed=seed, drop_stream=sid, s_out=s_out)
+
+    def _ln_bwd_of_product(self, a, b, res, st, k, i, p, seed, sid, G, cb):
+        """The LayerNorm backward of norm{k} (layer i) on its incoming gradient a @ b + res:
+        returns (dS, dY) -- one launch (imgcap_gemm_ln_bwd) or the GEMM (beta = 1 into res) +
+        imgcap_add_layernorm_bwd pair."""
+        fp = self.fp
+        gam = fp.f32(self._lw(i, f"norm{k}.weight"))
+        gg, gb = G(self._lw(i, f"norm{k}.weight")), G(self._lw(i, f"norm{k}.bias"))
+        dy = torch.empty_like(res)
+        if self._fused_ln():
+            ds = K.gemm_ln_bwd(a, b, st[f"s{k}"], st[f"mu{k}"], st[f"rs{k}"], gam, gg, gb, cb, res=res, drop_p=p,
+                               seed=seed, drop_stream=sid, dr=dy)
+            return ds, dy
+        K.gemm(a, b, out=res, beta=1.0)
+        ds = K.add_layernorm_bwd(res, st[f"s{k}"], st[f"mu{k}"], st[f"rs{k}"], gam, gg, gb, drop_p=p, seed=seed,
+                                 drop_stream=sid, dr=dy, cb=cb)
+        return ds, dy
 
     def greedy(self, encoder_out, start_id, end_id, maxlen):
         """transformerDecoder.py:110-160 (forwardWithoutTeacherForcing) with a key/value cache.
@@ -352,26 +377,26 @@ class TransformerEngine:
         dx = K.gemm(dlogits, fp.w("fc_out.weight"), K=V)                    # [BL, d]
         nkv = 2 * d * self.layers
         dkv_all = torch.empty(BP, nkv, device=dev, dtype=ct)  # every layer's dK | dV (forward's kv_all layout)
+        carry = None  # (dS3, dY3) of layer i, made by layer i+1's last product (fused LayerNorm backward)
         for i in reversed(range(self.layers)):
             lw = lambda n: self._lw(i, n)  # noqa: E731
             st = s["layers"][i]
             # x3 = LN3(x2 + drop(y3))
-            dy3 = torch.empty_like(dx)
-            ds3 = K.add_layernorm_bwd(dx, st["s3"], st["mu3"], st["rs3"], fp.f32(lw("norm3.weight")),
-                                      G(lw("norm3.weight")), G(lw("norm3.bias")), drop_p=p, seed=seed,
-                                      drop_stream=_s(i, 5), dr=dy3, cb=cb)
+            if carry is None:
+                dy3 = torch.empty_like(dx)
+                ds3 = K.add_layernorm_bwd(dx, st["s3"], st["mu3"], st["rs3"], fp.f32(lw("norm3.weight")),
+                                          G(lw("norm3.weight")), G(lw("norm3.bias")), drop_p=p, seed=seed,
+                                          drop_stream=_s(i, 5), dr=dy3, cb=cb)
+            else:
+                ds3, dy3 = carry
             # y3 = hdn W2^T + b2 ; hdn = drop(relu(x2 W1^T + b1))
             wgb.add(dy3, st["hdn"], out=G(lw("linear2.weight")), trans_a=True)
             cb.add(dy3, G(lw("linear2.bias")))
             dpre = K.gemm(dy3, fp.w(lw("linear2.weight")), aux=st["hdn"], aux_scale=1.0 / (1.0 - p))
             wgb.add(dpre, st["x2"], out=G(lw("linear1.weight")), trans_a=True)
             cb.add(dpre, G(lw("linear1.bias")))
-            K.gemm(dpre, fp.w(lw("linear1.weight")), out=ds3, beta=1.0)      # dx2 = ds3 + dpre W1
-            # x2 = LN2(x1 + drop(y2))
-            dy2 = torch.empty_like(dx)
-            ds2 = K.add_layernorm_bwd(ds3, st["s2"], st["mu2"], st["rs2"], fp.f32(lw("norm2.weight")),
-                                      G(lw("norm2.weight")), G(lw("norm2.bias")), drop_p=p, seed=seed,
-                                      drop_stream=_s(i, 3), dr=dy2, cb=cb)
+            # x2 = LN2(x1 + drop(y2)), on its incoming gradient dx2 = ds3 + dpre W1
+            ds2, dy2 = self._ln_bwd_of_product(dpre, fp.w(lw("linear1.weight")), ds3, st, 2, i, p, seed, _s(i, 3), G, cb)
             wgb.add(dy2, st["o2"], out=G(lw("multihead_attn.out_proj.weight")), trans_a=True)
             cb.add(dy2, G(lw("multihead_attn.out_proj.bias")))
             do2 = K.gemm(dy2, fp.w(lw("multihead_attn.out_proj.weight")))
@@ -388,12 +413,8 @@ class TransformerEngine:
             cb.add(dq2, gb[:d])
             wgb.add(dkv2, s["mem"], out=gw[d:], trans_a=True)
             cb.add(dkv2, gb[d:])
-            K.gemm(dq2, wq[:d], out=ds2, beta=1.0)                            # dx1 = ds2 + dq2 W_q
-            # x1 = LN1(x + drop(y))
-            dy = torch.empty_like(dx)
-            ds1 = K.add_layernorm_bwd(ds2, st["s1"], st["mu1"], st["rs1"], fp.f32(lw("norm1.weight")),
-                                      G(lw("norm1.weight")), G(lw("norm1.bias")), drop_p=p, seed=seed,
-                                      drop_stream=_s(i, 1), dr=dy, cb=cb)
+            # x1 = LN1(x + drop(y)), on its incoming gradient dx1 = ds2 + dq2 W_q
+            ds1, dy = self._ln_bwd_of_product(dq2, wq[:d], ds2, st, 1, i, p, seed, _s(i, 1), G, cb)
             wgb.add(dy, st["o"], out=G(lw("self_attn.out_proj.weight")), trans_a=True)
             cb.add(dy, G(lw("self_attn.out_proj.bias")))
             do = K.gemm(dy, fp.w(lw("self_attn.out_proj.weight")))
@@ -405,8 +426,13 @@ class TransformerEngine:
                       dv=dqkv[:, 2 * d:], lddv=3 * d, bwd=True)
             wgb.add(dqkv, st["x"], out=G(lw("self_attn.in_proj_weight")), trans_a=True)
             cb.add(dqkv, G(lw("self_attn.in_proj_bias")))
-            K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
-            dx = ds1
+            if i > 0:
+                # layer i-1's LN3 on its incoming gradient dx = ds1 + dqkv W_in
+                carry = self._ln_bwd_of_product(dqkv, fp.w(lw("self_attn.in_proj_weight")), ds1, s["layers"][i - 1],
+                                                3, i - 1, p, seed, _s(i - 1, 5), G, cb)
+            else:
+                K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
+                dx = ds1
             if bucket_hook is not None and (i == 0 or not self.merged_layer_bucket):
                 # layer i's gradients final (merged: every layer's): that bucket's all-reduce
                 wgb.run()
