@@ -81,12 +81,6 @@ _SIGS = {
     "imgcap_add_layernorm_bwd": [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                                  c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "imgcap_add_layernorm_bwd_blocks": [c_int],
-    "imgcap_gemm_add_ln_fwd": [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_float,
-                               c_uint64, c_uint32, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int64, c_void_p,
-                               c_void_p, c_void_p],
-    "imgcap_gemm_ln_bwd": [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
-                           c_void_p, c_void_p, c_void_p, c_float, c_uint64, c_uint32, c_void_p, c_void_p, c_int64,
-                           c_void_p, c_void_p],
     "imgcap_convnext_stem": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p],
     "imgcap_convnext_stem_u8": [c_int, c_int, c_int, c_int, c_int] + [c_void_p] * 9,

@@ -407,7 +407,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 #include "gemm256.h"
 #include "gemm_mx.h"
 #include "gemm_pt.h"
-#include "gemm_rowln.h"
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,

@@ -335,43 +335,6 @@ def add_layernorm_bwd(dy, s, mean, rstd, gamma, dgamma, dbeta, *, drop_p=0.0, se
     return dx
 
 
-def gemm_add_ln(a, w, bias, x, gamma, beta, eps, *, drop_p=0.0, seed=0, drop_stream=0, s_out=None, y=None):
-    """LN(x + dropout(a @ w.T + bias)) in one launch (imgcap_gemm_add_ln_fwd; bf16, w [512, K]):
-    returns (y, mean, rstd) like add_layernorm, s_out receives the pre-norm sum."""
-    _check_dev(a, w, bias, x, gamma, beta)
-    M, Kd = a.shape
-    if w.shape != (512, Kd):
-        raise ValueError(f"gemm_add_ln: weight {tuple(w.shape)}, want (512, {Kd})")
-    y = torch.empty(M, 512, device=a.device, dtype=a.dtype) if y is None else y
-    s_out = torch.empty_like(y) if s_out is None else s_out
-    mean = torch.empty(M, device=a.device, dtype=torch.float32)
-    rstd = torch.empty_like(mean)
-    _abi.call("imgcap_gemm_add_ln_fwd", M, Kd, a.data_ptr(), _ld(a, False), w.data_ptr(), _ld(w, True),
-              bias.data_ptr(), x.data_ptr(), x.stride(0), drop_p, seed, drop_stream, gamma.data_ptr(), beta.data_ptr(),
-              eps, s_out.data_ptr(), y.data_ptr(), y.stride(0), mean.data_ptr(), rstd.data_ptr(), stream())
-    return y, mean, rstd
-
-
-def gemm_ln_bwd(a, b, s, mean, rstd, gamma, dgamma, dbeta, cb, *, res=None, drop_p=0.0, seed=0, drop_stream=0,
-                dx=None, dr=None):
-    """LayerNorm backward on the product a @ b (+ res) in one launch (imgcap_gemm_ln_bwd; bf16,
-    b [K, 512]): returns dS; dr = dS * dropout mask; dgamma / dbeta (+=) deferred to the
-    ColsumBatch ``cb`` through the kernel's per-block partials."""
-    _check_dev(a, b, s, mean, rstd, gamma, res, dr)
-    M, Kd = a.shape
-    if tuple(b.shape) != (Kd, 512):
-        raise ValueError(f"gemm_ln_bwd: b {tuple(b.shape)}, want ({Kd}, 512)")
-    dx = torch.empty(M, 512, device=a.device, dtype=a.dtype) if dx is None else dx
-    part = torch.empty((M + 31) // 32, 2, 512, device=a.device, dtype=torch.float32)
-    cb.add(part[:, 0], dgamma, beta=1.0)
-    cb.add(part[:, 1], dbeta, beta=1.0)
-    _abi.call("imgcap_gemm_ln_bwd", M, Kd, a.data_ptr(), _ld(a, False), b.data_ptr(), _ld(b, False), ptr(res),
-              0 if res is None else res.stride(0), s.data_ptr(), s.stride(0), mean.data_ptr(), rstd.data_ptr(),
-              gamma.data_ptr(), drop_p, seed, drop_stream, dx.data_ptr(), ptr(dr), dx.stride(0), part.data_ptr(),
-              stream())
-    return dx
-
-
 def ce_fwd(logits, targets, V, lse, loss, hit5):
     n = targets.numel()
     _abi.call("imgcap_ce_fwd", dt(logits), n, V, logits.data_ptr(), logits.stride(0), targets.data_ptr(),

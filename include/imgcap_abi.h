@@ -204,24 +204,6 @@ int imgcap_add_layernorm_bwd(int dtype, int rows, int cols, const void* dy, cons
                              float drop_p, uint64_t seed, uint32_t drop_stream,
                              void* dx, void* dr, float* dgamma, float* dbeta, float* part, void* stream);
 int imgcap_add_layernorm_bwd_blocks(int rows);
-/* The post-norm block's last Linear and its add + LayerNorm in one launch (bf16; N = d_model =
- * 512, K % 64 == 0): y = A W^T + bias (A [M, K], W [512, K] the nn.Linear weight), s = x +
- * dropout(y) (mask index row * 512 + column on drop_stream, as imgcap_add_layernorm_fwd),
- * out = LN(s) * gamma + beta; s, mean, rstd saved for the backward.  Replaces imgcap_gemm +
- * imgcap_add_layernorm_fwd at transformerDecoder.py:82,104 (norm_first=False). */
-int imgcap_gemm_add_ln_fwd(int M, int K, const void* A, int64_t lda, const void* W, int64_t ldw,
-                           const float* bias, const void* x, int64_t ldx, float drop_p, uint64_t seed,
-                           uint32_t drop_stream, const float* gamma, const float* beta, float eps,
-                           void* s_out, void* y, int64_t ldo, float* mean, float* rstd, void* stream);
-/* The LayerNorm backward on the product that makes its incoming gradient: dx = A B (+ res)
- * (A [M, K], B [K, 512] row-major, res [M, 512] or NULL), dS = LN_bwd(dx; s, mean, rstd, gamma),
- * dr = dS * dropout mask (dr may be NULL), part[ceil(M / 32)][2][512] = per-block sums of
- * dx * xhat and dx (dgamma / dbeta partials for imgcap_colsum_multi).  Replaces imgcap_gemm(...,
- * beta = 1) + imgcap_add_layernorm_bwd. */
-int imgcap_gemm_ln_bwd(int M, int K, const void* A, int64_t lda, const void* B, int64_t ldb,
-                       const void* res, int64_t ldr, const void* s, int64_t lds, const float* mean,
-                       const float* rstd, const float* gamma, float drop_p, uint64_t seed,
-                       uint32_t drop_stream, void* ds, void* dr, int64_t ldo, float* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * ConvNeXt trunk (torchvision features reached via encoder.py:24), NHWC activations.

@@ -692,57 +692,3 @@ def test_embedding_bwd_long_runs_chunked_order(hip_device, dtype, n, V, dim, run
     r64 = torch.zeros(V, dim, dtype=torch.float64).index_add_(0, ids, x.double())
     assert ((got.double() - r64).norm() / r64.norm()).item() < 1e-6
 
-
-@pytest.mark.parametrize("M,Kd,p", [(3328, 512, 0.1), (1000, 1536, 0.0), (45, 512, 0.2)])
-def test_gemm_add_ln_matches_gemm_then_add_ln(hip_device, M, Kd, p):
-    """imgcap_gemm_add_ln_fwd (row-complete 32 x 512 tiles, LayerNorm on the accumulators) against
-    the unfused imgcap_gemm + imgcap_add_layernorm_fwd on the same operands and dropout stream:
-    the same bf16 roundings, so the pre-norm sum s and the mask agree exactly up to the GEMM's
-    accumulation order, the outputs to bf16 rounding.  Ragged M (a partial last row block)."""
-    dev = hip_device
-    g = torch.Generator().manual_seed(M + Kd)
-    a = (torch.randn(M, Kd, generator=g) * 0.5).to(torch.bfloat16).to(dev)
-    w = (torch.randn(512, Kd, generator=g) / Kd ** 0.5).to(torch.bfloat16).to(dev)
-    bias = torch.randn(512, generator=g).to(dev)
-    x = torch.randn(M, 512, generator=g).to(torch.bfloat16).to(dev)
-    gam, bet = (torch.rand(512, generator=g) + 0.5).to(dev), torch.randn(512, generator=g).to(dev)
-    s_f = torch.empty(M, 512, device=dev, dtype=torch.bfloat16)
-    y_f, mu_f, rs_f = K.gemm_add_ln(a, w, bias, x, gam, bet, 1e-5, drop_p=p, seed=77, drop_stream=9, s_out=s_f)
-    yl = K.gemm(a, w, trans_b=True, bias=bias)
-    s_u = torch.empty_like(s_f)
-    y_u, mu_u, rs_u = K.add_layernorm(x, yl, gam, bet, 1e-5, drop_p=p, seed=77, drop_stream=9, s_out=s_u)
-    torch.cuda.synchronize()
-    assert torch.equal(s_f == x, s_u == x)  # the same dropped entries (s = x exactly where y is masked)
-    assert _rel(s_f.float().cpu(), s_u.float().cpu()) < 1e-2
-    assert _rel(y_f.float().cpu(), y_u.float().cpu()) < 1e-2
-    assert _rel(mu_f.cpu(), mu_u.cpu()) < 1e-2 and _rel(rs_f.cpu(), rs_u.cpu()) < 1e-3
-
-
-@pytest.mark.parametrize("M,Kd,p,with_res", [(3328, 1536, 0.1, True), (1000, 512, 0.0, True), (45, 512, 0.2, False)])
-def test_gemm_ln_bwd_matches_gemm_then_add_ln_bwd(hip_device, M, Kd, p, with_res):
-    """imgcap_gemm_ln_bwd (LayerNorm backward on the accumulators of dx = A B + res) against
-    imgcap_gemm(beta = 1) + imgcap_add_layernorm_bwd: dS, the masked dY and the deferred
-    dgamma / dbeta (per-block partials through a ColsumBatch)."""
-    dev = hip_device
-    g = torch.Generator().manual_seed(M * 3 + Kd)
-    a = (torch.randn(M, Kd, generator=g) * 0.3).to(torch.bfloat16).to(dev)
-    b = (torch.randn(Kd, 512, generator=g) / Kd ** 0.5).to(torch.bfloat16).to(dev)
-    res = torch.randn(M, 512, generator=g).to(torch.bfloat16).to(dev) if with_res else None
-    x, r = torch.randn(M, 512, generator=g).to(torch.bfloat16).to(dev), torch.randn(M, 512, generator=g).to(torch.bfloat16).to(dev)
-    gam, bet = (torch.rand(512, generator=g) + 0.5).to(dev), torch.randn(512, generator=g).to(dev)
-    s = torch.empty_like(x)
-    _, mean, rstd = K.add_layernorm(x, r, gam, bet, 1e-5, s_out=s)
-    cb = K.ColsumBatch()
-    dg_f, db_f = torch.zeros(512, device=dev), torch.zeros(512, device=dev)
-    dr_f = torch.empty_like(x)
-    ds_f = K.gemm_ln_bwd(a, b, s, mean, rstd, gam, dg_f, db_f, cb, res=res, drop_p=p, seed=5, drop_stream=4, dr=dr_f)
-    cb.run()
-    dx = res.clone() if with_res else torch.zeros(M, 512, device=dev, dtype=torch.bfloat16)
-    K.gemm(a, b, out=dx, beta=1.0 if with_res else 0.0)
-    dg_u, db_u = torch.zeros(512, device=dev), torch.zeros(512, device=dev)
-    dr_u = torch.empty_like(x)
-    ds_u = K.add_layernorm_bwd(dx, s, mean, rstd, gam, dg_u, db_u, drop_p=p, seed=5, drop_stream=4, dr=dr_u)
-    torch.cuda.synchronize()
-    for f, u in ((ds_f, ds_u), (dr_f, dr_u), (dg_f, dg_u), (db_f, db_u)):
-        assert _rel(f.float().cpu(), u.float().cpu()) < 2e-2
-    assert torch.equal(dr_f == 0, dr_u == 0) or p == 0.0

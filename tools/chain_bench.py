@@ -78,22 +78,3 @@ print(f"dmem: 6 accumulating GEMMs {us(dmem_per_layer):.1f} us, one stacked-K GE
       f"{us(lambda: K.gemm(dkv_all, wkv, out=dmem, split_k=-1)):.1f} us "
       f"(no split {us(lambda: K.gemm(dkv_all, wkv, out=dmem)):.1f})", flush=True)
 
-# post-norm blocks: fused GEMM + add + LayerNorm (forward) / LayerNorm backward on the product
-o = torch.randn(BL, d, device=dev).to(bf)
-w_out = (torch.randn(d, d, device=dev) / 23).to(bf)
-b_out = torch.randn(d, device=dev)
-x1 = torch.empty_like(x)
-print(f"out-proj + add_ln fwd: GEMM + add_ln {us(lambda: K.add_layernorm(x, K.gemm(o, w_out, trans_b=True, bias=b_out), g, b, 1e-5, drop_p=0.1, seed=3, s_out=s_out, y=x1)):.2f} us, "
-      f"fused {us(lambda: K.gemm_add_ln(o, w_out, b_out, x, g, b, 1e-5, drop_p=0.1, seed=3, s_out=s_out, y=x1)):.2f} us", flush=True)
-for kd in (512, 1536):
-    dz = torch.randn(BL, kd, device=dev).to(bf)
-    wb = (torch.randn(kd, d, device=dev) / kd ** 0.5).to(bf)
-    res = torch.randn(BL, d, device=dev).to(bf)
-
-    def unfused():
-        K.gemm(dz, wb, out=res, beta=1.0)
-        K.add_layernorm_bwd(res, s_out, mean, rstd, g, dg, db, drop_p=0.1, seed=3, dx=dx, dr=dr, cb=K.ColsumBatch())
-
-    print(f"LN bwd on dx = dZ W + res (K={kd}): GEMM + add_ln_bwd {us(unfused):.2f} us, fused "
-          f"{us(lambda: K.gemm_ln_bwd(dz, wb, s_out, mean, rstd, g, dg, db, K.ColsumBatch(), res=res, drop_p=0.1, seed=3, dx=dx, dr=dr)):.2f} us",
-          flush=True)
