@@ -533,6 +533,10 @@ extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* id
   const size_t rank_bytes = ((size_t)n * sizeof(int) + 15) / 16 * 16;
   const size_t idx_bytes = (2 * (size_t)n * sizeof(int) + 15) / 16 * 16;
   const int nchunks = (n + EMB_CH - 1) / EMB_CH;
+  // workspace: ranks + sorted indices (12 B per position) and two dim-wide fp32 slots per chunk for
+  // runs crossing a chunk boundary -- ~n * dim / 8 bytes plus 12 n: 0.6 MB at C3 (n = 3,328,
+  // dim = 512), 256 MiB at the limits (n = 2^20, dim = 2048); the library workspace keeps its
+  // high-water mark for the process (imgcap_workspace_needed / _attach size it)
   int* rank = (int*)workspace(rank_bytes + idx_bytes + (size_t)nchunks * 2 * dim * sizeof(float), st);
   if (!rank) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_embedding_bwd: ") + last_error());
   int* spos = rank + rank_bytes / sizeof(int);

@@ -116,7 +116,10 @@ class FlatParams:
     def adam_step(self, lr, clip, grad_div=1.0, betas=(0.9, 0.999), eps=1e-8, skip=None):
         """clip_gradient (clamp +-clip) then Adam, fused; refreshes the bf16 shadow.  ``skip``: a
         device fp32 word (the step's hand-off error count); nonzero at run time leaves the
-        parameters, moments and shadow unchanged (the step count still advances)."""
+        parameters, moments and shadow unchanged, but the host-side step count still advances
+        (the skip word is only read on the device): a caller that catches the hand-off error from
+        drain_metrics and keeps training runs Adam's bias correction one step ahead of the
+        updates applied -- unlike torch.optim.Adam, which never takes a skipped step."""
         self.sync_shadow()
         self.step_count += 1
         K.clamp_adam(self.flat, self.grad, self.m, self.v, self.shadow, lr, self.step_count, clip,
