@@ -115,15 +115,6 @@ class _EncoderTrain(torch.autograd.Function):
         return (None, None) + grads
 
 
-def _drain(gen):
-    """Run a step generator to its end; its return value."""
-    while True:
-        try:
-            next(gen)
-        except StopIteration as e:
-            return e.value
-
-
 class Encoder(nn.Module):
     def __init__(self, encoded_image_size=7, variant="base", compute_dtype=torch.bfloat16, frozen_fp8=False):
         super().__init__()
@@ -254,13 +245,6 @@ class Encoder(nn.Module):
     def _run_frozen(self, images, upto=8, sd=None):
         """Stem + children [1, upto) of the trunk on the frozen fast path (no saved state).
         Returns (x NHWC in the compute dtype, index of the next CNBlock for the SD scales)."""
-        return _drain(self._run_frozen_steps(images, upto, sd))
-
-    def _run_frozen_steps(self, images, upto=8, sd=None):
-        """_run_frozen as a generator that yields after the stem, each CNBlock and each
-        downsample (the launches in between are issued on the caller's current stream): the
-        pipelined trainer interleaves the CAPTURE of the encoder branch with the decoder's, so
-        the HIP graph's enqueue order alternates between the branches."""
         pk = self._pack()
         if self._packed_epoch != self._weights_epoch:
             self._refresh_trainable(pk, upto)
@@ -272,7 +256,6 @@ class Encoder(nn.Module):
         if images.dtype == torch.uint8 and "norm" not in pk:  # train.py:152 ImageNet normalisation
             pk["norm"] = (torch.tensor(IMAGENET_MEAN, device=dev), torch.tensor(IMAGENET_STD, device=dev))
         K.convnext_stem(images, *pk["stem"], x, norm=pk.get("norm"))
-        yield
         bid = 0
         for st, (blocks, down) in enumerate(pk["stages"]):
             if 1 + 2 * st >= upto:
@@ -323,14 +306,12 @@ class Encoder(nn.Module):
                     K.gemm(hid, blk["w2"], trans_b=True, bias=blk["b2"], colscale=blk["gamma"], rowscale=rs,
                            rows_per_scale=h * w, res=x2, out=x2)
                 bid += 1
-                yield
             if down is not None and 2 + 2 * st < upto:
                 patches = torch.empty(B * (h // 2) * (w // 2), 4 * C, device=dev, dtype=ct)
                 K.ln_patchify2(x, down["lnw"], down["lnb"], patches)
                 C2 = down["w"].shape[0]
                 x = torch.empty(B, h // 2, w // 2, C2, device=dev, dtype=ct)
                 K.gemm(patches, down["w"], trans_b=True, bias=down["b"], out=x.view(-1, C2))
-                yield
         return x, bid
 
     def release_retired(self):
@@ -359,17 +340,10 @@ class Encoder(nn.Module):
         if self.trainable() and torch.is_grad_enabled():
             eng = self.engine()
             return _EncoderTrain.apply(eng, images, *eng.fp.params.values())
-        return _drain(self.forward_steps(images))
-
-    def forward_steps(self, images):
-        """The frozen forward as a generator (see _run_frozen_steps); its return value is
-        forward()'s output."""
-        if not images.is_cuda:
-            raise RuntimeError("Encoder.forward runs on the HIP kernels only; move images to the GPU")
         images = as_input(images)
         B = images.shape[0]
         sd = self._sd_scales(B, images.device) if self.training else None
-        x, _ = yield from self._run_frozen_steps(images, 8, sd)
+        x, _ = self._run_frozen(images, 8, sd)
         s = self.enc_image_size
         if x.shape[1] == s and x.shape[2] == s:
             return x

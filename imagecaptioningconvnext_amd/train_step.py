@@ -37,9 +37,6 @@ from . import kernels as K
 # step ("start") or after the decoder forward ("bwd": the encoder overlaps the backward only).
 # Measured (bench, 1x MI355X, two runs each): C2 8,254 vs 8,366 img/s (within spread), C3 16,605
 # vs 15,108, C4 7,007 vs 6,117 -- "start" stays the default.
-# where the pipelined capture issues the encoder branch: "start" (all of it before the decoder),
-# "bwd" (after the decoder forward) or "interleave" (the Transformer step: a slice of the encoder
-# after each decoder layer's forward and backward)
 PIPE_FORK = os.environ.get("IMGCAP_PIPE_FORK", "start")
 
 
@@ -221,15 +218,14 @@ class TeacherForcedTrainer:
         self._feat_meta = (tuple(feats.shape), feats.dtype)
         return self._dec(feats, caps, caplens, es)
 
-    def _dec(self, feats, caps, caplens, es=None, mid=None, tick=None):
+    def _dec(self, feats, caps, caplens, es=None, mid=None):
         self.decoder.train()
-        tk = {} if tick is None or self.lstm else {"tick": tick}
         if self.lstm:
             s = self.eng.forward(feats, caps, caplens, fixed_T=self._cur_T if self._cur_T else True, alphaC=self.alphaC)
         else:
             if self._cur_T:  # length bucket: the first _cur_T positions (bucket_T)
                 caps = caps[:, :self._cur_T]
-            s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id, **tk)
+            s = self.eng.forward(feats, caps, caplens, pad_id=self.pad_id)
         if mid is not None:
             mid()
         hook = self._buckets is not None and self._hook_mode is not None
@@ -246,7 +242,7 @@ class TeacherForcedTrainer:
                 self._bucket_hook()
             self.enc_eng.backward(es, s["denc"].reshape(feats.shape), **kw)
         else:
-            self.eng.backward(s, **kw, **tk)
+            self.eng.backward(s, **kw)
         if hook and self._hook_mode == "eager":
             self._issued = self._next_bucket
         return s["metrics"]
@@ -412,17 +408,10 @@ class TeacherForcedTrainer:
                     side.wait_stream(cur)
                     with torch.cuda.stream(side):
                         P["feats"][k].copy_(self._encode(P["img"]))
-                tick = None
-                if PIPE_FORK == "interleave" and not self.lstm:
-                    tick, drain = self._encoder_slices(P, k, cur, side)
-                elif PIPE_FORK != "bwd":
+                if PIPE_FORK != "bwd":
                     fork()
-                if os.environ.get("IMGCAP_PIPE_PROBE"):  # diagnostics: a one-block kernel heading the decoder branch
-                    self._seed_ctr.add_(0)
                 m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k],
-                              mid=fork if PIPE_FORK == "bwd" else None, tick=tick)
-                if tick is not None:
-                    drain()
+                              mid=fork if PIPE_FORK == "bwd" else None)
                 cur.wait_stream(side)
                 if split:
                     g = self._end_split_capture(gs)
@@ -432,33 +421,6 @@ class TeacherForcedTrainer:
             pool = g[0].pool() if split else g.pool()
             S["graphs"].append(g)
             S["metrics"].append(m)
-
-    def _encoder_slices(self, P, k, cur, side, per_tick=2):
-        """The encoder branch of a pipelined capture as slices: the side stream forks from the
-        capture stream once (with the first slice, before the decoder); each tick() issues the
-        next `per_tick` steps of the encoder (Encoder.forward_steps) on the side stream; drain()
-        issues the rest and the copy into the feature slot.  Only the capture ORDER changes: the
-        branches have the same nodes and edges as the one-shot fork."""
-        side.wait_stream(cur)
-        state = {"gen": None, "done": False}
-
-        def run(n):
-            if state["done"]:
-                return
-            with torch.cuda.stream(side), torch.no_grad(), K.workspace_slot(1):
-                if state["gen"] is None:
-                    self.encoder.train()
-                    state["gen"] = self.encoder.forward_steps(P["img"])
-                for _ in range(n):
-                    try:
-                        next(state["gen"])
-                    except StopIteration as e:
-                        P["feats"][k].copy_(e.value)
-                        state["done"] = True
-                        return
-
-        run(per_tick)
-        return (lambda: run(per_tick)), (lambda: run(1 << 30))
 
     def _pipe_step(self, imgs, caps, caplens, T=None):
         """Returns the metrics tensor of the previous batch (None on the first call).  T: this

@@ -98,7 +98,7 @@ class TransformerEngine:
 
     # ---------------------------------------------------------------------------------------
     def forward(self, encoder_out, encoded_captions, caption_lengths, *, key_ids=None, pad_id=0, dropout=None,
-                loss=True, tick=None):
+                loss=True):
         fp, ct, dev = self.fp, self.ct, encoder_out.device
         d, ff, V = self.d, self.ff, self.V
         p = self.dec.dropout_p if (dropout is None and self.dec.training) else (dropout or 0.0)
@@ -168,8 +168,6 @@ class TransformerEngine:
                       s2=s2, mu2=mu2, rs2=rs2, x2=x2, hdn=hdn, s3=s3, mu3=mu3, rs3=rs3)
             s["layers"].append(st)
             x = x3
-            if tick is not None:  # the pipelined capture issues a slice of the encoder branch here
-                tick()
         s["mem"] = mem
         s["xL"] = x
         # the decode mask, position l's target caps[:, l+1] (-1 past the decode length) and the zeroed
@@ -345,7 +343,7 @@ class TransformerEngine:
             out.append(self.fp.span([n for n in self.fp.params if n.startswith(pre)]))
         return out
 
-    def backward(self, s, dlogits=None, gbuf=None, want_denc=False, bucket_hook=None, tick=None):
+    def backward(self, s, dlogits=None, gbuf=None, want_denc=False, bucket_hook=None):
         """Gradients of the step into ``gbuf`` (default fp.grad).  With ``bucket_hook`` (DDP) a
         layer's deferred weight / bias gradients run as their own grouped launches when its
         backward is done and the hook is called once per layer (grad_buckets() order), so its
@@ -425,8 +423,6 @@ class TransformerEngine:
             else:
                 K.gemm(dqkv, fp.w(lw("self_attn.in_proj_weight")), out=ds1, beta=1.0)  # dx = ds1 + dqkv W_in
                 dx = ds1
-            if tick is not None:
-                tick()
             if bucket_hook is not None and (i == 0 or not self.merged_layer_bucket):
                 # layer i's gradients final (merged: every layer's): that bucket's all-reduce
                 wgb.run()
