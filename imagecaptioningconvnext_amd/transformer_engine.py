@@ -368,6 +368,7 @@ class TransformerEngine:
         nkv = 2 * d * self.layers
         dkv_all = torch.empty(BP, nkv, device=dev, dtype=ct)  # every layer's dK | dV (forward's kv_all layout)
         carry = None  # (dS3, dY3) of layer i, made at the end of layer i+1's iteration
+
         for i in reversed(range(self.layers)):
             lw = lambda n: self._lw(i, n)  # noqa: E731
             st = s["layers"][i]
