@@ -558,8 +558,16 @@ __global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, in
   constexpr int PSTEP = NT / NV;                      // pixels per load instruction of the block
   constexpr int NPF = (TR * WP + PSTEP - 1) / PSTEP;  // loads per thread for TR new rows
   const long R = (long)B * H;
-  const long rb = (long)blockIdx.x * TR;              // the block's first output row
-  const int cb = blockIdx.y * DW_CT;
+  // 1-D grid of (row tile, channel block) slots laid out XCD-contiguously: XCD x = b % 8 runs
+  // slots x*q + min(x, r) + 0, 1, ... in dispatch order, so the C / DW_CT channel blocks of one
+  // row tile run back to back on one XCD and share its L2 lines (a 32-channel bf16 chunk is half
+  // a 128-byte line; with the channel block as blockIdx.y the other half was fetched again
+  // ~1/3 of the launch later, through another XCD's L2: 170 MB per C3 stage-1 launch against 77)
+  const int ncb = C / DW_CT;
+  const int gsz = gridDim.x, b8 = blockIdx.x % 8, g8q = gsz / 8, g8r = gsz % 8;
+  const int gslot = b8 * g8q + min(b8, g8r) + blockIdx.x / 8;
+  const long rb = (long)(gslot / ncb) * TR;           // the block's first output row
+  const int cb = (gslot % ncb) * DW_CT;
   uint4* img = (uint4*)dsm;
   auto slot = [&](int rr, int px, int s) { return rr * RS + SPPX * px + px / PW + s; };
   constexpr int SPV = VE * (int)sizeof(LT) / 16;  // LDS slots per loaded 16-byte vector (1 or 2)
@@ -1102,7 +1110,7 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
 #define DWR_ALL(P, WC)                                                                                      \
   do {                                                                                                     \
     dw_roll_attr<T, P, WC>();                                                                              \
-    hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8>), dim3((unsigned)tiles, C / DW_CT), dim3(256), shm_r1, \
+    hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8>), dim3((unsigned)(tiles * (C / DW_CT))), dim3(256), shm_r1, \
                        st, B, H, C, (const T*)x, w, bias, (T*)y, (const T*)res, flip);                     \
   } while (0)
   if (W == 56 || W == 28 || W == 14 || W == 7 || W == 64 || W == 32 || W == 16 || W == 8) {
