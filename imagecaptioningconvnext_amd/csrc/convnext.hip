@@ -885,10 +885,17 @@ __global__ __launch_bounds__(512) void dwconv7_cp_kernel(int H, int C, const bf1
                                                          bf16* __restrict__ y, const bf16* __restrict__ res, int flip) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int HB = (H + R - 1) / R;  // R output rows per block (R = 2: each weight row loaded once for both)
-  const long r = blockIdx.x;       // b * HB + row block
+  // (row block, channel group) slots XCD-contiguous: the blocks an XCD runs in dispatch order
+  // are consecutive rows, so the 6 input rows two neighbours share come from that XCD's L2 (with
+  // row blocks dealt round-robin over the 8 XCDs every input row was fetched ~6 times: 57 MB per
+  // C3 stage-3 launch for a 9.6 MB input)
+  const int gy = gridDim.y, gsz = gridDim.x * gy;
+  const int lin = blockIdx.x + blockIdx.y * gridDim.x, b8 = lin % 8;
+  const int gslot = b8 * (gsz / 8) + min(b8, gsz % 8) + lin / 8;
+  const long r = gslot / gy;       // b * HB + row block
   const int h = (int)(r % HB) * R;
   const long b = r / HB;
-  const int c = (blockIdx.y * (blockDim.x >> 6) + wv) * 128 + 2 * lane;
+  const int c = ((gslot % gy) * (blockDim.x >> 6) + wv) * 128 + 2 * lane;
   // the 7 weight pairs of kernel row kh (requested with that row's input, one row ahead)
   // buffer loads: per-lane byte offset in a VGPR, the wave-uniform pixel / tap offset in an SGPR
   // (64-bit addresses per load cost two VGPRs each and spilled); rows outside the image read 0
