@@ -540,8 +540,8 @@ __host__ __device__ constexpr int dw_roll_row_slots(int W, int PW, int sppx) {
 // buffer loads whose range check supplies the zero halo.  Variants measured and removed (round 3,
 // tools/microbench.py dw): 2-4 row tiles per block with a ring (halo fetched once; one block per
 // CU, 1.2-3x slower) and bf16 staged as fp32 (1.2x slower).
-template <typename T, int PW, int WC, int NC, int CT = DW_CT>
-__global__ __launch_bounds__(64 * CT / NC) void dwconv7_roll_kernel(int B, int H, int C, const T* __restrict__ x,
+template <typename T, int PW, int WC, int NC>
+__global__ __launch_bounds__(64 * DW_CT / NC) void dwconv7_roll_kernel(int B, int H, int C, const T* __restrict__ x,
                                                            const float* __restrict__ w,
                                                            const float* __restrict__ bias, T* __restrict__ y,
                                                            const T* res, int flip) {
@@ -549,9 +549,9 @@ __global__ __launch_bounds__(64 * CT / NC) void dwconv7_roll_kernel(int B, int H
   static_assert(WC > 0, "compile-time width");
   using LT = T;  // LDS element type
   constexpr int VE = 16 / sizeof(T);
-  constexpr int NV = CT / VE;
-  constexpr int SPPX = CT * (int)sizeof(LT) / 16;  // 16-byte slots per pixel
-  constexpr int NT = 64 * CT / NC;
+  constexpr int NV = DW_CT / VE;
+  constexpr int SPPX = DW_CT * (int)sizeof(LT) / 16;  // 16-byte slots per pixel
+  constexpr int NT = 64 * DW_CT / NC;
   constexpr int W = WC, GW = W / PW, TR = 64 / GW, WP = W + 6;
   constexpr int RS = dw_roll_row_slots(WC, PW, SPPX);
   constexpr int RING = TR + 6;
@@ -559,15 +559,15 @@ __global__ __launch_bounds__(64 * CT / NC) void dwconv7_roll_kernel(int B, int H
   constexpr int NPF = (TR * WP + PSTEP - 1) / PSTEP;  // loads per thread for TR new rows
   const long R = (long)B * H;
   // 1-D grid of (row tile, channel block) slots laid out XCD-contiguously: XCD x = b % 8 runs
-  // slots x*q + min(x, r) + 0, 1, ... in dispatch order, so the C / CT channel blocks of one
+  // slots x*q + min(x, r) + 0, 1, ... in dispatch order, so the C / DW_CT channel blocks of one
   // row tile run back to back on one XCD and share its L2 lines (a 32-channel bf16 chunk is half
   // a 128-byte line; with the channel block as blockIdx.y the other half was fetched again
   // ~1/3 of the launch later, through another XCD's L2: 170 MB per C3 stage-1 launch against 77)
-  const int ncb = C / CT;
+  const int ncb = C / DW_CT;
   const int gsz = gridDim.x, b8 = blockIdx.x % 8, g8q = gsz / 8, g8r = gsz % 8;
   const int gslot = b8 * g8q + min(b8, g8r) + blockIdx.x / 8;
   const long rb = (long)(gslot / ncb) * TR;           // the block's first output row
-  const int cb = (gslot % ncb) * CT;
+  const int cb = (gslot % ncb) * DW_CT;
   uint4* img = (uint4*)dsm;
   auto slot = [&](int rr, int px, int s) { return rr * RS + SPPX * px + px / PW + s; };
   constexpr int SPV = VE * (int)sizeof(LT) / 16;  // LDS slots per loaded 16-byte vector (1 or 2)
@@ -858,10 +858,10 @@ using namespace imgcap;
 namespace {
 // the rolling kernel's staged rows can exceed the default 64 KB of dynamic LDS: raise the limit
 // once per instantiation (first launch, before any capture)
-template <typename T, int P, int WC, int CT>
+template <typename T, int P, int WC>
 void dw_roll_attr() {
   static const bool done = [] {
-    (void)hipFuncSetAttribute((const void*)dwconv7_roll_kernel<T, P, WC, 8, CT>,
+    (void)hipFuncSetAttribute((const void*)dwconv7_roll_kernel<T, P, WC, 8>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
@@ -1112,25 +1112,13 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
   dim3 grid((unsigned)((R + TR - 1) / TR), C / DW_CT);
   // the rolling kernel (compile-time widths, 8 channels per lane, bf16 / fp32)
   const long tiles = (R + TR - 1) / TR;
-  // channels per block: 16 (2 waves, half the LDS image: ~5 blocks per CU overlap one tile's
-  // loads with another's FMAs) at the wide bf16 stages, 32 otherwise (IMGCAP_DW_ROLL_CT: A/B)
-  static const int ct_env = [] {
-    const char* e = getenv("IMGCAP_DW_ROLL_CT");
-    return e ? atoi(e) : 0;
-  }();
-  const int CTS = (ct_env == 16 || ct_env == 32) ? ct_env : (sizeof(T) == 2 && W >= 28 ? 16 : 32);
-  const int sppx = CTS * (int)sizeof(T) / 16;
+  const int sppx = DW_CT * (int)sizeof(T) / 16;
   const size_t shm_r1 = (size_t)(TR + 6) * dw_roll_row_slots(W, PW, sppx) * 16;
-#define DWR_CT(P, WC, CT_)                                                                                  \
+#define DWR_ALL(P, WC)                                                                                      \
   do {                                                                                                     \
-    dw_roll_attr<T, P, WC, CT_>();                                                                         \
-    hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8, CT_>), dim3((unsigned)(tiles * (C / CT_))),        \
-                       dim3(64 * CT_ / 8), shm_r1, st, B, H, C, (const T*)x, w, bias, (T*)y, (const T*)res, flip); \
-  } while (0)
-#define DWR_ALL(P, WC)              \
-  do {                              \
-    if (CTS == 16) DWR_CT(P, WC, 16); \
-    else DWR_CT(P, WC, 32);         \
+    dw_roll_attr<T, P, WC>();                                                                              \
+    hipLaunchKernelGGL((dwconv7_roll_kernel<T, P, WC, 8>), dim3((unsigned)(tiles * (C / DW_CT))), dim3(256), shm_r1, \
+                       st, B, H, C, (const T*)x, w, bias, (T*)y, (const T*)res, flip);                     \
   } while (0)
   if (W == 56 || W == 28 || W == 14 || W == 7 || W == 64 || W == 32 || W == 16 || W == 8) {
     switch (W) {
@@ -1147,7 +1135,6 @@ int dwconv7_launch(int B, int H, int W, int C, const void* x, const float* w, co
     return 0;
   }
 #undef DWR_ALL
-#undef DWR_CT
   // other widths: the runtime-width channel-tiled kernel
 #define DW_(P)                                                                                                  \
   hipLaunchKernelGGL((dwconv7_kernel<T, P, 0, 8>), grid, dim3(256), shm, st, B, H, W, C, (const T*)x, w, bias, \
