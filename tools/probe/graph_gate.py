@@ -9,7 +9,9 @@ import sys
 import torch
 
 NA = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+KIND = sys.argv[2] if len(sys.argv) > 2 else "sleep"  # "sleep": one block each; "wide": grid-filling
 dev = torch.device("cuda:0")
+big = torch.ones(64 << 20, device=dev)  # 256 MB: a grid-filling elementwise kernel of ~60 us
 side, cap = torch.cuda.Stream(), torch.cuda.Stream()
 x = torch.zeros(1024, device=dev)
 g = torch.cuda.CUDAGraph()
@@ -18,11 +20,25 @@ with torch.cuda.stream(cap):
     cur = torch.cuda.current_stream()
     x.add_(1)
     side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        for _ in range(NA):
-            torch.cuda._sleep(40_000)
-    for _ in range(5):
-        x.mul_(1.0001)
+    ORDER = sys.argv[3] if len(sys.argv) > 3 else "afirst"
+
+    def branch_a():
+        with torch.cuda.stream(side):
+            for _ in range(NA):
+                if KIND == "sleep":
+                    torch.cuda._sleep(40_000)
+                else:
+                    big.mul_(1.0000001)
+
+    def branch_b():
+        for _ in range(5):
+            x.mul_(1.0001)
+    if ORDER == "afirst":
+        branch_a()
+        branch_b()
+    else:
+        branch_b()
+        branch_a()
     cur.wait_stream(side)
     g.capture_end()
 torch.cuda.synchronize()
