@@ -63,6 +63,17 @@ _SYMBOL = {
 }
 
 
+def _dw_symbol(fn, dtype_id, W, C):
+    """The kernel convnext.hip's depthwise dispatch launches (dw_cp_fits, dwconv7_launch)."""
+    bf = dtype_id == _abi.BF16
+    ln = fn == "imgcap_dwconv7_ln"
+    if bf and os.environ.get("IMGCAP_DW_CP", "") != "0" and W in (7, 14) and C % 128 == 0 and (not ln or C <= 1024):
+        return "dwconv7_cp_kernel"
+    if ln:
+        return "dwconv7_ln_kernel"
+    return "dwconv7_roll_kernel" if W in (56, 28, 14, 7, 64, 32, 16, 8) else "dwconv7_kernel"
+
+
 def _esz(dtype_id):
     return 4 if dtype_id == _abi.F32 else 2
 
@@ -119,6 +130,8 @@ def _work(fn, a):
         return sym, sym, "mfma", 2.0 * B * T * macs, _mfma_peak(d.dtype), (B, T, E, D)
     if fn in ("imgcap_mha_fwd", "imgcap_mha_bwd"):
         m = a[0]._obj
+        if m.dtype == _abi.BF16:  # mha.hip dispatch: the bf16 kernels (natural LDS images)
+            sym = sym.replace("_kernel", "_bf16_kernel")
         f = 2.0 * m.B * m.H * m.Lq * m.Lk * m.dh * (2 if fn.endswith("fwd") else 5)
         if m.causal:
             f *= 0.5
@@ -129,6 +142,8 @@ def _work(fn, a):
         return nm, nm, "mfma", 16.0 * M * C * C, PEAK_BF16_TFLOPS, (M, C)
     if fn in ("imgcap_dwconv7", "imgcap_dwconv7_ln", "imgcap_dwconv7_wgrad"):
         e = _esz(a[0])
+        if fn != "imgcap_dwconv7_wgrad":
+            sym = _dw_symbol(fn, a[0], a[3], a[4])
         n = a[1] * a[2] * a[3] * a[4]
         return sym, sym, "hbm", 2.0 * n * e + 50 * a[4] * 4, PEAK_HBM_GBS, (a[1], a[2], a[3], a[4])
     if fn == "imgcap_dwconv7_bwd_data":
