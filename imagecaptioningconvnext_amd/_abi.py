@@ -12,6 +12,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("IMGCAP_LIB") or os.path.join(_HERE, "libimgcap_hip.so")
 
 F32, BF16 = 0, 1
+# imgcap_gemm_plan kinds of the stream-tile configs 1..6 (IMGCAP_GEMM_PT .. IMGCAP_GEMM_PT128K)
+GEMM_PT = 8
 FP8MX = 2
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU = 0, 1, 2, 3
 
@@ -69,6 +71,7 @@ _SIGS = {
     "imgcap_gemm_plan": [c_int] * 6 + [c_int64, c_int64, c_int, c_int, c_void_p],
     "imgcap_gemm_plan_ep": [c_int] * 6 + [c_int64, c_int64, c_int, c_void_p, c_void_p],
     "imgcap_gemm_set_pt": [c_int],
+    "imgcap_gemm_get_pt": [],
     "imgcap_dwconv7": [c_int] * 5 + [c_void_p] * 5,
     "imgcap_cnblock_mlp": [c_int, c_int] + [c_void_p] * 9 + [c_int, c_void_p, c_void_p],
     "imgcap_stochastic_depth_scales": [c_int, c_int, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p],
@@ -137,6 +140,8 @@ _SIGS = {
 }
 
 _lib = None
+# include/imgcap_abi.h IMGCAP_ABI_VERSION (tests/test_abi_cpu.py checks the two agree)
+ABI_VERSION = 6
 
 
 def lib():
@@ -153,6 +158,9 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = c_int
+        if L.imgcap_version() != ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH}: ABI revision {L.imgcap_version()}, this binding expects "
+                               f"{ABI_VERSION} (include/imgcap_abi.h IMGCAP_ABI_VERSION): rebuild the library")
         _lib = L
     return _lib
 

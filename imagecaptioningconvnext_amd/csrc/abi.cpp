@@ -28,12 +28,19 @@ const uint64_t* g_seed_ctr = nullptr;
 // imgcap_workspace_needed reports the size to attach.  Only a (device, slot) the caller never
 // attached falls back to a library-owned, grow-only allocation (a grown buffer is not freed: a
 // captured HIP graph may still reference it).
+// One scratch buffer serves every call of a slot, so two streams of ONE captured graph must never
+// both request it: their nodes are unordered unless the code joined them, and the round-5 scratch
+// race was exactly that.  Each slot remembers the capture (id) and stream of its last
+// request; a request from another stream of the same capture is refused (nothing is enqueued, the
+// call fails with the message below) -- a check in the library, not a convention of two callers.
 constexpr int MAX_DEV = 64;
 struct Ws {
   void* p = nullptr;
   size_t bytes = 0;
   size_t needed = 0;
   bool caller = false;
+  unsigned long long cap_id = 0;  // capture of the last request made while capturing (0: none)
+  hipStream_t cap_stream = nullptr;
 };
 static std::mutex g_ws_mu;
 static Ws g_ws[MAX_DEV][2];
@@ -49,10 +56,22 @@ static Ws* ws_entry(int slot) {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return nullptr;
   return &g_ws[dev][slot];
 }
-void* workspace(size_t bytes, hipStream_t) {
+void* workspace(size_t bytes, hipStream_t stream) {
   std::lock_guard<std::mutex> lk(g_ws_mu);
   Ws* w = ws_entry(g_ws_slot);
   if (!w) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  if (stream && hipStreamGetCaptureInfo(stream, &cs, &cid) == hipSuccess && cs == hipStreamCaptureStatusActive) {
+    if (w->cap_id == cid && w->cap_stream != stream) {
+      set_error("library workspace: slot " + std::to_string(g_ws_slot) +
+                " scratch requested from two streams of one captured graph (unordered branches would share it; "
+                "select another slot with imgcap_workspace_slot on one of them)");
+      return nullptr;
+    }
+    w->cap_id = cid;
+    w->cap_stream = stream;
+  }
   w->needed = std::max(w->needed, bytes);
   if (bytes <= w->bytes) return w->p;
   if (w->caller) {
@@ -91,7 +110,7 @@ extern "C" int imgcap_set_seed_counter(const uint64_t* counter) {
 }
 
 extern "C" const char* imgcap_last_error_string(void) { return imgcap::g_last_error.c_str(); }
-extern "C" int imgcap_version(void) { return 1; }
+extern "C" int imgcap_version(void) { return IMGCAP_ABI_VERSION; }
 
 extern "C" int imgcap_workspace_attach(int slot, void* ptr, uint64_t bytes) {
   if (slot < 0 || slot > 1) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_attach: slot 0 or 1");

@@ -117,13 +117,26 @@ DEV float block_sum(float v, float* red) {
 // recompute it instead of storing it.
 // 32-bit arithmetic: the key (seed, stream) is uniform across a launch and folds once; per
 // element, the counter times an odd constant XOR the key through murmur3's fmix32 -- a bijection
-// of the counter for a fixed key, ~10 VALU operations (the round-4 64-bit mix cost ~30, 1.3-1.5 us
-// per attention / add+LayerNorm launch at dropout 0.1)
+// of the counter for a fixed key, ~11 VALU operations (the round-4 64-bit mix cost ~30, 1.3-1.5 us
+// per attention / add+LayerNorm launch at dropout 0.1).  The key goes in twice: XORed into the
+// counter, and its own fmix32 image after the first multiply, so two sites' masks are not the
+// same function of XOR-shifted counters.  Trade-off, kept deliberately: 2^32 key
+// streams, so over ~2^16 (site, step) pairs two may draw the same mask (birthday bound); dropout
+// needs independent-looking masks per site, not cryptographic separation.
+DEV uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  return x ^ (x >> 16);
+}
 DEV uint32_t hash3(uint64_t seed, uint32_t stream, uint64_t idx) {
   const uint32_t key = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x85EBCA6Bu) ^ ((stream + 1u) * 0x9E3779B9u);
+  const uint32_t key2 = fmix32(key ^ 0x5BD1E995u);  // launch-uniform: hoisted out of element loops
   uint32_t x = ((uint32_t)idx * 0xCC9E2D51u) ^ ((uint32_t)(idx >> 32) * 0x1B873593u) ^ key;
   x ^= x >> 16;
   x *= 0x85EBCA6Bu;
+  x ^= key2;
   x ^= x >> 13;
   x *= 0xC2B2AE35u;
   x ^= x >> 16;

@@ -586,7 +586,7 @@ static double pt_estimate(int c, int M, int N, int K, int cus) {
 // epilogue's operands (and the residual of a transposed layout) only by spilling, so those forms
 // take the 64x32 / 64x48 wave tiles
 static bool pt_allowed(int c, int ek, bool ak, bool bk, int K) {
-  if (K % (64 * pt_cfg(c).ks)) return false;  // 128-deep k-steps: no K tail
+  if (pt_cfg(c).ks > 1 && K % (64 * pt_cfg(c).ks)) return false;  // 128-deep k-steps: no K tail
   if (c == 6) return ek == 0 || (ek == 1 && ak && bk);
   if (ek == 2) return c == 3;
   if (ek == 1 && !(ak && bk)) return c == 3 || c == 4;
@@ -1290,6 +1290,8 @@ extern "C" int imgcap_gemm_set_pt(int mode) {
   g_gemm_pt_mode = mode;
   return 0;
 }
+
+extern "C" int imgcap_gemm_get_pt(void) { return g_gemm_pt_mode; }
 
 extern "C" int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda,
                                    int64_t ldb, int batch, const imgcap_epilogue* epi, int* splits) {

@@ -627,6 +627,10 @@ static int check(const imgcap_mha_desc* d) {
                  "mha: q/k/v must be 16-byte aligned with 16-byte row strides");
   return 0;
 }
+// the bf16 kernels write 4 consecutive outputs per lane as one 8-byte store
+static bool out_ok(int dtype, const void* p, long ld) {
+  return dtype != IMGCAP_BF16 || (((uintptr_t)p & 7) == 0 && ld % 4 == 0);
+}
 
 }  // namespace imgcap
 
@@ -634,6 +638,7 @@ using namespace imgcap;
 
 extern "C" int imgcap_mha_fwd(const imgcap_mha_desc* d, void* stream) {
   if (int rc = check(d)) return rc;
+  IMGCAP_REQUIRE(out_ok(d->dtype, d->o, d->ldo), "mha fwd: bf16 o must be 8-byte aligned with ldo % 4 == 0");
   const dim3 grid(d->B * d->H);
   if (d->dtype == IMGCAP_BF16)
     hipLaunchKernelGGL(mha_fwd_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, *d, g_seed_ctr);
@@ -649,6 +654,8 @@ extern "C" int imgcap_mha_bwd(const imgcap_mha_desc* d, void* stream) {
   IMGCAP_REQUIRE(d->kv_rows == 0 || d->kv_rows == d->Lk, "mha bwd: kv_rows (key/value cache stride) is fwd-only");
   const int vec = d->dtype == IMGCAP_F32 ? 4 : 8;
   IMGCAP_REQUIRE(d->lddo % vec == 0 && aligned16(d->dout), "mha bwd: dout alignment");
+  IMGCAP_REQUIRE(out_ok(d->dtype, d->dq, d->lddq) && out_ok(d->dtype, d->dk, d->lddk) && out_ok(d->dtype, d->dv, d->lddv),
+                 "mha bwd: bf16 dq / dk / dv must be 8-byte aligned with pitches % 4 == 0");
   const dim3 grid(d->B * d->H);
   static bool attr_set = false;
   if (!attr_set) {  // the f32 backward needs > 64 KiB of dynamic LDS

@@ -9,7 +9,7 @@ import os
 import torch
 
 from . import _abi
-from ._abi import ACT_DGELU, ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, Epilogue  # noqa: F401
+from ._abi import ACT_DGELU, ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, GEMM_PT, Epilogue  # noqa: F401
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -66,6 +66,38 @@ class workspace_slot:
         _abi.call("imgcap_workspace_slot", 0)
 
 
+# ---- stream forks inside captured steps --------------------------------------------------------
+# A side stream forked from the capturing stream must be joined back before capture_end: an
+# un-joined branch leaves the graph without its tail (round 5 saw a host segfault inside the
+# runtime's capture_end in a variant that swapped the two branches' streams).  The
+# engines and the trainer fork and join through these two calls, and the trainer asserts before
+# every capture_end that nothing forked is still open.
+_open_forks = {}
+
+
+def fork(side, src):
+    """``side`` waits for ``src``'s work so far and is recorded as an open branch."""
+    side.wait_stream(src)
+    _open_forks[side.cuda_stream] = side
+
+
+def join(dst, side, event=None):
+    """``dst`` waits for ``side`` (for ``event``, which the caller recorded as side's LAST work of
+    the branch); the branch is closed."""
+    if event is None:
+        dst.wait_stream(side)
+    else:
+        dst.wait_event(event)
+    _open_forks.pop(side.cuda_stream, None)
+
+
+def assert_joined(where):
+    if _open_forks:
+        names = ", ".join(hex(k) for k in _open_forks)
+        _open_forks.clear()
+        raise RuntimeError(f"{where}: side stream(s) {names} forked inside the capture and never joined")
+
+
 def gemm_set_policy(glds256):
     """-1 by shape (default), 0 never, 1 always use the 256x256 GEMM tile where eligible."""
     _abi.call("imgcap_gemm_set_policy", int(glds256))
@@ -76,6 +108,26 @@ def gemm_set_pt(mode):
     wherever eligible (cost-model tile), 2..7 wherever eligible with tile 256x128 / 128x256 /
     128x128 / 128x192 / 128x128 (4 waves, two blocks a CU) / 128x128 (128-deep k-steps)."""
     _abi.call("imgcap_gemm_set_pt", int(mode))
+
+
+def gemm_get_pt():
+    """The stream-tile policy currently set (imgcap_gemm_get_pt)."""
+    return int(_abi.lib().imgcap_gemm_get_pt())
+
+
+class gemm_pt_mode:
+    """``with gemm_pt_mode(m):`` -- the stream-tile policy m inside, the previous one restored after
+    (tests and tools: a hard-coded reset would change the library default for later callers)."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = gemm_get_pt()
+        gemm_set_pt(self.mode)
+
+    def __exit__(self, *a):
+        gemm_set_pt(self.prev)
 
 
 def gemm_plan(dtype, a_kmajor, b_kmajor, M, N, K, lda, ldb, batch=1, split_k=0, ep=None):

@@ -163,10 +163,10 @@ class LstmEngine:
                     setattr(sd, k, v.data_ptr())
             st = main if i == 0 else self._streams[i - 1]
             if i:
-                st.wait_stream(main)
+                K.fork(st, main)
             _abi.call(fn, ctypes.byref(sd), st.cuda_stream)
         for st in self._streams[:len(rows) - 1]:
-            main.wait_stream(st)
+            K.join(main, st)
 
     # ---------------------------------------------------------------------------------------
     def _side_stream(self, dev):
@@ -241,7 +241,7 @@ class LstmEngine:
         side = self._side_stream(dev)
         # att1 = enc W_ea (decoder.py:61, hoisted out of the loop) on the side stream, beside the
         # init_h / init_c and W_ih-embedding products (no library scratch: 64x64 tile, one pass)
-        side.wait_stream(main)
+        K.fork(side, main)
         with torch.cuda.stream(side):
             att1 = K.gemm(enc_s.view(B * P, E), w["wea"], trans_b=True, bias=w["bea"])
             ev_att1 = torch.cuda.Event()
@@ -282,7 +282,7 @@ class LstmEngine:
                                       torch.full_like(caps_s[:, 1:T + 1], -1)).reshape(-1)
         main.wait_event(ev_att1)
         self._launch("imgcap_lstm_tf_fwd", d)
-        main.wait_stream(side)
+        K.join(main, side)
         for t_ in (wzh_t, watt_t, tmask) + ((targets,) if loss else ()):
             t_.record_stream(main)
         # ---- fc(dropout(h)) over all B*T rows (decoder.py:109) ----------------------------------
@@ -307,7 +307,7 @@ class LstmEngine:
 
             # the attention regulariser (train.py:268: its value and d alpha, which the backward
             # recurrence reads) on the side stream, beside the vocab projection and the CE
-            side.wait_stream(main)
+            K.fork(side, main)
             with torch.cuda.stream(side):
                 _abi.call("imgcap_attn_reg", B, T, P, alphas.data_ptr(), dl.data_ptr(), alphaC, dalpha.data_ptr(),
                           reg.data_ptr(), K.stream())
@@ -315,7 +315,7 @@ class LstmEngine:
                 ev_reg.record(side)
 
             def finalize():
-                main.wait_event(ev_reg)
+                K.join(main, side, ev_reg)
                 K.loss_finalize(lrow, hit, targets, reg, metrics)
             K.ce_train(logits, targets, V, metrics, lse, lrow, hit, dlogits, finalize)
             self._fold_status(metrics[4:5], init=True)  # the forward recurrence's error word
@@ -446,7 +446,7 @@ class LstmEngine:
                      drop_ld=D)
         main = torch.cuda.current_stream(dev)
         side = self._side_stream(dev)
-        side.wait_stream(main)
+        K.fork(side, main)
         with torch.cuda.stream(side):  # no library scratch on this stream (no split-K, one-pass colsum)
             # the gradient buffer is cleared here, beside the recurrence (60 MB at C2, not on the
             # critical path); the main stream joins this stream before its first gradient write
@@ -501,7 +501,7 @@ class LstmEngine:
         # the two branches: the grouped GEMMs and colsum_multi take none).  With DDP the early
         # bucket's all-reduce takes that window instead (the hook after the embedding gradient).
         if par_tail:
-            side.wait_stream(main)
+            K.fork(side, main)
             with torch.cuda.stream(side):
                 if "metrics" in s:
                     self._fold_status(s["metrics"][4:5])  # the backward recurrence's error word
@@ -521,7 +521,7 @@ class LstmEngine:
         if not par_tail:
             # embedding: d_emb = dgates W_ih[:, :M]  -> scatter-add rows
             demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)
-            main.wait_stream(side)  # gbuf cleared, fc dW / db (beside the recurrence) done
+            K.join(main, side)  # gbuf cleared, fc dW / db (beside the recurrence) done
             K.embedding_bwd(s["ids"], demb, _G.g("embedding.weight"))
         # init_h / init_c from dh0, dc0
         dinit = torch.cat([dh, dc], dim=1).to(ct)
@@ -537,7 +537,7 @@ class LstmEngine:
         wgb.run()
         cb.run()
         if par_tail:
-            main.wait_stream(side)  # the embedding gradient and the metrics' error word
+            K.join(main, side)  # the embedding gradient and the metrics' error word
         s["denc"] = None
         if want_denc:
             # decoder.py:26 (att1 = enc W_ea), :64-66 (mean -> init_h/c), :102-103 (context)

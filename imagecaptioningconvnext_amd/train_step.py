@@ -67,7 +67,7 @@ class _SeqGraphs:
 
 class TeacherForcedTrainer:
     def __init__(self, encoder, decoder, *, lstm, decoder_lr=1e-4, encoder_lr=1e-4, grad_clip=5.0, alphaC=1.0,
-                 pad_id=0, process_group=None, graph=False, pipeline=False, len_buckets=True):
+                 pad_id=0, process_group=None, graph=False, pipeline=False, len_buckets=True, collectives="auto"):
         self.encoder = encoder
         self.decoder = decoder
         self.lstm = lstm
@@ -78,6 +78,15 @@ class TeacherForcedTrainer:
         self.pad_id = pad_id
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        # the DDP path (buckets, hooks, split graphs, the comm stream, the metric all-reduce): with
+        # more than one rank ("auto"), or "always" -- one rank of an initialised process group going
+        # through every collective of the step (tests: a 1-rank RCCL group executes the same
+        # schedule the 8-rank node does, bitwise the no-collective step)
+        if collectives not in ("auto", "always"):
+            raise ValueError("collectives: 'auto' or 'always'")
+        if collectives == "always" and not (dist.is_available() and dist.is_initialized()):
+            raise ValueError("collectives='always' needs an initialised process group")
+        self.ddp = self.world > 1 or collectives == "always"
         self.eng = decoder.engine()
         self._metric_log = []
         # LSTM length buckets (decoder.py:91,100-111: steps t >= a caption's decode length do no
@@ -117,9 +126,9 @@ class TeacherForcedTrainer:
         self._next_bucket = 0    # hook calls so far in the step being run / captured
         self._issued = 0         # buckets already in flight when _update runs
         self._comm = None
-        if self.world > 1 and torch.cuda.is_available() and self.eng.fp.grad.is_cuda:
+        if self.ddp and torch.cuda.is_available() and self.eng.fp.grad.is_cuda:
             self._comm = torch.cuda.Stream(device=self.eng.fp.grad.device)
-        if self.world > 1:
+        if self.ddp:
             # DDP construction broadcasts rank 0's parameters (trainMultiGPU.py:233); the encoder is
             # broadcast too because its weights are randomly initialised here (SURVEY.md §7 v)
             dist.broadcast(self.eng.fp.flat, 0, group=process_group)
@@ -139,7 +148,7 @@ class TeacherForcedTrainer:
         bucket covers is reduced in _update.  Every element is summed once either way, so the
         averaged gradients are the same as one all-reduce of each flat buffer."""
         self._buckets = None
-        if self.world == 1 or not hasattr(self.eng, "grad_buckets"):
+        if not self.ddp or not hasattr(self.eng, "grad_buckets"):
             return
         if hasattr(self.eng, "merged_layer_bucket"):
             # pipelined frozen-encoder schedule: the next batch's encoder branch joins the captured
@@ -287,8 +296,9 @@ class TeacherForcedTrainer:
             cur = torch.cuda.current_stream()
             if not joined:
                 for st in (join or ()):
-                    cur.wait_stream(st)
+                    K.join(cur, st)
                 joined.append(True)
+            K.assert_joined("split capture")
             graphs[-1].capture_end()
             g = torch.cuda.CUDAGraph()
             g.capture_begin(pool=graphs[0].pool())
@@ -301,6 +311,7 @@ class TeacherForcedTrainer:
     def _end_split_capture(self, graphs):
         self._hook_mode = None
         self._split = None
+        K.assert_joined("split capture")
         graphs[-1].capture_end()
         return tuple(graphs)
 
@@ -342,6 +353,7 @@ class TeacherForcedTrainer:
             self._seed_ctr.add_(1)
             feats, es = self._enc_part(self._inputs[0])
             self._feat_slot.copy_(feats)
+            K.assert_joined("encoder graph")
         self._enc_saved = es  # the fine-tuned children's activations live in ge's pool
         if self._buckets is not None:  # decoder half split at the bucket hooks (DDP)
             cap = torch.cuda.Stream(device=dev)
@@ -357,6 +369,7 @@ class TeacherForcedTrainer:
         gd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gd):
             self._metrics = self._dec(self._feat_slot, self._inputs[1], self._inputs[2], es)
+            K.assert_joined("decoder graph")
         self._graph = _SeqGraphs(ge, gd)
 
     # ---- encoder / decoder pipeline ------------------------------------------------------------
@@ -405,17 +418,18 @@ class TeacherForcedTrainer:
                 cur = torch.cuda.current_stream(dev)
 
                 def fork(k=k, cur=cur):
-                    side.wait_stream(cur)
+                    K.fork(side, cur)
                     with torch.cuda.stream(side):
                         P["feats"][k].copy_(self._encode(P["img"]))
                 if PIPE_FORK != "bwd":
                     fork()
                 m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k],
                               mid=fork if PIPE_FORK == "bwd" else None)
-                cur.wait_stream(side)
+                K.join(cur, side)
                 if split:
                     g = self._end_split_capture(gs)
                 else:
+                    K.assert_joined("pipelined step graph")
                     g.capture_end()
             main.wait_stream(cap)
             pool = g[0].pool() if split else g.pool()
@@ -539,7 +553,7 @@ class TeacherForcedTrainer:
         ranks (trainMultiGPU.py:96-108, 398-403), reduced before the update so every rank skips
         the same steps."""
         fp = self.eng.fp
-        if self.world == 1:
+        if not self.ddp:
             red = m.clone()
         else:
             zero = torch.zeros((), device=m.device, dtype=m.dtype)
@@ -547,7 +561,7 @@ class TeacherForcedTrainer:
             dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.pg)
             red[0] = red[0] / red[1]  # global token-weighted mean loss, back in m's layout
         skip = red[4:5] if red.numel() > 4 else None
-        if self.world > 1:
+        if self.ddp:
             # the buckets issued during the backward are in flight on the comm stream; the ranges
             # none of them covers follow on the same stream, then clip + Adam wait for all of it
             issued = self._buckets[:self._issued] if self._buckets else []

@@ -449,7 +449,7 @@ class TransformerEngine:
             # are independent, and the step ends with them alone on the chip
             main = torch.cuda.current_stream(dev)
             side = self._side_stream(dev)
-            side.wait_stream(main)
+            K.fork(side, main)
             # the operands the side stream reads were allocated on the main stream: held until the
             # join, so the caching allocator cannot hand their blocks to a main-stream allocation
             # while the column sums still read them (the round-4 side-stream drift)
@@ -457,7 +457,7 @@ class TransformerEngine:
             with torch.cuda.stream(side):
                 cb.run()
             wgb.run()
-            main.wait_stream(side)
+            K.join(main, side)
             del held
         else:
             wgb.run()

@@ -49,6 +49,10 @@ int imgcap_workspace_slot(int slot);
 int imgcap_workspace_attach(int slot, void* ptr, uint64_t bytes);
 /* Largest scratch request seen so far in `slot` on the current device (what to attach). */
 int imgcap_workspace_needed(int slot, uint64_t* bytes);
+/* ABI revision of this header; imgcap_version() returns the library's.  Bumped whenever an
+ * entry point changes meaning or arity (6: imgcap_add_layernorm_bwd's per-block partials
+ * argument, imgcap_gemm_get_pt; bindings refuse a library of another revision). */
+#define IMGCAP_ABI_VERSION 6
 int imgcap_version(void);
 
 /* Device-resident step counter mixed into every dropout / stochastic-depth seed at kernel
@@ -152,6 +156,8 @@ int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M, int N, int
  * IMGCAP_GEMM_PT128K; a config not built for the call's epilogue form or K falls back to the cost
  * model). */
 int imgcap_gemm_set_pt(int mode);
+/* The current stream-tile policy (what imgcap_gemm_set_pt last set; -1 unless changed). */
+int imgcap_gemm_get_pt(void);
 /* Kernel-selection policy for A/B tests and benchmarks: glds256 >= 1 serves every eligible
  * GEMM (bf16, unsplit, 16-byte operand pitches) with the 256x256 tile (1: 64-deep k-steps x 2
  * stages, 2: 32-deep x 4 stages, 3: 32-deep x 3 stages), 0 never, 4 = the 128x128 LDS-DMA tile

@@ -7,6 +7,18 @@ transformer_tf_forward models/transformerDecoder.py:88-108 (+ PositionalEncoding
                        torch.nn.TransformerDecoderLayer's post-norm (norm_first=False) math
                        with ReLU FFN, as constructed at transformerDecoder.py:82-83.
 Dropout is the identity here (parity runs use p=0 / eval, SURVEY.md §7 hard part iv).
+
+``numerics="bf16"`` (transformer_tf_forward) emulates the HIP bf16 build's storage points, so the
+bf16 gates measure the engine rather than bf16 itself (as oracle/convnext.py's mode does for the
+encoder).  Every tensor the engine keeps in bf16 is rounded to bf16 here, in the forward (value)
+and in the backward (its gradient), at the same place: GEMM outputs after bias / ReLU, the
+embedding + positional sum, each residual sum s = x + y the LayerNorm reads and the LayerNorm
+output, the attention probabilities before P V, the score gradient dS before dQ = dS K /
+dK = dS^T Q, the logits and dlogits.  Sums the engine forms in fp32 stay fp32 (softmax, LayerNorm
+statistics, the memory gradient over the six layers' K/V products, weight-gradient products,
+bias column sums); the encoder_proj weight gradient reads the memory gradient rounded to bf16,
+its bias gradient the fp32 one (transformer_engine.py backward).  Weights are given already
+rounded (the engine multiplies its bf16 shadow copies).
 """
 import math
 
@@ -16,6 +28,78 @@ import torch.nn.functional as F
 
 def _lin(x, p, name):
     return x @ p[name + ".weight"].t() + p[name + ".bias"]
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _RoundBoth(torch.autograd.Function):
+    """bf16 storage point: the value rounded in the forward, its gradient in the backward."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return _bf(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _bf(g)
+
+
+class _RoundValue(torch.autograd.Function):
+    """An MFMA operand rounded to bf16 whose gradient stays fp32 (the attention probabilities)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return _bf(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGrad(torch.autograd.Function):
+    """Identity forward; the gradient rounded to bf16 (dS before the dQ / dK products)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        return _bf(g)
+
+
+class _ProjBf16(torch.autograd.Function):
+    """memory = enc W^T + b with the engine's gradients: dW from the fp32 memory gradient rounded
+    to bf16 (dmem_c), db from the fp32 one, d enc = bf16(dmem) W."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return _bf(x @ w.t() + b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        gc = _bf(g)
+        gx = gc @ w
+        gw = gc.reshape(-1, gc.shape[-1]).t() @ x.reshape(-1, x.shape[-1])
+        gb = g.reshape(-1, g.shape[-1]).sum(0)
+        return gx, gw, gb
+
+
+_IDENT = staticmethod(lambda t: t)
+
+
+class _Fp32:
+    both = value = grad = _IDENT
+
+
+class _Bf16:
+    both = staticmethod(_RoundBoth.apply)
+    value = staticmethod(_RoundValue.apply)
+    grad = staticmethod(_RoundGrad.apply)
 
 
 def lstm_tf_forward(p, encoder_out, encoded_captions, caption_lengths):
@@ -69,52 +153,78 @@ def positional_encoding(embed_dim, max_len, dtype=torch.float32):
     return pe.unsqueeze(0).to(dtype)
 
 
-def _mha(xq, xkv, p, pre, nhead, attn_mask=None, key_pad=None):
-    """torch MultiheadAttention (batch-first restatement): packed in_proj [3d, d], out_proj."""
+def _mha(xq, xkv, p, pre, nhead, attn_mask=None, key_pad=None, nm=_Fp32, kv=None):
+    """torch MultiheadAttention (batch-first restatement): packed in_proj [3d, d], out_proj.
+    ``kv`` (bf16 mode): the cross-attention K | V already projected (the engine's one GEMM over
+    every layer's stacked W_kv, a storage point of its own)."""
     B, Lq, d = xq.shape
     Lk = xkv.shape[1]
     W, bias = p[pre + ".in_proj_weight"], p[pre + ".in_proj_bias"]
-    q = xq @ W[:d].t() + bias[:d]
-    k = xkv @ W[d:2 * d].t() + bias[d:2 * d]
-    v = xkv @ W[2 * d:].t() + bias[2 * d:]
+    if nm is _Fp32:
+        q = xq @ W[:d].t() + bias[:d]
+        k = xkv @ W[d:2 * d].t() + bias[d:2 * d]
+        v = xkv @ W[2 * d:].t() + bias[2 * d:]
+    elif xq is xkv:  # self-attention: one qkv GEMM
+        qkv = nm.both(xq @ W.t() + bias)
+        q, k, v = qkv[..., :d], qkv[..., d:2 * d], qkv[..., 2 * d:]
+    else:
+        q = nm.both(xq @ W[:d].t() + bias[:d])
+        if kv is None:
+            kv = nm.both(xkv @ W[d:].t() + bias[d:])
+        k, v = kv[..., :d], kv[..., d:]
     dh = d // nhead
-    q = q.view(B, Lq, nhead, dh).transpose(1, 2)
-    k = k.view(B, Lk, nhead, dh).transpose(1, 2)
-    v = v.view(B, Lk, nhead, dh).transpose(1, 2)
-    s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    q = q.reshape(B, Lq, nhead, dh).transpose(1, 2)
+    k = k.reshape(B, Lk, nhead, dh).transpose(1, 2)
+    v = v.reshape(B, Lk, nhead, dh).transpose(1, 2)
+    s = nm.grad(q @ k.transpose(-1, -2)) / math.sqrt(dh)
     if attn_mask is not None:
         s = s.masked_fill(attn_mask.view(1, 1, Lq, Lk), float("-inf"))
     if key_pad is not None:
         s = s.masked_fill(key_pad.view(B, 1, 1, Lk), float("-inf"))
     a = torch.softmax(s, dim=-1)
-    o = (a @ v).transpose(1, 2).reshape(B, Lq, d)
+    o = nm.both((nm.value(a) @ v).transpose(1, 2).reshape(B, Lq, d))
     return o @ p[pre + ".out_proj.weight"].t() + p[pre + ".out_proj.bias"]
 
 
 def transformer_tf_forward(p, encoder_out, encoded_captions, caption_lengths, tgt_key_padding_mask,
-                           nhead, num_layers, pe=None):
-    """Returns (predictions[B,L,V], encoded_captions, decode_lengths)."""
+                           nhead, num_layers, pe=None, numerics="fp32"):
+    """Returns (predictions[B,L,V], encoded_captions, decode_lengths).  ``numerics``: "fp32", or
+    "bf16" (the HIP bf16 build's storage points, module docstring)."""
+    nm = {"fp32": _Fp32, "bf16": _Bf16}[numerics]
     B = encoder_out.size(0)
     E = encoder_out.size(-1)
     dls = (caption_lengths.squeeze(1) - 1).tolist()                          # transformerDecoder.py:92
     enc = encoder_out.reshape(B, -1, E)
-    if "encoder_proj.weight" in p:
-        mem = _lin(enc, p, "encoder_proj")                                   # transformerDecoder.py:95
+    if "encoder_proj.weight" in p:                                           # transformerDecoder.py:95
+        if nm is _Fp32:
+            mem = _lin(enc, p, "encoder_proj")
+        else:
+            mem = _ProjBf16.apply(enc, p["encoder_proj.weight"], p["encoder_proj.bias"])
     else:
         mem = enc
     x = p["embedding.weight"][encoded_captions]                              # :97
     L, d = x.shape[1], x.shape[2]
     if pe is None:
         pe = positional_encoding(d, L)
-    x = x + pe[:, :L].to(x.dtype)                                            # :98 (dropout = id)
+    x = nm.both(x + pe[:, :L].to(x.dtype))                                   # :98 (dropout = id)
     causal = torch.triu(torch.ones(L, L, dtype=torch.bool), diagonal=1)     # :102
+    kv_all = None
+    if nm is not _Fp32:  # the engine's stacked cross-attention K | V GEMM (one storage point)
+        pl = [f"transformer_decoder.layers.{li}.multihead_attn." for li in range(num_layers)]
+        wkv = torch.cat([p[q + "in_proj_weight"][d:] for q in pl])
+        bkv = torch.cat([p[q + "in_proj_bias"][d:] for q in pl])
+        kv_all = nm.both(mem @ wkv.t() + bkv)
+
+    def add_ln(x, y, pre, k):
+        s = nm.both(x + nm.both(y))
+        return nm.both(F.layer_norm(s, (d,), p[pre + f"norm{k}.weight"], p[pre + f"norm{k}.bias"], 1e-5))
+
     for li in range(num_layers):                                             # :104
         pre = f"transformer_decoder.layers.{li}."
-        x = F.layer_norm(x + _mha(x, x, p, pre + "self_attn", nhead, causal, tgt_key_padding_mask),
-                         (d,), p[pre + "norm1.weight"], p[pre + "norm1.bias"], 1e-5)
-        x = F.layer_norm(x + _mha(x, mem, p, pre + "multihead_attn", nhead),
-                         (d,), p[pre + "norm2.weight"], p[pre + "norm2.bias"], 1e-5)
-        ff = _lin(torch.relu(_lin(x, p, pre + "linear1")), p, pre + "linear2")
-        x = F.layer_norm(x + ff, (d,), p[pre + "norm3.weight"], p[pre + "norm3.bias"], 1e-5)
-    preds = _lin(x, p, "fc_out")                                             # :106
+        x = add_ln(x, _mha(x, x, p, pre + "self_attn", nhead, causal, tgt_key_padding_mask, nm), pre, 1)
+        kv = None if kv_all is None else kv_all[..., 2 * d * li:2 * d * (li + 1)]
+        x = add_ln(x, _mha(x, mem, p, pre + "multihead_attn", nhead, nm=nm, kv=kv), pre, 2)
+        ff = _lin(nm.both(torch.relu(_lin(x, p, pre + "linear1"))), p, pre + "linear2")
+        x = add_ln(x, ff, pre, 3)
+    preds = nm.both(_lin(x, p, "fc_out"))                                    # :106
     return preds, encoded_captions, dls

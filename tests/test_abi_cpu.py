@@ -21,7 +21,12 @@ def test_library_loads_and_exports_all():
     L = _abi.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.imgcap_version() == 1
+    assert L.imgcap_version() == _abi.ABI_VERSION
+
+
+def test_abi_version_matches_header():
+    m = re.search(r"#define\s+IMGCAP_ABI_VERSION\s+(\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == _abi.ABI_VERSION
 
 
 def _declared_arity():

@@ -48,6 +48,39 @@ def test_encoder_vs_oracle(hip_device, variant, hw, dtype):
         assert _rel(out, ref) < 1.5e-2
 
 
+@pytest.mark.parametrize("variant,B", [("tiny", 64), ("base", 32)])
+def test_encoder_bench_batch_vs_emulating_oracle(hip_device, variant, B):
+    """The encoder at the batch the bench runs (C3: Tiny B = 64; C4: Base B = 32 per GPU), so the
+    by-shape stream-tile GEMM plan (stage-3 M = 12,544 / 6,272 rows: imgcap_gemm pt_by_shape) and
+    the XCD-contiguous block slots of both depthwise kernels run at the sizes they were tuned for
+    (VERDICT r5 weak 2).  The GPU encodes the whole batch and the oracle (bf16-emulating, and fp32)
+    restates every image of it (a few seconds on the host)."""
+    from imagecaptioningconvnext_amd import kernels as K
+    from imagecaptioningconvnext_amd.models.encoder import Encoder
+    from oracle.convnext import VARIANTS
+    assert K.gemm_get_pt() == -1  # the library default plan (no earlier test left another one set)
+    sd = make_params(convnext.param_shapes(variant), 5)
+    enc = Encoder(variant=variant, compute_dtype=torch.bfloat16)
+    enc.load_state_dict(sd)
+    enc = enc.to(hip_device).eval()
+    g = torch.Generator().manual_seed(16)
+    img = torch.randn(B, 3, 224, 224, generator=g)
+    with torch.no_grad():
+        out = enc(img.to(hip_device)).float().cpu()
+        pick = list(range(B))
+        sub = img
+        emu = convnext.encoder_forward(sd, variant, sub, numerics="bf16")
+        ref = convnext.encoder_forward(sd, variant, sub)
+    E = VARIANTS[variant][0][3]
+    assert out.shape == (B, 7, 7, E)
+    err, err32 = _rel(out[pick], emu), _rel(out[pick], ref)
+    print(f"{variant} B={B} bf16 vs bf16-emulating oracle {err:.2e}, vs fp32 {err32:.2e}")
+    assert err < BF16_EMU_TOL
+    assert err32 < 1.5e-2
+    for j, i in enumerate(pick):  # every image on its own, not only the batch norm
+        assert _rel(out[i], emu[j]) < BF16_EMU_TOL, i
+
+
 def test_encoder_stochastic_depth_train_mode(hip_device):
     """train(): per-sample row drop of residual branches; deterministic per seed; eval unaffected."""
     from imagecaptioningconvnext_amd.models.encoder import Encoder

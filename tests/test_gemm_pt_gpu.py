@@ -1,8 +1,10 @@
 """Stream-tile GEMM (csrc/gemm_pt.h): every operand layout, tile config and epilogue form
 against a PyTorch fp32 reference on the bf16-rounded operands, and against the LDS-staged kernels
 (imgcap_gemm_set_pt(0)) on the same call.  Ragged M / N (rows and columns past the last tile), K
-tails (K % 64 != 0; the 128-deep k-step config takes only K % 128 == 0 and passes the rest on), grids with more tiles than CUs (persistent rounds, the cross-tile prefetch)
-and fewer."""
+tails (K % 64 != 0, on the 64-deep configs; the 128-deep k-step config takes only K % 128 == 0 and
+passes the rest on to the cost model's choice -- the plain test asserts which stream-tile config
+served each call), grids with more tiles than CUs (persistent rounds, the cross-tile prefetch) and
+fewer.  Every test restores the policy it found (the library default is -1, by shape)."""
 import pytest
 import torch
 
@@ -45,12 +47,17 @@ LAYOUTS = [(False, True), (False, False), (True, True), (True, False)]
 def test_pt_plain_matches_fp32(hip_device, M, N, Kd, ta, tb, cfg):
     from imagecaptioningconvnext_amd import kernels as K
     a, b, ref = _operands(hip_device, M, N, Kd, ta, tb, 1)
-    try:
-        K.gemm_set_pt(cfg)
+    with K.gemm_pt_mode(cfg):
+        # the call is served by a stream-tile config (a silent fallback to the LDS-staged
+        # kernels would pass the numbers below without exercising the K tail)
+        ep = K.Epilogue()
+        ep.c_dtype, ep.alpha = K.BF16, 1.0
+        kind, _ = K.gemm_plan(K.BF16, int(not ta), int(tb), M, N, Kd, a.stride(0), b.stride(0), ep=ep)
+        assert K.GEMM_PT <= kind <= K.GEMM_PT + 5, kind
+        if Kd % 128 == 0 or cfg != 7:
+            assert kind == K.GEMM_PT + cfg - 2, (kind, cfg)
         out = K.gemm(a, b, trans_a=ta, trans_b=tb)
         torch.cuda.synchronize()
-    finally:
-        K.gemm_set_pt(0)
     err = (out.float().cpu() - ref).abs().max() / ref.abs().max()
     assert err < 8e-3, err
 
@@ -72,8 +79,7 @@ def test_pt_epilogues_match_fp32_and_lds_kernels(hip_device, cfg, form):
     aux_in = torch.randn(M, N, generator=g).to(bf)
 
     def run(mode):
-        K.gemm_set_pt(mode)
-        try:
+        with K.gemm_pt_mode(mode):
             out = old.clone().to(dev)
             aux = None
             kw = {}
@@ -92,8 +98,6 @@ def test_pt_epilogues_match_fp32_and_lds_kernels(hip_device, cfg, form):
             K.gemm(a, b, trans_b=True, out=out, **kw)
             torch.cuda.synchronize()
             return out.float().cpu(), None if aux is None else aux.float().cpu()
-        finally:
-            K.gemm_set_pt(0)
 
     got, got_aux = run(cfg)
     base, base_aux = run(0)
@@ -130,12 +134,9 @@ def test_pt_persistent_rounds_and_xcd_slots(hip_device):
     for (M, N, Kd) in [(12544, 384, 1536), (6272, 1536, 64), (3328, 2048, 72), (7000, 600, 136), (3136, 520, 768)]:
         a, b, ref = _operands(hip_device, M, N, Kd, False, True, 11)
         for cfg in (2, 3, 4, 5, 6, 7):
-            K.gemm_set_pt(cfg)
-            try:
+            with K.gemm_pt_mode(cfg):
                 out = K.gemm(a, b, trans_b=True)
                 torch.cuda.synchronize()
-            finally:
-                K.gemm_set_pt(0)
             err = (out.float().cpu() - ref).abs().max() / ref.abs().max()
             assert err < 8e-3, (M, N, Kd, cfg, float(err))
 
@@ -143,11 +144,8 @@ def test_pt_persistent_rounds_and_xcd_slots(hip_device):
 def test_pt_bitwise_repeatable(hip_device):
     from imagecaptioningconvnext_amd import kernels as K
     a, b, _ = _operands(hip_device, 5000, 1536, 384, False, True, 5)
-    K.gemm_set_pt(1)
-    try:
+    with K.gemm_pt_mode(1):
         o1 = K.gemm(a, b, trans_b=True, act=K.ACT_GELU)
         o2 = K.gemm(a, b, trans_b=True, act=K.ACT_GELU)
         torch.cuda.synchronize()
-    finally:
-        K.gemm_set_pt(0)
     assert torch.equal(o1, o2)

@@ -2,7 +2,8 @@
 round 5 scratch race").
 
 The library's split-reduction scratch is one buffer per workspace slot, and a slot is shared by
-every stream of a schedule branch.  The LSTM backward runs the embedding gradient -- a scratch
+every stream of a schedule branch (the library refuses a slot's scratch to a second stream of one
+captured graph: the last test).  The LSTM backward runs the embedding gradient -- a scratch
 user -- on a side stream beside the main stream's grouped weight-gradient GEMMs and bias column
 sums, so those two entry points must never request scratch: a round-5 two-pass column sum that
 did faulted the LSTM checkpoint test with an illegal address.  The check: attach a 16-byte caller
@@ -60,3 +61,50 @@ def test_side_stream_entry_points_take_no_library_scratch(hip_device):
     torch.testing.assert_close(outs[0], x.float().sum(0), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(outs[1], xf[:, :512].sum(0), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(g, a.float().t() @ b.float(), rtol=2e-2, atol=2e-1)
+
+
+def test_library_refuses_one_slot_scratch_from_two_streams_of_a_capture(hip_device):
+    """The library-side guard (csrc/abi.cpp workspace): inside ONE captured graph, a slot's scratch
+    requested from a second stream is refused before anything is enqueued (two unordered branches
+    would share the buffer -- the round-5 race); the same calls on one stream, or with the second
+    stream on its own slot, capture and replay normally."""
+    from imagecaptioningconvnext_amd import kernels as K
+    dev = hip_device
+    a = torch.randn(256, 4096, device=dev).to(torch.bfloat16)
+    b = torch.randn(4096, 256, device=dev).to(torch.bfloat16)
+    want = a.float() @ b.float()
+    out1, out2 = torch.zeros(256, 256, device=dev), torch.zeros(256, 256, device=dev)
+    K.gemm(a, b, out=out1, split_k=4)  # warm-up: workspaces attached and large enough
+    torch.cuda.synchronize()
+    main = torch.cuda.Stream(device=dev)
+    side = torch.cuda.Stream(device=dev)
+    for use_slot in (False, True):
+        g = torch.cuda.CUDAGraph()
+        err = None
+        with torch.cuda.stream(main):
+            g.capture_begin()
+            K.gemm(a, b, out=out1, split_k=4)
+            K.fork(side, main)
+            with torch.cuda.stream(side):
+                try:
+                    if use_slot:
+                        with K.workspace_slot(1):
+                            K.gemm(a, b, out=out2, split_k=4)
+                    else:
+                        K.gemm(a, b, out=out2, split_k=4)
+                except RuntimeError as e:
+                    err = str(e)
+            K.join(main, side)
+            K.assert_joined("test")
+            g.capture_end()
+        if use_slot:
+            assert err is None
+            out1.zero_()
+            out2.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            torch.testing.assert_close(out1, want, rtol=1e-3, atol=1e-2)
+            torch.testing.assert_close(out2, want, rtol=1e-3, atol=1e-2)
+        else:
+            assert err is not None and "two streams of one captured graph" in err, err
+        del g

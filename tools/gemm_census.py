@@ -74,11 +74,8 @@ for k, (a, b, n, kw) in sorted(calls.items(), key=lambda kv: -kv[1][2] * kv[1][0
         kw2["out"] = orig(a, b, **kw)
     row = []
     for m in MODES:
-        K.gemm_set_pt(m)
-        try:
+        with K.gemm_pt_mode(m):
             row.append(time_launch(lambda: orig(a, b, **kw2), reps=reps))
-        finally:
-            K.gemm_set_pt(0)
     for m, t in zip(MODES, row):
         tot[m] += n * t
     best_tot += n * min(row)

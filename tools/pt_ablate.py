@@ -29,9 +29,8 @@ for (M, N, Kd) in ((12544, 384, 1536), (12544, 1536, 384), (4096, 4096, 4096), (
     b = torch.randn(N, Kd, device=dev).to(bf)
     out = torch.empty(M, N, device=dev, dtype=bf)
     for c, (bm, bn) in cfgs.items():
-        K.gemm_set_pt(c)
-        t = time_launch(lambda: K.gemm(a, b, trans_b=True, out=out), reps=20)
-        K.gemm_set_pt(0)
+        with K.gemm_pt_mode(c):
+            t = time_launch(lambda: K.gemm(a, b, trans_b=True, out=out), reps=20)
         tiles = ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
         steps = -(-tiles // (512 if c == 6 else 256)) * ((Kd + 63) // 64)
         row.append(f"{M}x{N}x{Kd} {bm}x{bn}: {t * 1e6:7.1f} us {t * 1e9 / steps:6.0f} ns/step")

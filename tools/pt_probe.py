@@ -19,9 +19,8 @@ for (M, N, Kd) in [(12544, 1536, 384), (12544, 384, 1536), (3136, 768, 3072), (4
     out = torch.empty(M, N, device=dev, dtype=bf)
     row = []
     for mode in (0, 2, 3, 4):
-        K.gemm_set_pt(mode)
-        row.append(time_launch(lambda: K.gemm(a, b, trans_b=True, out=out), reps=10))
-    K.gemm_set_pt(0)
+        with K.gemm_pt_mode(mode):
+            row.append(time_launch(lambda: K.gemm(a, b, trans_b=True, out=out), reps=10))
     f = 2.0 * M * N * Kd
     print(f"{tag:10s} {M:6d} {N:5d} {Kd:5d} | " + " ".join(f"{t * 1e6:7.1f}" for t in row) + " us | " +
           " ".join(f"{f / t / 1e12:5.0f}" for t in row) + " TF", flush=True)

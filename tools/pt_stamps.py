@@ -26,6 +26,7 @@ def run(M, N, Kd):
     a = torch.randn(M, Kd, device=dev).to(bf)
     b = torch.randn(N, Kd, device=dev).to(bf)
     out = torch.empty(M, N, device=dev, dtype=bf)
+    prev = K.gemm_get_pt()
     K.gemm_set_pt(cfg)
     st = torch.zeros(1024 * 64 * 8, device=dev, dtype=torch.int64)  # [block][iteration][phase]
     for _ in range(3):
@@ -35,7 +36,7 @@ def run(M, N, Kd):
     K.gemm(a, b, trans_b=True, out=out)
     torch.cuda.synchronize()
     L.imgcap_debug_stamps(None)
-    K.gemm_set_pt(0)
+    K.gemm_set_pt(prev)
     s = st.view(1024, 64, 8).cpu().double()
     used = s[:, :, 0] > 0
     names = ["mfma0+reads", "wait", "barrier", "issue/eload", "reads+mfma1", "epi"]
