@@ -108,7 +108,7 @@ _SIGS = {
     "imgcap_lstm_sync_words": [ctypes.POINTER(LstmDesc)],
     "imgcap_mha_fwd": [ctypes.POINTER(MhaDesc), c_void_p],
     "imgcap_mha_bwd": [ctypes.POINTER(MhaDesc), c_void_p],
-    "imgcap_attn_reg": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
+    "imgcap_attn_reg": [c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "imgcap_dropout": [c_int, c_int64, c_void_p, c_float, c_uint64, c_uint32, c_void_p, c_void_p],
     "imgcap_loss_finalize": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "imgcap_tf_targets": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
@@ -192,7 +192,7 @@ def _attach(dev, slot, nbytes):
 
 def _grow_workspaces(dev):
     need = c_uint64(0)
-    for slot in (0, 1):
+    for slot in (0, 1, 2):
         lib().imgcap_workspace_needed(slot, ctypes.byref(need))
         if need.value > _ws[(dev, slot)].numel():
             _attach(dev, slot, need.value * 5 // 4)
@@ -204,6 +204,7 @@ def call(name, *args):
     if dev is not None and (dev, 0) not in _ws:
         _attach(dev, 0, _WS_INITIAL)
         _attach(dev, 1, _WS_INITIAL)
+        _attach(dev, 2, _WS_INITIAL // 4)
     rc = getattr(lib(), name)(*args)
     if rc == IMGCAP_EWORKSPACE and dev is not None:  # nothing was enqueued: grow, then retry once
         _grow_workspaces(dev)

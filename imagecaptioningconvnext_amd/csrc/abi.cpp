@@ -21,8 +21,8 @@ const uint64_t* g_seed_ctr = nullptr;
 
 // Scratch for split reductions (GEMM split-K partials, colsum / LayerNorm-gradient slices),
 // per device and per slot.  Two slots: work that may run concurrently on another stream (the
-// trainer's encoder beside the decoder) selects slot 1 with imgcap_workspace_slot; kernels of
-// one slot run one after another.  The caller attaches its own buffer per (device, slot) with
+// trainer's encoder beside the decoder) selects slot 1 with imgcap_workspace_slot, the decoder
+// engines' own side streams slot 2; kernels of one slot run one after another.  The caller attaches its own buffer per (device, slot) with
 // imgcap_workspace_attach (the Python side does, from the PyTorch caching allocator); a request
 // larger than the attached buffer fails with IMGCAP_EWORKSPACE before anything is launched, and
 // imgcap_workspace_needed reports the size to attach.  Only a (device, slot) the caller never
@@ -43,7 +43,8 @@ struct Ws {
   hipStream_t cap_stream = nullptr;
 };
 static std::mutex g_ws_mu;
-static Ws g_ws[MAX_DEV][2];
+constexpr int NSLOT = 3;
+static Ws g_ws[MAX_DEV][NSLOT];
 static std::vector<void*> g_ws_retired;
 static thread_local int g_ws_slot = 0;
 int set_workspace_slot(int slot) {
@@ -113,19 +114,19 @@ extern "C" const char* imgcap_last_error_string(void) { return imgcap::g_last_er
 extern "C" int imgcap_version(void) { return IMGCAP_ABI_VERSION; }
 
 extern "C" int imgcap_workspace_attach(int slot, void* ptr, uint64_t bytes) {
-  if (slot < 0 || slot > 1) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_attach: slot 0 or 1");
+  if (slot < 0 || slot >= imgcap::NSLOT) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_attach: slot 0, 1 or 2");
   if (ptr && ((uintptr_t)ptr & 255)) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_attach: 256-byte alignment");
   return imgcap::attach_workspace(slot, ptr, (size_t)bytes);
 }
 
 extern "C" int imgcap_workspace_needed(int slot, uint64_t* bytes) {
-  if (slot < 0 || slot > 1 || !bytes) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_needed: slot 0 or 1");
+  if (slot < 0 || slot >= imgcap::NSLOT || !bytes) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_needed: slot 0, 1 or 2");
   *bytes = imgcap::workspace_needed(slot);
   return IMGCAP_OK;
 }
 
 extern "C" int imgcap_workspace_slot(int slot) {
-  if (slot < 0 || slot > 1) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_slot: 0 or 1");
+  if (slot < 0 || slot >= imgcap::NSLOT) return imgcap::fail(IMGCAP_EINVAL, "imgcap_workspace_slot: 0, 1 or 2");
   imgcap::set_workspace_slot(slot);
   return IMGCAP_OK;
 }

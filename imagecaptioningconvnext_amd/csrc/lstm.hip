@@ -816,11 +816,13 @@ extern "C" int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream) {
 }
 
 extern "C" int imgcap_attn_reg(int B, int T, int P, const float* alphas, const int32_t* dl, float alphaC,
-                               float* dalpha, float* reg_out, void* stream) {
+                               float* dalpha, float* reg_out, float* part, void* stream) {
   IMGCAP_REQUIRE(P <= MAXP, "imgcap_attn_reg: P must be <= 64");
   if (B == 0) return 0;
-  float* part = (float*)workspace((size_t)B * sizeof(float), (hipStream_t)stream);
-  if (!part) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_attn_reg: ") + last_error());
+  if (!part) {
+    part = (float*)workspace((size_t)B * sizeof(float), (hipStream_t)stream);
+    if (!part) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_attn_reg: ") + last_error());
+  }
   hipLaunchKernelGGL(attn_reg_kernel, dim3(B), dim3(REG_TS * MAXP), 0, (hipStream_t)stream, B, T, P, alphas, dl, alphaC,
                      dalpha, part);
   hipLaunchKernelGGL(attn_reg_sum_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, B, P, alphaC, part, reg_out);

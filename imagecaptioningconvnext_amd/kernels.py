@@ -52,18 +52,25 @@ def record_gemms(recorder):
     _gemm_recorder = recorder
 
 
+_cur_slot = [0]
+
+
 class workspace_slot:
-    """Context manager: library scratch slot 1 for work that runs beside slot-0 work on another
-    stream (imgcap_workspace_slot)."""
+    """Context manager: library scratch slot for work that runs beside slot-0 work on another
+    stream (imgcap_workspace_slot): 1 the trainer's pipelined encoder branch, 2 the decoder
+    engines' side streams.  Restores the slot it found."""
 
     def __init__(self, slot=1):
         self.slot = slot
 
     def __enter__(self):
+        self.prev = _cur_slot[0]
         _abi.call("imgcap_workspace_slot", self.slot)
+        _cur_slot[0] = self.slot
 
     def __exit__(self, *a):
-        _abi.call("imgcap_workspace_slot", 0)
+        _abi.call("imgcap_workspace_slot", self.prev)
+        _cur_slot[0] = self.prev
 
 
 # ---- stream forks inside captured steps --------------------------------------------------------

@@ -303,14 +303,14 @@ class LstmEngine:
             # backward() starts from these dlogits
             dlogits = torch.empty(B * T, self.Vpad, **ctd)
             dalpha = torch.empty(B, T, P, **f32)
-            reg = torch.empty(1, **f32)
+            reg = torch.empty(1 + B, **f32)  # the value, then the per-row partials (no library scratch)
 
             # the attention regulariser (train.py:268: its value and d alpha, which the backward
             # recurrence reads) on the side stream, beside the vocab projection and the CE
             K.fork(side, main)
             with torch.cuda.stream(side):
                 _abi.call("imgcap_attn_reg", B, T, P, alphas.data_ptr(), dl.data_ptr(), alphaC, dalpha.data_ptr(),
-                          reg.data_ptr(), K.stream())
+                          reg.data_ptr(), reg[1:].data_ptr(), K.stream())
                 ev_reg = torch.cuda.Event()
                 ev_reg.record(side)
 
@@ -502,7 +502,7 @@ class LstmEngine:
         # bucket's all-reduce takes that window instead (the hook after the embedding gradient).
         if par_tail:
             K.fork(side, main)
-            with torch.cuda.stream(side):
+            with torch.cuda.stream(side), K.workspace_slot(2):  # its own scratch slot (library check)
                 if "metrics" in s:
                     self._fold_status(s["metrics"][4:5])  # the backward recurrence's error word
                 demb = K.gemm(dgates, w["wih"][:, :M], K=4 * D)

@@ -109,7 +109,7 @@ def greedy_loss(predictions, sequences, captions, wordMap, maxlen, alphas=None, 
         dalpha = torch.empty(B, T, P, **f32)
         dl = torch.full((B,), T, device=dev, dtype=torch.int32)
         _abi.call("imgcap_attn_reg", B, T, P, alphas.contiguous().data_ptr(), dl.data_ptr(), alphaC,
-                  dalpha.data_ptr(), reg.data_ptr(), K.stream())
+                  dalpha.data_ptr(), reg.data_ptr(), None, K.stream())
     metrics = torch.empty(4, **f32)
     K.loss_finalize(lrow, hit, tg, reg, metrics)
     return metrics, n

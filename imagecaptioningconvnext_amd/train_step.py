@@ -58,6 +58,23 @@ def _complement(ranges, n):
     return out
 
 
+def _abandon_capture(g, streams):
+    """A call failed inside a capture: join the forked streams and end the capture, so the
+    exception reaches the caller instead of the graph's destructor aborting the process (a
+    CUDAGraph destroyed while its stream still captures)."""
+    cur = torch.cuda.current_stream()
+    for st in streams:
+        try:
+            cur.wait_stream(st)
+        except Exception:  # noqa: BLE001 -- best effort; the original error is re-raised
+            pass
+    K._open_forks.clear()
+    try:
+        g.capture_end()
+    except Exception:  # noqa: BLE001
+        pass
+
+
 class _SeqGraphs:
     """The sequential-schedule step as two captured graphs (encoder half, decoder half)."""
 
@@ -414,18 +431,23 @@ class TeacherForcedTrainer:
                 else:
                     g = torch.cuda.CUDAGraph()
                     g.capture_begin(pool=pool)
-                self._seed_ctr.add_(1)
-                cur = torch.cuda.current_stream(dev)
+                try:
+                    self._seed_ctr.add_(1)
+                    cur = torch.cuda.current_stream(dev)
 
-                def fork(k=k, cur=cur):
-                    K.fork(side, cur)
-                    with torch.cuda.stream(side):
-                        P["feats"][k].copy_(self._encode(P["img"]))
-                if PIPE_FORK != "bwd":
-                    fork()
-                m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k],
-                              mid=fork if PIPE_FORK == "bwd" else None)
-                K.join(cur, side)
+                    def fork(k=k, cur=cur):
+                        K.fork(side, cur)
+                        with torch.cuda.stream(side):
+                            P["feats"][k].copy_(self._encode(P["img"]))
+                    if PIPE_FORK != "bwd":
+                        fork()
+                    m = self._dec(P["feats"][1 - k], P["caps"][1 - k], P["lens"][1 - k],
+                                  mid=fork if PIPE_FORK == "bwd" else None)
+                    K.join(cur, side)
+                except BaseException:
+                    self._hook_mode, self._split = None, None
+                    _abandon_capture(gs[-1] if split else g, (side,))
+                    raise
                 if split:
                     g = self._end_split_capture(gs)
                 else:

@@ -41,8 +41,10 @@ enum { IMGCAP_OK = 0, IMGCAP_EINVAL = -1, IMGCAP_EUNSUPPORTED = -2, IMGCAP_EWORK
 enum { IMGCAP_ACT_NONE = 0, IMGCAP_ACT_GELU = 1, IMGCAP_ACT_RELU = 2, IMGCAP_ACT_DGELU = 3 };
 
 const char* imgcap_last_error_string(void);
-/* Split-reduction scratch slot (0 default, 1) of the calling thread: calls whose kernels may
- * run concurrently with slot-0 work on another stream (the trainer's encoder pipeline) use 1. */
+/* Split-reduction scratch slot (0 default, 1, 2) of the calling thread: calls whose kernels may
+ * run concurrently with slot-0 work on another stream use another slot (the trainer's encoder
+ * pipeline 1, the decoder engines' side streams 2).  Inside one captured graph the library
+ * refuses a slot's scratch to a second stream (the call fails, nothing is enqueued). */
 int imgcap_workspace_slot(int slot);
 /* Attach the caller's device buffer (256-byte aligned; NULL detaches) as the split-reduction
  * scratch of `slot` on the current device. */
@@ -419,9 +421,11 @@ int imgcap_lstm_tf_bwd(const imgcap_lstm_desc* d, void* stream);
 int imgcap_lstm_denc(int B, int T, int P, int E, const float* alphas, const float* dawe, const float* base,
                      const int64_t* sort_ind, float* denc, void* stream);
 /* train.py:269: reg = alphaC*mean_{b,p}(1-sum_t alpha)^2 -> *reg_out;
- * dalpha[b,t,p] = d reg / d alpha[b,t,p] (0 where t >= dl[b]) */
+ * dalpha[b,t,p] = d reg / d alpha[b,t,p] (0 where t >= dl[b]).  part: B floats of per-row partial
+ * sums, caller-owned (NULL: library scratch -- not from a stream that runs beside other scratch
+ * users; the LSTM engine calls this on its side stream and passes its own). */
 int imgcap_attn_reg(int B, int T, int P, const float* alphas, const int32_t* dl, float alphaC, float* dalpha,
-                    float* reg_out, void* stream);
+                    float* reg_out, float* part, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Multi-head attention of nn.TransformerDecoderLayer (transformerDecoder.py:82,104): one

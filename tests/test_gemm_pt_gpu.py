@@ -54,7 +54,7 @@ def test_pt_plain_matches_fp32(hip_device, M, N, Kd, ta, tb, cfg):
         ep.c_dtype, ep.alpha = K.BF16, 1.0
         kind, _ = K.gemm_plan(K.BF16, int(not ta), int(tb), M, N, Kd, a.stride(0), b.stride(0), ep=ep)
         assert K.GEMM_PT <= kind <= K.GEMM_PT + 5, kind
-        if Kd % 128 == 0 or cfg != 7:
+        if cfg in (2, 3, 4, 5):  # configs built for every layout and K tail (6: k-major only; 7: K % 128)
             assert kind == K.GEMM_PT + cfg - 2, (kind, cfg)
         out = K.gemm(a, b, trans_a=ta, trans_b=tb)
         torch.cuda.synchronize()

@@ -7,11 +7,13 @@ reference's step (decoder.py:69-113, train.py:263-291: packed CE + the doubly st
 term, backward, clamp +-5, Adam) is the oracle's fp32 restatement on the engine's bf16 weight copies
 and features; dropout 0.  The encoder is a pass-through (the batch is encoder features).
 
-Gates (bf16 storage against fp32; measured on MI355X): loss 2e-3 relative, tokens
-exact, top-5 within 0.5 points, predictions 1e-2, attention weights 1e-2, every gradient tensor
-within GRAD_TOL of the oracle's, and the first Adam step in the oracle's direction wherever the two
-gradients agree in sign with margin.  The LSTM has no post-norm chain of ReLU masks (one ReLU, in the
-attention scores), so its bf16 gradients stay close to fp32 and one fixed gate holds."""
+Gates (bf16 storage against fp32; measured on MI355X round 6: loss 1e-7 relative, top-5 equal,
+predictions 1.8e-3, alphas 5.2e-4, worst gradient tensor 4.4e-3 (attention.decoder_att.weight)):
+loss 2e-3 relative, tokens exact, top-5 within 0.5 points, predictions 5e-3, alphas 2e-3, every
+gradient tensor within GRAD_TOL of the oracle's, and the first Adam step in the oracle's direction
+wherever the two gradients agree in sign with margin.  The LSTM has no post-norm chain of ReLU masks
+(one ReLU, in the attention scores), so its bf16 gradients stay close to fp32 and one fixed gate
+holds."""
 import pytest
 import torch
 
@@ -21,7 +23,7 @@ from oracle import decoders, shapes, train_step
 pytestmark = pytest.mark.gpu
 
 V, L, E, A, D, M = 9490, 52, 768, 512, 512, 512
-GRAD_TOL = 3e-2
+GRAD_TOL = 1e-2
 
 
 class PassThrough(torch.nn.Module):
@@ -84,7 +86,7 @@ def test_lstm_b32_bf16_pipelined_graph_step_vs_oracle(hip_device):
     assert abs(g_loss - loss.item()) <= 2e-3 * loss.item(), (g_loss, loss.item())
     assert g_tok == sum(dls)
     assert abs(g_top5 - top5) <= 0.5, (g_top5, top5)
-    assert e_pred < 1e-2 and e_al < 1e-2, (e_pred, e_al)
+    assert e_pred < 5e-3 and e_al < 2e-3, (e_pred, e_al)
     assert errs[0][0] <= GRAD_TOL, errs[:4]
 
     # post-Adam parameters: Adam's first step moves an entry by lr * g / (|g| + eps)

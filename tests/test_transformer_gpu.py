@@ -53,11 +53,11 @@ def _ref_attention(q, k, v, causal, key_pad, emulate=False):
 
 
 # bf16: against the kernel's own rounding points evaluated in fp64 (what remains is the outputs'
-# bf16 rounding and the fp32 accumulation order), and against plain fp32 attention with the round-5
-# gates
+# bf16 rounding and the fp32 accumulation order: measured fwd 1.5-1.6e-3, dq / dk / dv 1.6-1.7e-3
+# at every shape, round 6), and against plain fp32 attention with the round-5 gates
 
 
-@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 4e-3)])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2.5e-3)])
 @pytest.mark.parametrize("Lq,Lk,causal", [(52, 52, True), (52, 49, False), (12, 12, True), (64, 64, True)])
 def test_mha_kernel_fwd_bwd(hip_device, dtype, tol, Lq, Lk, causal):
     from imagecaptioningconvnext_amd import _abi
@@ -109,7 +109,7 @@ def test_mha_kernel_fwd_bwd(hip_device, dtype, tol, Lq, Lk, causal):
     for name, got, r in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
         e = _rel(got.view(B, -1, H, 64).transpose(1, 2), r)
         print(f"  {name} {e:.2e}")
-        assert e < tol * 2
+        assert e < (tol if emu else tol * 2)
     if emu:
         for got, r in ((dq, q3.grad), (dk, k3.grad), (dv, v3.grad)):
             assert _rel(got.view(B, -1, H, 64).transpose(1, 2), r) < 4e-2

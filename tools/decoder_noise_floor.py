@@ -21,7 +21,9 @@ V, L, D, H = 9490, 52, 512, 8
 
 def grads(p, feats, caps, lens, layers, numerics, dtype):
     rb = lambda t: t.to(torch.bfloat16).to(dtype)  # noqa: E731
-    pr = {k: rb(v).clone().requires_grad_(True) for k, v in p.items()}
+    # the engine's operands: bf16 GEMM weight matrices, fp32 biases / norms / embedding table
+    pr = {k: (rb(v) if v.dim() == 2 and k != "embedding.weight" else v.to(dtype)).clone().requires_grad_(True)
+          for k, v in p.items()}
     preds, cs, dls = decoders.transformer_tf_forward(pr, rb(feats), caps, lens, caps == 0, H, layers,
                                                      numerics=numerics)
     loss, _, _ = train_step.transformer_loss(preds, cs, dls)
