@@ -14,6 +14,8 @@ LIB_PATH = os.environ.get("IMGCAP_LIB") or os.path.join(_HERE, "libimgcap_hip.so
 F32, BF16 = 0, 1
 # imgcap_gemm_plan kinds of the stream-tile configs 1..6 (IMGCAP_GEMM_PT .. IMGCAP_GEMM_PT128K)
 GEMM_PT = 8
+# ... and of the weight-stationary short-K kernel (8-wave / 4-wave blocks)
+GEMM_WS, GEMM_WS4 = 14, 15
 FP8MX = 2
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU = 0, 1, 2, 3
 
@@ -72,6 +74,8 @@ _SIGS = {
     "imgcap_gemm_plan_ep": [c_int] * 6 + [c_int64, c_int64, c_int, c_void_p, c_void_p],
     "imgcap_gemm_set_pt": [c_int],
     "imgcap_gemm_get_pt": [],
+    "imgcap_gemm_set_ws": [c_int],
+    "imgcap_gemm_get_ws": [],
     "imgcap_dwconv7": [c_int] * 5 + [c_void_p] * 5,
     "imgcap_cnblock_mlp": [c_int, c_int] + [c_void_p] * 9 + [c_int, c_void_p, c_void_p],
     "imgcap_stochastic_depth_scales": [c_int, c_int, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p],

@@ -407,6 +407,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(int M, int N, int S,
 #include "gemm256.h"
 #include "gemm_mx.h"
 #include "gemm_pt.h"
+#include "gemm_ws.h"
 
 // ---------------------------------------------------------------------------------------
 // skinny kernel: M <= 16*MT rows, A [M][K] and B [N][K] both k-major.  Block = 16 columns,
@@ -773,11 +774,127 @@ static int pt_launch(int cfg, int ak, int bk, int M, int N, int K, const bf16* A
   return 0;
 }
 
+// ---- weight-stationary short-K kernel (gemm_ws.h): selection and launch ------------------------
+// IMGCAP_GEMM_WS / imgcap_gemm_set_ws: -1 by shape (default), 0 never, 1 wherever eligible (blocks
+// of 8 waves), 2 wherever eligible (blocks of 4 waves, two per CU)
+static int g_gemm_ws_mode = [] {
+  const char* e = getenv("IMGCAP_GEMM_WS");
+  return e ? atoi(e) : -1;
+}();
+
+// 0: not eligible / not chosen; 1: 8-wave blocks (256 columns); 2: 4-wave blocks (128 columns)
+static int ws_plan(int ak, int bk, int M, int N, int K, long lda, long ldb, long ldc, const void* C, int batch,
+                   int split, const imgcap_epilogue* ep) {
+  const int mode = g_gemm_ws_mode;
+  if (mode == 0 || !ak || !bk || batch != 1 || split != 1 || (K != 384 && K != 512) || M < 64) return 0;
+  if (lda % 8 || ldb % 8 || ldc % 4 || N % 4 || ((uintptr_t)C & 7)) return 0;
+  if (ep) {
+    if (ep->c_dtype != IMGCAP_BF16 || ep->res || ep->aux || ep->beta != 0.f || ep->rowscale) return 0;
+    if (ep->act != IMGCAP_ACT_NONE && ep->act != IMGCAP_ACT_GELU && ep->act != IMGCAP_ACT_RELU) return 0;
+  }
+  if ((int64_t)(M - 1) * ldc + N > 0x3fffffffLL || (int64_t)(N - 1) * ldb + K > 0x3fffffffLL) return 0;
+  if (mode == 1 || mode == 2) return mode;
+  // by shape (tools/ws_bench.py, round 6, us per launch against the plan without this kernel):
+  // 12544x1536x384 +GELU 32.2 vs 39.9 (4-wave blocks), 25088x1536x384 50.0 vs 64.5, 50176x192x384
+  // 18.8 vs 21.7, 3136x6144x512 (the decoder's stacked memory K/V) 32.4 vs 40.2 (8-wave blocks).
+  // Elsewhere -- the decoder's 3328-row d = 512 products, C4's 6272x2048x512 -- the per-block weight
+  // slice load (the kernel's fixed cost, ~8-10 us) is not amortised and the 64x64 LDS tile stays.
+  if (N % 8 != 0 || (ep && ep->colscale)) return 0;
+  if (K == 384 && M >= 8192 && (N >= 1024 || N == 192)) return 2;
+  if (K == 512 && N >= 4096 && M >= 2048) return 1;
+  return 0;
+}
+
+template <int KS, int NW, int S>
+void wsp_go(const WsArgs& a, int act, dim3 grid, hipStream_t st) {
+  if (act == IMGCAP_ACT_GELU) hipLaunchKernelGGL((gemm_wsp_kernel<KS, NW, S, 1>), grid, dim3(NW * 64), 0, st, a);
+  else if (act == IMGCAP_ACT_RELU) hipLaunchKernelGGL((gemm_wsp_kernel<KS, NW, S, 2>), grid, dim3(NW * 64), 0, st, a);
+  else hipLaunchKernelGGL((gemm_wsp_kernel<KS, NW, S, 0>), grid, dim3(NW * 64), 0, st, a);
+}
+
+template <int KS, int NW, int S, bool STG = false>
+void ws_go(const WsArgs& a, int act, dim3 grid, hipStream_t st) {
+  if (act == IMGCAP_ACT_GELU) hipLaunchKernelGGL((gemm_ws_kernel<KS, NW, S, 1, STG>), grid, dim3(NW * 64), 0, st, a);
+  else if (act == IMGCAP_ACT_RELU) hipLaunchKernelGGL((gemm_ws_kernel<KS, NW, S, 2, STG>), grid, dim3(NW * 64), 0, st, a);
+  else hipLaunchKernelGGL((gemm_ws_kernel<KS, NW, S, 0, STG>), grid, dim3(NW * 64), 0, st, a);
+}
+
+static int ws_launch(int cfg, int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb, void* C, long ldc,
+                     const imgcap_epilogue& ep, hipStream_t st) {
+  const int NW = cfg == 1 ? 8 : 4, bpc = cfg == 1 ? 1 : 2;
+  WsArgs a;
+  a.A = A;
+  a.B = B;
+  a.C = C;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.M = M;
+  a.N = N;
+  a.slices = (N + 32 * NW - 1) / (32 * NW);
+  const int nchunks = (M + 31) / 32;
+  const int want = std::max(1, device_cus() * bpc / a.slices);
+  a.chunks_per = (nchunks + want - 1) / want;
+  a.row_groups = (nchunks + a.chunks_per - 1) / a.chunks_per;
+  a.ep = ep;
+  a.seed_ctr = g_seed_ctr;
+  a.b_bytes = ((int64_t)(N - 1) * ldb + K) * 2;
+  a.c_bytes = ((int64_t)(M - 1) * ldc + N) * 2;
+  const dim3 grid(a.slices * a.row_groups);
+  static const int deep = [] {  // A/B switch: deeper A-chunk rings (IMGCAP_WS_DEEP=1)
+    const char* e = getenv("IMGCAP_WS_DEEP");
+    return e ? atoi(e) : 0;
+  }();
+  static const int stg = [] {  // output tile staged through LDS (default; IMGCAP_WS_STG=0: 8-byte stores)
+    const char* e = getenv("IMGCAP_WS_STG");
+    return e ? atoi(e) : 1;
+  }();
+  static const int pipe = [] {  // A/B switch: the software-pipelined form (IMGCAP_WS_PIPE=1)
+    const char* e = getenv("IMGCAP_WS_PIPE");
+    return e ? atoi(e) : 0;
+  }();
+  if (pipe && !ep.colscale) {
+    if (K == 384) {
+      if (NW == 8) wsp_go<24, 8, 4>(a, ep.act, grid, st);
+      else wsp_go<24, 4, 3>(a, ep.act, grid, st);
+    } else {
+      if (NW == 8) wsp_go<32, 8, 3>(a, ep.act, grid, st);
+      else wsp_go<32, 4, 2>(a, ep.act, grid, st);
+    }
+  } else if (stg && N % 8 == 0) {
+    if (K == 384) {
+      if (NW == 8) ws_go<24, 8, 5, true>(a, ep.act, grid, st);
+      else ws_go<24, 4, 2, true>(a, ep.act, grid, st);
+    } else {
+      if (NW == 8) ws_go<32, 8, 4, true>(a, ep.act, grid, st);
+      else ws_go<32, 4, 2, true>(a, ep.act, grid, st);
+    }
+  } else if (K == 384) {
+    if (NW == 8) {
+      if (deep) ws_go<24, 8, 6>(a, ep.act, grid, st);
+      else ws_go<24, 8, 3>(a, ep.act, grid, st);
+    } else {
+      ws_go<24, 4, 3>(a, ep.act, grid, st);
+    }
+  } else {
+    if (NW == 8) {
+      if (deep) ws_go<32, 8, 4>(a, ep.act, grid, st);
+      else ws_go<32, 8, 3>(a, ep.act, grid, st);
+    } else {
+      ws_go<32, 4, 2>(a, ep.act, grid, st);
+    }
+  }
+  IMGCAP_CHECK_LAUNCH("imgcap_gemm(weight-stationary)");
+  return 0;
+}
+
 template <typename T>
 static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, long lda, long sA, const void* B,
                          long ldb, long sB, void* C, long ldc, long sC, int batch, const imgcap_epilogue& ep,
                          int vec_ok, hipStream_t st, int split) {
   if constexpr (sizeof(T) == 2) {
+    const int wc = ws_plan(ak, bk, M, N, K, lda, ldb, ldc, C, batch, split, &ep);
+    if (wc) return ws_launch(wc, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, C, ldc, ep, st);
     const int pc = pt_plan(ak, bk, M, N, K, lda, ldb, batch, split, &ep, vec_ok != 0);
     if (pc) return pt_launch(pc, ak, bk, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, C, ldc, ep, st);
   }
@@ -1293,10 +1410,24 @@ extern "C" int imgcap_gemm_set_pt(int mode) {
 
 extern "C" int imgcap_gemm_get_pt(void) { return g_gemm_pt_mode; }
 
+extern "C" int imgcap_gemm_set_ws(int mode) {
+  IMGCAP_REQUIRE(mode >= -1 && mode <= 2, "imgcap_gemm_set_ws: -1..2");
+  g_gemm_ws_mode = mode;
+  return 0;
+}
+
+extern "C" int imgcap_gemm_get_ws(void) { return g_gemm_ws_mode; }
+
 extern "C" int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda,
                                    int64_t ldb, int batch, const imgcap_epilogue* epi, int* splits) {
   const int split = (epi == nullptr || epi->split_k == 0 || epi->split_k == 1) ? 1 : epi->split_k;
   if (dtype == IMGCAP_BF16) {
+    // (the C pointer / ldc of the call are not known here: an aligned C with ldc = N is assumed)
+    const int wc = ws_plan(a_kmajor, b_kmajor, M, N, K, lda, ldb, (N + 3) / 4 * 4, nullptr, batch, split, epi);
+    if (wc) {
+      if (splits) *splits = 1;
+      return IMGCAP_GEMM_WS + wc - 1;
+    }
     const int pc = pt_plan(a_kmajor, b_kmajor, M, N, K, lda, ldb, batch, split, epi, true);
     if (pc) {
       if (splits) *splits = 1;

@@ -9,7 +9,7 @@ import os
 import torch
 
 from . import _abi
-from ._abi import ACT_DGELU, ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, GEMM_PT, Epilogue  # noqa: F401
+from ._abi import ACT_DGELU, ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, GEMM_PT, GEMM_WS, GEMM_WS4, Epilogue  # noqa: F401
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -120,6 +120,30 @@ def gemm_set_pt(mode):
 def gemm_get_pt():
     """The stream-tile policy currently set (imgcap_gemm_get_pt)."""
     return int(_abi.lib().imgcap_gemm_get_pt())
+
+
+def gemm_set_ws(mode):
+    """Weight-stationary short-K GEMM (imgcap_gemm_set_ws): -1 by shape, 0 never, 1 / 2 wherever
+    eligible with 8- / 4-wave blocks."""
+    _abi.call("imgcap_gemm_set_ws", int(mode))
+
+
+def gemm_get_ws():
+    return int(_abi.lib().imgcap_gemm_get_ws())
+
+
+class gemm_ws_mode:
+    """``with gemm_ws_mode(m):`` -- the weight-stationary policy m inside, the previous one after."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = gemm_get_ws()
+        gemm_set_ws(self.mode)
+
+    def __exit__(self, *a):
+        gemm_set_ws(self.prev)
 
 
 class gemm_pt_mode:

@@ -146,7 +146,7 @@ enum { IMGCAP_GEMM_SKINNY = 1, IMGCAP_GEMM_TILED64 = 2, IMGCAP_GEMM_TILED128 = 3
         * 128x192 tiles of 8 waves; 128x128 of 4 waves, two blocks a CU; 128x128 of 8 waves with
         * 128-deep k-steps */
        IMGCAP_GEMM_PT = 8, IMGCAP_GEMM_PT128X256 = 9, IMGCAP_GEMM_PT128 = 10, IMGCAP_GEMM_PT128X192 = 11,
-       IMGCAP_GEMM_PT128X2 = 12, IMGCAP_GEMM_PT128K = 13 };
+       IMGCAP_GEMM_PT128X2 = 12, IMGCAP_GEMM_PT128K = 13, IMGCAP_GEMM_WS = 14, IMGCAP_GEMM_WS4 = 15 };
 int imgcap_gemm_plan(int dtype, int a_kmajor, int b_kmajor, int M, int N, int K, int64_t lda, int64_t ldb,
                      int batch, int split_k, int* splits);
 /* The same, knowing the call's epilogue (the persistent-tile kernel serves bf16 outputs only). */
@@ -160,6 +160,12 @@ int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M, int N, int
 int imgcap_gemm_set_pt(int mode);
 /* The current stream-tile policy (what imgcap_gemm_set_pt last set; -1 unless changed). */
 int imgcap_gemm_get_pt(void);
+/* Weight-stationary short-K kernel (K = 384 / 512, A and B k-major, bf16 C; epilogue: alpha,
+ * bias, GELU / ReLU, dropout, column scale): -1 by shape (default), 0 never, 1 wherever eligible
+ * with 8-wave blocks (IMGCAP_GEMM_WS), 2 with 4-wave blocks (IMGCAP_GEMM_WS4); checked before
+ * the stream-tile policy. */
+int imgcap_gemm_set_ws(int mode);
+int imgcap_gemm_get_ws(void);
 /* Kernel-selection policy for A/B tests and benchmarks: glds256 >= 1 serves every eligible
  * GEMM (bf16, unsplit, 16-byte operand pitches) with the 256x256 tile (1: 64-deep k-steps x 2
  * stages, 2: 32-deep x 4 stages, 3: 32-deep x 3 stages), 0 never, 4 = the 128x128 LDS-DMA tile
