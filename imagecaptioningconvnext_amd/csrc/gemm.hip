@@ -586,7 +586,16 @@ static double pt_estimate(int c, int M, int N, int K, int cus) {
 // configs instantiated per (epilogue kind, layout): the 64x64-per-wave tiles hold the general
 // epilogue's operands (and the residual of a transposed layout) only by spilling, so those forms
 // take the 64x32 / 64x48 wave tiles
+// The 256x128 / 128x256 configs (1, 2) never won a shape in the step census (DESIGN §3f') and are
+// built only into the diagnostic library (make diag, IMGCAP_STAMPS), with the 128x64 LDS-DMA tile
+// (imgcap_gemm_set_policy 7): the product library holds the kernels its plans can pick.
+#ifdef IMGCAP_STAMPS
+constexpr bool kDiagGemmVariants = true;
+#else
+constexpr bool kDiagGemmVariants = false;
+#endif
 static bool pt_allowed(int c, int ek, bool ak, bool bk, int K) {
+  if (c <= 2 && !kDiagGemmVariants) return false;
   if (pt_cfg(c).ks > 1 && K % (64 * pt_cfg(c).ks)) return false;  // 128-deep k-steps: no K tail
   if (c == 6) return ek == 0 || (ek == 1 && ak && bk);
   if (ek == 2) return c == 3;
@@ -659,6 +668,7 @@ static int pt_plan(int ak, int bk, int M, int N, int K, long lda, long ldb, int 
 
 // explicit instantiations of the stream-tile kernels pt_allowed admits (the host stubs of kernel
 // templates first named inside the launcher template were otherwise left undefined)
+#ifdef IMGCAP_STAMPS
 template __global__ void gemm_pt_kernel<256, 128, 4, 2, 3, true, true, 0>(PtArgs);
 template __global__ void gemm_pt_kernel<256, 128, 4, 2, 3, true, true, 1>(PtArgs);
 template __global__ void gemm_pt_kernel<256, 128, 4, 2, 3, true, false, 0>(PtArgs);
@@ -669,6 +679,7 @@ template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, true, true, 1>(PtArgs
 template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, true, false, 0>(PtArgs);
 template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, false, true, 0>(PtArgs);
 template __global__ void gemm_pt_kernel<128, 256, 2, 4, 3, false, false, 0>(PtArgs);
+#endif
 template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, true, 0>(PtArgs);
 template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, true, 1>(PtArgs);
 template __global__ void gemm_pt_kernel<128, 128, 2, 4, 4, true, true, 2>(PtArgs);
@@ -718,12 +729,14 @@ void pt_launch_t(int cfg, int ek, int G, const PtArgs& a, hipStream_t st) {
       if (ek == 0) PT_L(128, 128, 2, 2, 2, 0);
       else PT_L(128, 128, 2, 2, 2, 1);
     }
-  } else if (cfg == 1) {
-    if (ek == 0) PT_L(256, 128, 4, 2, 3, 0);
-    else if constexpr (AKV && BKV) PT_L(256, 128, 4, 2, 3, 1);
-  } else {
-    if (ek == 0) PT_L(128, 256, 2, 4, 3, 0);
-    else if constexpr (AKV && BKV) PT_L(128, 256, 2, 4, 3, 1);
+  } else if constexpr (kDiagGemmVariants) {
+    if (cfg == 1) {
+      if (ek == 0) PT_L(256, 128, 4, 2, 3, 0);
+      else if constexpr (AKV && BKV) PT_L(256, 128, 4, 2, 3, 1);
+    } else {
+      if (ek == 0) PT_L(128, 256, 2, 4, 3, 0);
+      else if constexpr (AKV && BKV) PT_L(128, 256, 2, 4, 3, 1);
+    }
   }
 #undef PT_L
 }
@@ -968,7 +981,7 @@ static int gemm_dispatch(int ak, int bk, int M, int N, int K, const void* A, lon
       if (S64 == 4) GS_S(AKV, BKV, 4);                                                                             \
       else if (S64 == 3) GS_S(AKV, BKV, 3);                                                                        \
       else GS_S(AKV, BKV, 2);                                                                                      \
-    } else {                                                                                                       \
+    } else if constexpr (kDiagGemmVariants) {                                                                       \
       hipLaunchKernelGGL((gemm_glds_kernel<128, 64, AKV, BKV, 2>), grid, dim3(256), 0, st, a, lda, b, ldb, C, ldc, M, \
                          N, K, ep, vec_ok, g_seed_ctr, 0, grp);                                                    \
     }                                                                                                              \
@@ -1404,6 +1417,8 @@ extern "C" int imgcap_transpose(int dtype, int rows, int cols, const void* in, i
 
 extern "C" int imgcap_gemm_set_pt(int mode) {
   IMGCAP_REQUIRE(mode >= -1 && mode <= PT_NCFG + 1, "imgcap_gemm_set_pt: -1..7");
+  if ((mode == 2 || mode == 3) && !kDiagGemmVariants)
+    return fail(IMGCAP_EUNSUPPORTED, "imgcap_gemm_set_pt(2|3): the 256x128 / 128x256 tiles are in the diagnostic build only");
   g_gemm_pt_mode = mode;
   return 0;
 }
@@ -1441,6 +1456,8 @@ extern "C" int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M,
 
 extern "C" int imgcap_gemm_set_policy(int glds256) {
   IMGCAP_REQUIRE(glds256 >= -1 && glds256 <= 8, "imgcap_gemm_set_policy: -1..8");
+  if (glds256 == 7 && !kDiagGemmVariants)
+    return fail(IMGCAP_EUNSUPPORTED, "imgcap_gemm_set_policy(7): the 128x64 tile is in the diagnostic build only");
   g_gemm256_mode = glds256;
   return 0;
 }

@@ -156,7 +156,8 @@ int imgcap_gemm_plan_ep(int dtype, int a_kmajor, int b_kmajor, int M, int N, int
  * products, where a step census measured it ahead of the LDS-staged tiles), 0 never, 1 wherever
  * eligible (tile by the cost model), 2..7 wherever eligible with config 1..6 (IMGCAP_GEMM_PT ..
  * IMGCAP_GEMM_PT128K; a config not built for the call's epilogue form or K falls back to the cost
- * model). */
+ * model).  Configs 1 / 2 (modes 2 / 3: 256x128, 128x256) exist in the diagnostic build only; the
+ * product library returns IMGCAP_EUNSUPPORTED for those modes. */
 int imgcap_gemm_set_pt(int mode);
 /* The current stream-tile policy (what imgcap_gemm_set_pt last set; -1 unless changed). */
 int imgcap_gemm_get_pt(void);
@@ -171,7 +172,8 @@ int imgcap_gemm_get_ws(void);
  * stages, 2: 32-deep x 4 stages, 3: 32-deep x 3 stages), 0 never, 4 = the 128x128 LDS-DMA tile
  * wherever eligible, 5 = register-staged tiles only, -1 by shape (default); 6 = the 64x64
  * LDS-DMA tile wherever eligible and unsplit; 7 / 8 = by shape, but grids under 128 128x128
- * tiles on the 128x64 LDS-DMA tile / the register-staged 64x64 tile.
+ * tiles on the 128x64 LDS-DMA tile (diagnostic build only: IMGCAP_EUNSUPPORTED in the product
+ * library) / the register-staged 64x64 tile.
  * Process-wide; set before capturing graphs. */
 int imgcap_gemm_set_policy(int glds256);
 int imgcap_transpose(int dtype, int rows, int cols, const void* in, int64_t ldi, void* out, int64_t ldo,

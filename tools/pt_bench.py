@@ -19,7 +19,8 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 # IMGCAP_GEMM_PT modes: 0 the LDS-staged plan, c + 1 stream-tile config c, 1 the cost-model pick (last)
 NAMES = {0: "old", 2: "256x128", 3: "128x256", 4: "128x128", 5: "128x192", 6: "128x128b2", 7: "128x128k",
          8: "256x128w", 9: "256x256w", 10: "128x256w", 1: "auto"}
-MODES = [int(m) for m in os.environ.get("PT_MODES", "0 2 3 4 5 6 7 8 9 10 1").split()]
+# (modes 2 / 3 need the diagnostic library: IMGCAP_LIB=build/libimgcap_hip_diag.so)
+MODES = [int(m) for m in os.environ.get("PT_MODES", "0 4 5 6 7 1").split()]
 
 SHAPES = [
     # C3 (Tiny, B=64) encoder
