@@ -402,6 +402,31 @@ DEV void mi_store(char* img, const RowVecs<bf16>& rv) {
         acc[j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(XFRAG(j_, kk_), y_, acc[j_], 0, 0, 0); \
     }                                                                              \
   } while (0)
+// The probability / dS images (P~ in the forward; P~ and dS in the backward) are written by the
+// MFMA epilogue, one 8-byte piece (4 columns) of 16 different rows per 16-lane group: in the row
+// images above those 16 pieces fall on 4 bank pairs (ds_write_b64 banks by (a/4) mod 32), a 4-way
+// conflict (SQ: 0.87 / 0.92 conflict cycles per LDS instruction, round 6).  These images swizzle
+// both the 16-byte slot (by row bits 0, 1, 3) and the 8-byte half inside it (by row bit 2): the
+// 16 rows of a write group land on 16 distinct 8-byte positions of the 128-byte bank window, and
+// the k-contiguous (ds_read_b128, aligned slot, halves swapped back in registers) and transposed
+// (ds_read_b64_tr_b16) operand reads stay conflict-free (bank model: tools/lds_bank_model.py).
+DEV int mp_sa(int r) { return (r & 3) | ((r >> 1) & 4); }
+DEV int mp_sb(int r) { return (r >> 2) & 1; }
+DEV int mp_off(int r, int c) { return r * 128 + (((c >> 3) ^ mp_sa(r)) << 4) + ((((c >> 2) & 1) ^ mp_sb(r)) << 3) + ((c & 3) << 1); }
+DEV bf16x8 mp_frag_k(const char* img, int row0, int kk, int lane) {
+  const int r = row0 + (lane & 15);
+  const uint4 v = *(const uint4*)(img + r * 128 + (((4 * kk + (lane >> 4)) ^ mp_sa(r)) << 4));
+  const uint4 w = mp_sb(r) ? make_uint4(v.z, v.w, v.x, v.y) : v;
+  return __builtin_bit_cast(bf16x8, w);
+}
+DEV bf16x8 mp_frag_t(const char* img, int col0, int kk, int lane) {
+  const int fr = lane & 15, g = lane >> 4;
+  const int kr = kk * 32 + 8 * g + (fr >> 2), col = col0 + 4 * (fr & 3);
+  const mi_v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mi_lds_v4s16*)(img + mp_off(kr, col)));
+  const mi_v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((mi_lds_v4s16*)(img + mp_off(kr + 4, col)));
+  const mi_v8s16 all = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, all);
+}
 DEV uint2 mi_pack4(float a, float b, float c, float e) {
   const bf16x2 lo = {(bf16)a, (bf16)b}, hi = {(bf16)c, (bf16)e};
   return make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
@@ -480,14 +505,14 @@ __global__ __launch_bounds__(256) void mha_fwd_bf16_kernel(imgcap_mha_desc d, co
       s[jb][r] = pv;
       if (d.probs && i < d.Lq && j < d.Lk) d.probs[((long)bh * d.Lq + i) * d.Lk + j] = pv;
     }
-    *(uint2*)(Ps + mi_off(i, 16 * jb + 4 * fq)) = mi_pack4(s[jb][0], s[jb][1], s[jb][2], s[jb][3]);
+    *(uint2*)(Ps + mp_off(i, 16 * jb + 4 * fq)) = mi_pack4(s[jb][0], s[jb][1], s[jb][2], s[jb][3]);
   }
   // a wave reads back only its own 16 rows of P~: LDS operations of one wave complete in order
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   f32x4 o[4];
 #define XV(cb, kk) mi_frag_t(Vs, 16 * (cb), kk, lane)
-#define YP(kk) mi_frag_k(Ps, row0, kk, lane)
+#define YP(kk) mp_frag_k(Ps, row0, kk, lane)
   MI_MM(o, XV, YP);
 #undef XV
 #undef YP
@@ -570,15 +595,15 @@ __global__ __launch_bounds__(256) void mha_bwd_bf16_kernel(imgcap_mha_desc d, co
       ds[r] = p[jb][r] * (dp[jb][r] - dot);
       pt[r] = p[jb][r] * ms[jb][r];
     }
-    *(uint2*)(Pt + mi_off(i, 16 * jb + 4 * fq)) = mi_pack4(pt[0], pt[1], pt[2], pt[3]);
-    *(uint2*)(dSs + mi_off(i, 16 * jb + 4 * fq)) = mi_pack4(ds[0], ds[1], ds[2], ds[3]);
+    *(uint2*)(Pt + mp_off(i, 16 * jb + 4 * fq)) = mi_pack4(pt[0], pt[1], pt[2], pt[3]);
+    *(uint2*)(dSs + mp_off(i, 16 * jb + 4 * fq)) = mi_pack4(ds[0], ds[1], ds[2], ds[3]);
   }
   __syncthreads();  // dV / dK sum over every wave's query rows
   const int j = row0 + fr;  // key row of the dV / dK phase
   f32x4 acc[4];
   // dV[j][c] = sum_i P~[i][j] dO[i][c]
 #define XO(cb, kk) mi_frag_t(dOs, 16 * (cb), kk, lane)
-#define YP(kk) mi_frag_t(Pt, row0, kk, lane)
+#define YP(kk) mp_frag_t(Pt, row0, kk, lane)
   MI_MM(acc, XO, YP);
 #undef XO
 #undef YP
@@ -589,7 +614,7 @@ __global__ __launch_bounds__(256) void mha_bwd_bf16_kernel(imgcap_mha_desc d, co
   }
   // dK[j][c] = scale sum_i dS[i][j] Q[i][c]
 #define XQ(cb, kk) mi_frag_t(Qs, 16 * (cb), kk, lane)
-#define YS(kk) mi_frag_t(dSs, row0, kk, lane)
+#define YS(kk) mp_frag_t(dSs, row0, kk, lane)
   MI_MM(acc, XQ, YS);
 #undef XQ
 #undef YS
@@ -602,7 +627,7 @@ __global__ __launch_bounds__(256) void mha_bwd_bf16_kernel(imgcap_mha_desc d, co
   }
   // dQ[i][c] = scale sum_j dS[i][j] K[j][c]
 #define XKT(cb, kk) mi_frag_t(Ks, 16 * (cb), kk, lane)
-#define YS(kk) mi_frag_k(dSs, row0, kk, lane)
+#define YS(kk) mp_frag_k(dSs, row0, kk, lane)
   MI_MM(acc, XKT, YS);
 #undef XKT
 #undef YS
