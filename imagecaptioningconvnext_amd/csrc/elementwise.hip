@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void embedding_fwd8_kernel(int n, int dim, con
 //                are summed with integer atomics (exact, order-free)
 //   emb_scatter: sorted position / id at that rank
 //   emb_segsum:  one wave per sorted index; a run's first index reads the run's positions a
-//                window of 64 at a time and sums their rows in order
+//                window of EMB_CH at a time and sums their rows in order
 constexpr int EMB_CHUNK = 128;  // ids per rank workgroup: many small workgroups fill the chip
 constexpr int EMB_MAXN = 1 << 20;
 __global__ __launch_bounds__(256) void emb_rank_kernel(int n, const int64_t* __restrict__ ids,
@@ -143,7 +143,10 @@ __global__ __launch_bounds__(256) void emb_scatter_kernel(int n, const int64_t* 
 }
 
 constexpr int EMB_MAXDIM = 2048;  // columns: 8 per lane, at most 4 passes of 512
-constexpr int EMB_CH = 64;        // sorted indices per chunk (one wave's share of a long run)
+// sorted indices per chunk (one wave's share of a long run).  16, not 64: the bench's captions all
+// start with <start>, a 64-position run that one wave summed in 8 dependent load rounds (55.8 us
+// per launch in the C3 step, rocprof round 6); as 4 pieces the rounds run on 4 waves
+constexpr int EMB_CH = 16;
 // The rows of each id summed in position order, in chunks of the sorted index array aligned to
 // EMB_CH: a wave owns a chunk's piece of a run (the run's head, or the chunk's first index when
 // the run started in an earlier chunk).  A run inside one chunk is added to the table directly; a
@@ -260,7 +263,18 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(int n, int dim, const 
   const int id = sid[last];
   if (sid[last + 1] != id) return;                     // no run crosses this chunk's end
   if (k > 0 && sid[k * EMB_CH - 1] == id) return;      // it started in an earlier chunk
+  // the continuation chunks k+1 .. k+cnt, found 64 at a time (lane l tests chunk base + l) instead
+  // of one dependent id load per chunk
+  int cnt = 0;
+  for (int base = k + 1;; base += 64) {
+    const int jc = base + lane;
+    const unsigned long long m = __ballot(jc * EMB_CH < n && sid[jc * EMB_CH] == id);
+    const int run = ~m ? __ffsll((long long)~m) - 1 : 64;
+    cnt += run;
+    if (run < 64) break;
+  }
   constexpr int NC = EMB_MAXDIM / 512;
+  constexpr int PB = 8;  // continuation pieces in flight before their (ordered) additions
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int c0 = c * 512 + lane * 8;
@@ -269,10 +283,20 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(int n, int dim, const 
     const float* h = ws + ((long)k * 2 + 1) * dim + c0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) t[e] = c0 + e < dim ? h[e] : 0.f;
-    for (int jc = k + 1; jc * EMB_CH < n && sid[jc * EMB_CH] == id; ++jc) {
-      const float* q = ws + (long)jc * 2 * dim + c0;
+    for (int j0 = 0; j0 < cnt; j0 += PB) {
+      float q[PB][8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) t[e] += c0 + e < dim ? q[e] : 0.f;
+      for (int u = 0; u < PB; ++u) {
+        const float* qp = ws + (long)(k + 1 + min(j0 + u, cnt - 1)) * 2 * dim + c0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q[u][e] = c0 + e < dim ? qp[e] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        if (j0 + u >= cnt) break;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] += q[u][e];
+      }
     }
     float* tp = dtable + (long)id * dim + c0;
 #pragma unroll
@@ -534,8 +558,8 @@ extern "C" int imgcap_embedding_bwd(int dtype, int n, int dim, const int64_t* id
   const size_t idx_bytes = (2 * (size_t)n * sizeof(int) + 15) / 16 * 16;
   const int nchunks = (n + EMB_CH - 1) / EMB_CH;
   // workspace: ranks + sorted indices (12 B per position) and two dim-wide fp32 slots per chunk for
-  // runs crossing a chunk boundary -- ~n * dim / 8 bytes plus 12 n: 0.6 MB at C3 (n = 3,328,
-  // dim = 512), 256 MiB at the limits (n = 2^20, dim = 2048); the library workspace keeps its
+  // runs crossing a chunk boundary -- ~n * dim / 2 bytes plus 12 n: 0.9 MB at C3 (n = 3,328,
+  // dim = 512), 1 GiB at the limits (n = 2^20, dim = 2048); the library workspace keeps its
   // high-water mark for the process (imgcap_workspace_needed / _attach size it)
   int* rank = (int*)workspace(rank_bytes + idx_bytes + (size_t)nchunks * 2 * dim * sizeof(float), st);
   if (!rank) return fail(IMGCAP_EWORKSPACE, std::string("imgcap_embedding_bwd: ") + last_error());

@@ -654,8 +654,8 @@ def test_tf_targets_match_reference_formulas(hip_device, B, L):
                                          (256, 3, 64, 0)])
 def test_embedding_bwd_long_runs_chunked_order(hip_device, dtype, n, V, dim, run):
     """A padding id occupying thousands of positions (captions padded to L) is summed by many
-    waves: the sorted index array is cut at multiples of 64, each piece of a run is added in
-    position order and the pieces of a run in chunk order.  The table must be bitwise that fp32
+    waves: the sorted index array is cut at multiples of 16 (EMB_CH), each piece of a run is added
+    in position order and the pieces of a run in chunk order.  The table must be bitwise that fp32
     order (restated here), and within fp32 rounding of the fp64 sum."""
     from imagecaptioningconvnext_amd import kernels as K
     g = torch.Generator().manual_seed(n + run)
@@ -674,7 +674,7 @@ def test_embedding_bwd_long_runs_chunked_order(hip_device, dtype, n, V, dim, run
             e += 1
         pieces, a = [], i
         while a < e:
-            b = min(e, (a // 64 + 1) * 64)
+            b = min(e, (a // 16 + 1) * 16)
             acc = torch.zeros(dim)
             for t in range(a, b):
                 acc = acc + x[order[t]]
