@@ -83,7 +83,14 @@ _open_forks = {}
 
 
 def fork(side, src):
-    """``side`` waits for ``src``'s work so far and is recorded as an open branch."""
+    """``side`` waits for ``src``'s work so far and is recorded as an open branch.  A branch forked
+    from a stream that is itself an open branch is refused: inside a HIP graph capture that nesting
+    (M -> S -> X, X joined to S, S to M) crashes hipStreamEndCapture with a segfault on ROCm 7.2
+    (tools/probe/capture_refork.py "nested"), so every fork starts from a stream that
+    is not a branch.  Checked in eager runs too: the engines run the same code eagerly first."""
+    if src.cuda_stream in _open_forks and src.cuda_stream != side.cuda_stream:
+        raise RuntimeError(f"stream {hex(src.cuda_stream)} is an open branch: forking {hex(side.cuda_stream)} from "
+                           "it would nest branches, which crashes HIP graph capture (DESIGN §2b)")
     side.wait_stream(src)
     _open_forks[side.cuda_stream] = side
 

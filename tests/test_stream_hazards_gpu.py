@@ -108,3 +108,37 @@ def test_library_refuses_one_slot_scratch_from_two_streams_of_a_capture(hip_devi
         else:
             assert err is not None and "two streams of one captured graph" in err, err
         del g
+
+
+def test_nested_fork_refused_before_it_reaches_the_capture(hip_device):
+    """A branch forked from an open branch (M -> S -> X) crashes hipStreamEndCapture with a
+    segfault on ROCm 7.2 (tools/probe/capture_refork.py "nested").  kernels.fork
+    refuses it -- eagerly and inside a capture -- and the capture that asked for it still ends and
+    replays normally once its open branch is joined."""
+    from imagecaptioningconvnext_amd import kernels as K
+    dev = hip_device
+    x = torch.zeros(1024, device=dev)
+    S, X = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    main = torch.cuda.current_stream(dev)
+    K.fork(S, main)
+    with pytest.raises(RuntimeError, match="open branch"):
+        K.fork(X, S)
+    K.join(main, S)
+    K.assert_joined("eager")
+    torch.cuda.synchronize()
+    cap = torch.cuda.Stream(device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(cap):
+        g.capture_begin()
+        K.fork(S, cap)
+        with torch.cuda.stream(S):
+            x.add_(1.0)
+            with pytest.raises(RuntimeError, match="open branch"):
+                K.fork(X, S)
+        K.join(cap, S)
+        K.assert_joined("test")
+        g.capture_end()
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(x, torch.full_like(x, 2.0))

@@ -8,13 +8,17 @@ dropout 0.5) into HIP graphs and times the replays:
   two32   : two B = 32 chains on two streams in one graph (own gradient buffers, scratch slot 1
             for the second chain)
 usage: python tools/probe/dec_split.py [reps]"""
+import faulthandler
 import os
 import sys
+
+faulthandler.enable()
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from imagecaptioningconvnext_amd import kernels as K  # noqa: E402
+from imagecaptioningconvnext_amd import transformer_engine as TE  # noqa: E402
 from imagecaptioningconvnext_amd.models.transformerDecoder import TransformerDecoder  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
@@ -44,6 +48,7 @@ def timed(fn):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    print("eager ok", flush=True)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         fn()
@@ -66,10 +71,13 @@ side = torch.cuda.Stream(device=dev)
 
 def two():
     main = torch.cuda.current_stream(dev)
+    print("two: fork", flush=True)
     K.fork(side, main)
     with torch.cuda.stream(side), K.workspace_slot(1):
         chain(b32b, g2)
+    print("two: side chain issued", flush=True)
     chain(b32a, None)
+    print("two: main chain issued", flush=True)
     K.join(main, side)
 
 
@@ -77,5 +85,10 @@ t64 = timed(lambda: chain(b64, None))
 print(f"one64: {t64:8.1f} us", flush=True)
 t32 = timed(lambda: chain(b32a, None))
 print(f"one32: {t32:8.1f} us  ({t32 / t64:.2f} of one64)", flush=True)
+# (the engine's tail side stream stays off here: one stream forked from two different capturing
+# streams of one capture crashed hipStreamEndCapture -- tools/probe/capture_refork.py)
+TE.TAIL_FORK = False
+t1 = timed(lambda: chain(b64, None))
+print(f"one64 without the tail fork: {t1:8.1f} us", flush=True)
 t2 = timed(two)
 print(f"two32: {t2:8.1f} us  ({t2 / t64:.2f} of one64)", flush=True)
