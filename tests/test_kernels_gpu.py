@@ -40,7 +40,8 @@ def test_gemm_layouts(hip_device, dtype, tol, ta, tb, M, N, Kd):
         ref = a.bfloat16().float() @ b.bfloat16().float()
     assert _rel(out.cpu(), ref) < tol
     if dtype == torch.bfloat16:  # the same product on the 256x256 tile (forced), the small-grid
-        for pol in (1, 2, 3, 0, 6, 7, 8):  # 64x64 / 128x64 LDS-DMA tiles and the register-staged one
+        for pol in (1, 2, 3, 0, 6, 8):  # 64x64 LDS-DMA tile and the register-staged one (the 128x64 tile,
+            # policy 7, is in the diagnostic build only: tests/test_gemm_pt_gpu.py checks the refusal)
             K.gemm_set_policy(pol)
             try:
                 out = K.gemm(ad, bd, trans_a=ta, trans_b=tb, out_dtype=torch.float32)
@@ -94,7 +95,7 @@ def test_gemm_auto_split_with_epilogue(hip_device, dtype, tol):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
-@pytest.mark.parametrize("policy", [-1, 1, 2, 7, 8])
+@pytest.mark.parametrize("policy", [-1, 1, 2, 8])
 def test_gemm_epilogues(hip_device, dtype, tol, policy):
     K.gemm_set_policy(policy)
     try:

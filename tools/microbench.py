@@ -241,8 +241,7 @@ def small():
         w = (torch.randn(N, Kd, device=dev) if tb else torch.randn(Kd, N, device=dev)).to(bf)
         bias = torch.randn(N, device=dev)
         fl = 2.0 * M * N * Kd
-        for pol, name in ((-1, "auto"), (4, "glds128"), (5, "tiled"), (6, "glds64"), (7, "glds128x64"),
-                          (8, "tiled64")):
+        for pol, name in ((-1, "auto"), (4, "glds128"), (5, "tiled"), (6, "glds64"), (8, "tiled64")):
             K.gemm_set_policy(pol)
             t = time_launch(lambda: K.gemm(a, w, trans_b=tb, bias=bias))
             print(f"M={M} N={N} K={Kd} tb={int(tb)} {name:8s}: {t * 1e6:7.1f} us {fl / t / 1e12:6.1f} TF")
