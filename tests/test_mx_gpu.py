@@ -65,6 +65,23 @@ def test_gemm_mx_matches_dequantized_product(hip_device, M, N, Kd):
     assert _rel(K.mx_dequant(*hq), F.gelu(ref)) < 0.04
 
 
+@pytest.mark.parametrize("M,N,Kd", [(12544, 768, 3072), (12544, 3072, 768), (50176, 384, 1536)])
+def test_gemm_mx_c5_shapes(hip_device, M, N, Kd):
+    """The C5 frozen-stage shapes (ConvNeXt-Large stage 3 at B = 64, stage 2's second Linear): the
+    product of the dequantised operands within the MFMA's fp32 accumulation error of the fp64
+    product (measured 1.0e-5 at K = 3072; the gate of the test above), bitwise repeatable."""
+    from imagecaptioningconvnext_amd import kernels as K
+    g = torch.Generator().manual_seed(M + N + Kd)
+    a, b = torch.randn(M, Kd, generator=g), torch.randn(N, Kd, generator=g) / Kd ** 0.5
+    bias = torch.randn(N, generator=g)
+    aq, bq = K.mx_quant_rows(a.to(hip_device)), K.mx_quant_rows(b.to(hip_device))
+    ref = K.mx_dequant(*aq).double() @ K.mx_dequant(*bq).double().t() + bias.to(hip_device).double()
+    o1 = K.gemm_mx(aq, bq, bias=bias.to(hip_device), out_dtype=torch.float32)
+    o2 = K.gemm_mx(aq, bq, bias=bias.to(hip_device), out_dtype=torch.float32)
+    assert torch.equal(o1, o2)
+    assert _rel(o1, ref) < 5e-5
+
+
 def test_gemm_mx_residual_epilogue(hip_device):
     """bf16 out = x + gamma * rowscale * (A B^T + b): the second Linear of the frozen CNBlock."""
     from imagecaptioningconvnext_amd import kernels as K
