@@ -158,9 +158,12 @@ def _work(fn, a):
     if fn == "imgcap_add_layernorm_fwd":  # x (+ r) read, y (+ s_out) written
         n = a[1] * a[2] * _esz(a[0])
         return sym, sym, "hbm", n * (2 + (a[4] is not None) + (a[11] is not None)), PEAK_HBM_GBS, (a[1], a[2])
-    if fn == "imgcap_add_layernorm_bwd":  # dy, s read, dx (+ dr) written (+ fp32 dy*xhat)
+    if fn == "imgcap_add_layernorm_bwd":  # dy, s read, dx (+ dr) written (+ the per-block partials)
         n = a[1] * a[2]
-        b = n * _esz(a[0]) * (3 + (a[12] is not None)) + (n * 4 if a[15] is not None else 0)
+        part = 0
+        if a[15] is not None:  # [nblk][2][cols] fp32 gamma / beta partials (the caller's column sums)
+            part = _abi.lib().imgcap_add_layernorm_bwd_blocks(a[1]) * 2 * a[2] * 4
+        b = n * _esz(a[0]) * (3 + (a[12] is not None)) + part
         return sym, sym, "hbm", b, PEAK_HBM_GBS, (a[1], a[2])
     if fn == "imgcap_clamp_adam":  # p, g, m, v read; p, m, v written (fp32) + bf16 shadow written
         n = a[0]
