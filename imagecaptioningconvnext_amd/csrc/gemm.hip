@@ -818,12 +818,14 @@ static int ws_plan(int ak, int bk, int M, int N, int K, long lda, long ldb, long
   return 0;
 }
 
+#ifdef IMGCAP_STAMPS
 template <int KS, int NW, int S>
 void wsp_go(const WsArgs& a, int act, dim3 grid, hipStream_t st) {
   if (act == IMGCAP_ACT_GELU) hipLaunchKernelGGL((gemm_wsp_kernel<KS, NW, S, 1>), grid, dim3(NW * 64), 0, st, a);
   else if (act == IMGCAP_ACT_RELU) hipLaunchKernelGGL((gemm_wsp_kernel<KS, NW, S, 2>), grid, dim3(NW * 64), 0, st, a);
   else hipLaunchKernelGGL((gemm_wsp_kernel<KS, NW, S, 0>), grid, dim3(NW * 64), 0, st, a);
 }
+#endif
 
 template <int KS, int NW, int S, bool STG = false>
 void ws_go(const WsArgs& a, int act, dim3 grid, hipStream_t st) {
@@ -854,19 +856,24 @@ static int ws_launch(int cfg, int M, int N, int K, const bf16* A, long lda, cons
   a.b_bytes = ((int64_t)(N - 1) * ldb + K) * 2;
   a.c_bytes = ((int64_t)(M - 1) * ldc + N) * 2;
   const dim3 grid(a.slices * a.row_groups);
-  static const int deep = [] {  // A/B switch: deeper A-chunk rings (IMGCAP_WS_DEEP=1)
-    const char* e = getenv("IMGCAP_WS_DEEP");
-    return e ? atoi(e) : 0;
-  }();
   static const int stg = [] {  // output tile staged through LDS (default; IMGCAP_WS_STG=0: 8-byte stores)
     const char* e = getenv("IMGCAP_WS_STG");
     return e ? atoi(e) : 1;
   }();
-  static const int pipe = [] {  // A/B switch: the software-pipelined form (IMGCAP_WS_PIPE=1)
+#ifdef IMGCAP_STAMPS  // diagnostic build: the measured-slower forms (gemm_ws.h)
+  static const int deep = [] {  // deeper A-chunk rings (IMGCAP_WS_DEEP=1)
+    const char* e = getenv("IMGCAP_WS_DEEP");
+    return e ? atoi(e) : 0;
+  }();
+  static const int pipe = [] {  // the software-pipelined form (IMGCAP_WS_PIPE=1)
     const char* e = getenv("IMGCAP_WS_PIPE");
     return e ? atoi(e) : 0;
   }();
+#else
+  constexpr int deep = 0, pipe = 0;
+#endif
   if (pipe && !ep.colscale) {
+#ifdef IMGCAP_STAMPS
     if (K == 384) {
       if (NW == 8) wsp_go<24, 8, 4>(a, ep.act, grid, st);
       else wsp_go<24, 4, 3>(a, ep.act, grid, st);
@@ -874,6 +881,7 @@ static int ws_launch(int cfg, int M, int N, int K, const bf16* A, long lda, cons
       if (NW == 8) wsp_go<32, 8, 3>(a, ep.act, grid, st);
       else wsp_go<32, 4, 2>(a, ep.act, grid, st);
     }
+#endif
   } else if (stg && N % 8 == 0) {
     if (K == 384) {
       if (NW == 8) ws_go<24, 8, 5, true>(a, ep.act, grid, st);
@@ -884,15 +892,21 @@ static int ws_launch(int cfg, int M, int N, int K, const bf16* A, long lda, cons
     }
   } else if (K == 384) {
     if (NW == 8) {
+#ifdef IMGCAP_STAMPS
       if (deep) ws_go<24, 8, 6>(a, ep.act, grid, st);
-      else ws_go<24, 8, 3>(a, ep.act, grid, st);
+      else
+#endif
+        ws_go<24, 8, 3>(a, ep.act, grid, st);
     } else {
       ws_go<24, 4, 3>(a, ep.act, grid, st);
     }
   } else {
     if (NW == 8) {
+#ifdef IMGCAP_STAMPS
       if (deep) ws_go<32, 8, 4>(a, ep.act, grid, st);
-      else ws_go<32, 8, 3>(a, ep.act, grid, st);
+      else
+#endif
+        ws_go<32, 8, 3>(a, ep.act, grid, st);
     } else {
       ws_go<32, 4, 2>(a, ep.act, grid, st);
     }
