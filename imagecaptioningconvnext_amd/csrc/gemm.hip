@@ -68,11 +68,16 @@ DEV void epi_vec8(const imgcap_epilogue& ep, const EpiFlags& f, void* C, long ci
   }
   if (ep.act == IMGCAP_ACT_GELU) {
     if (f.aux) store_pre8(ep, m, n0, v);  // pre-activation kept for the backward pass
+    if (ep.c_dtype != IMGCAP_F32) {  // bf16 / MX out: the sigmoid form (common.h: |error| <= 5.5e-5)
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {  // erf by a 1.5e-7-accurate polynomial (common.h gelu_fast2)
-      const f32x2 g = gelu_fast2(f32x2{v[j], v[j + 1]});
-      v[j] = g[0];
-      v[j + 1] = g[1];
+      for (int j = 0; j < 8; ++j) v[j] = gelu_sig(v[j]);
+    } else {  // fp32 out: erf by a 1.5e-7-accurate polynomial
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const f32x2 g = gelu_fast2(f32x2{v[j], v[j + 1]});
+        v[j] = g[0];
+        v[j + 1] = g[1];
+      }
     }
   } else if (ep.act == IMGCAP_ACT_RELU) {
 #pragma unroll
@@ -142,7 +147,7 @@ DEV void epi_scalar(const imgcap_epilogue& ep, void* C, long cidx, int m, int n,
   if (ep.bias) v += ep.bias[n];
   if (ep.act == IMGCAP_ACT_GELU) {
     if (ep.aux) store_from_f((void*)ep.aux, (long)m * ep.ldaux + n, ep.c_dtype, v);
-    v = gelu_fast(v);
+    v = ep.c_dtype != IMGCAP_F32 ? gelu_sig(v) : gelu_fast(v);
   } else if (ep.act == IMGCAP_ACT_RELU) {
     v = fmaxf(v, 0.f);
   }
@@ -300,11 +305,16 @@ DEV void epilogue_tile(const imgcap_epilogue& ep, const float* tile, int LDT, in
       for (int j = 0; j < 8; ++j) x[j] = v[u][j] * ep.alpha + bias[j];
       if (ep.act == IMGCAP_ACT_GELU) {
         if (pre_gelu) store_pre8(ep, m, n, x);
+        if (ep.c_dtype != IMGCAP_F32) {  // bf16 / MX out: the sigmoid form (|error| <= 5.5e-5)
 #pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const f32x2 g = gelu_fast2(f32x2{x[j], x[j + 1]});
-          x[j] = g[0];
-          x[j + 1] = g[1];
+          for (int j = 0; j < 8; ++j) x[j] = gelu_sig(x[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const f32x2 g = gelu_fast2(f32x2{x[j], x[j + 1]});
+            x[j] = g[0];
+            x[j + 1] = g[1];
+          }
         }
       } else if (ep.act == IMGCAP_ACT_RELU) {
 #pragma unroll

@@ -525,11 +525,7 @@ __global__ __launch_bounds__(WM* WN * 64, WPE) void gemm_pt_kernel(PtArgs a) {
           if (ep.act == IMGCAP_ACT_GELU) {
             if (aux_out) pt_st64(rs_aux, off(m, n, ep.ldaux), pt_u32x2{pt_pack(x[0], x[1]), pt_pack(x[2], x[3])});
 #pragma unroll
-            for (int r = 0; r < 4; r += 2) {
-              const f32x2 gg = gelu_fast2(f32x2{x[r], x[r + 1]});
-              x[r] = gg[0];
-              x[r + 1] = gg[1];
-            }
+            for (int r = 0; r < 4; ++r) x[r] = gelu_sig(x[r]);
           } else if (ep.act == IMGCAP_ACT_RELU) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) x[r] = fmaxf(x[r], 0.f);
