@@ -308,6 +308,10 @@ def mx():
         print(f"bf16 gemm M={M} N={N} K={Kd}: {t * 1e6:7.1f} us {fl / t / 1e12:7.1f} TF")
         t = time_launch(lambda: K.gemm_mx(aq, wq))
         print(f"mx   gemm M={M} N={N} K={Kd}: {t * 1e6:7.1f} us {fl / t / 1e12:7.1f} TF (bf16 out)")
+        t = time_launch(lambda: K.gemm_mx(aq, wq, act=K.ACT_GELU))
+        print(f"mx   gemm M={M} N={N} K={Kd}: {t * 1e6:7.1f} us {fl / t / 1e12:7.1f} TF (GELU + bf16 out)")
+        t = time_launch(lambda: K.gemm_mx(aq, wq, out_dtype="mx"))
+        print(f"mx   gemm M={M} N={N} K={Kd}: {t * 1e6:7.1f} us {fl / t / 1e12:7.1f} TF (MX out)")
         t = time_launch(lambda: K.gemm_mx(aq, wq, act=K.ACT_GELU, out_dtype="mx"))
         print(f"mx   gemm M={M} N={N} K={Kd}: {t * 1e6:7.1f} us {fl / t / 1e12:7.1f} TF (GELU + MX out)")
     x = torch.randn(M, C, device=dev).to(bf)
