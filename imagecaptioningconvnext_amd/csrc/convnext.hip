@@ -38,7 +38,7 @@ template <> struct StemIn<uint8_t> {
 // padded to STEM_PS floats (16-byte rows; the pixels of a wave read distinct banks).  Per pixel
 // the arithmetic is unchanged: bias, then k = 0..47 in order, LayerNorm sums over j then cv.
 constexpr int STEM_PS = 52;
-template <typename T, typename TI = float>
+template <typename T, typename TI = float, int PX = 2>
 __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0, const TI* __restrict__ img,
                                                     const float* __restrict__ w, const float* __restrict__ bias,
                                                     const float* __restrict__ lw, const float* __restrict__ lb,
@@ -68,37 +68,47 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
     *(f32x4*)(patch + q * STEM_PS + ci * 16 + kh * 4) = v;
   }
   __syncthreads();
-  const int half = npx / 2;
+  // PX patches per thread (q, q + npx/PX, ...), each weight vector read from LDS serving all PX;
+  // the patch values come 4 k at a time (one ds_read_b128 per patch): with PX = 4 a thread reads
+  // 48 / 4 * PX + 48 * 2 vectors for 48 * 8 * PX FMAs instead of 48 * 2 scalars + 48 * 2 vectors
+  // for 48 * 16 (the kernel is LDS-issue bound)
+  const int half = npx / PX;
   const int q = threadIdx.x / CV, cv = threadIdx.x % CV, c0 = cv * 8;
-  const int qp[2] = {q, q + half};
-  bool active[2];
+  int qp[PX];
+  bool active[PX];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) active[u] = q < half && px0 + qp[u] < total;
-  float acc[2][8];
+  for (int u = 0; u < PX; ++u) {
+    qp[u] = q + u * half;
+    active[u] = q < half && px0 + qp[u] < total;
+  }
+  float acc[PX][8];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < PX; ++u)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[u][j] = 0.f;
   if (q < half) {
     const f32x4 b0 = *(const f32x4*)(bias + c0), b1 = *(const f32x4*)(bias + c0 + 4);
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < PX; ++u)
 #pragma unroll
       for (int j = 0; j < 4; ++j) { acc[u][j] = b0[j]; acc[u][j + 4] = b1[j]; }
-    const float* pa = patch + qp[0] * STEM_PS;
-    const float* pb = patch + qp[1] * STEM_PS;
-#pragma unroll 8
-    for (int k = 0; k < 48; ++k) {
-      const float xa = pa[k], xb = pb[k];
-      const f32x4 w0 = *(const f32x4*)(ws + k * C0 + c0), w1 = *(const f32x4*)(ws + k * C0 + c0 + 4);
+#pragma unroll 2
+    for (int k4 = 0; k4 < 48; k4 += 4) {
+      f32x4 xp[PX];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[0][j] += xa * w0[j]; acc[0][j + 4] += xa * w1[j];
-        acc[1][j] += xb * w0[j]; acc[1][j + 4] += xb * w1[j];
+      for (int u = 0; u < PX; ++u) xp[u] = *(const f32x4*)(patch + qp[u] * STEM_PS + k4);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int k = k4 + kk;
+        const f32x4 w0 = *(const f32x4*)(ws + k * C0 + c0), w1 = *(const f32x4*)(ws + k * C0 + c0 + 4);
+#pragma unroll
+        for (int u = 0; u < PX; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { acc[u][j] += xp[u][kk] * w0[j]; acc[u][j + 4] += xp[u][kk] * w1[j]; }
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PX; ++u) {
       if (!active[u]) continue;
       float s = 0.f;
 #pragma unroll
@@ -109,7 +119,7 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
   __syncthreads();
   if (cv == 0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PX; ++u) {
       if (!active[u]) continue;
       float s = 0.f;
       for (int i = 0; i < CV; ++i) s += red[qp[u] * CV + i];
@@ -117,9 +127,11 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
     }
   }
   __syncthreads();
-  float mean[2] = {0.f, 0.f};
+  float mean[PX];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < PX; ++u) mean[u] = 0.f;
+#pragma unroll
+  for (int u = 0; u < PX; ++u) {
     if (!active[u]) continue;
     mean[u] = stat[qp[u] * 2];
     float s = 0.f;
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
   __syncthreads();
   if (cv == 0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PX; ++u) {
       if (!active[u]) continue;
       float s = 0.f;
       for (int i = 0; i < CV; ++i) s += red[qp[u] * CV + i];
@@ -142,7 +154,7 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
     const f32x4 g0 = *(const f32x4*)(lw + c0), g1 = *(const f32x4*)(lw + c0 + 4);
     const f32x4 h0 = *(const f32x4*)(lb + c0), h1 = *(const f32x4*)(lb + c0 + 4);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PX; ++u) {
       if (!active[u]) continue;
       const float rstd = stat[qp[u] * 2 + 1];
       float o[8];
@@ -165,11 +177,22 @@ __global__ __launch_bounds__(1024) void stem_kernel(int B, int H, int W, int C0,
   }
 }
 
-// pixels per stem block (even: two per thread) and its LDS bytes
-static int stem_npx(int C0) {
-  int npx = 2 * (1024 / (C0 / 8));
+// patches per stem thread, pixels per stem block (a multiple of it) and its LDS bytes.  4 patches
+// per thread where the channel count gives the block enough threads (tools/gpu/r6_stem.sh, µs at
+// 224x224, outputs bitwise equal): C0 = 128 B = 32 56.7 -> 44.6, C0 = 192 B = 64 148 -> 130;
+// C0 = 96 (Tiny) keeps 2: 35.3 vs 43.4 at B = 32, 64 vs 72 at B = 64.  IMGCAP_STEM_PX=2/4 overrides.
+static int stem_px(int C0) {
+  static const int v = [] {
+    const char* e = getenv("IMGCAP_STEM_PX");
+    return e ? atoi(e) : 0;
+  }();
+  if (v == 2 || v == 4) return v;
+  return C0 >= 128 ? 4 : 2;
+}
+static int stem_npx(int C0, int px) {
+  int npx = px * (1024 / (C0 / 8));
   if (npx > 128) npx = 128;
-  return npx & ~1;
+  return npx / px * px;
 }
 static size_t stem_lds(int C0, int npx) {
   return (48 * (size_t)C0 + (size_t)npx * STEM_PS + (size_t)npx * (C0 / 8) + (size_t)npx * 2) * sizeof(float);
@@ -1198,17 +1221,21 @@ extern "C" int imgcap_convnext_stem(int dtype, int B, int H, int W, int C0, cons
   const long total = (long)B * (H / 4) * (W / 4);
   if (total == 0) return 0;
   const int CV = C0 / 8;
-  const int npx = stem_npx(C0);
-  const int threads = ((npx / 2 * CV + 63) / 64) * 64;
+  const int px = stem_px(C0);
+  const int npx = stem_npx(C0, px);
+  const int threads = ((npx / px * CV + 63) / 64) * 64;
   dim3 grid((unsigned)((total + npx - 1) / npx));
   const size_t shm = stem_lds(C0, npx);
   IMGCAP_REQUIRE(shm <= 160 * 1024, "imgcap_convnext_stem: LDS");
-  if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL((stem_kernel<bf16, float>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, images,
-                       w, bias, ln_w, ln_b, (bf16*)out, npx, nullptr, nullptr);
-  else
-    hipLaunchKernelGGL((stem_kernel<float, float>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0,
-                       images, w, bias, ln_w, ln_b, (float*)out, npx, nullptr, nullptr);
+#define STEM_(T, PXN)                                                                                     \
+  hipLaunchKernelGGL((stem_kernel<T, float, PXN>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, \
+                     images, w, bias, ln_w, ln_b, (T*)out, npx, nullptr, nullptr)
+  if (dtype == IMGCAP_BF16) {
+    if (px == 4) STEM_(bf16, 4); else STEM_(bf16, 2);
+  } else {
+    if (px == 4) STEM_(float, 4); else STEM_(float, 2);
+  }
+#undef STEM_
   IMGCAP_CHECK_LAUNCH("imgcap_convnext_stem");
   return 0;
 }
@@ -1223,17 +1250,21 @@ extern "C" int imgcap_convnext_stem_u8(int dtype, int B, int H, int W, int C0, c
   const long total = (long)B * (H / 4) * (W / 4);
   if (total == 0) return 0;
   const int CV = C0 / 8;
-  const int npx = stem_npx(C0);
-  const int threads = ((npx / 2 * CV + 63) / 64) * 64;
+  const int px = stem_px(C0);
+  const int npx = stem_npx(C0, px);
+  const int threads = ((npx / px * CV + 63) / 64) * 64;
   dim3 grid((unsigned)((total + npx - 1) / npx));
   const size_t shm = stem_lds(C0, npx);
   IMGCAP_REQUIRE(shm <= 160 * 1024, "imgcap_convnext_stem_u8: LDS");
-  if (dtype == IMGCAP_BF16)
-    hipLaunchKernelGGL((stem_kernel<bf16, uint8_t>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0,
-                       images, w, bias, ln_w, ln_b, (bf16*)out, npx, mean3, std3);
-  else
-    hipLaunchKernelGGL((stem_kernel<float, uint8_t>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0,
-                       images, w, bias, ln_w, ln_b, (float*)out, npx, mean3, std3);
+#define STEM_(T, PXN)                                                                                       \
+  hipLaunchKernelGGL((stem_kernel<T, uint8_t, PXN>), grid, dim3(threads), shm, (hipStream_t)stream, B, H, W, C0, \
+                     images, w, bias, ln_w, ln_b, (T*)out, npx, mean3, std3)
+  if (dtype == IMGCAP_BF16) {
+    if (px == 4) STEM_(bf16, 4); else STEM_(bf16, 2);
+  } else {
+    if (px == 4) STEM_(float, 4); else STEM_(float, 2);
+  }
+#undef STEM_
   IMGCAP_CHECK_LAUNCH("imgcap_convnext_stem_u8");
   return 0;
 }
