@@ -645,6 +645,10 @@ static int pt_choose(int M, int N, int K, int ek, bool ak, bool bk) {
 static int pt_by_shape(int M, int N, int K, int ek, bool ak, bool bk) {
   if (!(ak && bk) || ek > 1) return 0;
   int c = 0;
+  // (round 6: Tiny's stage-4 first Linear 3136x3072x768 on 128x192 and Base's stage-3 first Linear
+  // 6272x2048x512 on 128x128 two a CU ran 30.1 / 30.3 µs against 32.8 / 32.1 alone, but the steps
+  // fell: C4 8,396 / 8,346 -> 8,232 / 8,221, C3 19,871 / 19,838 -> 19,742 / 19,749 img/s on one box,
+  // tools/gpu/r6_ptrule.sh -- the census rule above holds)
   if (N == 384 && M >= 8192) c = 4;
   else if (N == 256 && M >= 8192) c = 5;
   else if (N == 512 && K >= 1024 && M >= 4096) c = 6;
@@ -819,11 +823,12 @@ static int ws_plan(int ak, int bk, int M, int N, int K, long lda, long ldb, long
   if (mode == 1 || mode == 2) return mode;
   // by shape (tools/ws_bench.py, round 6, us per launch against the plan without this kernel):
   // 12544x1536x384 +GELU 32.2 vs 39.9 (4-wave blocks), 25088x1536x384 50.0 vs 64.5, 50176x192x384
-  // 18.8 vs 21.7, 3136x6144x512 (the decoder's stacked memory K/V) 32.4 vs 40.2 (8-wave blocks).
+  // 18.8 vs 21.7, 3136x6144x512 (the decoder's stacked memory K/V) 32.4 vs 40.2 (8-wave blocks);
+  // with the sigmoid-form GELU in both epilogues also C2's 6272x1536x384 +GELU 20.0 vs 22.4.
   // Elsewhere -- the decoder's 3328-row d = 512 products, C4's 6272x2048x512 -- the per-block weight
   // slice load (the kernel's fixed cost, ~8-10 us) is not amortised and the 64x64 LDS tile stays.
   if (N % 8 != 0 || (ep && ep->colscale)) return 0;
-  if (K == 384 && M >= 8192 && (N >= 1024 || N == 192)) return 2;
+  if (K == 384 && M >= 4096 && (N >= 1024 || N == 192)) return 2;
   if (K == 512 && N >= 4096 && M >= 2048) return 1;
   return 0;
 }

@@ -73,10 +73,10 @@ def case(name, M, N, Kd, form):
     tt = time_launch(lambda: torch.matmul(a, b.t()), reps=reps)
     f = 2.0 * M * N * Kd
     cells = " ".join(f"{t * 1e6:7.1f}" for t in row)
-    best = min(row[1:-1])
+    best = min(row[1:-1]) if len(row) > 2 else row[-1]
     print(f"{name:18s} {M:6d} {N:5d} {Kd:5d} | {cells} | blaslt {tt * 1e6:7.1f} | "
-          f"old {f / row[0] / 1e12:6.0f} TF  st-best {f / best / 1e12:6.0f} TF  st-auto {f / row[6] / 1e12:6.0f} TF "
-          f"({row[0] / row[6]:.2f}x)", flush=True)
+          f"old {f / row[0] / 1e12:6.0f} TF  st-best {f / best / 1e12:6.0f} TF  st-auto {f / row[-1] / 1e12:6.0f} TF "
+          f"({row[0] / row[-1]:.2f}x)", flush=True)
 
 
 print(f"{'shape':18s} {'M':>6s} {'N':>5s} {'K':>5s} | " + " ".join(f"{NAMES[m]:>7s}" for m in MODES) + " | us",
